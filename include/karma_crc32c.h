@@ -1,0 +1,106 @@
+/* include/karma_crc32c.h -- C ABI of the MI355X CRC-32C engine (libkarma_crc32c.so).
+ *
+ * Plain C: pointers, sizes and integer status codes; no HIP, torch or C++
+ * types.  Streams are passed as `karma_stream_t` (a hipStream_t cast to
+ * void*, NULL = the default stream).  Device-pointer ("d_") entry points are
+ * stream-ordered and asynchronous: they enqueue work on `stream` and return;
+ * the caller synchronises.  Host-pointer ("h_") entry points are synchronous.
+ *
+ * Reference interfaces each entry point replaces:
+ *   karma_crc32c_extend_host        crc32c::Extend        karma-util/crc32c.h:16, crc32c.cc:275-376
+ *   karma_crc32c_batch_fixed        crc32c::Value per record, as called by
+ *                                   segment_file::append_record  karma-store/segment_file.cc:22
+ *   karma_crc32c_batch_ragged       crc32c::Value per payload, as called by
+ *                                   wal::scan_record             karma-store/wal.cc:60
+ *   karma_crc32c_stream             crc32c::Extend over one long buffer (a 64 MiB segment image)
+ *   karma_crc32c_*_sharded / gather the same, records sharded over GPUs, CRCs gathered over RCCL
+ *
+ * Errors: 0 = success, negative = KARMA_E_* below.  No entry point throws.
+ * There is no CPU fallback behind the device entry points: without a usable
+ * MI355X they return KARMA_E_NO_DEVICE.
+ */
+#ifndef KARMA_CRC32C_H_
+#define KARMA_CRC32C_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KARMA_CRC32C_ABI_VERSION 1
+
+#define KARMA_OK 0
+#define KARMA_E_INVALID (-1)    /* bad argument (null pointer with n > 0, misuse) */
+#define KARMA_E_NO_DEVICE (-2)  /* no HIP device / runtime unavailable */
+#define KARMA_E_HIP (-3)        /* a HIP runtime call failed */
+#define KARMA_E_NOMEM (-4)      /* device or host allocation failed */
+#define KARMA_E_RCCL (-5)       /* an RCCL call failed */
+
+typedef void* karma_stream_t;         /* hipStream_t */
+typedef struct karma_comm* karma_comm_t;
+#define KARMA_UNIQUE_ID_BYTES 128     /* == sizeof(ncclUniqueId) */
+
+int karma_crc32c_abi_version(void);
+const char* karma_crc32c_strerror(int status);
+/* Thread-local detail of the last failure (HIP/RCCL error string), or "". */
+const char* karma_crc32c_last_error(void);
+
+/* ---- host, single buffer ------------------------------------------------- */
+/* crc32c::Extend(init_crc, data, n); total, never fails. */
+uint32_t karma_crc32c_extend_host(uint32_t init_crc, const void* data, size_t n);
+/* The same through the portable slicing-by-8 path only (the default path uses
+ * the SSE4.2 CRC32 instruction when present); tests compare the two. */
+uint32_t karma_crc32c_extend_host_portable(uint32_t init_crc, const void* data, size_t n);
+
+/* ---- device-resident batches (stream-ordered) ---------------------------- */
+/* d_out[r] = Extend(init_r, d_data + r*rec_bytes, rec_bytes), r < n_rec,
+ * init_r = d_init ? d_init[r] : init.  Any rec_bytes and alignment. */
+int karma_crc32c_batch_fixed(const void* d_data, size_t rec_bytes, size_t n_rec, const uint32_t* d_init,
+                             uint32_t init, uint32_t* d_out, karma_stream_t stream);
+
+/* d_out[r] = Extend(init_r, d_arena + d_off[r], d_len[r]).  Records may be
+ * unaligned, empty, in any order and may overlap.  total_len sizes the unit
+ * table: pass sum(d_len) (or any upper bound) to stay fully asynchronous;
+ * pass 0 when unknown and the call reads the unit count back (one host sync). */
+int karma_crc32c_batch_ragged(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
+                              size_t total_len, const uint32_t* d_init, uint32_t init, uint32_t* d_out,
+                              karma_stream_t stream);
+
+/* *d_out = Extend(init, d_data, n): one long buffer split over the whole GPU
+ * and folded back with a polynomial combine. */
+int karma_crc32c_stream(uint32_t init, const void* d_data, size_t n, uint32_t* d_out, karma_stream_t stream);
+
+/* ---- host-memory batches (synchronous; H2D, kernel, D2H overlapped) ------- */
+int karma_crc32c_batch_fixed_host(const void* h_data, size_t rec_bytes, size_t n_rec, uint32_t init,
+                                  uint32_t* h_out, int device);
+int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, const uint64_t* h_off,
+                                   const uint32_t* h_len, size_t n_rec, uint32_t init, uint32_t* h_out, int device);
+
+/* ---- multi-GPU: one process per GPU, RCCL over xGMI ---------------------- */
+int karma_crc32c_get_unique_id(void* uid, size_t uid_bytes);
+int karma_crc32c_comm_init(karma_comm_t* comm, int nranks, const void* uid, int rank);
+int karma_crc32c_comm_destroy(karma_comm_t comm);
+/* d_recv (root only, count*nranks words) <- every rank's d_send (count words), rank order. */
+int karma_crc32c_gather_u32(karma_comm_t comm, const uint32_t* d_send, size_t count, uint32_t* d_recv, int root,
+                            karma_stream_t stream);
+/* This rank's shard of a fixed-size batch, then the gather of its CRCs to root. */
+int karma_crc32c_batch_fixed_sharded(karma_comm_t comm, const void* d_local, size_t rec_bytes, size_t n_local,
+                                     uint32_t init, uint32_t* d_local_out, uint32_t* d_all_out, int root,
+                                     karma_stream_t stream);
+
+/* ---- synthetic data and probes (bench / tests) ---------------------------- */
+/* d_dst[i] = byte (first_byte + i) of the little-endian splitmix64 stream of
+ * `seed` (word j = mix(seed + (j+1)*0x9E3779B97F4A7C15)); first_byte % 8 == 0. */
+int karma_fill_splitmix64(void* d_dst, size_t n_bytes, uint64_t seed, uint64_t first_byte, karma_stream_t stream);
+/* Read-only streaming probe (xor of all 16-byte words) for the achievable HBM rate. */
+int karma_stream_probe(const void* d_src, size_t n_bytes, uint32_t* d_out, karma_stream_t stream);
+/* Number of compute units of the current device (grid sizing, reporting). */
+int karma_device_cu_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KARMA_CRC32C_H_ */

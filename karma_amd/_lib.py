@@ -1,0 +1,88 @@
+"""ctypes binding of libkarma_crc32c.so (the C ABI in include/karma_crc32c.h).
+
+The shared library is built in-tree (``karma_amd/lib/``, see ``__graft_entry__.build``)
+so it travels with the repository snapshot.  There is no fallback: if the library is
+missing, importing the device entry points raises ``KarmaUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libkarma_crc32c.so")
+
+KARMA_OK = 0
+KARMA_E_INVALID = -1
+KARMA_E_NO_DEVICE = -2
+KARMA_E_HIP = -3
+KARMA_E_NOMEM = -4
+KARMA_E_RCCL = -5
+UNIQUE_ID_BYTES = 128
+
+_c = ctypes
+_vp, _sz, _u32, _u64, _i = _c.c_void_p, _c.c_size_t, _c.c_uint32, _c.c_uint64, _c.c_int
+
+# name -> (restype, argtypes); mirrors include/karma_crc32c.h one to one
+SIGNATURES = {
+    "karma_crc32c_abi_version": (_i, []),
+    "karma_crc32c_strerror": (_c.c_char_p, [_i]),
+    "karma_crc32c_last_error": (_c.c_char_p, []),
+    "karma_crc32c_extend_host": (_u32, [_u32, _vp, _sz]),
+    "karma_crc32c_extend_host_portable": (_u32, [_u32, _vp, _sz]),
+    "karma_crc32c_batch_fixed": (_i, [_vp, _sz, _sz, _vp, _u32, _vp, _vp]),
+    "karma_crc32c_batch_ragged": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp]),
+    "karma_crc32c_stream": (_i, [_u32, _vp, _sz, _vp, _vp]),
+    "karma_crc32c_batch_fixed_host": (_i, [_vp, _sz, _sz, _u32, _vp, _i]),
+    "karma_crc32c_batch_ragged_host": (_i, [_vp, _sz, _vp, _vp, _sz, _u32, _vp, _i]),
+    "karma_crc32c_get_unique_id": (_i, [_vp, _sz]),
+    "karma_crc32c_comm_init": (_i, [_c.POINTER(_vp), _i, _vp, _i]),
+    "karma_crc32c_comm_destroy": (_i, [_vp]),
+    "karma_crc32c_gather_u32": (_i, [_vp, _vp, _sz, _vp, _i, _vp]),
+    "karma_crc32c_batch_fixed_sharded": (_i, [_vp, _vp, _sz, _sz, _u32, _vp, _vp, _i, _vp]),
+    "karma_fill_splitmix64": (_i, [_vp, _sz, _u64, _u64, _vp]),
+    "karma_stream_probe": (_i, [_vp, _sz, _vp, _vp]),
+    "karma_device_cu_count": (_i, []),
+}
+
+
+class KarmaUnavailable(ImportError):
+    """libkarma_crc32c.so is not built / not loadable."""
+
+
+class KarmaError(RuntimeError):
+    """A C ABI call returned a non-zero status."""
+
+    def __init__(self, fn: str, status: int, detail: str):
+        super().__init__(f"{fn} failed: status {status} ({detail})")
+        self.fn = fn
+        self.status = status
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded library (loaded once).  Raises KarmaUnavailable when it is missing."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise KarmaUnavailable(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        try:
+            handle = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the host
+            raise KarmaUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = handle
+    return _LIB
+
+
+def check(fn: str, status: int) -> None:
+    if status != KARMA_OK:
+        L = lib()
+        detail = L.karma_crc32c_strerror(status).decode()
+        extra = L.karma_crc32c_last_error().decode()
+        raise KarmaError(fn, status, f"{detail}: {extra}" if extra else detail)

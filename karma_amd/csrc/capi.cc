@@ -1,0 +1,510 @@
+// karma_amd/csrc/capi.cc -- the C ABI (include/karma_crc32c.h): argument
+// checks, unit planning, per-device table blobs, per-stream workspaces and
+// the RCCL communicator.  Every device entry point is stream-ordered and
+// returns a KARMA_E_* status; nothing throws across the ABI and nothing falls
+// back to the CPU.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "engine.h"
+#include "karma_crc32c.h"
+
+using namespace karma::engine;
+
+namespace {
+
+thread_local std::string g_last;
+
+int fail(int code, const std::string& what) {
+    g_last = what;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    g_last = std::string(what) + ": " + hipGetErrorString(e);
+    return e == hipErrorOutOfMemory ? KARMA_E_NOMEM : KARMA_E_HIP;
+}
+
+#define KARMA_HIP(expr)                                 \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+#define KARMA_RC(expr)          \
+    do {                        \
+        int _rc = (expr);       \
+        if (_rc) return _rc;    \
+    } while (0)
+
+constexpr uint64_t kMinSplitUnit = 2048;  // smallest unit when records are split
+constexpr uint64_t kOverdecompose = 4;    // units per group before splitting records
+
+uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+uint64_t round_up(uint64_t a, uint64_t m) { return ceil_div(a, m) * m; }
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct DevState {
+    bool ready = false;
+    int cu = 0;
+    uint32_t* blob = nullptr;
+    std::map<uint64_t, uint32_t*> comb;  // unit bytes -> combine blob
+};
+
+struct Workspace {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+
+// One lock for the library state; held across planning and enqueueing so a
+// workspace is never reallocated between another call's lookup and launch.
+std::mutex g_mu;
+std::vector<DevState> g_dev;
+std::map<std::pair<int, void*>, Workspace> g_ws;
+
+int current_device(int* dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(KARMA_E_NO_DEVICE, "no HIP device visible");
+    KARMA_HIP(hipGetDevice(dev));
+    return 0;
+}
+
+// Caller holds g_mu.
+int dev_state(int dev, DevState** out) {
+    if ((int)g_dev.size() <= dev) g_dev.resize(dev + 1);
+    DevState& d = g_dev[dev];
+    if (!d.ready) {
+        hipDeviceProp_t prop;
+        KARMA_HIP(hipGetDeviceProperties(&prop, dev));
+        d.cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 1;
+        std::vector<uint32_t> host(kBlobWords);
+        build_stream_blob(host.data());
+        KARMA_HIP(hipMalloc(&d.blob, kBlobWords * sizeof(uint32_t)));
+        KARMA_HIP(hipMemcpy(d.blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+        d.ready = true;
+    }
+    *out = &d;
+    return 0;
+}
+
+int comb_blob(DevState& d, uint64_t unit_bytes, const uint32_t** out) {
+    auto it = d.comb.find(unit_bytes);
+    if (it == d.comb.end()) {
+        std::vector<uint32_t> host(kCombWords);
+        build_combine_blob(unit_bytes, host.data());
+        uint32_t* p = nullptr;
+        KARMA_HIP(hipMalloc(&p, kCombWords * sizeof(uint32_t)));
+        KARMA_HIP(hipMemcpy(p, host.data(), kCombWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+        it = d.comb.emplace(unit_bytes, p).first;
+    }
+    *out = it->second;
+    return 0;
+}
+
+int workspace(int dev, hipStream_t s, size_t bytes, void** out) {
+    Workspace& w = g_ws[{dev, (void*)s}];
+    if (w.bytes < bytes) {
+        if (w.ptr) {
+            KARMA_HIP(hipStreamSynchronize(s));
+            KARMA_HIP(hipFree(w.ptr));
+            w.ptr = nullptr;
+            w.bytes = 0;
+        }
+        const size_t want = align256(bytes + bytes / 4);
+        KARMA_HIP(hipMalloc(&w.ptr, want));
+        w.bytes = want;
+    }
+    *out = w.ptr;
+    return 0;
+}
+
+// ---- fixed-size records ---------------------------------------------------
+int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, size_t n_rec, const uint32_t* d_init,
+                 uint32_t init, uint32_t* d_out, hipStream_t s) {
+    const uint64_t groups = (uint64_t)ds.cu * kWavesPerBlock * kGroupsPerWave;
+    const uint64_t target = kOverdecompose * groups;
+    uint64_t unit, k;
+    if (rec_bytes <= (size_t)kChunk || n_rec >= target) {
+        unit = round_up(std::max<uint64_t>(rec_bytes, 1), kChunk);
+        k = 1;
+    } else {
+        const uint64_t k_ideal = ceil_div(target, n_rec);
+        unit = std::max<uint64_t>(kMinSplitUnit, round_up(ceil_div(rec_bytes, k_ideal), kChunk));
+        k = ceil_div(rec_bytes, unit);
+        if (k == 1) unit = round_up(rec_bytes, kChunk);
+    }
+    FixedArgs a;
+    a.arena = static_cast<const uint8_t*>(d_data);
+    a.rec_bytes = rec_bytes;
+    a.n_rec = n_rec;
+    a.init = d_init;
+    a.init_scalar = init;
+    a.unit_bytes = unit;
+    a.units_per_rec = k;
+    a.out = d_out;
+    a.partial = nullptr;
+    a.blob = ds.blob;
+    if (k == 1) {
+        KARMA_HIP(launch_fixed(a, ds.cu, s));
+        return 0;
+    }
+    const size_t part_bytes = align256(n_rec * k * sizeof(uint32_t));
+    const size_t lvl_bytes = align256(n_rec * ceil_div(k, 64) * sizeof(uint32_t));
+    void* ws = nullptr;
+    KARMA_RC(workspace(dev, s, part_bytes + 2 * lvl_bytes, &ws));
+    a.partial = static_cast<uint32_t*>(ws);
+    uint32_t* bufs[2] = {reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + part_bytes),
+                         reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + part_bytes + lvl_bytes)};
+    KARMA_HIP(launch_fixed(a, ds.cu, s));
+    const uint32_t* in = a.partial;
+    uint64_t k_in = k, d = unit;
+    for (int which = 0;; which ^= 1) {
+        const uint64_t k_out = ceil_div(k_in, 64);
+        const uint32_t* cb = nullptr;
+        KARMA_RC(comb_blob(ds, d, &cb));
+        uint32_t* outs = k_out == 1 ? nullptr : bufs[which];
+        KARMA_HIP(launch_combine_fixed(a, in, k_in, outs, k_out, cb, s));
+        if (k_out == 1) break;
+        in = outs;
+        k_in = k_out;
+        d *= 64;
+    }
+    return 0;
+}
+
+// ---- ragged records -------------------------------------------------------
+struct RaggedLayout {
+    size_t base_off, sums_off, rec_off, part_off, total;
+};
+
+RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
+    RaggedLayout L;
+    L.base_off = 0;
+    L.sums_off = align256((n_rec + 1) * sizeof(uint64_t));
+    L.rec_off = L.sums_off + align256(ragged_scan_blocks(n_rec) * sizeof(uint64_t));
+    L.part_off = L.rec_off + align256(cap * sizeof(uint64_t));
+    L.total = L.part_off + align256(cap * sizeof(uint32_t));
+    return L;
+}
+
+void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
+    char* b = static_cast<char*>(ws);
+    a.unit_base = reinterpret_cast<uint64_t*>(b + L.base_off);
+    a.block_sums = reinterpret_cast<uint64_t*>(b + L.sums_off);
+    a.unit_rec = reinterpret_cast<uint64_t*>(b + L.rec_off);
+    a.partial = reinterpret_cast<uint32_t*>(b + L.part_off);
+    a.unit_cap = cap;
+}
+
+int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_off, const uint32_t* d_len,
+                  size_t n_rec, size_t total_len, const uint32_t* d_init, uint32_t init, uint32_t* d_out,
+                  hipStream_t s) {
+    RaggedArgs a;
+    a.arena = static_cast<const uint8_t*>(d_arena);
+    a.off = d_off;
+    a.len = d_len;
+    a.n_rec = n_rec;
+    a.init = d_init;
+    a.init_scalar = init;
+    a.unit_bytes = kDefaultUnit;
+    a.out = d_out;
+    a.blob = ds.blob;
+    KARMA_RC(comb_blob(ds, kDefaultUnit, &a.comb_blob));
+    uint64_t cap;
+    void* ws = nullptr;
+    if (total_len > 0) {
+        cap = n_rec + ceil_div(total_len, kDefaultUnit);
+        const RaggedLayout L = ragged_layout(n_rec, cap);
+        KARMA_RC(workspace(dev, s, L.total, &ws));
+        bind_ragged(a, ws, L, cap);
+        KARMA_HIP(launch_ragged_scan(a, s));
+    } else {
+        // Unknown total: scan, read the unit count back, size the table, rescan if it moved.
+        cap = n_rec;
+        RaggedLayout L = ragged_layout(n_rec, cap);
+        KARMA_RC(workspace(dev, s, L.total, &ws));
+        bind_ragged(a, ws, L, cap);
+        KARMA_HIP(launch_ragged_scan(a, s));
+        uint64_t units = 0;
+        KARMA_HIP(hipMemcpyAsync(&units, a.unit_base + n_rec, sizeof(units), hipMemcpyDeviceToHost, s));
+        KARMA_HIP(hipStreamSynchronize(s));
+        cap = std::max<uint64_t>(units, 1);
+        L = ragged_layout(n_rec, cap);
+        void* ws2 = nullptr;
+        KARMA_RC(workspace(dev, s, L.total, &ws2));
+        bind_ragged(a, ws2, L, cap);
+        if (ws2 != ws) KARMA_HIP(launch_ragged_scan(a, s));
+    }
+    KARMA_HIP(launch_ragged_main(a, ds.cu, s));
+    return 0;
+}
+
+struct Locked {
+    std::lock_guard<std::mutex> lk{g_mu};
+    int dev = 0;
+    DevState* ds = nullptr;
+    int rc = 0;
+    Locked() {
+        rc = current_device(&dev);
+        if (!rc) rc = dev_state(dev, &ds);
+    }
+};
+
+}  // namespace
+
+struct karma_comm {
+    ncclComm_t nc = nullptr;
+    int rank = 0, nranks = 1;
+};
+
+extern "C" {
+
+int karma_crc32c_abi_version(void) { return KARMA_CRC32C_ABI_VERSION; }
+
+const char* karma_crc32c_strerror(int status) {
+    switch (status) {
+        case KARMA_OK: return "ok";
+        case KARMA_E_INVALID: return "invalid argument";
+        case KARMA_E_NO_DEVICE: return "no usable HIP device";
+        case KARMA_E_HIP: return "HIP runtime error";
+        case KARMA_E_NOMEM: return "out of memory";
+        case KARMA_E_RCCL: return "RCCL error";
+        default: return "unknown status";
+    }
+}
+
+const char* karma_crc32c_last_error(void) { return g_last.c_str(); }
+
+int karma_device_cu_count(void) {
+    Locked L;
+    if (L.rc) return L.rc;
+    return L.ds->cu;
+}
+
+int karma_crc32c_batch_fixed(const void* d_data, size_t rec_bytes, size_t n_rec, const uint32_t* d_init,
+                             uint32_t init, uint32_t* d_out, karma_stream_t stream) {
+    if (n_rec == 0) return KARMA_OK;
+    if (!d_out || (!d_data && rec_bytes)) return fail(KARMA_E_INVALID, "batch_fixed: null pointer");
+    Locked L;
+    if (L.rc) return L.rc;
+    return fixed_locked(L.dev, *L.ds, d_data, rec_bytes, n_rec, d_init, init, d_out, (hipStream_t)stream);
+}
+
+int karma_crc32c_batch_ragged(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
+                              size_t total_len, const uint32_t* d_init, uint32_t init, uint32_t* d_out,
+                              karma_stream_t stream) {
+    if (n_rec == 0) return KARMA_OK;
+    if (!d_out || !d_off || !d_len) return fail(KARMA_E_INVALID, "batch_ragged: null pointer");
+    Locked L;
+    if (L.rc) return L.rc;
+    return ragged_locked(L.dev, *L.ds, d_arena, d_off, d_len, n_rec, total_len, d_init, init, d_out,
+                         (hipStream_t)stream);
+}
+
+int karma_crc32c_stream(uint32_t init, const void* d_data, size_t n, uint32_t* d_out, karma_stream_t stream) {
+    return karma_crc32c_batch_fixed(d_data, n, 1, nullptr, init, d_out, stream);
+}
+
+}  // extern "C"
+
+// ---- host-memory batches ------------------------------------------------------
+namespace {
+
+struct HostPin {
+    void* p = nullptr;
+    bool registered = false;
+    HostPin(const void* ptr, size_t bytes) {
+        hipPointerAttribute_t attr;
+        if (!ptr || !bytes) return;
+        if (hipPointerGetAttributes(&attr, ptr) == hipSuccess && attr.type == hipMemoryTypeHost) return;  // pinned
+        (void)hipGetLastError();
+        if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) == hipSuccess) {
+            p = const_cast<void*>(ptr);
+            registered = true;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    ~HostPin() {
+        if (registered) (void)hipHostUnregister(p);
+    }
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+int select_device(int device) {
+    if (device >= 0) KARMA_HIP(hipSetDevice(device));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int karma_crc32c_batch_fixed_host(const void* h_data, size_t rec_bytes, size_t n_rec, uint32_t init,
+                                  uint32_t* h_out, int device) {
+    if (n_rec == 0) return KARMA_OK;
+    if (!h_out || (!h_data && rec_bytes)) return fail(KARMA_E_INVALID, "batch_fixed_host: null pointer");
+    KARMA_RC(select_device(device));
+    // Chunks of ~64 MiB alternate over two streams: H2D(i+1) overlaps kernel(i).
+    const size_t chunk_recs = std::max<size_t>(1, rec_bytes ? (size_t(64) << 20) / std::max<size_t>(rec_bytes, 1) : n_rec);
+    const size_t nchunks = (n_rec + chunk_recs - 1) / chunk_recs;
+    const size_t slot_bytes = chunk_recs * rec_bytes;
+    HostPin pin_in(h_data, n_rec * rec_bytes);
+    HostPin pin_out(h_out, n_rec * sizeof(uint32_t));
+    DevBuf din, dout;
+    const int nslots = nchunks > 1 ? 2 : 1;
+    KARMA_HIP(hipMalloc(&din.p, std::max<size_t>(1, slot_bytes * nslots)));
+    KARMA_HIP(hipMalloc(&dout.p, chunk_recs * sizeof(uint32_t) * nslots));
+    hipStream_t st[2] = {nullptr, nullptr};
+    for (int i = 0; i < nslots; ++i) KARMA_HIP(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    int rc = 0;
+    for (size_t c = 0; c < nchunks && !rc; ++c) {
+        const int sl = (int)(c % nslots);
+        const size_t r0 = c * chunk_recs;
+        const size_t nr = std::min(chunk_recs, n_rec - r0);
+        char* dslot = static_cast<char*>(din.p) + sl * slot_bytes;
+        uint32_t* oslot = static_cast<uint32_t*>(dout.p) + sl * chunk_recs;
+        hipError_t e = hipMemcpyAsync(dslot, static_cast<const char*>(h_data) + r0 * rec_bytes, nr * rec_bytes,
+                                      hipMemcpyHostToDevice, st[sl]);
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "H2D");
+            break;
+        }
+        rc = karma_crc32c_batch_fixed(dslot, rec_bytes, nr, nullptr, init, oslot, st[sl]);
+        if (rc) break;
+        e = hipMemcpyAsync(h_out + r0, oslot, nr * sizeof(uint32_t), hipMemcpyDeviceToHost, st[sl]);
+        if (e != hipSuccess) rc = hip_fail(e, "D2H");
+    }
+    for (int i = 0; i < nslots; ++i) {
+        hipError_t e = hipStreamSynchronize(st[i]);
+        if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+        (void)hipStreamDestroy(st[i]);
+    }
+    return rc;
+}
+
+int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, const uint64_t* h_off,
+                                   const uint32_t* h_len, size_t n_rec, uint32_t init, uint32_t* h_out, int device) {
+    if (n_rec == 0) return KARMA_OK;
+    if (!h_out || !h_off || !h_len || (!h_arena && arena_bytes)) return fail(KARMA_E_INVALID, "batch_ragged_host");
+    KARMA_RC(select_device(device));
+    uint64_t total = 0;
+    for (size_t r = 0; r < n_rec; ++r) {
+        if (h_off[r] + h_len[r] > arena_bytes) return fail(KARMA_E_INVALID, "batch_ragged_host: record past arena");
+        total += h_len[r];
+    }
+    HostPin pin(h_arena, arena_bytes);
+    DevBuf da, doff, dlen, dout;
+    KARMA_HIP(hipMalloc(&da.p, std::max<size_t>(arena_bytes, 16)));
+    KARMA_HIP(hipMalloc(&doff.p, n_rec * sizeof(uint64_t)));
+    KARMA_HIP(hipMalloc(&dlen.p, n_rec * sizeof(uint32_t)));
+    KARMA_HIP(hipMalloc(&dout.p, n_rec * sizeof(uint32_t)));
+    hipStream_t s = nullptr;
+    KARMA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    int rc = 0;
+    hipError_t e = hipMemcpyAsync(da.p, h_arena, arena_bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(doff.p, h_off, n_rec * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dlen.p, h_len, n_rec * sizeof(uint32_t), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) rc = hip_fail(e, "H2D");
+    if (!rc)
+        rc = karma_crc32c_batch_ragged(da.p, static_cast<uint64_t*>(doff.p), static_cast<uint32_t*>(dlen.p), n_rec,
+                                       total, nullptr, init, static_cast<uint32_t*>(dout.p), s);
+    if (!rc) {
+        e = hipMemcpyAsync(h_out, dout.p, n_rec * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) rc = hip_fail(e, "D2H");
+    }
+    e = hipStreamSynchronize(s);
+    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
+// ---- multi-GPU --------------------------------------------------------------------
+int karma_crc32c_get_unique_id(void* uid, size_t uid_bytes) {
+    if (!uid || uid_bytes < sizeof(ncclUniqueId)) return fail(KARMA_E_INVALID, "get_unique_id: buffer too small");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(KARMA_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(uid, &id, sizeof(id));
+    return 0;
+}
+
+int karma_crc32c_comm_init(karma_comm_t* comm, int nranks, const void* uid, int rank) {
+    if (!comm || !uid || nranks < 1 || rank < 0 || rank >= nranks) return fail(KARMA_E_INVALID, "comm_init");
+    karma_comm* c = new (std::nothrow) karma_comm;
+    if (!c) return fail(KARMA_E_NOMEM, "comm_init");
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    ncclResult_t r = ncclCommInitRank(&c->nc, nranks, id, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return fail(KARMA_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    c->rank = rank;
+    c->nranks = nranks;
+    *comm = c;
+    return 0;
+}
+
+int karma_crc32c_comm_destroy(karma_comm_t comm) {
+    if (!comm) return 0;
+    ncclResult_t r = ncclCommDestroy(comm->nc);
+    delete comm;
+    if (r != ncclSuccess) return fail(KARMA_E_RCCL, std::string("ncclCommDestroy: ") + ncclGetErrorString(r));
+    return 0;
+}
+
+int karma_crc32c_gather_u32(karma_comm_t comm, const uint32_t* d_send, size_t count, uint32_t* d_recv, int root,
+                            karma_stream_t stream) {
+    if (!comm || (!d_send && count)) return fail(KARMA_E_INVALID, "gather_u32");
+    if (comm->rank == root && !d_recv && count) return fail(KARMA_E_INVALID, "gather_u32: root needs d_recv");
+    ncclResult_t r = ncclGather(d_send, d_recv, count, ncclUint32, root, comm->nc, (hipStream_t)stream);
+    if (r != ncclSuccess) return fail(KARMA_E_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
+    return 0;
+}
+
+int karma_crc32c_batch_fixed_sharded(karma_comm_t comm, const void* d_local, size_t rec_bytes, size_t n_local,
+                                     uint32_t init, uint32_t* d_local_out, uint32_t* d_all_out, int root,
+                                     karma_stream_t stream) {
+    if (!comm) return fail(KARMA_E_INVALID, "batch_fixed_sharded: null comm");
+    KARMA_RC(karma_crc32c_batch_fixed(d_local, rec_bytes, n_local, nullptr, init, d_local_out, stream));
+    return karma_crc32c_gather_u32(comm, d_local_out, n_local, d_all_out, root, stream);
+}
+
+// ---- synthetic data / probes -----------------------------------------------------
+int karma_fill_splitmix64(void* d_dst, size_t n_bytes, uint64_t seed, uint64_t first_byte, karma_stream_t stream) {
+    if (!n_bytes) return 0;
+    if (!d_dst || (first_byte & 7u) || (reinterpret_cast<uintptr_t>(d_dst) & 15u))
+        return fail(KARMA_E_INVALID, "fill_splitmix64: null, first_byte % 8 or destination not 16-byte aligned");
+    int dev;
+    KARMA_RC(current_device(&dev));
+    KARMA_HIP(launch_fill_splitmix(static_cast<uint8_t*>(d_dst), n_bytes, seed, first_byte, (hipStream_t)stream));
+    return 0;
+}
+
+int karma_stream_probe(const void* d_src, size_t n_bytes, uint32_t* d_out, karma_stream_t stream) {
+    if (!d_out || (!d_src && n_bytes) || (reinterpret_cast<uintptr_t>(d_src) & 15u))
+        return fail(KARMA_E_INVALID, "stream_probe: null or source not 16-byte aligned");
+    Locked L;
+    if (L.rc) return L.rc;
+    KARMA_HIP(launch_stream_probe(static_cast<const uint8_t*>(d_src), n_bytes, d_out, L.ds->cu * 2,
+                                  (hipStream_t)stream));
+    return 0;
+}
+
+}  // extern "C"

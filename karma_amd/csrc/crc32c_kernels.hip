@@ -1,0 +1,597 @@
+// karma_amd/csrc/crc32c_kernels.hip -- CRC-32C engine kernels for MI355X (gfx950).
+//
+// Replaces, for batches, the per-record call crc32c::Value/Extend
+// (karma-util/crc32c.h:16-19, crc32c.cc:275-376) made by
+// segment_file::append_record (karma-store/segment_file.cc:22) and
+// wal::scan_record (karma-store/wal.cc:60).  DESIGN.md §3 derives the math;
+// in short, with R(X) the CRC register after byte X and Z_d "advance d zero
+// bytes" (gf2.h):
+//
+//   * a record body is cut into units (<= unit_bytes, end-aligned), a unit
+//     into 128-byte chunks; 8 lanes (a "group") own one unit, each lane a
+//     16-byte window per chunk = four 4-byte word slots;
+//   * each slot keeps a pending register  acc = Z_128(acc) ^ word
+//     (the reference's STEP4 with a 128-byte instead of 16-byte stride,
+//     crc32c.cc:293-309), looked up in bank-replicated LDS tables so the
+//     32 lanes of a ds_read_b32 half-wave never conflict;
+//   * lane fold  c = Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0))))  (STEP4W, :312-319)
+//     and a 3-level group tree  v_l = Z_{16*2^d}(v_l) ^ v_{l+2^d}  give the
+//     unit's register contribution;
+//   * the record's initial register (~init advanced over the unaligned head
+//     bytes) is xored into the first body word, so no shift by a data-
+//     dependent length is ever needed; units of one record are folded by the
+//     combine kernels with Z_{unit*2^d}; the unaligned tail bytes are
+//     stepped one at a time (STEP1, :286-290).
+#include <hip/hip_runtime.h>
+
+#include "engine.h"
+
+namespace karma {
+namespace engine {
+namespace {
+
+// ---- LDS image of the streaming kernel -------------------------------------
+// [0, 128 KiB): Z_S slicing tables, bank-replicated.  Byte address of
+//   table k, entry e, for lane L:  (k>>1)<<16 | e<<8 | (k&1)<<7 | (L&31)<<2
+// so one v_perm_b32 builds it from the register (entry = byte k) and a
+// per-lane constant, and every ds_read_b32 lane group hits 32 distinct banks.
+// [128 KiB, +17 KiB): Z4, Z16, Z32, Z64 slicing tables and the byte table.
+constexpr int kRepWords = 32768;
+constexpr int kSmallBase = kRepWords;
+constexpr int kSmallWords = kBlobWords - 1024;
+constexpr int kLdsWords = kRepWords + kSmallWords;  // 148,480 bytes
+constexpr int kLZ4 = kSmallBase + (kBlobZ4 - 1024);
+constexpr int kLZ16 = kSmallBase + (kBlobZ16 - 1024);
+constexpr int kLZ32 = kSmallBase + (kBlobZ32 - 1024);
+constexpr int kLZ64 = kSmallBase + (kBlobZ64 - 1024);
+constexpr int kLT8 = kSmallBase + (kBlobT8 - 1024);
+
+constexpr uint32_t kSel0 = 0x0c0c0004u;  // {X.b0, acc.b0, 0, 0}
+constexpr uint32_t kSel1 = 0x0c0c0105u;  // {X.b1, acc.b1, 0, 0}
+constexpr uint32_t kSel2 = 0x0c070204u;  // {X.b0, acc.b2, X.b3, 0}
+constexpr uint32_t kSel3 = 0x0c070305u;  // {X.b1, acc.b3, X.b3, 0}
+
+__device__ __forceinline__ uint32_t lds_at_byte(const uint32_t* lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(lds) + byte_addr);
+}
+
+// acc <- Z_S(acc) ^ w  through the replicated tables.
+__device__ __forceinline__ uint32_t stride_step(const uint32_t* lds, uint32_t X, uint32_t acc, uint32_t w) {
+    const uint32_t i0 = __builtin_amdgcn_perm(X, acc, kSel0);
+    const uint32_t i1 = __builtin_amdgcn_perm(X, acc, kSel1);
+    const uint32_t i2 = __builtin_amdgcn_perm(X, acc, kSel2);
+    const uint32_t i3 = __builtin_amdgcn_perm(X, acc, kSel3);
+    return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
+}
+
+// Z(x) for a map stored as four plain 256-entry tables at word `base`.
+__device__ __forceinline__ uint32_t zmap(const uint32_t* lds, int base, uint32_t x) {
+    return lds[base + (x & 255u)] ^ lds[base + 256 + ((x >> 8) & 255u)] ^ lds[base + 512 + ((x >> 16) & 255u)] ^
+           lds[base + 768 + (x >> 24)];
+}
+
+// One data byte (STEP1).
+__device__ __forceinline__ uint32_t byte_step(const uint32_t* lds, int t8, uint32_t r, uint32_t b) {
+    return lds[t8 + ((r ^ b) & 255u)] ^ (r >> 8);
+}
+
+// Record bytes live in device global memory: load through address space 1 so
+// hipcc emits global_load_dwordx4 (vmcnt only) instead of flat loads, whose
+// lgkmcnt share would serialise them against the LDS table lookups.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) { return *(gu32x4*)(p); }
+
+__device__ __forceinline__ const uint8_t* pmin(const uint8_t* a, const uint8_t* b) { return a < b ? a : b; }
+__device__ __forceinline__ const uint8_t* pmax(const uint8_t* a, const uint8_t* b) { return a > b ? a : b; }
+__device__ __forceinline__ const uint8_t* floor16(const uint8_t* p) {
+    return reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+}
+__device__ __forceinline__ const uint8_t* ceil16(const uint8_t* p) {
+    return reinterpret_cast<const uint8_t*>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
+}
+
+// Register after bytes [from, to) of the aligned 16-byte block `blk`.
+__device__ uint32_t bytes_in_block(const uint32_t* lds, int t8, uint32_t r, const uint8_t* blk, uint32_t from,
+                                   uint32_t to) {
+    if (from >= to) return r;
+    const u32x4 v = ld16(blk);
+    // walk the block as a 128-bit shift register (no dynamically indexed vector)
+    uint64_t lo = v.x | ((uint64_t)v.y << 32), hi = v.z | ((uint64_t)v.w << 32);
+    for (uint32_t i = 0; i < to; ++i) {
+        if (i >= from) r = byte_step(lds, t8, r, (uint32_t)lo & 255u);
+        lo = (lo >> 8) | (hi << 56);
+        hi >>= 8;
+    }
+    return r;
+}
+
+// Whole record byte by byte (records with no aligned 16-byte block inside).
+__device__ uint32_t short_record(const uint32_t* lds, int t8, const uint8_t* p, uint64_t n, uint32_t init) {
+    uint32_t r = ~init;
+    const uint8_t* e = p + n;
+    const uint8_t* q = p;
+    while (q < e) {
+        const uint8_t* blk = floor16(q);
+        const uint32_t to = (uint32_t)((e - blk) < 16 ? (e - blk) : 16);
+        r = bytes_in_block(lds, t8, r, blk, (uint32_t)(q - blk), to);
+        q = blk + 16;
+    }
+    return ~r;
+}
+
+struct Geom {
+    const uint8_t* a;  // first aligned body byte
+    const uint8_t* b;  // end of the aligned body
+    const uint8_t* e;  // record end
+    bool is_short;     // no aligned 16-byte block inside (includes n == 0)
+};
+
+__device__ __forceinline__ Geom geom(const uint8_t* p, uint64_t n) {
+    Geom g;
+    g.e = p + n;
+    g.a = ceil16(p);
+    g.b = floor16(g.e);
+    g.is_short = (g.b - g.a) < 16;
+    return g;
+}
+
+// Register contribution of the 16-aligned span [us, ue) with 128-byte chunks
+// end-aligned to ue; `inj` is xored into the word at `inj_at`.  Every lane of
+// the wave must call this (it ends in cross-lane shuffles); the result is
+// valid in group lane 0.
+__device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, uint32_t l, const uint8_t* us,
+                                               const uint8_t* ue, const uint8_t* inj_at, uint32_t inj) {
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    const int64_t span = ue - us;
+    if (span > 0) {
+        const int64_t nch = (span + kChunk - 1) / kChunk;
+        const uint8_t* w = ue - nch * kChunk + 16 * l;
+        {
+            u32x4 v = (w >= us) ? ld16(w) : u32x4{0u, 0u, 0u, 0u};
+            if (w == inj_at) v.x ^= inj;
+            a0 = v.x;
+            a1 = v.y;
+            a2 = v.z;
+            a3 = v.w;
+        }
+        int64_t rem = nch - 1;
+        w += kChunk;
+        // window of the last chunk: prefetches past the end re-read it.  Chunks
+        // after chunk 0 are always full; with a single (possibly partial) chunk
+        // fall back to the unit's last 16 bytes so no load leaves [us, ue).
+        const uint8_t* last = ue - kChunk + 16 * l;
+        if (last < us) last = ue - 16;
+        u32x4 n0 = ld16(pmin(w, last));
+        u32x4 n1 = ld16(pmin(w + kChunk, last));
+        u32x4 n2 = ld16(pmin(w + 2 * kChunk, last));
+        u32x4 n3 = ld16(pmin(w + 3 * kChunk, last));
+        while (rem >= 4) {
+            const u32x4 v0 = n0, v1 = n1, v2 = n2, v3 = n3;
+            w += 4 * kChunk;
+            n0 = ld16(pmin(w, last));
+            n1 = ld16(pmin(w + kChunk, last));
+            n2 = ld16(pmin(w + 2 * kChunk, last));
+            n3 = ld16(pmin(w + 3 * kChunk, last));
+            a0 = stride_step(lds, X, a0, v0.x);
+            a1 = stride_step(lds, X, a1, v0.y);
+            a2 = stride_step(lds, X, a2, v0.z);
+            a3 = stride_step(lds, X, a3, v0.w);
+            a0 = stride_step(lds, X, a0, v1.x);
+            a1 = stride_step(lds, X, a1, v1.y);
+            a2 = stride_step(lds, X, a2, v1.z);
+            a3 = stride_step(lds, X, a3, v1.w);
+            a0 = stride_step(lds, X, a0, v2.x);
+            a1 = stride_step(lds, X, a1, v2.y);
+            a2 = stride_step(lds, X, a2, v2.z);
+            a3 = stride_step(lds, X, a3, v2.w);
+            a0 = stride_step(lds, X, a0, v3.x);
+            a1 = stride_step(lds, X, a1, v3.y);
+            a2 = stride_step(lds, X, a2, v3.z);
+            a3 = stride_step(lds, X, a3, v3.w);
+            rem -= 4;
+        }
+        if (rem > 0) {
+            a0 = stride_step(lds, X, a0, n0.x);
+            a1 = stride_step(lds, X, a1, n0.y);
+            a2 = stride_step(lds, X, a2, n0.z);
+            a3 = stride_step(lds, X, a3, n0.w);
+        }
+        if (rem > 1) {
+            a0 = stride_step(lds, X, a0, n1.x);
+            a1 = stride_step(lds, X, a1, n1.y);
+            a2 = stride_step(lds, X, a2, n1.z);
+            a3 = stride_step(lds, X, a3, n1.w);
+        }
+        if (rem > 2) {
+            a0 = stride_step(lds, X, a0, n2.x);
+            a1 = stride_step(lds, X, a1, n2.y);
+            a2 = stride_step(lds, X, a2, n2.z);
+            a3 = stride_step(lds, X, a3, n2.w);
+        }
+    }
+    // lane fold (crc32c.cc STEP4W order): c = Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0))))
+    uint32_t c = zmap(lds, kLZ4, a0);
+    c = zmap(lds, kLZ4, c ^ a1);
+    c = zmap(lds, kLZ4, c ^ a2);
+    c = zmap(lds, kLZ4, c ^ a3);
+    // group tree over 8 lanes: v_l = Z_{16*2^d}(v_l) ^ v_{l+2^d}
+    uint32_t t = __shfl_down(c, 1, kGroupLanes);
+    c = zmap(lds, kLZ16, c) ^ t;
+    t = __shfl_down(c, 2, kGroupLanes);
+    c = zmap(lds, kLZ32, c) ^ t;
+    t = __shfl_down(c, 4, kGroupLanes);
+    c = zmap(lds, kLZ64, c) ^ t;
+    return c;
+}
+
+__device__ __forceinline__ void load_stream_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
+    for (int i = threadIdx.x; i < kSmallWords; i += blockDim.x) lds[kSmallBase + i] = blob[1024 + i];
+    // word index = region*16384 + row*64 + half*32 + lane32; table k = region*2 + half
+    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
+    for (int i = threadIdx.x; i < kRepWords / 4; i += blockDim.x) {
+        const int idx = i * 4;
+        const int region = idx >> 14, row = (idx >> 6) & 255, half = (idx >> 5) & 1;
+        const uint32_t v = blob[kBlobStride + (region * 2 + half) * 256 + row];
+        l4[i] = u32x4{v, v, v, v};
+    }
+}
+
+__device__ __forceinline__ uint32_t lane_const() {
+    const uint32_t l32 = threadIdx.x & 31u;
+    return (l32 * 4u) | ((128u + l32 * 4u) << 8) | (1u << 24);
+}
+
+// Per-unit work shared by the fixed and ragged kernels.  Returns the unit's
+// register contribution (valid in group lane 0).
+__device__ __forceinline__ uint32_t unit_work(const uint32_t* lds, uint32_t X, uint32_t l, bool valid,
+                                              const uint8_t* p, uint32_t init, const Geom& g, uint64_t j,
+                                              uint64_t k, uint64_t umax) {
+    const uint8_t* us = nullptr;
+    const uint8_t* ue = nullptr;
+    const uint8_t* inj_at = nullptr;
+    uint32_t inj = 0;
+    if (valid && !g.is_short) {
+        ue = g.b - (int64_t)((k - 1 - j) * umax);
+        const uint8_t* us_raw = ue - (int64_t)umax;
+        us = pmax(us_raw, g.a);
+        if (us > ue) us = ue;
+        if (g.a >= us_raw && g.a < ue) {
+            uint32_t h = ~init;
+            if (p < g.a) h = bytes_in_block(lds, kLT8, h, g.a - 16, (uint32_t)(p - (g.a - 16)), 16u);
+            inj_at = g.a;
+            inj = h;
+        }
+    }
+    return group_unit(lds, X, l, us, ue, inj_at, inj);
+}
+
+// ---- fixed-size records --------------------------------------------------------
+__global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
+    __shared__ uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const uint64_t k = A.units_per_rec;
+    const uint64_t U = A.n_rec * k;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t wb = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); wb * kGroupsPerWave < U;
+         wb += nwaves) {
+        const uint64_t u = wb * kGroupsPerWave + grp;
+        const bool valid = u < U;
+        uint64_t r = 0, j = 0;
+        if (valid) {
+            if (k == 1) {
+                r = u;
+            } else {
+                r = u / k;
+                j = u - r * k;
+            }
+        }
+        const uint8_t* p = A.arena + r * A.rec_bytes;
+        const uint32_t init = valid ? (A.init ? A.init[r] : A.init_scalar) : 0u;
+        const Geom g = geom(p, A.rec_bytes);
+        uint32_t R = unit_work(lds, X, l, valid, p, init, g, j, k, A.unit_bytes);
+        if (valid && l == 0) {
+            if (g.is_short) {
+                A.out[r] = short_record(lds, kLT8, p, A.rec_bytes, init);
+            } else if (k == 1) {
+                if (g.e > g.b) R = bytes_in_block(lds, kLT8, R, g.b, 0u, (uint32_t)(g.e - g.b));
+                A.out[r] = ~R;
+            } else {
+                A.partial[u] = R;
+            }
+        }
+    }
+}
+
+// ---- ragged records: unit table ------------------------------------------------
+__device__ __forceinline__ uint64_t units_of(const uint8_t* arena, uint64_t off, uint32_t len, uint64_t umax) {
+    const Geom g = geom(arena + off, len);
+    if (g.is_short) return 1;
+    const uint64_t body = (uint64_t)(g.b - g.a);
+    return (body + umax - 1) / umax;
+}
+
+// Inclusive wave scan of 64-bit values.
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(x, d);
+        if (lane >= d) x += t;
+    }
+    return x;
+}
+
+// Exclusive block scan (blockDim.x == 1024).
+__device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint64_t inc = wave_incl_scan(v);
+    if (lane == 63) sm[wave] = inc;
+    __syncthreads();
+    if (wave == 0) {
+        uint64_t s = lane < nw ? sm[lane] : 0;
+        s = wave_incl_scan(s);
+        if (lane < nw) sm[lane] = s;
+    }
+    __syncthreads();
+    const uint64_t pre = wave ? sm[wave - 1] : 0;
+    total = sm[nw - 1];
+    __syncthreads();
+    return pre + inc - v;
+}
+
+__global__ __launch_bounds__(1024) void k_ragged_scan1(RaggedArgs A) {
+    __shared__ uint64_t sm[16];
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t cnt = r < A.n_rec ? units_of(A.arena, A.off[r], A.len[r], A.unit_bytes) : 0;
+    uint64_t total;
+    const uint64_t ex = block_excl_scan(cnt, sm, total);
+    if (r < A.n_rec) A.unit_base[r] = ex;
+    if (threadIdx.x == 0) A.block_sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_ragged_scan2(RaggedArgs A, uint64_t nblocks) {
+    __shared__ uint64_t sm[16];
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nblocks; base += blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t v = i < nblocks ? A.block_sums[i] : 0;
+        uint64_t total;
+        const uint64_t ex = block_excl_scan(v, sm, total);
+        if (i < nblocks) A.block_sums[i] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) A.unit_base[A.n_rec] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_ragged_fill(RaggedArgs A) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.n_rec) return;
+    const uint64_t base = A.unit_base[r] + A.block_sums[r / 1024];
+    A.unit_base[r] = base;
+    const uint64_t cnt = units_of(A.arena, A.off[r], A.len[r], A.unit_bytes);
+    for (uint64_t j = 0; j < cnt && base + j < A.unit_cap; ++j) A.unit_rec[base + j] = r;
+}
+
+__global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
+    __shared__ uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const uint64_t U_all = A.unit_base[A.n_rec];
+    const uint64_t U = U_all < A.unit_cap ? U_all : A.unit_cap;  // memory-safe if the caller's bound was low
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t wb = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); wb * kGroupsPerWave < U;
+         wb += nwaves) {
+        const uint64_t u = wb * kGroupsPerWave + grp;
+        const bool valid = u < U;
+        uint64_t r = 0, j = 0, k = 1, off = 0;
+        uint32_t n = 0, init = 0;
+        if (valid) {
+            r = A.unit_rec[u];
+            const uint64_t b0 = A.unit_base[r];
+            k = A.unit_base[r + 1] - b0;
+            j = u - b0;
+            off = A.off[r];
+            n = A.len[r];
+            init = A.init ? A.init[r] : A.init_scalar;
+        }
+        const uint8_t* p = A.arena + off;
+        const Geom g = geom(p, n);
+        uint32_t R = unit_work(lds, X, l, valid, p, init, g, j, k, A.unit_bytes);
+        if (valid && l == 0) {
+            if (g.is_short) {
+                A.out[r] = short_record(lds, kLT8, p, n, init);
+            } else if (k == 1) {
+                if (g.e > g.b) R = bytes_in_block(lds, kLT8, R, g.b, 0u, (uint32_t)(g.e - g.b));
+                A.out[r] = ~R;
+            } else {
+                A.partial[u] = R;
+            }
+        }
+    }
+}
+
+// ---- combine kernels ----------------------------------------------------------
+// Tree over the 64 lanes of a wave: lane 0 gets  XOR_l Z_{D*(63-l)}(v_l).
+__device__ __forceinline__ uint32_t wave_tree(const uint32_t* lds, uint32_t v) {
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        const uint32_t t = __shfl_down(v, 1u << d, 64);
+        v = zmap(lds, d * 1024, v) ^ t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void load_comb_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
+    for (int i = threadIdx.x; i < kCombWords; i += blockDim.x) lds[i] = blob[i];
+}
+
+__global__ __launch_bounds__(256) void k_combine_ragged(RaggedArgs A) {
+    __shared__ uint32_t lds[kCombWords];
+    load_comb_tables(lds, A.comb_blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < A.n_rec; r += nwaves) {
+        const uint64_t b0 = A.unit_base[r];
+        const uint64_t k = A.unit_base[r + 1] - b0;
+        if (k <= 1 || b0 + k > A.unit_cap) continue;  // finished by the unit kernel / over capacity
+        const uint64_t nb = (k + 63) / 64;
+        const int64_t pad = (int64_t)(nb * 64 - k);
+        uint32_t acc = 0;
+        for (uint64_t blk = 0; blk < nb; ++blk) {
+            const int64_t idx = (int64_t)(blk * 64 + lane) - pad;
+            uint32_t v = idx >= 0 ? A.partial[b0 + idx] : 0u;
+            v = wave_tree(lds, v);
+            acc = zmap(lds, 6 * 1024, acc) ^ v;
+        }
+        if (lane == 0) {
+            const uint8_t* p = A.arena + A.off[r];
+            const Geom g = geom(p, A.len[r]);
+            if (g.e > g.b) acc = bytes_in_block(lds, kCombT8, acc, g.b, 0u, (uint32_t)(g.e - g.b));
+            A.out[r] = ~acc;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_combine_fixed(FixedArgs A, const uint32_t* in, uint64_t k_in, uint32_t* outs,
+                                                      uint64_t k_out, const uint32_t* comb) {
+    __shared__ uint32_t lds[kCombWords];
+    load_comb_tables(lds, comb);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t total = A.n_rec * k_out;
+    const int64_t pad = (int64_t)(k_out * 64 - k_in);
+    for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < total; t += nwaves) {
+        const uint64_t r = t / k_out;
+        const uint64_t o = t - r * k_out;
+        const int64_t idx = (int64_t)(o * 64 + lane) - pad;
+        uint32_t v = idx >= 0 ? in[r * k_in + idx] : 0u;
+        v = wave_tree(lds, v);
+        if (lane == 0) {
+            if (k_out == 1) {
+                const uint8_t* p = A.arena + r * A.rec_bytes;
+                const Geom g = geom(p, A.rec_bytes);
+                if (g.e > g.b) v = bytes_in_block(lds, kCombT8, v, g.b, 0u, (uint32_t)(g.e - g.b));
+                A.out[r] = ~v;
+            } else {
+                outs[r * k_out + o] = v;
+            }
+        }
+    }
+}
+
+// ---- synthetic data and a read-only streaming probe ---------------------------
+__device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t i) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// dst[i] = byte (first_byte + i) of the stream; first_byte must be a multiple of 8.
+__global__ __launch_bounds__(256) void k_fill_splitmix(uint8_t* dst, uint64_t n_bytes, uint64_t seed,
+                                                      uint64_t first_word) {
+    const uint64_t n16 = n_bytes / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        const uint64_t w0 = splitmix_word(seed, first_word + 2 * i);
+        const uint64_t w1 = splitmix_word(seed, first_word + 2 * i + 1);
+        reinterpret_cast<u32x4*>(dst)[i] =
+            u32x4{(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        for (uint64_t b = n16 * 16; b < n_bytes; ++b) {
+            const uint64_t w = splitmix_word(seed, first_word + b / 8);
+            dst[b] = (uint8_t)(w >> (8 * (b & 7)));
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_stream_probe(const uint8_t* src, uint64_t n_bytes, uint32_t* out) {
+    const uint64_t n16 = n_bytes / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t x = 0;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const u32x4 a = ld16(src + 16 * i), b = ld16(src + 16 * (i + stride));
+        const u32x4 c = ld16(src + 16 * (i + 2 * stride)), d = ld16(src + 16 * (i + 3 * stride));
+        x ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    }
+    for (; i < n16; i += stride) {
+        const u32x4 a = ld16(src + 16 * i);
+        x ^= a.x ^ a.y ^ a.z ^ a.w;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x ^= __shfl_xor(x, d, 64);
+    if ((threadIdx.x & 63) == 0) atomicXor(out, x);
+}
+
+}  // namespace
+
+// ---- launchers ----------------------------------------------------------------
+hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
+    if (a.n_rec == 0) return hipSuccess;
+    const uint64_t units = a.n_rec * a.units_per_rec;
+    const uint64_t need = (units + kGroupsPerWave * kWavesPerBlock - 1) / (kGroupsPerWave * kWavesPerBlock);
+    const int grid = (int)(need < (uint64_t)grid_blocks ? need : (uint64_t)grid_blocks);
+    hipLaunchKernelGGL(k_units_fixed, dim3(grid), dim3(kBlockThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_combine_fixed(const FixedArgs& a, const uint32_t* in_states, uint64_t k_in, uint32_t* out_states,
+                                uint64_t k_out, const uint32_t* comb_blob, hipStream_t s) {
+    const uint64_t waves = a.n_rec * k_out;
+    uint64_t blocks = (waves + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_combine_fixed, dim3((unsigned)blocks), dim3(256), 0, s, a, in_states, k_in, out_states,
+                       k_out, comb_blob);
+    return hipGetLastError();
+}
+
+uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + 1023) / 1024; }
+
+hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
+    if (a.n_rec == 0) return hipSuccess;
+    const uint64_t nb = ragged_scan_blocks(a.n_rec);
+    hipLaunchKernelGGL(k_ragged_scan1, dim3((unsigned)nb), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_ragged_scan2, dim3(1), dim3(1024), 0, s, a, nb);
+    return hipGetLastError();
+}
+
+hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
+    if (a.n_rec == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ragged_fill, dim3((unsigned)((a.n_rec + 255) / 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_units_ragged, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    uint64_t cblocks = (a.n_rec + 3) / 4;
+    if (cblocks > 4096) cblocks = 4096;
+    hipLaunchKernelGGL(k_combine_ragged, dim3((unsigned)cblocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n_bytes, uint64_t seed, uint64_t first_byte, hipStream_t s) {
+    if (n_bytes == 0) return hipSuccess;
+    uint64_t blocks = (n_bytes / 16 + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_fill_splitmix, dim3((unsigned)blocks), dim3(256), 0, s, dst, n_bytes, seed, first_byte / 8);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_probe(const uint8_t* src, uint64_t n_bytes, uint32_t* out, int grid_blocks, hipStream_t s) {
+    hipLaunchKernelGGL(k_stream_probe, dim3(grid_blocks), dim3(1024), 0, s, src, n_bytes, out);
+    return hipGetLastError();
+}
+
+}  // namespace engine
+}  // namespace karma

@@ -1,0 +1,88 @@
+// karma_amd/csrc/engine.h -- internal interface between the C ABI (capi.cc)
+// and the gfx950 kernels (crc32c_kernels.hip).  Not installed; the public
+// surface is include/karma_crc32c.h and include/karma-util/crc32c.h.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace karma {
+namespace engine {
+
+// ---- geometry of the streaming kernel -----------------------
+constexpr int kGroupLanes = 8;                 // lanes that share one unit
+constexpr int kChunk = 16 * kGroupLanes;       // bytes a group consumes per step (S)
+constexpr int kBlockThreads = 1024;            // one workgroup per CU
+constexpr int kWavesPerBlock = kBlockThreads / 64;
+constexpr int kGroupsPerWave = 64 / kGroupLanes;
+constexpr uint64_t kDefaultUnit = 4096;        // unit size for ragged batches
+
+// ---- table blob of the streaming kernel (uint32 words) ---------------------
+constexpr int kBlobStride = 0;     // Z_S slicing tables, 4 x 256
+constexpr int kBlobZ4 = 1024;      // Z_4   (in-lane fold)
+constexpr int kBlobZ16 = 2048;     // Z_16  (group tree, level 0)
+constexpr int kBlobZ32 = 3072;     // Z_32  (level 1)
+constexpr int kBlobZ64 = 4096;     // Z_64  (level 2)
+constexpr int kBlobT8 = 5120;      // byte table (one zero byte, low byte index)
+constexpr int kBlobWords = 5376;
+
+// ---- table blob of the combine kernels --------------------------------------
+// maps Z_{D * 2^k}, k = 0..6 (k = 6 is the Horner step of 64 states), then T8.
+constexpr int kCombMaps = 7;
+constexpr int kCombT8 = kCombMaps * 1024;
+constexpr int kCombWords = kCombT8 + 256;
+
+// Host builders (gf2.h): fill a blob for stride kChunk / for unit size D.
+void build_stream_blob(uint32_t* out /*kBlobWords*/);
+void build_combine_blob(uint64_t unit_bytes, uint32_t* out /*kCombWords*/);
+
+struct FixedArgs {
+    const uint8_t* arena;      // record r at arena + r * rec_bytes
+    uint64_t rec_bytes;
+    uint64_t n_rec;
+    const uint32_t* init;      // per-record init crc, or nullptr -> init_scalar
+    uint32_t init_scalar;
+    uint64_t unit_bytes;       // multiple of kChunk
+    uint64_t units_per_rec;    // k (same for every record)
+    uint32_t* out;             // final crc per record (written when k == 1)
+    uint32_t* partial;         // per-unit register contributions (k > 1)
+    const uint32_t* blob;      // kBlobWords, device
+};
+
+struct RaggedArgs {
+    const uint8_t* arena;
+    const uint64_t* off;       // payload offset per record
+    const uint32_t* len;       // payload length per record
+    uint64_t n_rec;
+    const uint32_t* init;
+    uint32_t init_scalar;
+    uint64_t unit_bytes;
+    uint64_t* unit_base;       // n_rec + 1 entries: exclusive scan of units per record
+    uint64_t* unit_rec;        // unit -> record (unit_cap entries)
+    uint64_t unit_cap;         // capacity of unit_rec / partial
+    uint64_t* block_sums;      // scan scratch
+    uint32_t* out;
+    uint32_t* partial;
+    const uint32_t* blob;
+    const uint32_t* comb_blob; // kCombWords for unit_bytes
+};
+
+// Launchers (stream-ordered, no allocation, no synchronisation).
+hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s);
+// One combine level for the fixed layout: k_in states per record -> k_out = ceil(k_in / 64).
+hipError_t launch_combine_fixed(const FixedArgs& a, const uint32_t* in_states, uint64_t k_in, uint32_t* out_states,
+                                uint64_t k_out, const uint32_t* comb_blob, hipStream_t s);
+uint64_t ragged_scan_blocks(uint64_t n_rec);
+// Ragged: scan (units per record -> unit_base, total at unit_base[n_rec]),
+// then fill (unit -> record), the unit kernel and the per-record combine.
+hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
+hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s);
+
+// Synthetic data: bytes of the counter-based splitmix64 stream.
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n_bytes, uint64_t seed, uint64_t first_byte, hipStream_t s);
+// Read-only streaming probe (achievable-HBM reference): xor-reduces n_bytes.
+hipError_t launch_stream_probe(const uint8_t* src, uint64_t n_bytes, uint32_t* out, int grid_blocks, hipStream_t s);
+
+}  // namespace engine
+}  // namespace karma

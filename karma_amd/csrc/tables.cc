@@ -1,0 +1,29 @@
+// karma_amd/csrc/tables.cc -- host builders of the kernels' table blobs (gf2.h).
+#include "engine.h"
+#include "gf2.h"
+
+namespace karma {
+namespace engine {
+
+void build_stream_blob(uint32_t* out) {
+    using gf2::Map;
+    gf2::slicing_tables(Map::zero_bytes(kChunk), out + kBlobStride);
+    gf2::slicing_tables(Map::zero_bytes(4), out + kBlobZ4);
+    gf2::slicing_tables(Map::zero_bytes(16), out + kBlobZ16);
+    gf2::slicing_tables(Map::zero_bytes(32), out + kBlobZ32);
+    gf2::slicing_tables(Map::zero_bytes(64), out + kBlobZ64);
+    gf2::byte_table(out + kBlobT8);
+}
+
+void build_combine_blob(uint64_t unit_bytes, uint32_t* out) {
+    using gf2::Map;
+    Map m = Map::zero_bytes(unit_bytes);
+    for (int k = 0; k < kCombMaps; ++k) {
+        gf2::slicing_tables(m, out + k * 1024);
+        m = Map::compose(m, m);  // Z_{D*2^(k+1)}
+    }
+    gf2::byte_table(out + kCombT8);
+}
+
+}  // namespace engine
+}  // namespace karma
