@@ -1,0 +1,320 @@
+#!/usr/bin/env python3
+"""bench.py -- CRC32C GiB/s, device-resident, batched WAL records, on 1..8 MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
+``torch.distributed.run`` with one rank per GPU.  One "step" = one pass of the hot path over
+one batch: every rank checksums its shard of records (``karma_crc32c_batch_fixed``) and, for
+N > 1, the per-record CRCs are gathered to rank 0 over RCCL (``karma_crc32c_gather_u32``).
+Rank 0 prints ONE JSON line.
+
+Default workload = BASELINE.json configs[1]: 1M x 4 KiB records per GPU (weak scaling), bytes
+of the splitmix64 stream generated on the device before timing (inputs resident in HBM).
+Other workloads (``--workload ragged|stream|host``) measure configs[2], configs[3] and the
+PCIe-inclusive host-memory path; they are reported in DESIGN.md, not by the driver.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, GB/s (MI355X_MICROARCH.md chip table)
+GIB = float(1 << 30)
+METRIC = "CRC32C GiB/s device-resident, batched WAL records, 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="fixed", choices=["fixed", "ragged", "stream", "host"])
+    p.add_argument("--records-per-gpu", type=int, default=1 << 20)
+    p.add_argument("--rec-bytes", type=int, default=4096)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_fixed_4k.json"),
+                   help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/profile.sh)")
+    return p.parse_args()
+
+
+# ---------------------------------------------------------------------------------------------
+def cpu_baseline(rec_bytes: int, threads: int) -> dict:
+    """Reference crc32c (oracle/_ref, built from /root/reference/karma-util/crc32c.cc) on host cores.
+
+    Bounded sample: 65536 records of rec_bytes of the same splitmix64 stream, repeated for
+    ~2 s on `threads` threads and ~2 s on one thread.
+    """
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib  # the CPU checker; only the cpu_baseline leg touches it
+    import synth
+    n = 65536 if rec_bytes <= 4096 else max(1, (256 << 20) // rec_bytes)
+    buf = synth.splitmix_np(42, 0, n * rec_bytes).copy()
+    out = np.empty(n, dtype=np.uint32)
+    ref = oracle_lib.ref()
+    kind = "reference" if ref is not None else "port"
+
+    def run(nthr):
+        if ref is not None:
+            ref.ref_crc32c_fixed_mt(buf.ctypes.data, rec_bytes, n, out.ctypes.data, nthr)
+        else:
+            oracle_lib.port().oracle_fixed_crcs(buf.ctypes.data, rec_bytes, n, out.ctypes.data, nthr)
+
+    def rate(nthr, budget):
+        run(nthr)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            run(nthr)
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt > budget:
+                return reps * n * rec_bytes / dt / GIB, reps
+
+    multi, reps_m = rate(threads, 2.0)
+    single, reps_s = rate(1, 2.0)
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(multi, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"{n} x {rec_bytes} B splitmix64 records ({n * rec_bytes >> 20} MiB), crc32c::Value per "
+                      f"record, round-robin over {threads} std::threads, repeated {reps_m}x (~2 s)",
+            "single_thread_value": round(single, 3), "cpu_model": cpu, "host_cores_visible": os.cpu_count()}
+
+
+def pmc_traffic(path: str, workload: str, n_bytes_per_launch: int):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload or int(d.get("payload_bytes_per_launch", -1)) != n_bytes_per_launch:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+# ---------------------------------------------------------------------------------------------
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import karma_amd as K
+    from karma_amd import _lib
+
+    L = _lib.lib()
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    comm = None
+    if world > 1:
+        import ctypes
+        uid = (ctypes.c_char * _lib.UNIQUE_ID_BYTES)()
+        if rank == 0:
+            _lib.check("get_unique_id", L.karma_crc32c_get_unique_id(uid, _lib.UNIQUE_ID_BYTES))
+        obj = [bytes(uid) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (ctypes.c_char * _lib.UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
+        comm = ctypes.c_void_p()
+        _lib.check("comm_init", L.karma_crc32c_comm_init(ctypes.byref(comm), world, uid, rank))
+
+    wl = args.workload
+    n_rec = args.records_per_gpu
+    rec = args.rec_bytes
+    info = {}
+    if wl == "fixed":
+        payload = n_rec * rec
+        arena = torch.empty(payload, dtype=torch.uint8, device=dev)
+        K.fill_splitmix64(arena, args.seed, first_byte=rank * payload)
+        out = torch.empty(n_rec, dtype=torch.uint32, device=dev)
+
+        def crc_step():
+            st = L.karma_crc32c_batch_fixed(arena.data_ptr(), rec, n_rec, None, 0, out.data_ptr(), sh)
+            if st:
+                _lib.check("batch_fixed", st)
+
+        algo_bytes = n_rec * (rec + 4)
+        workload_desc = f"{n_rec} x {rec} B records per GPU, batched CRC32C (BASELINE configs[1] shape)"
+    elif wl == "ragged":
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import synth
+        # configs[2]: log-uniform 64 B .. 64 KiB payloads packed like a segment image (8-B headers), ~4 GiB
+        target = 4 << 30
+        count = int(target / (((65536 - 64) / np.log(1024)) + 8))
+        lens = synth.loguniform_lengths(7, count, 64, 65536)
+        offs, arena_bytes = synth.ragged_layout(lens, header=8)
+        arena = torch.empty(arena_bytes + 16, dtype=torch.uint8, device=dev)
+        K.fill_splitmix64(arena, args.seed + rank)
+        d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+        d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+        out = torch.empty(count, dtype=torch.uint32, device=dev)
+        total = int(lens.sum())
+        n_rec = count
+        payload = total
+
+        def crc_step():
+            st = L.karma_crc32c_batch_ragged(arena.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), count, total,
+                                             None, 0, out.data_ptr(), sh)
+            if st:
+                _lib.check("batch_ragged", st)
+
+        algo_bytes = total + count * (4 + 8 + 4)
+        workload_desc = f"{count} ragged records, log-uniform 64 B-64 KiB ({total / GIB:.2f} GiB payload), " \
+                        f"segment-image layout (BASELINE configs[2])"
+    elif wl == "stream":
+        seg = 64 << 20
+        nseg = 64
+        n_rec, rec = nseg, seg
+        payload = nseg * seg
+        arena = torch.empty(payload, dtype=torch.uint8, device=dev)
+        K.fill_splitmix64(arena, args.seed, first_byte=rank * payload)
+        out = torch.empty(nseg, dtype=torch.uint32, device=dev)
+
+        def crc_step():
+            st = L.karma_crc32c_batch_fixed(arena.data_ptr(), seg, nseg, None, 0, out.data_ptr(), sh)
+            if st:
+                _lib.check("batch_fixed(stream)", st)
+
+        algo_bytes = payload + nseg * 4
+        workload_desc = f"{nseg} distinct 64 MiB segment scans per step (chunked CRC + polynomial combine, " \
+                        f"BASELINE configs[3])"
+    else:  # host: PCIe-inclusive end-to-end from pageable host memory
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import synth
+        n_rec = min(n_rec, 1 << 18)
+        payload = n_rec * rec
+        host = synth.splitmix_np(args.seed, rank * payload, payload).copy()
+        hout = np.empty(n_rec, dtype=np.uint32)
+        out = None
+
+        def crc_step():
+            st = L.karma_crc32c_batch_fixed_host(host.ctypes.data, rec, n_rec, 0, hout.ctypes.data, local)
+            if st:
+                _lib.check("batch_fixed_host", st)
+
+        algo_bytes = payload + n_rec * 4
+        workload_desc = f"{n_rec} x {rec} B records in pageable host memory -> H2D -> kernel -> D2H (synchronous)"
+
+    gather_buf = torch.empty(n_rec * world, dtype=torch.uint32, device=dev) if (comm is not None and rank == 0) else None
+
+    def gather_step():
+        if comm is None or out is None:
+            return
+        st = L.karma_crc32c_gather_u32(comm, out.data_ptr(), n_rec, gather_buf.data_ptr() if gather_buf is not None
+                                       else None, 0, sh)
+        if st:
+            _lib.check("gather_u32", st)
+
+    # ---- warmup -------------------------------------------------------------------------
+    for _ in range(args.warmup):
+        crc_step()
+        gather_step()
+    torch.cuda.synchronize()
+
+    # ---- timed region: K steps between barrier + synchronize --------------------------------
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        crc_step()
+        ev[i][1].record(stream)
+        gather_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_avg = float(np.mean(kern_ms))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_avg], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_max = float(t[0]), float(t[1])
+    else:
+        kern_max = kern_avg
+
+    # ---- self-check: a sample of records against the host crc32c::Extend (product path) ----
+    check = {}
+    if out is not None and rank == 0 and wl in ("fixed", "stream"):
+        idx = np.unique(np.concatenate([np.arange(min(64, n_rec)), np.random.default_rng(1).integers(0, n_rec, 64)]))
+        got = out.cpu().numpy()
+        bad = 0
+        for r in idx[: 16 if wl == "stream" else len(idx)]:
+            b = arena[int(r) * rec:(int(r) + 1) * rec].cpu().numpy()
+            bad += int(K.Value(b) != int(got[r]))
+        check = {"sampled_records": int(len(idx[: 16 if wl == "stream" else len(idx)])), "mismatches": bad}
+
+    if rank == 0:
+        total_bytes = payload * world * args.steps
+        value = total_bytes / elapsed / GIB
+        achieved = algo_bytes / (kern_avg * 1e-3) / 1e9
+        traffic = pmc_traffic(args.pmc, wl, payload) if wl == "fixed" else None
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: little-endian splitmix64 byte stream generated on the device before timing",
+            "config": {"workload": workload_desc, "records_per_gpu": int(n_rec), "rec_bytes": int(rec),
+                       "parallelism": f"record-sharded x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
+                       "kernel": "k_units_fixed" if wl in ("fixed", "stream") else
+                                 ("k_units_ragged" if wl == "ragged" else "host->device pipeline")},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": int(algo_bytes),
+                         "kernel_ms_avg": round(kern_avg, 4), "kernel_ms_max_over_ranks": round(kern_max, 4)},
+            "compute_only_gibs": round(payload * world / (kern_max * 1e-3) / GIB, 2),
+        }
+        if check:
+            res["self_check"] = check
+        if world == 1 and not args.no_cpu_baseline and wl in ("fixed", "host"):
+            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+            res["cpu_baseline"] = cpu_baseline(rec, thr)
+        elif world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+
+    if comm is not None:
+        L.karma_crc32c_comm_destroy(comm)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
