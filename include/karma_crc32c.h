@@ -53,6 +53,8 @@ uint32_t karma_crc32c_extend_host(uint32_t init_crc, const void* data, size_t n)
 /* The same through the portable slicing-by-8 path only (the default path uses
  * the SSE4.2 CRC32 instruction when present); tests compare the two. */
 uint32_t karma_crc32c_extend_host_portable(uint32_t init_crc, const void* data, size_t n);
+/* CRC-32C of A || B from crc_a = CRC(A), crc_b = CRC(B) and len_b = |B| (host, GF(2)). */
+uint32_t karma_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
 /* ---- device-resident batches (stream-ordered) ---------------------------- */
 /* d_out[r] = Extend(init_r, d_data + r*rec_bytes, rec_bytes), r < n_rec,

@@ -5,6 +5,7 @@ GPU batch API (fixed-size, ragged and single-stream) over the C ABI in
 ``include/karma_crc32c.h``.  See DESIGN.md.
 """
 from .crc32c import (  # noqa: F401
+    Combine,
     Extend,
     Mask,
     Unmask,

@@ -30,6 +30,7 @@ SIGNATURES = {
     "karma_crc32c_last_error": (_c.c_char_p, []),
     "karma_crc32c_extend_host": (_u32, [_u32, _vp, _sz]),
     "karma_crc32c_extend_host_portable": (_u32, [_u32, _vp, _sz]),
+    "karma_crc32c_combine": (_u32, [_u32, _u32, _u64]),
     "karma_crc32c_batch_fixed": (_i, [_vp, _sz, _sz, _vp, _u32, _vp, _vp]),
     "karma_crc32c_batch_ragged": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp]),
     "karma_crc32c_stream": (_i, [_u32, _vp, _sz, _vp, _vp]),

@@ -62,6 +62,11 @@ def Value(data) -> int:
     return Extend(0, data)
 
 
+def Combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    """CRC-32C of A || B from Value(A), Value(B) and len(B) (host GF(2) shift)."""
+    return int(_lib.lib().karma_crc32c_combine(crc_a & _M32, crc_b & _M32, len_b))
+
+
 def Mask(crc: int) -> int:
     """crc32c::Mask (reference crc32c.h:28-31): rotate right by 15 bits, add kMaskDelta."""
     crc &= _M32

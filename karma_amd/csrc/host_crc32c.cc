@@ -119,6 +119,14 @@ extern "C" uint32_t karma_crc32c_extend_host(uint32_t init_crc, const void* data
     return crc32c::Extend(init_crc, static_cast<const char*>(data), n);
 }
 
+// crc32c_combine: CRC of A || B from CRC(A), CRC(B) and |B|.  With Z_n = "advance the
+// register over n zero bytes" (gf2.h), Value(A || B) = Z_|B|(Value(A)) ^ Value(B); the
+// same identity gives Extend(c, D) = Z_|D|(c) ^ Value(D).  This is the algebra the GPU
+// combine kernels run with table lookups.
+extern "C" uint32_t karma_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+    return karma::gf2::Map::zero_bytes(len_b).apply(crc_a) ^ crc_b;
+}
+
 extern "C" uint32_t karma_crc32c_extend_host_portable(uint32_t init_crc, const void* data, size_t n) {
     return karma::host_extend_portable(init_crc, data, n);
 }

@@ -1,0 +1,262 @@
+"""Parity of the gfx950 kernels with the oracle (run on the MI355X box: pytest -m gpu).
+
+Bit-exact comparisons through the C ABI (karma_amd wraps it with ctypes) against
+oracle/crc32c_port.c (itself pinned to the reference build by tests/test_oracle.py) and the
+committed golden fixtures; full BASELINE sizes (configs 2-4) are checked record by record.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib
+import synth
+from golden_inputs import ragged_inputs
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import karma_amd as K  # noqa: E402
+from karma_amd import _lib  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def raw(dev):
+    rng = np.random.default_rng(5)
+    host = rng.integers(0, 256, size=(1 << 23) + 64, dtype=np.uint8)
+    return host, torch.from_numpy(host).to(dev)
+
+
+def _eq(got, want):
+    got = np.asarray(got, dtype=np.uint32)
+    want = np.asarray(want, dtype=np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first {[(int(i), hex(int(got[i])), hex(int(want[i]))) for i in bad[:4]]}"
+
+
+def test_native_library_is_what_runs(dev):
+    buf = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    K.value_batch_fixed(buf, 4096)
+    torch.cuda.synchronize()
+    maps = open("/proc/self/maps").read()
+    assert os.path.realpath(_lib.LIB_PATH) in maps
+    assert K.device_cu_count() >= 1
+
+
+@pytest.mark.parametrize("rec", [1, 2, 3, 4, 7, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 127, 128, 129, 255, 256,
+                                 257, 1000, 2047, 2048, 2049, 4095, 4096, 4097, 8192, 65535, 65536, 100000])
+@pytest.mark.parametrize("mis", [0, 1, 4, 8, 13])
+def test_fixed_sizes_and_alignments(raw, rec, mis):
+    host, dbuf = raw
+    n = min(3000, ((1 << 23) - mis) // rec)
+    got = K.value_batch_fixed(dbuf[mis: mis + n * rec], rec).cpu().numpy()
+    _eq(got, oracle_lib.fixed_crcs(host[mis: mis + n * rec], rec))
+
+
+@pytest.mark.parametrize("rec,n", [(1 << 23, 1), (3 << 20, 2), ((1 << 22) - 7, 2), (1 << 20, 8), (123457, 60),
+                                   (777777, 10), (40000, 200)])
+@pytest.mark.parametrize("mis", [0, 3])
+def test_split_records_multilevel_combine(raw, rec, n, mis):
+    host, dbuf = raw
+    if mis + n * rec > host.size:
+        n = (host.size - mis) // rec
+    got = K.value_batch_fixed(dbuf[mis: mis + n * rec], rec).cpu().numpy()
+    _eq(got, oracle_lib.fixed_crcs(host[mis: mis + n * rec], rec))
+
+
+def test_init_array_and_scalar(raw, dev):
+    host, dbuf = raw
+    rng = np.random.default_rng(9)
+    for rec, n in [(333, 2000), (4096, 500), (20, 1000), (70000, 40)]:
+        init = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+        got = K.value_batch_fixed(dbuf[: n * rec], rec, init=torch.from_numpy(init).to(dev)).cpu().numpy()
+        want = [oracle_lib.extend(int(init[r]), host[r * rec:(r + 1) * rec].tobytes()) for r in range(n)]
+        _eq(got, want)
+        got = K.value_batch_fixed(dbuf[: n * rec], rec, init=0xDEADBEEF).cpu().numpy()
+        want = [oracle_lib.extend(0xDEADBEEF, host[r * rec:(r + 1) * rec].tobytes()) for r in range(n)]
+        _eq(got, want)
+
+
+@pytest.mark.parametrize("key", ["ragged_replay_mix", "ragged_small_init", "ragged_tiny_unaligned"])
+@pytest.mark.parametrize("with_total", [True, False])
+def test_ragged_golden(records, dev, key, with_total):
+    data, offs, lens, init, want = ragged_inputs(records[key])
+    got = K.extend_batch_ragged(torch.from_numpy(data).to(dev), torch.from_numpy(offs.astype(np.int64)).to(dev),
+                                torch.from_numpy(lens.astype(np.int32)).to(dev),
+                                init=None if init is None else torch.from_numpy(init).to(dev),
+                                total_len=int(lens.sum()) if with_total else None).cpu().numpy()
+    _eq(got, want)
+
+
+def test_ragged_edge_lengths_every_alignment(raw, dev):
+    host, dbuf = raw
+    offs, lens = [], []
+    for a in range(16):  # every start alignment mod 16 ...
+        for n in range(0, 301):  # ... times every length 0..300 (head / body / tail / short paths)
+            i = len(offs)
+            offs.append(((i * 397) % (1 << 22)) // 16 * 16 + a)
+            lens.append(n)
+    offs = np.array(offs, dtype=np.uint64)
+    lens = np.array(lens, dtype=np.uint32)
+    init = synth.splitmix_words(77, 0, offs.size).astype(np.uint32)
+    got = K.extend_batch_ragged(dbuf, torch.from_numpy(offs.astype(np.int64)).to(dev),
+                                torch.from_numpy(lens.astype(np.int32)).to(dev),
+                                init=torch.from_numpy(init).to(dev)).cpu().numpy()
+    _eq(got, oracle_lib.ragged_crcs(host, offs, lens, init))
+
+
+def test_ragged_overlapping_large_and_end_of_buffer(raw, dev):
+    host, dbuf = raw
+    size = (1 << 23) + 64
+    rng = np.random.default_rng(4)
+    lens = np.concatenate([rng.integers(0, 300000, 500), [size, size - 1, 1 << 20, 5, 0, 17, 1 << 22]]).astype(np.uint32)
+    offs = np.array([int(rng.integers(0, size - int(n) + 1)) for n in lens[:-7]] +
+                    [0, 1, size - (1 << 20), size - 5, size, size - 17, 3], dtype=np.uint64)
+    got = K.extend_batch_ragged(dbuf, torch.from_numpy(offs.astype(np.int64)).to(dev),
+                                torch.from_numpy(lens.astype(np.int32)).to(dev)).cpu().numpy()
+    _eq(got, oracle_lib.ragged_crcs(host, offs, lens))
+
+
+def test_empty_batches(dev):
+    buf = torch.zeros(16, dtype=torch.uint8, device=dev)
+    out = torch.full((1,), 7, dtype=torch.int32, device=dev)
+    assert _lib.lib().karma_crc32c_batch_fixed(buf.data_ptr(), 16, 0, None, 0, out.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    assert int(out.item()) == 7  # nothing written for zero records
+    # zero-length records: Extend(c, D, 0) = c
+    outs = torch.zeros(5, dtype=torch.uint32, device=dev)
+    assert _lib.lib().karma_crc32c_batch_fixed(None, 0, 5, None, 0x55, outs.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    _eq(outs.cpu().numpy(), [0x55] * 5)
+    e = torch.zeros(0, dtype=torch.int64, device=dev)
+    assert K.extend_batch_ragged(buf, e, e.to(torch.int32)).numel() == 0
+    z = torch.zeros(0, dtype=torch.uint8, device=dev)
+    assert int(K.extend_stream(0x1234, z).item()) == 0x1234  # Extend(c, D, 0) = c
+
+
+def test_stream_64mib_pattern_kat(dev):
+    pat = torch.from_numpy(np.frombuffer(synth.pattern(64 << 20), dtype=np.uint8).copy()).to(dev)
+    assert int(K.extend_stream(0, pat).item()) == 0x0C49B210
+    # streaming semantics: Extend(Value(A), B) == Value(A || B) at an unaligned cut
+    a, b = pat[: 12345677], pat[12345677:]
+    va = int(K.extend_stream(0, a).item())
+    assert int(K.extend_stream(va, b).item()) == 0x0C49B210
+    assert K.Combine(va, int(K.extend_stream(0, b).item()), b.numel()) == 0x0C49B210
+
+
+def test_stream_1gib_with_init(dev):
+    n = 1 << 30
+    buf = torch.empty(n, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 1234)
+    got = int(K.extend_stream(0xCAFEF00D, buf).item())
+    want = int(oracle_lib.splitmix_fixed_crcs(1234, n, 0, 1, init=0xCAFEF00D, threads=1)[0])
+    assert got == want
+
+
+def test_config2_full_1m_x_4k(dev):
+    n, rec = 1 << 20, 4096
+    buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 42)
+    got = K.value_batch_fixed(buf, rec).cpu().numpy()
+    want = oracle_lib.splitmix_fixed_crcs(42, rec, 0, n, threads=16)
+    _eq(got, want)
+    # size-independent properties at full size: a flipped byte changes exactly that record,
+    # and by the CRC's linearity the change equals Value(delta) ^ Value(zeros)
+    r, pos = 777777, 1234
+    old = int(got[r])
+    buf[r * rec + pos] ^= 0x40
+    got2 = K.value_batch_fixed(buf, rec).cpu().numpy()
+    changed = np.nonzero(got2 != got)[0]
+    assert changed.tolist() == [r]
+    delta = np.zeros(rec, np.uint8)
+    delta[pos] = 0x40
+    assert int(got2[r]) ^ old == K.Value(delta) ^ K.Value(np.zeros(rec, np.uint8))
+
+
+def test_config3_full_ragged_replay_mix(dev):
+    count = int((4 << 30) / (((65536 - 64) / np.log(1024)) + 8))
+    lens = synth.loguniform_lengths(7, count, 64, 65536)
+    offs, arena = synth.ragged_layout(lens, header=8)
+    buf = torch.empty(arena + 16, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 42)
+    got = K.extend_batch_ragged(buf, torch.from_numpy(offs.astype(np.int64)).to(dev),
+                                torch.from_numpy(lens.astype(np.int32)).to(dev), total_len=int(lens.sum()))
+    host = buf.cpu().numpy()
+    _eq(got.cpu().numpy(), oracle_lib.ragged_crcs(host, offs, lens, threads=16))
+
+
+def test_config4_64_segments_of_64mib(dev):
+    seg, nseg = 64 << 20, 64
+    buf = torch.empty(seg * nseg, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 42)
+    got = K.value_batch_fixed(buf, seg).cpu().numpy()
+    _eq(got, oracle_lib.splitmix_fixed_crcs(42, seg, 0, nseg, threads=16))
+
+
+def test_config5_shards_concatenate_to_whole_batch(dev):
+    # 8 record shards computed separately (as 8 ranks would) == the unsharded batch
+    from karma_amd.shard import shard_range
+    n, rec = 1 << 17, 4096
+    buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 42)
+    whole = K.value_batch_fixed(buf, rec).cpu().numpy()
+    parts = []
+    for r in range(8):
+        lo, hi = shard_range(n, 8, r)
+        sub = torch.empty((hi - lo) * rec, dtype=torch.uint8, device=dev)
+        K.fill_splitmix64(sub, 42, first_byte=lo * rec)  # the rank's own slice of the global stream
+        parts.append(K.value_batch_fixed(sub, rec).cpu().numpy())
+    _eq(np.concatenate(parts), whole)
+
+
+def test_rccl_gather_world1(dev):
+    L = _lib.lib()
+    uid = (ctypes.c_char * _lib.UNIQUE_ID_BYTES)()
+    _lib.check("uid", L.karma_crc32c_get_unique_id(uid, _lib.UNIQUE_ID_BYTES))
+    comm = ctypes.c_void_p()
+    _lib.check("init", L.karma_crc32c_comm_init(ctypes.byref(comm), 1, uid, 0))
+    try:
+        n, rec = 4096, 4096
+        buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
+        K.fill_splitmix64(buf, 5)
+        loc = torch.empty(n, dtype=torch.uint32, device=dev)
+        allc = torch.empty(n, dtype=torch.uint32, device=dev)
+        s = torch.cuda.current_stream().cuda_stream
+        _lib.check("sharded", L.karma_crc32c_batch_fixed_sharded(comm, buf.data_ptr(), rec, n, 0, loc.data_ptr(),
+                                                                 allc.data_ptr(), 0, s))
+        torch.cuda.synchronize()
+        _eq(allc.cpu().numpy(), oracle_lib.splitmix_fixed_crcs(5, rec, 0, n))
+    finally:
+        L.karma_crc32c_comm_destroy(comm)
+
+
+def test_host_memory_paths(raw):
+    host, _ = raw
+    rec = 4096
+    n = host.size // rec
+    got = K.value_batch_fixed_host(host[: n * rec], rec)
+    _eq(got, oracle_lib.fixed_crcs(host[: n * rec], rec))
+    big = synth.splitmix_np(8, 0, 300 << 20).copy()  # > one 64 MiB chunk: exercises the 2-stream pipeline
+    got = K.value_batch_fixed_host(big, 1000)
+    _eq(got, oracle_lib.fixed_crcs(big[: (big.size // 1000) * 1000], 1000))
+    lens = synth.uniform_lengths(2, 5000, 0, 3000)
+    offs, arena = synth.ragged_layout(lens, header=8)
+    got = K.extend_batch_ragged_host(host[: arena], offs, lens, init=0x77)
+    _eq(got, oracle_lib.ragged_crcs(host, offs, lens, np.full(lens.size, 0x77, np.uint32)))
+
+
+def test_rejects_bad_arguments(dev):
+    L = _lib.lib()
+    buf = torch.zeros(64, dtype=torch.uint8, device=dev)
+    assert L.karma_fill_splitmix64(buf.data_ptr() + 1, 32, 1, 0, None) == _lib.KARMA_E_INVALID
+    assert L.karma_fill_splitmix64(buf.data_ptr(), 32, 1, 3, None) == _lib.KARMA_E_INVALID
+    with pytest.raises(ValueError):
+        K.value_batch_fixed(buf, 7)

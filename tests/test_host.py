@@ -1,0 +1,141 @@
+"""Host side of the boundary (no GPU needed): the library loads and exports what include/*.h
+declares, crc32c::Extend / Value / Mask / Unmask match the reference golden vectors, the C++
+drop-in compiles and links like Karma's callers, device entry points refuse to run without a
+GPU (no CPU fallback), and the GF(2) combine identity the GPU combine kernels rely on holds."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import karma_amd as K
+from karma_amd import _lib
+from golden_inputs import case_bytes, case_init
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    names = set()
+    for fn in os.listdir(os.path.join(ROOT, "include")):
+        if fn.endswith(".h"):
+            text = open(os.path.join(ROOT, "include", fn)).read()
+            names |= set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(karma_\w+)\s*\(", text, flags=re.M))
+    return names
+
+
+def test_library_exports_every_declared_symbol(karma_lib):
+    declared = _declared_symbols()
+    assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
+    for name in sorted(declared):
+        assert hasattr(karma_lib, name), name
+        assert name in _lib.SIGNATURES, f"{name} missing from karma_amd/_lib.py"
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = {ln.split()[-1] for ln in out.stdout.splitlines() if " T " in ln}
+    # the drop-in C++ symbol crc32c::Extend(unsigned, const char*, unsigned long)
+    assert "_ZN6crc32c6ExtendEjPKcm" in exported
+    assert declared <= exported
+    # nothing but the ABI leaks out
+    assert all(s.startswith("karma_") or s == "_ZN6crc32c6ExtendEjPKcm" for s in exported)
+
+
+def test_abi_version_and_errors(karma_lib):
+    assert karma_lib.karma_crc32c_abi_version() == 1
+    assert karma_lib.karma_crc32c_strerror(0) == b"ok"
+    assert karma_lib.karma_crc32c_strerror(-2) == b"no usable HIP device"
+
+
+def test_host_extend_golden(vectors):
+    for c in vectors["kat"]:
+        assert K.Extend(case_init(c), case_bytes("kat", c)) == int(c["crc"], 16), c["name"]
+    for c in vectors["pattern"]:
+        if c["n"] <= (1 << 21):
+            assert K.Value(case_bytes("pattern", c)) == int(c["crc"], 16)
+    for c in vectors["splitmix"]:
+        assert K.Extend(case_init(c), case_bytes("splitmix", c)) == int(c["crc"], 16)
+
+
+def test_host_paths_agree_misaligned():
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, 20000, dtype=np.uint8)
+    L = _lib.lib()
+    for _ in range(500):
+        off = int(rng.integers(0, 16))
+        n = int(rng.integers(0, 19000))
+        init = int(rng.integers(0, 1 << 32))
+        a = L.karma_crc32c_extend_host(init, data.ctypes.data + off, n)
+        b = L.karma_crc32c_extend_host_portable(init, data.ctypes.data + off, n)
+        assert a == b
+
+
+def test_mask_unmask(vectors):
+    for m in vectors["mask"]:
+        assert K.Mask(int(m["crc"], 16)) == int(m["masked"], 16)
+        assert K.Unmask(int(m["masked"], 16)) == int(m["crc"], 16)
+    assert K.kMaskDelta == 0xA282EAD8
+
+
+def test_combine_identities():
+    # Value(A||B) = Z_|B|(Value(A)) ^ Value(B);  Extend(c, D) = Z_|D|(c) ^ Value(D)
+    rng = np.random.default_rng(2)
+    for _ in range(200):
+        a = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        assert K.Combine(K.Value(a), K.Value(b), len(b)) == K.Value(a + b)
+        c = int(rng.integers(0, 1 << 32))
+        assert K.Combine(c, K.Value(b), len(b)) == K.Extend(c, b)
+    # large shifts (the multi-level combine of a 64 MiB stream uses Z_{unit*64^k})
+    assert K.Combine(K.Value(b"x"), K.Value(b""), 0) == K.Value(b"x")
+
+
+def test_dropin_cpp_links_against_engine(karma_lib, tmp_path):
+    exe = tmp_path / "dropin_test"
+    cmd = ["g++", "-std=c++20", "-O1", "-UNDEBUG", "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "cpp", "dropin_test.cc"), "-L", os.path.dirname(_lib.LIB_PATH),
+           "-lkarma_crc32c", f"-Wl,-rpath,{os.path.dirname(_lib.LIB_PATH)}", "-o", str(exe)]
+    subprocess.run(cmd, check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "dropin_test: ok" in r.stdout
+    # it resolved crc32c::Extend from libkarma_crc32c.so, not from a copy of crc32c.cc
+    nm = subprocess.run(["nm", "-u", str(exe)], capture_output=True, text=True, check=True).stdout
+    assert "_ZN6crc32c6ExtendEjPKcm" in nm
+
+
+def _no_gpu():
+    try:
+        import torch
+        return not torch.cuda.is_available()
+    except Exception:
+        return True
+
+
+@pytest.mark.skipif(not _no_gpu(), reason="checks the no-device behaviour")
+def test_device_entry_points_refuse_without_gpu(karma_lib):
+    out = ctypes.c_uint32()
+    buf = ctypes.create_string_buffer(64)
+    st = karma_lib.karma_crc32c_batch_fixed(ctypes.addressof(buf), 16, 4, None, 0, ctypes.addressof(out), None)
+    assert st == _lib.KARMA_E_NO_DEVICE
+    st = karma_lib.karma_crc32c_stream(0, ctypes.addressof(buf), 64, ctypes.addressof(out), None)
+    assert st == _lib.KARMA_E_NO_DEVICE
+    assert b"no HIP device" in karma_lib.karma_crc32c_last_error()
+    with pytest.raises(_lib.KarmaError):
+        K.device_cu_count()
+
+
+def test_invalid_arguments_rejected_before_device(karma_lib):
+    # null output / data with records: KARMA_E_INVALID regardless of the device
+    assert karma_lib.karma_crc32c_batch_fixed(None, 16, 4, None, 0, None, None) == _lib.KARMA_E_INVALID
+    assert karma_lib.karma_crc32c_batch_ragged(None, None, None, 3, 0, None, 0, None, None) == _lib.KARMA_E_INVALID
+    # zero records is a no-op success
+    assert karma_lib.karma_crc32c_batch_fixed(None, 16, 0, None, 0, None, None) == 0
+
+
+def test_python_batch_api_rejects_host_tensors():
+    import torch
+    with pytest.raises(ValueError):
+        K.value_batch_fixed(torch.zeros(64, dtype=torch.uint8), 16)
+    with pytest.raises(ValueError):
+        K.extend_stream(0, torch.zeros(64, dtype=torch.uint8))
