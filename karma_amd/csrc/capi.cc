@@ -502,7 +502,7 @@ int karma_stream_probe(const void* d_src, size_t n_bytes, uint32_t* d_out, karma
         return fail(KARMA_E_INVALID, "stream_probe: null or source not 16-byte aligned");
     Locked L;
     if (L.rc) return L.rc;
-    KARMA_HIP(launch_stream_probe(static_cast<const uint8_t*>(d_src), n_bytes, d_out, L.ds->cu * 2,
+    KARMA_HIP(launch_stream_probe(static_cast<const uint8_t*>(d_src), n_bytes, d_out, L.ds->cu,
                                   (hipStream_t)stream));
     return 0;
 }

@@ -24,6 +24,8 @@
 //     stepped one at a time (STEP1, :286-290).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "engine.h"
 
 namespace karma {
@@ -136,10 +138,26 @@ __device__ __forceinline__ Geom geom(const uint8_t* p, uint64_t n) {
     return g;
 }
 
+template <bool NT>
+__device__ __forceinline__ u32x4 ldg(const uint8_t* p) {
+    if constexpr (NT) return __builtin_nontemporal_load((gu32x4*)(p));
+    return *(gu32x4*)(p);
+}
+
+__device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
+                                      uint32_t& a3, const u32x4& v) {
+    a0 = stride_step(lds, X, a0, v.x);
+    a1 = stride_step(lds, X, a1, v.y);
+    a2 = stride_step(lds, X, a2, v.z);
+    a3 = stride_step(lds, X, a3, v.w);
+}
+
 // Register contribution of the 16-aligned span [us, ue) with 128-byte chunks
 // end-aligned to ue; `inj` is xored into the word at `inj_at`.  Every lane of
 // the wave must call this (it ends in cross-lane shuffles); the result is
-// valid in group lane 0.
+// valid in group lane 0.  PF chunks are kept in flight per lane (software
+// pipelining across iterations); NT selects non-temporal loads.
+template <int PF, bool NT>
 __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, uint32_t l, const uint8_t* us,
                                                const uint8_t* ue, const uint8_t* inj_at, uint32_t inj) {
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
@@ -148,7 +166,7 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
         const int64_t nch = (span + kChunk - 1) / kChunk;
         const uint8_t* w = ue - nch * kChunk + 16 * l;
         {
-            u32x4 v = (w >= us) ? ld16(w) : u32x4{0u, 0u, 0u, 0u};
+            u32x4 v = (w >= us) ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
             if (w == inj_at) v.x ^= inj;
             a0 = v.x;
             a1 = v.y;
@@ -162,53 +180,23 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
         // fall back to the unit's last 16 bytes so no load leaves [us, ue).
         const uint8_t* last = ue - kChunk + 16 * l;
         if (last < us) last = ue - 16;
-        u32x4 n0 = ld16(pmin(w, last));
-        u32x4 n1 = ld16(pmin(w + kChunk, last));
-        u32x4 n2 = ld16(pmin(w + 2 * kChunk, last));
-        u32x4 n3 = ld16(pmin(w + 3 * kChunk, last));
-        while (rem >= 4) {
-            const u32x4 v0 = n0, v1 = n1, v2 = n2, v3 = n3;
-            w += 4 * kChunk;
-            n0 = ld16(pmin(w, last));
-            n1 = ld16(pmin(w + kChunk, last));
-            n2 = ld16(pmin(w + 2 * kChunk, last));
-            n3 = ld16(pmin(w + 3 * kChunk, last));
-            a0 = stride_step(lds, X, a0, v0.x);
-            a1 = stride_step(lds, X, a1, v0.y);
-            a2 = stride_step(lds, X, a2, v0.z);
-            a3 = stride_step(lds, X, a3, v0.w);
-            a0 = stride_step(lds, X, a0, v1.x);
-            a1 = stride_step(lds, X, a1, v1.y);
-            a2 = stride_step(lds, X, a2, v1.z);
-            a3 = stride_step(lds, X, a3, v1.w);
-            a0 = stride_step(lds, X, a0, v2.x);
-            a1 = stride_step(lds, X, a1, v2.y);
-            a2 = stride_step(lds, X, a2, v2.z);
-            a3 = stride_step(lds, X, a3, v2.w);
-            a0 = stride_step(lds, X, a0, v3.x);
-            a1 = stride_step(lds, X, a1, v3.y);
-            a2 = stride_step(lds, X, a2, v3.z);
-            a3 = stride_step(lds, X, a3, v3.w);
-            rem -= 4;
+        u32x4 nb[PF];
+#pragma unroll
+        for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, last));
+        while (rem >= PF) {
+            u32x4 cur[PF];
+#pragma unroll
+            for (int q = 0; q < PF; ++q) cur[q] = nb[q];
+            w += PF * kChunk;
+#pragma unroll
+            for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, last));
+#pragma unroll
+            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+            rem -= PF;
         }
-        if (rem > 0) {
-            a0 = stride_step(lds, X, a0, n0.x);
-            a1 = stride_step(lds, X, a1, n0.y);
-            a2 = stride_step(lds, X, a2, n0.z);
-            a3 = stride_step(lds, X, a3, n0.w);
-        }
-        if (rem > 1) {
-            a0 = stride_step(lds, X, a0, n1.x);
-            a1 = stride_step(lds, X, a1, n1.y);
-            a2 = stride_step(lds, X, a2, n1.z);
-            a3 = stride_step(lds, X, a3, n1.w);
-        }
-        if (rem > 2) {
-            a0 = stride_step(lds, X, a0, n2.x);
-            a1 = stride_step(lds, X, a1, n2.y);
-            a2 = stride_step(lds, X, a2, n2.z);
-            a3 = stride_step(lds, X, a3, n2.w);
-        }
+#pragma unroll
+        for (int q = 0; q < PF - 1; ++q)
+            if (rem > q) step4(lds, X, a0, a1, a2, a3, nb[q]);
     }
     // lane fold (crc32c.cc STEP4W order): c = Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0))))
     uint32_t c = zmap(lds, kLZ4, a0);
@@ -244,6 +232,7 @@ __device__ __forceinline__ uint32_t lane_const() {
 
 // Per-unit work shared by the fixed and ragged kernels.  Returns the unit's
 // register contribution (valid in group lane 0).
+template <int PF, bool NT>
 __device__ __forceinline__ uint32_t unit_work(const uint32_t* lds, uint32_t X, uint32_t l, bool valid,
                                               const uint8_t* p, uint32_t init, const Geom& g, uint64_t j,
                                               uint64_t k, uint64_t umax) {
@@ -263,10 +252,13 @@ __device__ __forceinline__ uint32_t unit_work(const uint32_t* lds, uint32_t X, u
             inj = h;
         }
     }
-    return group_unit(lds, X, l, us, ue, inj_at, inj);
+    return group_unit<PF, NT>(lds, X, l, us, ue, inj_at, inj);
 }
 
 // ---- fixed-size records --------------------------------------------------------
+constexpr int kRaggedPF = 4;
+constexpr bool kRaggedNT = true;
+template <int PF, bool NT>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     __shared__ uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
@@ -294,7 +286,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
         const uint8_t* p = A.arena + r * A.rec_bytes;
         const uint32_t init = valid ? (A.init ? A.init[r] : A.init_scalar) : 0u;
         const Geom g = geom(p, A.rec_bytes);
-        uint32_t R = unit_work(lds, X, l, valid, p, init, g, j, k, A.unit_bytes);
+        uint32_t R = unit_work<PF, NT>(lds, X, l, valid, p, init, g, j, k, A.unit_bytes);
         if (valid && l == 0) {
             if (g.is_short) {
                 A.out[r] = short_record(lds, kLT8, p, A.rec_bytes, init);
@@ -304,6 +296,91 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
             } else {
                 A.partial[u] = R;
             }
+        }
+    }
+}
+
+// ---- fixed-size fast path: one continuous load stream per group ----------------
+// Preconditions (checked by the host): arena 16-byte aligned, unit_bytes a
+// multiple of PF * 128 and rec_bytes == units_per_rec * unit_bytes.  Unit u
+// is then simply arena + u * unit_bytes, every chunk is full, and the group
+// walks its units back to back with a ring of PF chunk loads in flight that
+// runs across unit boundaries: the next unit's first loads are in flight
+// while the current unit's fold/tree epilogue runs.  Units of a wave have
+// the same length, so the epilogue (with its cross-lane shuffles) is
+// wave-uniform.
+template <int PF, bool NT>
+__global__ __launch_bounds__(kBlockThreads) void k_fixed_pipelined(FixedArgs A) {
+    __shared__ uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const uint64_t k = A.units_per_rec;
+    const uint64_t U = A.n_rec * k;
+    const uint64_t ub = A.unit_bytes;
+    const uint64_t C = ub / kChunk;  // chunks per unit, multiple of PF
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t wb0 = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const uint64_t nbt = (U + kGroupsPerWave - 1) / kGroupsPerWave;  // unit batches of 8
+    if (wb0 >= nbt) return;  // whole wave idle; no barrier follows
+    const uint64_t nb = (nbt - wb0 + nwaves - 1) / nwaves;
+    const uint8_t* lane_base = A.arena + 16 * l;
+    auto unit_of = [&](uint64_t b) -> uint64_t {
+        const uint64_t u = (wb0 + b * nwaves) * kGroupsPerWave + grp;
+        return u < U ? u : U - 1;  // idle groups re-read a valid unit, results dropped
+    };
+    u32x4 ring[PF];
+    uint64_t lb = 0, lc = PF;  // next chunk to load: batch lb, chunk lc
+    const uint8_t* lptr = lane_base + unit_of(0) * ub;
+#pragma unroll
+    for (int q = 0; q < PF; ++q) ring[q] = ldg<NT>(lptr + q * kChunk);
+    for (uint64_t b = 0; b < nb; ++b) {
+        const uint64_t u = (wb0 + b * nwaves) * kGroupsPerWave + grp;
+        const bool valid = u < U;
+        uint64_t r = u, j = 0;
+        if (k != 1) {
+            r = u / k;
+            j = u - r * k;
+        }
+        uint32_t inj = 0;
+        if (valid && j == 0 && l == 0) inj = ~(A.init ? A.init[r] : A.init_scalar);
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        for (uint64_t c = 0; c < C; c += PF) {
+            if (lc == C) {
+                lc = 0;
+                ++lb;
+                lptr = lane_base + unit_of(lb < nb ? lb : nb - 1) * ub;
+            }
+#pragma unroll
+            for (int q = 0; q < PF; ++q) {
+                u32x4 v = ring[q];
+                ring[q] = ldg<NT>(lptr + (lc + q) * kChunk);
+                if (q == 0) {
+                    v.x ^= inj;
+                    inj = 0;
+                }
+                step4(lds, X, a0, a1, a2, a3, v);
+            }
+            lc += PF;
+        }
+        uint32_t cfold = zmap(lds, kLZ4, a0);
+        cfold = zmap(lds, kLZ4, cfold ^ a1);
+        cfold = zmap(lds, kLZ4, cfold ^ a2);
+        cfold = zmap(lds, kLZ4, cfold ^ a3);
+        uint32_t t = __shfl_down(cfold, 1, kGroupLanes);
+        cfold = zmap(lds, kLZ16, cfold) ^ t;
+        t = __shfl_down(cfold, 2, kGroupLanes);
+        cfold = zmap(lds, kLZ32, cfold) ^ t;
+        t = __shfl_down(cfold, 4, kGroupLanes);
+        cfold = zmap(lds, kLZ64, cfold) ^ t;
+        if (valid && l == 0) {
+            if (k == 1)
+                A.out[u] = ~cfold;
+            else
+                A.partial[u] = cfold;
         }
     }
 }
@@ -406,7 +483,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
         }
         const uint8_t* p = A.arena + off;
         const Geom g = geom(p, n);
-        uint32_t R = unit_work(lds, X, l, valid, p, init, g, j, k, A.unit_bytes);
+        uint32_t R = unit_work<kRaggedPF, kRaggedNT>(lds, X, l, valid, p, init, g, j, k, A.unit_bytes);
         if (valid && l == 0) {
             if (g.is_short) {
                 A.out[r] = short_record(lds, kLT8, p, n, init);
@@ -518,18 +595,25 @@ __global__ __launch_bounds__(256) void k_fill_splitmix(uint8_t* dst, uint64_t n_
     }
 }
 
-__global__ __launch_bounds__(1024) void k_stream_probe(const uint8_t* src, uint64_t n_bytes, uint32_t* out) {
+// Read-only probe: each workgroup streams one contiguous slab with 8
+// non-temporal 16-byte loads per lane in flight (the fastest read shape of
+// tools/hbm_probe.hip on MI355X); xor-reduced so nothing is dead code.
+__global__ __launch_bounds__(256) void k_stream_probe(const uint8_t* src, uint64_t n_bytes, uint32_t* out) {
     const uint64_t n16 = n_bytes / 16;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = per * blockIdx.x, hi = lo + per < n16 ? lo + per : n16;
     uint32_t x = 0;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const u32x4 a = ld16(src + 16 * i), b = ld16(src + 16 * (i + stride));
-        const u32x4 c = ld16(src + 16 * (i + 2 * stride)), d = ld16(src + 16 * (i + 3 * stride));
-        x ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    uint64_t i = lo + threadIdx.x;
+    constexpr int U = 8;
+    for (; i + (U - 1) * blockDim.x < hi; i += U * blockDim.x) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ldg<true>(src + 16 * (i + u * blockDim.x));
+#pragma unroll
+        for (int u = 0; u < U; ++u) x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     }
-    for (; i < n16; i += stride) {
-        const u32x4 a = ld16(src + 16 * i);
+    for (; i < hi; i += blockDim.x) {
+        const u32x4 a = ldg<true>(src + 16 * i);
         x ^= a.x ^ a.y ^ a.z ^ a.w;
     }
 #pragma unroll
@@ -540,12 +624,37 @@ __global__ __launch_bounds__(1024) void k_stream_probe(const uint8_t* src, uint6
 }  // namespace
 
 // ---- launchers ----------------------------------------------------------------
+// Tuning variant of the streaming kernel (prefetch depth x load policy);
+// KARMA_CRC_VARIANT overrides the default for A/B measurements.
+static int fixed_variant() {
+    const char* e = getenv("KARMA_CRC_VARIANT");
+    return e ? atoi(e) : 0;
+}
+
+constexpr int kFastPF = 4;
+
+bool fixed_fast_path_ok(const FixedArgs& a) {
+    return (reinterpret_cast<uintptr_t>(a.arena) & 15u) == 0 && a.unit_bytes % (kChunk * kFastPF) == 0 &&
+           a.rec_bytes == a.units_per_rec * a.unit_bytes && a.rec_bytes > 0;
+}
+
 hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     const uint64_t units = a.n_rec * a.units_per_rec;
     const uint64_t need = (units + kGroupsPerWave * kWavesPerBlock - 1) / (kGroupsPerWave * kWavesPerBlock);
     const int grid = (int)(need < (uint64_t)grid_blocks ? need : (uint64_t)grid_blocks);
-    hipLaunchKernelGGL(k_units_fixed, dim3(grid), dim3(kBlockThreads), 0, s, a);
+    const int v = fixed_variant();
+    if (fixed_fast_path_ok(a) && v == 0) {
+        hipLaunchKernelGGL((k_fixed_pipelined<kFastPF, true>), dim3(grid), dim3(kBlockThreads), 0, s, a);
+        return hipGetLastError();
+    }
+    switch (v) {
+        case 2: hipLaunchKernelGGL((k_units_fixed<4, false>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_fixed_pipelined<4, false>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_fixed_pipelined<8, true>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((k_fixed_pipelined<2, true>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_units_fixed<4, true>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
+    }
     return hipGetLastError();
 }
 
@@ -589,7 +698,7 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n_bytes, uint64_t seed, u
 }
 
 hipError_t launch_stream_probe(const uint8_t* src, uint64_t n_bytes, uint32_t* out, int grid_blocks, hipStream_t s) {
-    hipLaunchKernelGGL(k_stream_probe, dim3(grid_blocks), dim3(1024), 0, s, src, n_bytes, out);
+    hipLaunchKernelGGL(k_stream_probe, dim3(grid_blocks), dim3(256), 0, s, src, n_bytes, out);
     return hipGetLastError();
 }
 

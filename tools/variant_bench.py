@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""A/B the streaming-kernel variants (KARMA_CRC_VARIANT) in ONE process, interleaved rounds.
+
+    python tools/variant_bench.py [variants...]
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import karma_amd as K  # noqa: E402
+
+variants = [int(v) for v in sys.argv[1:]] or [0, 1, 2, 3, 4, 5]
+dev = torch.device("cuda:0")
+n, rec = 1 << 20, 4096
+buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
+K.fill_splitmix64(buf, 42)
+out = torch.empty(n, dtype=torch.uint32, device=dev)
+ref = None
+res = {v: [] for v in variants}
+for rnd in range(6):
+    for v in variants:
+        os.environ["KARMA_CRC_VARIANT"] = str(v)
+        for _ in range(2):
+            K.value_batch_fixed(buf, rec, out=out)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(10):
+            K.value_batch_fixed(buf, rec, out=out)
+        b.record()
+        torch.cuda.synchronize()
+        res[v].append(a.elapsed_time(b) / 10)
+        got = out.cpu().numpy()
+        if ref is None:
+            ref = got.copy()
+        assert np.array_equal(got, ref), f"variant {v} differs"
+for v in variants:
+    ms = np.array(res[v])
+    print(f"variant {v}: median {np.median(ms):.4f} ms  min {ms.min():.4f}  -> {n * rec / np.median(ms) / 1e6:.1f} GB/s")
+pr = torch.zeros(1, dtype=torch.uint32, device=dev)
+for _ in range(3):
+    K.stream_probe(buf, pr)
+torch.cuda.synchronize()
+ts = []
+for _ in range(5):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(10):
+        K.stream_probe(buf, pr)
+    b.record()
+    torch.cuda.synchronize()
+    ts.append(a.elapsed_time(b) / 10)
+print(f"read probe (nt slab): median {np.median(ts):.4f} ms -> {n * rec / np.median(ts) / 1e6:.1f} GB/s")
