@@ -309,8 +309,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
 // while the current unit's fold/tree epilogue runs.  Units of a wave have
 // the same length, so the epilogue (with its cross-lane shuffles) is
 // wave-uniform.
-template <int PF, bool NT>
-__global__ __launch_bounds__(kBlockThreads) void k_fixed_pipelined(FixedArgs A) {
+template <int PF, bool NT, int THREADS, bool SLAB>
+__global__ __launch_bounds__(THREADS) void k_fixed_pipelined(FixedArgs A) {
+    constexpr int WPB = THREADS / 64;  // waves per block
     __shared__ uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
     __syncthreads();
@@ -322,14 +323,26 @@ __global__ __launch_bounds__(kBlockThreads) void k_fixed_pipelined(FixedArgs A) 
     const uint64_t U = A.n_rec * k;
     const uint64_t ub = A.unit_bytes;
     const uint64_t C = ub / kChunk;  // chunks per unit, multiple of PF
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t wb0 = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
+    const uint64_t wid = (uint64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
     const uint64_t nbt = (U + kGroupsPerWave - 1) / kGroupsPerWave;  // unit batches of 8
-    if (wb0 >= nbt) return;  // whole wave idle; no barrier follows
-    const uint64_t nb = (nbt - wb0 + nwaves - 1) / nwaves;
+    // batch b of this wave is global batch  first + b * step: grid-strided
+    // (step = nwaves) or one contiguous slab per wave (step = 1)
+    uint64_t first, nb, step;
+    if (SLAB) {
+        const uint64_t per = nbt / nwaves, extra = nbt % nwaves;
+        first = wid * per + (wid < extra ? wid : extra);
+        nb = per + (wid < extra ? 1 : 0);
+        step = 1;
+    } else {
+        first = wid;
+        nb = wid < nbt ? (nbt - wid + nwaves - 1) / nwaves : 0;
+        step = nwaves;
+    }
+    if (nb == 0) return;  // whole wave idle; no barrier follows
     const uint8_t* lane_base = A.arena + 16 * l;
     auto unit_of = [&](uint64_t b) -> uint64_t {
-        const uint64_t u = (wb0 + b * nwaves) * kGroupsPerWave + grp;
+        const uint64_t u = (first + b * step) * kGroupsPerWave + grp;
         return u < U ? u : U - 1;  // idle groups re-read a valid unit, results dropped
     };
     u32x4 ring[PF];
@@ -338,7 +351,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_fixed_pipelined(FixedArgs A) 
 #pragma unroll
     for (int q = 0; q < PF; ++q) ring[q] = ldg<NT>(lptr + q * kChunk);
     for (uint64_t b = 0; b < nb; ++b) {
-        const uint64_t u = (wb0 + b * nwaves) * kGroupsPerWave + grp;
+        const uint64_t u = (first + b * step) * kGroupsPerWave + grp;
         const bool valid = u < U;
         uint64_t r = u, j = 0;
         if (k != 1) {
@@ -381,6 +394,130 @@ __global__ __launch_bounds__(kBlockThreads) void k_fixed_pipelined(FixedArgs A) 
                 A.out[u] = ~cfold;
             else
                 A.partial[u] = cfold;
+        }
+    }
+}
+
+// Same walk with NS units per group processed side by side (NS independent
+// accumulator sets per lane: more LDS chains in flight per wave at the same
+// occupancy) and XOR3-folded lookups.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+__device__ __forceinline__ uint32_t stride_step3(const uint32_t* lds, uint32_t X, uint32_t acc, uint32_t w) {
+    const uint32_t i0 = __builtin_amdgcn_perm(X, acc, kSel0);
+    const uint32_t i1 = __builtin_amdgcn_perm(X, acc, kSel1);
+    const uint32_t i2 = __builtin_amdgcn_perm(X, acc, kSel2);
+    const uint32_t i3 = __builtin_amdgcn_perm(X, acc, kSel3);
+    const uint32_t t0 = lds_at_byte(lds, i0), t1 = lds_at_byte(lds, i1);
+    const uint32_t t2 = lds_at_byte(lds, i2), t3 = lds_at_byte(lds, i3);
+    return xor3(xor3(t0, t1, w), t2, t3);
+}
+
+template <int PF, int NS, int THREADS, bool X3>
+__global__ __launch_bounds__(THREADS) void k_fixed_multi(FixedArgs A) {
+    constexpr int WPB = THREADS / 64;
+    __shared__ uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const uint64_t k = A.units_per_rec;
+    const uint64_t U = A.n_rec * k;
+    const uint64_t ub = A.unit_bytes;
+    const uint64_t C = ub / kChunk;
+    const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
+    const uint64_t wid = (uint64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+    const uint64_t nbt = (U + kGroupsPerWave - 1) / kGroupsPerWave;
+    const uint64_t nb = wid < nbt ? (nbt - wid + nwaves - 1) / nwaves : 0;  // batches of this wave
+    if (nb == 0) return;
+    const uint64_t np = (nb + NS - 1) / NS;  // steps of NS batches
+    const uint8_t* lane_base = A.arena + 16 * l;
+    auto unit_of = [&](uint64_t b) -> uint64_t {
+        const uint64_t bb = b < nb ? b : nb - 1;
+        const uint64_t u = (wid + bb * nwaves) * kGroupsPerWave + grp;
+        return u < U ? u : U - 1;
+    };
+    u32x4 ring[NS][PF];
+    const uint8_t* lptr[NS];
+    uint64_t lp = 0, lc = PF;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        lptr[t] = lane_base + unit_of(t) * ub;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) ring[t][q] = ldg<true>(lptr[t] + q * kChunk);
+    }
+    for (uint64_t p = 0; p < np; ++p) {
+        uint32_t acc[NS][4];
+        uint32_t inj[NS];
+        uint64_t uu[NS];
+        bool valid[NS];
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            const uint64_t b = p * NS + t;
+            const uint64_t u = (wid + b * nwaves) * kGroupsPerWave + grp;
+            valid[t] = b < nb && u < U;
+            uu[t] = u;
+            uint64_t r = u, j = 0;
+            if (k != 1) {
+                r = u / k;
+                j = u - r * k;
+            }
+            inj[t] = (valid[t] && j == 0 && l == 0) ? ~(A.init ? A.init[r] : A.init_scalar) : 0u;
+            acc[t][0] = acc[t][1] = acc[t][2] = acc[t][3] = 0;
+        }
+        for (uint64_t c = 0; c < C; c += PF) {
+            if (lc == C) {
+                lc = 0;
+                ++lp;
+#pragma unroll
+                for (int t = 0; t < NS; ++t) lptr[t] = lane_base + unit_of(lp * NS + t) * ub;
+            }
+#pragma unroll
+            for (int q = 0; q < PF; ++q) {
+#pragma unroll
+                for (int t = 0; t < NS; ++t) {
+                    u32x4 v = ring[t][q];
+                    ring[t][q] = ldg<true>(lptr[t] + (lc + q) * kChunk);
+                    if (q == 0) {
+                        v.x ^= inj[t];
+                        inj[t] = 0;
+                    }
+                    if (X3) {
+                        acc[t][0] = stride_step3(lds, X, acc[t][0], v.x);
+                        acc[t][1] = stride_step3(lds, X, acc[t][1], v.y);
+                        acc[t][2] = stride_step3(lds, X, acc[t][2], v.z);
+                        acc[t][3] = stride_step3(lds, X, acc[t][3], v.w);
+                    } else {
+                        step4(lds, X, acc[t][0], acc[t][1], acc[t][2], acc[t][3], v);
+                    }
+                }
+            }
+            lc += PF;
+        }
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            uint32_t cf = zmap(lds, kLZ4, acc[t][0]);
+            cf = zmap(lds, kLZ4, cf ^ acc[t][1]);
+            cf = zmap(lds, kLZ4, cf ^ acc[t][2]);
+            cf = zmap(lds, kLZ4, cf ^ acc[t][3]);
+            uint32_t s1 = __shfl_down(cf, 1, kGroupLanes);
+            cf = zmap(lds, kLZ16, cf) ^ s1;
+            s1 = __shfl_down(cf, 2, kGroupLanes);
+            cf = zmap(lds, kLZ32, cf) ^ s1;
+            s1 = __shfl_down(cf, 4, kGroupLanes);
+            cf = zmap(lds, kLZ64, cf) ^ s1;
+            if (valid[t] && l == 0) {
+                if (k == 1)
+                    A.out[uu[t]] = ~cf;
+                else
+                    A.partial[uu[t]] = cf;
+            }
         }
     }
 }
@@ -644,15 +781,44 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     const uint64_t need = (units + kGroupsPerWave * kWavesPerBlock - 1) / (kGroupsPerWave * kWavesPerBlock);
     const int grid = (int)(need < (uint64_t)grid_blocks ? need : (uint64_t)grid_blocks);
     const int v = fixed_variant();
-    if (fixed_fast_path_ok(a) && v == 0) {
-        hipLaunchKernelGGL((k_fixed_pipelined<kFastPF, true>), dim3(grid), dim3(kBlockThreads), 0, s, a);
+    if (fixed_fast_path_ok(a) && (v == 0 || v >= 10)) {
+        const uint64_t ncu = (uint64_t)grid_blocks;
+#define KP(PF, T, SL)                                                                                             \
+    do {                                                                                                         \
+        const uint64_t nd = (units + (T / 64) * kGroupsPerWave - 1) / ((T / 64) * kGroupsPerWave);               \
+        hipLaunchKernelGGL((k_fixed_pipelined<PF, true, T, SL>), dim3((unsigned)(nd < ncu ? nd : ncu)), dim3(T), 0, \
+                           s, a);                                                                                \
+    } while (0)
+#define KM(PF, NS, T, X3)                                                                                        \
+    do {                                                                                                         \
+        const uint64_t nd = (units + (T / 64) * kGroupsPerWave - 1) / ((T / 64) * kGroupsPerWave);               \
+        hipLaunchKernelGGL((k_fixed_multi<PF, NS, T, X3>), dim3((unsigned)(nd < ncu ? nd : ncu)), dim3(T), 0, s, a); \
+    } while (0)
+        switch (v) {
+            case 10: KP(4, 1024, false); break;
+            case 11: KP(2, 1024, false); break;
+            case 12: KP(4, 512, false); break;
+            case 13: KP(8, 512, false); break;
+            case 14: KP(8, 256, false); break;
+            case 15: KP(4, 1024, true); break;
+            case 16: KP(4, 512, true); break;
+            case 17: KP(8, 256, true); break;
+            case 18: KP(2, 512, false); break;
+            case 20: KM(4, 1, 1024, true); break;
+            case 21: KM(4, 2, 1024, false); break;
+            case 22: KM(4, 2, 1024, true); break;
+            case 23: KM(2, 2, 1024, true); break;
+            case 24: KM(4, 2, 512, true); break;
+            case 25: KM(2, 2, 512, true); break;
+            case 26: KM(4, 1, 1024, false); break;
+            default: KP(4, 1024, false); break;
+        }
+#undef KP
+#undef KM
         return hipGetLastError();
     }
     switch (v) {
         case 2: hipLaunchKernelGGL((k_units_fixed<4, false>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
-        case 3: hipLaunchKernelGGL((k_fixed_pipelined<4, false>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_fixed_pipelined<8, true>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((k_fixed_pipelined<2, true>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
         default: hipLaunchKernelGGL((k_units_fixed<4, true>), dim3(grid), dim3(kBlockThreads), 0, s, a); break;
     }
     return hipGetLastError();

@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import karma_amd as K  # noqa: E402
 
-variants = [int(v) for v in sys.argv[1:]] or [0, 1, 2, 3, 4, 5]
+variants = [int(v) for v in sys.argv[1:]] or [10, 11, 12, 13, 14, 15, 16, 17, 18, 1]
 dev = torch.device("cuda:0")
 n, rec = 1 << 20, 4096
 buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
@@ -20,7 +20,7 @@ K.fill_splitmix64(buf, 42)
 out = torch.empty(n, dtype=torch.uint32, device=dev)
 ref = None
 res = {v: [] for v in variants}
-for rnd in range(6):
+for rnd in range(int(os.environ.get('ROUNDS', '8'))):
     for v in variants:
         os.environ["KARMA_CRC_VARIANT"] = str(v)
         for _ in range(2):
@@ -39,7 +39,8 @@ for rnd in range(6):
         assert np.array_equal(got, ref), f"variant {v} differs"
 for v in variants:
     ms = np.array(res[v])
-    print(f"variant {v}: median {np.median(ms):.4f} ms  min {ms.min():.4f}  -> {n * rec / np.median(ms) / 1e6:.1f} GB/s")
+    print(f"variant {v}: median {np.median(ms):.4f} ms  min {ms.min():.4f}  -> {n * rec / np.median(ms) / 1e6:.1f} GB/s"
+          f"  (best {n * rec / ms.min() / 1e6:.1f})  rounds {' '.join(f'{x:.3f}' for x in ms)}")
 pr = torch.zeros(1, dtype=torch.uint32, device=dev)
 for _ in range(3):
     K.stream_probe(buf, pr)
