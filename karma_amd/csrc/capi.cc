@@ -191,7 +191,7 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     L.base_off = 0;
     L.sums_off = align256((n_rec + 1) * sizeof(uint64_t));
     L.rec_off = L.sums_off + align256(ragged_scan_blocks(n_rec) * sizeof(uint64_t));
-    L.part_off = L.rec_off + align256(cap * sizeof(uint64_t));
+    L.part_off = L.rec_off + align256(cap * sizeof(UnitDesc));
     L.total = L.part_off + align256(cap * sizeof(uint32_t));
     return L;
 }
@@ -200,7 +200,7 @@ void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
     char* b = static_cast<char*>(ws);
     a.unit_base = reinterpret_cast<uint64_t*>(b + L.base_off);
     a.block_sums = reinterpret_cast<uint64_t*>(b + L.sums_off);
-    a.unit_rec = reinterpret_cast<uint64_t*>(b + L.rec_off);
+    a.desc = reinterpret_cast<UnitDesc*>(b + L.rec_off);
     a.partial = reinterpret_cast<uint32_t*>(b + L.part_off);
     a.unit_cap = cap;
 }

@@ -1,0 +1,269 @@
+// karma_amd/csrc/crc_device.h -- device-side building blocks shared by the
+// gfx950 kernels (crc_fixed.hip, crc_ragged.hip).
+//
+// Notation: R(X) is the CRC register of karma-util/crc32c.cc
+// after byte X (`l`, crc32c.cc:283), Z_d the linear map "advance the register
+// over d zero bytes" (gf2.h).  A 4-byte word step is R <- Z_4(R ^ w)
+// (crc32c.cc:293-299 with a 4-byte stride); a byte step is STEP1
+// (crc32c.cc:286-290).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "engine.h"
+
+namespace karma {
+namespace engine {
+namespace dev {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+
+// ---- LDS image of the streaming kernels ------------------------------------
+// [0, 128 KiB): the Z_S slicing tables, bank-replicated.  Byte address of
+//   table k, entry e, for lane L:  (k>>1)<<16 | e<<8 | (k&1)<<7 | (L&31)<<2
+// so one v_perm_b32 builds it from the register (entry = byte k) and a
+// per-lane constant, and the 32 lanes of each ds_read_b32 half-wave hit 32
+// distinct banks (no conflicts on random data).
+// [128 KiB, +17 KiB): Z4, Z16, Z32, Z64 slicing tables and the byte table.
+constexpr int kRepWords = 32768;
+constexpr int kSmallBase = kRepWords;
+constexpr int kSmallWords = kBlobWords - 1024;
+constexpr int kLdsWords = kRepWords + kSmallWords;  // 148,480 bytes
+constexpr int kLZ4 = kSmallBase + (kBlobZ4 - 1024);
+constexpr int kLZ16 = kSmallBase + (kBlobZ16 - 1024);
+constexpr int kLZ32 = kSmallBase + (kBlobZ32 - 1024);
+constexpr int kLZ64 = kSmallBase + (kBlobZ64 - 1024);
+constexpr int kLT8 = kSmallBase + (kBlobT8 - 1024);
+
+constexpr uint32_t kSel0 = 0x0c0c0004u;  // {X.b0, acc.b0, 0, 0}
+constexpr uint32_t kSel1 = 0x0c0c0105u;  // {X.b1, acc.b1, 0, 0}
+constexpr uint32_t kSel2 = 0x0c070204u;  // {X.b0, acc.b2, X.b3, 0}
+constexpr uint32_t kSel3 = 0x0c070305u;  // {X.b1, acc.b3, X.b3, 0}
+
+__device__ __forceinline__ uint32_t lds_at_byte(const uint32_t* lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(lds) + byte_addr);
+}
+
+// acc <- Z_S(acc) ^ w through the replicated tables (S = kChunk = 128 bytes).
+__device__ __forceinline__ uint32_t stride_step(const uint32_t* lds, uint32_t X, uint32_t acc, uint32_t w) {
+    const uint32_t i0 = __builtin_amdgcn_perm(X, acc, kSel0);
+    const uint32_t i1 = __builtin_amdgcn_perm(X, acc, kSel1);
+    const uint32_t i2 = __builtin_amdgcn_perm(X, acc, kSel2);
+    const uint32_t i3 = __builtin_amdgcn_perm(X, acc, kSel3);
+    return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
+}
+
+// Z(x) for a map stored as four plain 256-entry tables at word `base`.
+__device__ __forceinline__ uint32_t zmap(const uint32_t* lds, int base, uint32_t x) {
+    return lds[base + (x & 255u)] ^ lds[base + 256 + ((x >> 8) & 255u)] ^ lds[base + 512 + ((x >> 16) & 255u)] ^
+           lds[base + 768 + (x >> 24)];
+}
+
+// One data byte (STEP1).
+__device__ __forceinline__ uint32_t byte_step(const uint32_t* lds, int t8, uint32_t r, uint32_t b) {
+    return lds[t8 + ((r ^ b) & 255u)] ^ (r >> 8);
+}
+
+// Record bytes live in device global memory: loads go through address space 1
+// so hipcc emits global_load_dwordx4 (vmcnt only) instead of flat loads, whose
+// lgkmcnt share would serialise them against the LDS lookups.  NT = the
+// non-temporal policy (bytes are read exactly once).
+template <bool NT>
+__device__ __forceinline__ u32x4 ldg(const uint8_t* p) {
+    if constexpr (NT) return __builtin_nontemporal_load((gu32x4*)(p));
+    return *(gu32x4*)(p);
+}
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) { return *(gu32x4*)(p); }
+
+__device__ __forceinline__ const uint8_t* pmin(const uint8_t* a, const uint8_t* b) { return a < b ? a : b; }
+__device__ __forceinline__ const uint8_t* pmax(const uint8_t* a, const uint8_t* b) { return a > b ? a : b; }
+__device__ __forceinline__ const uint8_t* floor16(const uint8_t* p) {
+    return reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+}
+__device__ __forceinline__ const uint8_t* ceil16(const uint8_t* p) {
+    return reinterpret_cast<const uint8_t*>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
+}
+
+// Register after bytes [from, to) of the aligned 16-byte block `blk`
+// (0 <= from <= to <= 16): whole aligned words through Z4 (one LDS round trip
+// per word), the rest byte by byte.
+__device__ __forceinline__ uint32_t steps_in_block(const uint32_t* lds, int z4, int t8, uint32_t r, const uint8_t* blk,
+                                                   uint32_t from, uint32_t to) {
+    if (from >= to) return r;
+    const u32x4 v = ld16(blk);
+    // 128-bit shift register of the block, consumed from byte 0 upwards
+    uint64_t lo = v.x | ((uint64_t)v.y << 32), hi = v.z | ((uint64_t)v.w << 32);
+    uint32_t i = 0;
+    for (; i < to; ++i) {  // leading bytes until `from` is reached and 4-aligned
+        if (i >= from && (i & 3u) == 0 && i + 4 <= to) break;
+        if (i >= from) r = byte_step(lds, t8, r, (uint32_t)lo & 255u);
+        lo = (lo >> 8) | (hi << 56);
+        hi >>= 8;
+    }
+    for (; i + 4 <= to; i += 4) {  // whole words
+        r = zmap(lds, z4, r ^ (uint32_t)lo);
+        lo = (lo >> 32) | (hi << 32);
+        hi >>= 32;
+    }
+    for (; i < to; ++i) {  // trailing bytes
+        r = byte_step(lds, t8, r, (uint32_t)lo & 255u);
+        lo = (lo >> 8) | (hi << 56);
+        hi >>= 8;
+    }
+    return r;
+}
+
+// A whole record step by step (records with no aligned 16-byte block inside).
+__device__ __forceinline__ uint32_t short_record(const uint32_t* lds, int z4, int t8, const uint8_t* p, uint64_t n,
+                                                 uint32_t init) {
+    uint32_t r = ~init;
+    const uint8_t* e = p + n;
+    const uint8_t* q = p;
+    while (q < e) {
+        const uint8_t* blk = floor16(q);
+        const uint32_t to = (uint32_t)((e - blk) < 16 ? (e - blk) : 16);
+        r = steps_in_block(lds, z4, t8, r, blk, (uint32_t)(q - blk), to);
+        q = blk + 16;
+    }
+    return ~r;
+}
+
+struct Geom {
+    const uint8_t* a;  // first aligned body byte
+    const uint8_t* b;  // end of the aligned body
+    const uint8_t* e;  // record end
+    bool is_short;     // no aligned 16-byte block inside (includes n == 0)
+};
+
+__device__ __forceinline__ Geom geom(const uint8_t* p, uint64_t n) {
+    Geom g;
+    g.e = p + n;
+    g.a = ceil16(p);
+    g.b = floor16(g.e);
+    g.is_short = (g.b - g.a) < 16;
+    return g;
+}
+
+// Register entering the body: ~init advanced over the unaligned head [p, a).
+__device__ __forceinline__ uint32_t head_register(const uint32_t* lds, int z4, int t8, const uint8_t* p, const Geom& g,
+                                                  uint32_t init) {
+    uint32_t h = ~init;
+    if (p < g.a) h = steps_in_block(lds, z4, t8, h, g.a - 16, (uint32_t)(p - (g.a - 16)), 16u);
+    return h;
+}
+
+// Register after the unaligned tail [b, e) given the register at b.
+__device__ __forceinline__ uint32_t tail_register(const uint32_t* lds, int z4, int t8, uint32_t r, const Geom& g) {
+    if (g.e > g.b) r = steps_in_block(lds, z4, t8, r, g.b, 0u, (uint32_t)(g.e - g.b));
+    return r;
+}
+
+__device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
+                                      uint32_t& a3, const u32x4& v) {
+    a0 = stride_step(lds, X, a0, v.x);
+    a1 = stride_step(lds, X, a1, v.y);
+    a2 = stride_step(lds, X, a2, v.z);
+    a3 = stride_step(lds, X, a3, v.w);
+}
+
+// Register contribution of the 16-aligned span [us, ue): 128-byte chunks
+// end-aligned to ue, 8 lanes per group, lane l owns bytes [16l, 16l+16) of
+// every chunk as four word slots; `inj` is xored into the word at `inj_at`
+// (the body's first word carries the record's entering register).  PF chunk
+// loads stay in flight per lane.  Every lane of the wave must call this (it
+// ends in cross-lane shuffles); the result is valid in group lane 0.
+template <int PF, bool NT>
+__device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, uint32_t l, const uint8_t* us,
+                                               const uint8_t* ue, const uint8_t* inj_at, uint32_t inj) {
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    const int64_t span = ue - us;
+    if (span > 0) {
+        const int64_t nch = (span + kChunk - 1) / kChunk;
+        const uint8_t* w = ue - nch * kChunk + 16 * l;
+        {
+            u32x4 v = (w >= us) ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
+            if (w == inj_at) v.x ^= inj;
+            a0 = v.x;
+            a1 = v.y;
+            a2 = v.z;
+            a3 = v.w;
+        }
+        int64_t rem = nch - 1;
+        w += kChunk;
+        // Window of the last chunk: prefetches past the end re-read it.  Chunks
+        // after chunk 0 are always full; with a single (possibly partial) chunk
+        // fall back to the unit's last 16 bytes so no load leaves [us, ue).
+        const uint8_t* last = ue - kChunk + 16 * l;
+        if (last < us) last = ue - 16;
+        u32x4 nb[PF];
+#pragma unroll
+        for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, last));
+        while (rem >= PF) {
+            u32x4 cur[PF];
+#pragma unroll
+            for (int q = 0; q < PF; ++q) cur[q] = nb[q];
+            w += PF * kChunk;
+#pragma unroll
+            for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, last));
+#pragma unroll
+            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+            rem -= PF;
+        }
+#pragma unroll
+        for (int q = 0; q < PF - 1; ++q)
+            if (rem > q) step4(lds, X, a0, a1, a2, a3, nb[q]);
+    }
+    // lane fold (crc32c.cc STEP4W order): c = Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0))))
+    uint32_t c = zmap(lds, kLZ4, a0);
+    c = zmap(lds, kLZ4, c ^ a1);
+    c = zmap(lds, kLZ4, c ^ a2);
+    c = zmap(lds, kLZ4, c ^ a3);
+    // group tree over 8 lanes: v_l = Z_{16*2^d}(v_l) ^ v_{l+2^d}
+    uint32_t t = __shfl_down(c, 1, kGroupLanes);
+    c = zmap(lds, kLZ16, c) ^ t;
+    t = __shfl_down(c, 2, kGroupLanes);
+    c = zmap(lds, kLZ32, c) ^ t;
+    t = __shfl_down(c, 4, kGroupLanes);
+    c = zmap(lds, kLZ64, c) ^ t;
+    return c;
+}
+
+__device__ __forceinline__ void load_stream_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
+    for (int i = threadIdx.x; i < kSmallWords; i += blockDim.x) lds[kSmallBase + i] = blob[1024 + i];
+    // word index = region*16384 + row*64 + half*32 + lane32; table k = region*2 + half
+    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
+    for (int i = threadIdx.x; i < kRepWords / 4; i += blockDim.x) {
+        const int idx = i * 4;
+        const int region = idx >> 14, row = (idx >> 6) & 255, half = (idx >> 5) & 1;
+        const uint32_t v = blob[kBlobStride + (region * 2 + half) * 256 + row];
+        l4[i] = u32x4{v, v, v, v};
+    }
+}
+
+// Per-lane constant of the replicated-table address (see the LDS image above).
+__device__ __forceinline__ uint32_t lane_const() {
+    const uint32_t l32 = threadIdx.x & 31u;
+    return (l32 * 4u) | ((128u + l32 * 4u) << 8) | (1u << 24);
+}
+
+// ---- combine-blob LDS image: Z_{D*2^k} (k = 0..6), Z4, byte table ----------
+__device__ __forceinline__ void load_comb_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
+    for (int i = threadIdx.x; i < kCombWords; i += blockDim.x) lds[i] = blob[i];
+}
+
+// Tree over the 64 lanes of a wave with maps Z_{D*2^d}: lane 0 gets
+// XOR_l Z_{D*(63-l)}(v_l).
+__device__ __forceinline__ uint32_t wave_tree(const uint32_t* lds, uint32_t v) {
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        const uint32_t t = __shfl_down(v, 1u << d, 64);
+        v = zmap(lds, d * 1024, v) ^ t;
+    }
+    return v;
+}
+
+}  // namespace dev
+}  // namespace engine
+}  // namespace karma

@@ -28,9 +28,11 @@ constexpr int kBlobT8 = 5120;      // byte table (one zero byte, low byte index)
 constexpr int kBlobWords = 5376;
 
 // ---- table blob of the combine kernels --------------------------------------
-// maps Z_{D * 2^k}, k = 0..6 (k = 6 is the Horner step of 64 states), then T8.
+// maps Z_{D * 2^k}, k = 0..6 (k = 6 is the Horner step of 64 states), then Z4
+// and the byte table (head/tail steps).
 constexpr int kCombMaps = 7;
-constexpr int kCombT8 = kCombMaps * 1024;
+constexpr int kCombZ4 = kCombMaps * 1024;
+constexpr int kCombT8 = kCombZ4 + 1024;
 constexpr int kCombWords = kCombT8 + 256;
 
 // Host builders (gf2.h): fill a blob for stride kChunk / for unit size D.
@@ -50,6 +52,16 @@ struct FixedArgs {
     const uint32_t* blob;      // kBlobWords, device
 };
 
+// One unit of a ragged batch: the 16-aligned span [us, us + span) of a record
+// body and the value xored into its first word (the record's entering
+// register for the record's first unit, 0 otherwise).
+struct UnitDesc {
+    uint64_t us;
+    uint32_t span;
+    uint32_t inj;
+};
+static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
+
 struct RaggedArgs {
     const uint8_t* arena;
     const uint64_t* off;       // payload offset per record
@@ -59,12 +71,12 @@ struct RaggedArgs {
     uint32_t init_scalar;
     uint64_t unit_bytes;
     uint64_t* unit_base;       // n_rec + 1 entries: exclusive scan of units per record
-    uint64_t* unit_rec;        // unit -> record (unit_cap entries)
-    uint64_t unit_cap;         // capacity of unit_rec / partial
+    UnitDesc* desc;            // unit_cap entries, record order
+    uint64_t unit_cap;         // capacity of desc / partial
     uint64_t* block_sums;      // scan scratch
     uint32_t* out;
-    uint32_t* partial;
-    const uint32_t* blob;
+    uint32_t* partial;         // register contribution per unit
+    const uint32_t* blob;      // stream blob (kBlobWords)
     const uint32_t* comb_blob; // kCombWords for unit_bytes
 };
 

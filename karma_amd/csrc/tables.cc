@@ -22,6 +22,7 @@ void build_combine_blob(uint64_t unit_bytes, uint32_t* out) {
         gf2::slicing_tables(m, out + k * 1024);
         m = Map::compose(m, m);  // Z_{D*2^(k+1)}
     }
+    gf2::slicing_tables(Map::zero_bytes(4), out + kCombZ4);
     gf2::byte_table(out + kCombT8);
 }
 
