@@ -183,24 +183,29 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 
 // ---- ragged records -------------------------------------------------------
 struct RaggedLayout {
-    size_t base_off, sums_off, rec_off, part_off, total;
+    size_t fbase_off, pslot_off, sums_off, bucket_off, desc_off, part_off, total;
 };
 
 RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     RaggedLayout L;
-    L.base_off = 0;
-    L.sums_off = align256((n_rec + 1) * sizeof(uint64_t));
-    L.rec_off = L.sums_off + align256(ragged_scan_blocks(n_rec) * sizeof(uint64_t));
-    L.part_off = L.rec_off + align256(cap * sizeof(UnitDesc));
+    const uint64_t nb = ragged_scan_blocks(n_rec);
+    L.fbase_off = 0;
+    L.pslot_off = align256((n_rec + 2) * sizeof(uint64_t));
+    L.sums_off = L.pslot_off + align256(n_rec * sizeof(uint64_t));
+    L.bucket_off = L.sums_off + align256(nb * sizeof(uint64_t));
+    L.desc_off = L.bucket_off + align256(nb * kBuckets * sizeof(uint64_t));
+    L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
     L.total = L.part_off + align256(cap * sizeof(uint32_t));
     return L;
 }
 
 void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
     char* b = static_cast<char*>(ws);
-    a.unit_base = reinterpret_cast<uint64_t*>(b + L.base_off);
+    a.fbase = reinterpret_cast<uint64_t*>(b + L.fbase_off);
+    a.pslot = reinterpret_cast<uint64_t*>(b + L.pslot_off);
     a.block_sums = reinterpret_cast<uint64_t*>(b + L.sums_off);
-    a.desc = reinterpret_cast<UnitDesc*>(b + L.rec_off);
+    a.bucket_off = reinterpret_cast<uint64_t*>(b + L.bucket_off);
+    a.desc = reinterpret_cast<UnitDesc*>(b + L.desc_off);
     a.partial = reinterpret_cast<uint32_t*>(b + L.part_off);
     a.unit_cap = cap;
 }
@@ -235,7 +240,7 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         bind_ragged(a, ws, L, cap);
         KARMA_HIP(launch_ragged_scan(a, s));
         uint64_t units = 0;
-        KARMA_HIP(hipMemcpyAsync(&units, a.unit_base + n_rec, sizeof(units), hipMemcpyDeviceToHost, s));
+        KARMA_HIP(hipMemcpyAsync(&units, a.fbase + n_rec, sizeof(units), hipMemcpyDeviceToHost, s));
         KARMA_HIP(hipStreamSynchronize(s));
         cap = std::max<uint64_t>(units, 1);
         L = ragged_layout(n_rec, cap);

@@ -6,11 +6,14 @@
 // body end) so every group of 8 lanes gets at most one unit's worth of work
 // regardless of how skewed the record sizes are:
 //
-//   k_ragged_scan1/2   units per record -> exclusive scan (unit_base)
+//   k_ragged_scan1/2   full units per record -> exclusive scan (record order);
+//                      partial first units -> buckets by chunk count, longest
+//                      first, after all full units
 //   k_ragged_desc      one thread per record: entering register over the
 //                      unaligned head (crc32c.cc:323-329 analogue) and one
 //                      16-byte descriptor {span start, span length, inj} per unit
-//   k_units_ragged     the streaming kernel over the descriptor list
+//   k_units_ragged     the streaming kernel over the descriptor list: every
+//                      wave streams 8 units of (nearly) equal length
 //   k_ragged_finalize  one lane per record: Horner fold of its unit
 //                      contributions with Z_unit, unaligned tail bytes, ~R;
 //                      records with > 64 units are folded by the whole wave
@@ -28,10 +31,34 @@ using namespace dev;
 constexpr int kRaggedPF = 4;
 constexpr bool kRaggedNT = true;
 
-__device__ __forceinline__ uint64_t units_of(const Geom& g, uint64_t umax) {
-    if (g.is_short) return 1;
-    const uint64_t body = (uint64_t)(g.b - g.a);
-    return (body + umax - 1) / umax;
+constexpr int kScanBlock = 1024;
+
+// Unit layout of one record (units end-aligned to the aligned body end b):
+// unit 0 = [a, a + span0) (span0 in (0, unit]), unit j >= 1 = a + span0 + (j-1)*unit.
+// Unit 0 is "partial" when span0 < unit; every other unit is full.
+struct RecUnits {
+    Geom g;
+    uint64_t k;      // units (0 for short records: finalize does them alone)
+    uint64_t full;   // full units
+    uint32_t part;   // 1 if unit 0 is partial
+    uint32_t span0;  // bytes of unit 0
+    uint32_t c0;     // chunks of unit 0 (bucket of a partial unit)
+};
+
+__device__ __forceinline__ RecUnits rec_units(const RaggedArgs& A, uint64_t r) {
+    RecUnits u;
+    u.g = geom(A.arena + A.off[r], A.len[r]);
+    u.k = u.full = 0;
+    u.part = u.span0 = u.c0 = 0;
+    if (!u.g.is_short) {
+        const uint64_t body = (uint64_t)(u.g.b - u.g.a);
+        u.k = (body + A.unit_bytes - 1) / A.unit_bytes;
+        u.span0 = (uint32_t)(body - (u.k - 1) * A.unit_bytes);
+        u.part = u.span0 < A.unit_bytes ? 1u : 0u;
+        u.full = u.k - u.part;
+        u.c0 = (u.span0 + kChunk - 1) / kChunk;
+    }
+    return u;
 }
 
 // Inclusive wave scan of 64-bit values.
@@ -63,17 +90,28 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
     return pre + inc - v;
 }
 
-__global__ __launch_bounds__(1024) void k_ragged_scan1(RaggedArgs A) {
+// Per scan block: exclusive scan of full units, histogram of partial units by chunk count.
+__global__ __launch_bounds__(kScanBlock) void k_ragged_scan1(RaggedArgs A) {
     __shared__ uint64_t sm[16];
+    __shared__ uint32_t hist[kBuckets];
+    if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t cnt = r < A.n_rec ? units_of(geom(A.arena + A.off[r], A.len[r]), A.unit_bytes) : 0;
+    RecUnits u{};
+    if (r < A.n_rec) u = rec_units(A, r);
     uint64_t total;
-    const uint64_t ex = block_excl_scan(cnt, sm, total);
-    if (r < A.n_rec) A.unit_base[r] = ex;
+    const uint64_t ex = block_excl_scan(r < A.n_rec ? u.full : 0, sm, total);  // has barriers
+    if (r < A.n_rec) {
+        A.fbase[r] = ex;
+        if (u.part) atomicAdd(&hist[u.c0], 1u);
+    }
+    __syncthreads();
     if (threadIdx.x == 0) A.block_sums[blockIdx.x] = total;
+    if (threadIdx.x < kBuckets) A.bucket_off[(uint64_t)blockIdx.x * kBuckets + threadIdx.x] = hist[threadIdx.x];
 }
 
-__global__ __launch_bounds__(1024) void k_ragged_scan2(RaggedArgs A, uint64_t nblocks) {
+// Single block: full-unit offsets per scan block (slots [0, F)), then the
+// partial buckets from the longest (31 chunks) down to 1 chunk (slots [F, U)).
+__global__ __launch_bounds__(kScanBlock) void k_ragged_scan2(RaggedArgs A, uint64_t nblocks) {
     __shared__ uint64_t sm[16];
     uint64_t carry = 0;
     for (uint64_t base = 0; base < nblocks; base += blockDim.x) {
@@ -84,31 +122,50 @@ __global__ __launch_bounds__(1024) void k_ragged_scan2(RaggedArgs A, uint64_t nb
         if (i < nblocks) A.block_sums[i] = carry + ex;
         carry += total;
     }
-    if (threadIdx.x == 0) A.unit_base[A.n_rec] = carry;
+    const uint64_t F = carry;
+    for (int c = kBuckets - 1; c >= 1; --c) {
+        for (uint64_t base = 0; base < nblocks; base += blockDim.x) {
+            const uint64_t i = base + threadIdx.x;
+            const uint64_t v = i < nblocks ? A.bucket_off[i * kBuckets + c] : 0;
+            uint64_t total;
+            const uint64_t ex = block_excl_scan(v, sm, total);
+            if (i < nblocks) A.bucket_off[i * kBuckets + c] = carry + ex;
+            carry += total;
+        }
+    }
+    if (threadIdx.x == 0) {
+        A.fbase[A.n_rec] = carry;  // total units
+        A.fbase[A.n_rec + 1] = F;
+    }
 }
 
-__global__ __launch_bounds__(256) void k_ragged_desc(RaggedArgs A) {
-    __shared__ uint32_t lds[kCombWords];
-    load_comb_tables(lds, A.comb_blob);
+// One thread per record (block b = scan block b): final slots, the entering
+// register over the unaligned head, and the unit descriptors.
+__global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
+    __shared__ uint32_t lds[kCombWords - kCombZ4];  // Z4 then the byte table
+    __shared__ unsigned long long cnt[kBuckets];
+    for (int i = threadIdx.x; i < kCombWords - kCombZ4; i += blockDim.x) lds[i] = A.comb_blob[kCombZ4 + i];
+    if (threadIdx.x < kBuckets) cnt[threadIdx.x] = A.bucket_off[(uint64_t)blockIdx.x * kBuckets + threadIdx.x];
     __syncthreads();
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= A.n_rec) return;
-    const uint64_t base = A.unit_base[r] + A.block_sums[r / 1024];
-    A.unit_base[r] = base;
+    const RecUnits u = rec_units(A, r);
+    const uint64_t fb = A.fbase[r] + A.block_sums[blockIdx.x];
+    A.fbase[r] = fb;
+    if (u.k == 0) return;
     const uint8_t* p = A.arena + A.off[r];
-    const Geom g = geom(p, A.len[r]);
-    const uint64_t k = units_of(g, A.unit_bytes);
-    if (g.is_short) {
-        if (base < A.unit_cap) A.desc[base] = UnitDesc{0, 0, 0};
-        return;
-    }
     const uint32_t init = A.init ? A.init[r] : A.init_scalar;
-    const uint32_t h = head_register(lds, kCombZ4, kCombT8, p, g, init);
-    for (uint64_t j = 0; j < k && base + j < A.unit_cap; ++j) {
-        const uint8_t* ue = g.b - (int64_t)((k - 1 - j) * A.unit_bytes);
-        const uint8_t* us = pmax(ue - (int64_t)A.unit_bytes, g.a);
-        A.desc[base + j] = UnitDesc{reinterpret_cast<uint64_t>(us), (uint32_t)(ue - us), j == 0 ? h : 0u};
+    const uint32_t h = head_register(lds, 0, 1024, p, u.g, init);
+    const uint64_t ub = A.unit_bytes;
+    const uint8_t* fstart = u.g.a + (u.part ? u.span0 : 0u);
+    if (u.part) {
+        const uint64_t slot = atomicAdd(&cnt[u.c0], 1ull);
+        A.pslot[r] = slot;
+        if (slot < A.unit_cap) A.desc[slot] = UnitDesc{reinterpret_cast<uint64_t>(u.g.a), u.span0, h};
     }
+    for (uint64_t i = 0; i < u.full && fb + i < A.unit_cap; ++i)
+        A.desc[fb + i] = UnitDesc{reinterpret_cast<uint64_t>(fstart + i * ub), (uint32_t)ub,
+                                  (!u.part && i == 0) ? h : 0u};
 }
 
 // Descriptor load through address space 1 (global_load_dwordx4, vmcnt only): a
@@ -126,7 +183,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     const uint32_t l = lane & (kGroupLanes - 1);
     const uint32_t grp = lane / kGroupLanes;
     const uint32_t X = lane_const();
-    const uint64_t U_all = A.unit_base[A.n_rec];
+    const uint64_t U_all = A.fbase[A.n_rec];
     const uint64_t U = U_all < A.unit_cap ? U_all : A.unit_cap;  // memory-safe if the caller's bound was low
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t step = nwaves * kGroupsPerWave;
@@ -144,7 +201,14 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_ragged_finalize(RaggedArgs A) {
+// State of unit j of a record whose full units start at slot fb.
+__device__ __forceinline__ uint64_t unit_slot(uint64_t j, uint64_t fb, uint64_t ps, uint32_t part) {
+    return j == 0 ? (part ? ps : fb) : fb + j - part;
+}
+
+// One lane per record: Horner fold of the unit contributions (Z_unit), the
+// unaligned tail, ~R.  Records of more than 64 units: the whole wave folds them.
+__global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     __shared__ uint32_t lds[kCombWords];
     load_comb_tables(lds, A.comb_blob);
     __syncthreads();
@@ -154,58 +218,61 @@ __global__ __launch_bounds__(256) void k_ragged_finalize(RaggedArgs A) {
          r0 += nwaves * 64) {
         const uint64_t r = r0 + lane;
         const bool valid = r < A.n_rec;
-        uint64_t b0 = 0, k = 0;
+        RecUnits u{};
+        uint64_t fb = 0, ps = 0;
+        uint32_t init = 0;
         const uint8_t* p = A.arena;
-        uint32_t n = 0, init = 0;
         if (valid) {
-            b0 = A.unit_base[r];
-            k = A.unit_base[r + 1] - b0;
-            p = A.arena + A.off[r];
-            n = A.len[r];
+            u = rec_units(A, r);
+            fb = A.fbase[r];
+            if (u.part) ps = A.pslot[r];
             init = A.init ? A.init[r] : A.init_scalar;
+            p = A.arena + A.off[r];
         }
-        const Geom g = geom(p, n);
-        const bool ok = valid && b0 + k <= A.unit_cap;
-        uint32_t acc = 0, res = 0;
+        const bool ok = valid && fb + u.full <= A.unit_cap && (!u.part || ps < A.unit_cap);
+        uint32_t acc = 0;
         bool huge = false;
-        if (ok && !g.is_short) {
-            if (k <= 64) {
-                // Horner over the unit contributions, 8 loads in flight at a time
-                for (uint64_t j = 0; j < k; j += 8) {
+        if (ok && u.k > 0) {
+            if (u.k <= 64) {
+                acc = A.partial[unit_slot(0, fb, ps, u.part)];
+                for (uint64_t j = 1; j < u.k; j += 8) {  // 8 loads in flight at a time
                     uint32_t s[8];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) s[q] = j + q < k ? A.partial[b0 + j + q] : 0u;
+                    for (int q = 0; q < 8; ++q) s[q] = j + q < u.k ? A.partial[fb + j + q - u.part] : 0u;
 #pragma unroll
                     for (int q = 0; q < 8; ++q)
-                        if (j + q < k) acc = zmap(lds, 0, acc) ^ s[q];
+                        if (j + q < u.k) acc = zmap(lds, 0, acc) ^ s[q];
                 }
             } else {
                 huge = true;
             }
         }
-        // records of more than 64 units: the whole wave folds them, one at a time
         uint64_t hm = __ballot(huge);
         while (hm) {
             const int h = __ffsll((long long)hm) - 1;
             hm &= hm - 1;
-            const uint64_t hb0 = __shfl(b0, h), hk = __shfl(k, h);
+            const uint64_t hk = __shfl(u.k, h), hfb = __shfl(fb, h), hps = __shfl(ps, h);
+            const uint32_t hpart = __shfl(u.part, h);
             const uint64_t nb = (hk + 63) / 64;
             const int64_t pad = (int64_t)(nb * 64 - hk);
             uint32_t w = 0;
             for (uint64_t blk = 0; blk < nb; ++blk) {
                 const int64_t idx = (int64_t)(blk * 64 + lane) - pad;
-                uint32_t v = idx >= 0 ? A.partial[hb0 + idx] : 0u;
+                uint32_t v = idx >= 0 ? A.partial[unit_slot((uint64_t)idx, hfb, hps, hpart)] : 0u;
                 v = wave_tree(lds, v);
                 w = zmap(lds, 6 * 1024, w) ^ v;
             }
             w = __shfl(w, 0);
             if ((int)lane == h) acc = w;
         }
-        if (ok) {
-            if (g.is_short)
-                res = short_record(lds, kCombZ4, kCombT8, p, n, init);
-            else
-                res = ~tail_register(lds, kCombZ4, kCombT8, acc, g);
+        if (valid) {
+            uint32_t res = 0;
+            if (ok) {
+                if (u.k == 0)
+                    res = short_record(lds, kCombZ4, kCombT8, p, A.len[r], init);
+                else
+                    res = ~tail_register(lds, kCombZ4, kCombT8, acc, u.g);
+            }
             A.out[r] = res;
         }
     }
@@ -213,23 +280,25 @@ __global__ __launch_bounds__(256) void k_ragged_finalize(RaggedArgs A) {
 
 }  // namespace
 
-uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + 1023) / 1024; }
+uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock - 1) / kScanBlock; }
 
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
-    hipLaunchKernelGGL(k_ragged_scan1, dim3((unsigned)nb), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_ragged_scan2, dim3(1), dim3(1024), 0, s, a, nb);
+    hipLaunchKernelGGL(k_ragged_scan1, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+    hipLaunchKernelGGL(k_ragged_scan2, dim3(1), dim3(kScanBlock), 0, s, a, nb);
     return hipGetLastError();
 }
 
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)((a.n_rec + 255) / 256)), dim3(256), 0, s, a);
+    const uint64_t nb = ragged_scan_blocks(a.n_rec);
+    hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     hipLaunchKernelGGL(k_units_ragged, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
-    uint64_t fblocks = (a.n_rec + 255) / 256;  // 4 waves x 64 records per block
-    if (fblocks > 8192) fblocks = 8192;
-    hipLaunchKernelGGL(k_ragged_finalize, dim3((unsigned)fblocks), dim3(256), 0, s, a);
+    uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
+    const uint64_t cap = 2 * (uint64_t)grid_blocks;
+    if (fblocks > cap) fblocks = cap;
+    hipLaunchKernelGGL(k_ragged_finalize, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

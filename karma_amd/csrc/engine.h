@@ -62,6 +62,13 @@ struct UnitDesc {
 };
 static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
 
+// Ragged batches order their units for balance: all full units
+// (span == unit_bytes) first, in record order, then every record's partial
+// first unit bucketed by chunk count, longest first, so the 8 units a wave
+// streams together have (nearly) equal length.
+constexpr int kBuckets = 33;  // chunk counts 1..32 of a partial unit (index = chunks)
+static_assert(kDefaultUnit / kChunk < kBuckets, "a partial unit has at most unit/kChunk chunks");
+
 struct RaggedArgs {
     const uint8_t* arena;
     const uint64_t* off;       // payload offset per record
@@ -69,13 +76,16 @@ struct RaggedArgs {
     uint64_t n_rec;
     const uint32_t* init;
     uint32_t init_scalar;
-    uint64_t unit_bytes;
-    uint64_t* unit_base;       // n_rec + 1 entries: exclusive scan of units per record
-    UnitDesc* desc;            // unit_cap entries, record order
+    uint64_t unit_bytes;       // kDefaultUnit
+    uint64_t* fbase;           // n_rec + 2: slot of the record's first full unit;
+                               //   [n_rec] = total units, [n_rec+1] = full units
+    uint64_t* pslot;           // n_rec: slot of the record's partial unit
+    uint64_t* block_sums;      // per scan block: full-unit offset
+    uint64_t* bucket_off;      // per scan block x kBuckets: partial-unit offsets
+    UnitDesc* desc;            // unit_cap entries
     uint64_t unit_cap;         // capacity of desc / partial
-    uint64_t* block_sums;      // scan scratch
     uint32_t* out;
-    uint32_t* partial;         // register contribution per unit
+    uint32_t* partial;         // register contribution per unit slot
     const uint32_t* blob;      // stream blob (kBlobWords)
     const uint32_t* comb_blob; // kCombWords for unit_bytes
 };
@@ -88,8 +98,8 @@ bool fixed_fast_path_ok(const FixedArgs& a);
 hipError_t launch_combine_fixed(const FixedArgs& a, const uint32_t* in_states, uint64_t k_in, uint32_t* out_states,
                                 uint64_t k_out, const uint32_t* comb_blob, hipStream_t s);
 uint64_t ragged_scan_blocks(uint64_t n_rec);
-// Ragged: scan (units per record -> unit_base, total at unit_base[n_rec]),
-// then fill (unit -> record), the unit kernel and the per-record combine.
+// Ragged: scan (full-unit offsets + partial-unit buckets; total units at
+// fbase[n_rec]), then descriptors, the unit kernel and the per-record finalize.
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 
