@@ -191,7 +191,7 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     const uint64_t nb = ragged_scan_blocks(n_rec);
     L.fbase_off = 0;
     L.pslot_off = align256((n_rec + 2) * sizeof(uint64_t));
-    L.sums_off = L.pslot_off + align256(n_rec * sizeof(uint64_t));
+    L.sums_off = L.pslot_off + align256(2 * n_rec * sizeof(uint64_t));
     L.bucket_off = L.sums_off + align256(nb * sizeof(uint64_t));
     L.desc_off = L.bucket_off + align256(nb * kBuckets * sizeof(uint64_t));
     L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
@@ -227,7 +227,7 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
     uint64_t cap;
     void* ws = nullptr;
     if (total_len > 0) {
-        cap = n_rec + ceil_div(total_len, kDefaultUnit);
+        cap = 2 * n_rec + ceil_div(total_len, kDefaultUnit);
         const RaggedLayout L = ragged_layout(n_rec, cap);
         KARMA_RC(workspace(dev, s, L.total, &ws));
         bind_ragged(a, ws, L, cap);

@@ -168,59 +168,74 @@ __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t&
     a3 = stride_step(lds, X, a3, v.w);
 }
 
-// Register contribution of the 16-aligned span [us, ue): 128-byte chunks
-// end-aligned to ue, 8 lanes per group, lane l owns bytes [16l, 16l+16) of
-// every chunk as four word slots; `inj` is xored into the word at `inj_at`
-// (the body's first word carries the record's entering register).  PF chunk
-// loads stay in flight per lane.  Every lane of the wave must call this (it
-// ends in cross-lane shuffles); the result is valid in group lane 0.
+__device__ __forceinline__ const uint8_t* floor128(const uint8_t* p) {
+    return reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(kChunk - 1));
+}
+
+// Register contribution of the 16-aligned span [us, ue).  The span is read in
+// 128-byte chunks on the ABSOLUTE 128-byte grid (every group load is one whole
+// cache line, whatever the span's alignment), 8 lanes per group, lane l owning
+// bytes [16l, 16l+16) of each chunk as four word slots.  Windows before us are
+// zero (a zero prefix does not change the register); in the last chunk the
+// lanes past ue skip their step, so lane l's pending words end at a different
+// distance from ue: with m the lane holding the last window, lane l's end lies
+// 16*((m - l) mod 8) bytes before ue, and the group tree runs over the lanes
+// rotated by m + 1.  `inj` is xored into the word at `inj_at` (the body's first
+// word carries the record's entering register).  PF chunk loads stay in flight
+// per lane.  Every lane of the wave must call this (cross-lane shuffles); the
+// result is valid in group lane 0.
 template <int PF, bool NT>
 __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, uint32_t l, const uint8_t* us,
                                                const uint8_t* ue, const uint8_t* inj_at, uint32_t inj) {
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    const int64_t span = ue - us;
-    if (span > 0) {
-        const int64_t nch = (span + kChunk - 1) / kChunk;
-        const uint8_t* w = ue - nch * kChunk + 16 * l;
+    uint32_t m = kGroupLanes - 1;
+    if (ue > us) {
+        const uint8_t* base = floor128(us);
+        const int64_t nch = (ue - base + kChunk - 1) / kChunk;
+        m = (uint32_t)((reinterpret_cast<uintptr_t>(ue) - 16) >> 4) & (kGroupLanes - 1);
+        const uint8_t* w = base + 16 * l;
+        const uint8_t* wl = base + (nch - 1) * kChunk + 16 * l;  // this lane's window in the last chunk
+        const bool lok = wl < ue;
+        const uint8_t* lclamp = lok ? wl : ue - 16;               // always a valid address
         {
-            u32x4 v = (w >= us) ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
+            const bool ok = w >= us && w < ue;
+            u32x4 v = ok ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
             if (w == inj_at) v.x ^= inj;
             a0 = v.x;
             a1 = v.y;
             a2 = v.z;
             a3 = v.w;
         }
-        int64_t rem = nch - 1;
+        int64_t rem = nch - 1;  // chunks after chunk 0; the final one is masked per lane
         w += kChunk;
-        // Window of the last chunk: prefetches past the end re-read it.  Chunks
-        // after chunk 0 are always full; with a single (possibly partial) chunk
-        // fall back to the unit's last 16 bytes so no load leaves [us, ue).
-        const uint8_t* last = ue - kChunk + 16 * l;
-        if (last < us) last = ue - 16;
         u32x4 nb[PF];
 #pragma unroll
-        for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, last));
-        while (rem >= PF) {
+        for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
+        while (rem > PF) {  // PF full chunks (at least one more follows)
             u32x4 cur[PF];
 #pragma unroll
             for (int q = 0; q < PF; ++q) cur[q] = nb[q];
             w += PF * kChunk;
 #pragma unroll
-            for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, last));
+            for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
 #pragma unroll
             for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
             rem -= PF;
         }
 #pragma unroll
-        for (int q = 0; q < PF - 1; ++q)
-            if (rem > q) step4(lds, X, a0, a1, a2, a3, nb[q]);
+        for (int q = 0; q < PF; ++q) {
+            if (q < rem - 1 || (q == rem - 1 && lok)) step4(lds, X, a0, a1, a2, a3, nb[q]);
+        }
     }
     // lane fold (crc32c.cc STEP4W order): c = Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0))))
     uint32_t c = zmap(lds, kLZ4, a0);
     c = zmap(lds, kLZ4, c ^ a1);
     c = zmap(lds, kLZ4, c ^ a2);
     c = zmap(lds, kLZ4, c ^ a3);
-    // group tree over 8 lanes: v_l = Z_{16*2^d}(v_l) ^ v_{l+2^d}
+    // rotate so the lane holding the last window comes last (identity when m == 7)
+    const uint32_t lane = threadIdx.x & 63u;
+    c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + m + 1) & (kGroupLanes - 1))), 64);
+    // group tree over 8 lanes: v_t = Z_{16*2^d}(v_t) ^ v_{t+2^d}
     uint32_t t = __shfl_down(c, 1, kGroupLanes);
     c = zmap(lds, kLZ16, c) ^ t;
     t = __shfl_down(c, 2, kGroupLanes);
@@ -249,8 +264,17 @@ __device__ __forceinline__ uint32_t lane_const() {
 }
 
 // ---- combine-blob LDS image: Z_{D*2^k} (k = 0..6), Z4, byte table ----------
+template <int WORDS = kCombWords>
 __device__ __forceinline__ void load_comb_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
-    for (int i = threadIdx.x; i < kCombWords; i += blockDim.x) lds[i] = blob[i];
+    for (int i = threadIdx.x; i < WORDS; i += blockDim.x) lds[i] = blob[i];
+}
+
+// Z_L for L = 16n, 0 < n < 256 (binary decomposition over Z_{16*2^i}).
+__device__ __forceinline__ uint32_t zshift16(const uint32_t* lds, uint32_t x, uint32_t n) {
+#pragma unroll
+    for (int i = 0; i < kCombSmallMaps; ++i)
+        if (n & (1u << i)) x = zmap(lds, kCombSmall + i * 1024, x);
+    return x;
 }
 
 // Tree over the 64 lanes of a wave with maps Z_{D*2^d}: lane 0 gets

@@ -80,8 +80,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
 // adds the record tail and writes the CRC.  One wave per output state.
 __global__ __launch_bounds__(256) void k_combine_fixed(FixedArgs A, const uint32_t* in, uint64_t k_in, uint32_t* outs,
                                                       uint64_t k_out, const uint32_t* comb) {
-    __shared__ uint32_t lds[kCombWords];
-    load_comb_tables(lds, comb);
+    __shared__ uint32_t lds[kCombCoreWords];
+    load_comb_tables<kCombCoreWords>(lds, comb);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);

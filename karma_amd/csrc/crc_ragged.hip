@@ -33,30 +33,45 @@ constexpr bool kRaggedNT = true;
 
 constexpr int kScanBlock = 1024;
 
-// Unit layout of one record (units end-aligned to the aligned body end b):
-// unit 0 = [a, a + span0) (span0 in (0, unit]), unit j >= 1 = a + span0 + (j-1)*unit.
-// Unit 0 is "partial" when span0 < unit; every other unit is full.
+// Unit layout of one record: the aligned body [a, b) cut at absolute multiples
+// of U = unit_bytes.  Unit j = [max(a, (A0+j)U), min(b, (A0+j+1)U)), A0 = a/U,
+// k = ceil(b/U) - A0.  Only the first and the last unit can be partial.
 struct RecUnits {
     Geom g;
     uint64_t k;      // units (0 for short records: finalize does them alone)
     uint64_t full;   // full units
-    uint32_t part;   // 1 if unit 0 is partial
-    uint32_t span0;  // bytes of unit 0
-    uint32_t c0;     // chunks of unit 0 (bucket of a partial unit)
+    uint32_t part0;  // 1 if unit 0 is partial
+    uint32_t part1;  // 1 if unit k-1 (k >= 2) is partial
+    uint32_t c0, c1; // cache lines (chunks) of those partial units
+    uint32_t last;   // bytes of the last unit (the last Horner step's distance)
 };
+
+__device__ __forceinline__ uint32_t lines_of(const uint8_t* us, const uint8_t* ue) {
+    return (uint32_t)((ue - floor128(us) + kChunk - 1) / kChunk);
+}
 
 __device__ __forceinline__ RecUnits rec_units(const RaggedArgs& A, uint64_t r) {
     RecUnits u;
     u.g = geom(A.arena + A.off[r], A.len[r]);
     u.k = u.full = 0;
-    u.part = u.span0 = u.c0 = 0;
+    u.part0 = u.part1 = u.c0 = u.c1 = u.last = 0;
     if (!u.g.is_short) {
-        const uint64_t body = (uint64_t)(u.g.b - u.g.a);
-        u.k = (body + A.unit_bytes - 1) / A.unit_bytes;
-        u.span0 = (uint32_t)(body - (u.k - 1) * A.unit_bytes);
-        u.part = u.span0 < A.unit_bytes ? 1u : 0u;
-        u.full = u.k - u.part;
-        u.c0 = (u.span0 + kChunk - 1) / kChunk;
+        const uint64_t U = A.unit_bytes;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
+        const uint64_t A0 = a / U, A1 = (b + U - 1) / U;
+        u.k = A1 - A0;
+        const uintptr_t e0 = (A0 + 1) * U < b ? (A0 + 1) * U : b;
+        u.part0 = (e0 - a) < U ? 1u : 0u;
+        if (u.part0) u.c0 = lines_of(u.g.a, reinterpret_cast<const uint8_t*>(e0));
+        if (u.k >= 2) {
+            const uintptr_t s1 = (A1 - 1) * U;
+            u.part1 = (b - s1) < U ? 1u : 0u;
+            if (u.part1) u.c1 = lines_of(reinterpret_cast<const uint8_t*>(s1), u.g.b);
+            u.last = (uint32_t)(b - s1);
+        } else {
+            u.last = (uint32_t)(b - a);
+        }
+        u.full = u.k - u.part0 - u.part1;
     }
     return u;
 }
@@ -102,7 +117,8 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan1(RaggedArgs A) {
     const uint64_t ex = block_excl_scan(r < A.n_rec ? u.full : 0, sm, total);  // has barriers
     if (r < A.n_rec) {
         A.fbase[r] = ex;
-        if (u.part) atomicAdd(&hist[u.c0], 1u);
+        if (u.part0) atomicAdd(&hist[u.c0], 1u);
+        if (u.part1) atomicAdd(&hist[u.c1], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) A.block_sums[blockIdx.x] = total;
@@ -142,9 +158,9 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan2(RaggedArgs A, uint6
 // One thread per record (block b = scan block b): final slots, the entering
 // register over the unaligned head, and the unit descriptors.
 __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
-    __shared__ uint32_t lds[kCombWords - kCombZ4];  // Z4 then the byte table
+    __shared__ uint32_t lds[kCombCoreWords - kCombZ4];  // Z4 then the byte table
     __shared__ unsigned long long cnt[kBuckets];
-    for (int i = threadIdx.x; i < kCombWords - kCombZ4; i += blockDim.x) lds[i] = A.comb_blob[kCombZ4 + i];
+    for (int i = threadIdx.x; i < kCombCoreWords - kCombZ4; i += blockDim.x) lds[i] = A.comb_blob[kCombZ4 + i];
     if (threadIdx.x < kBuckets) cnt[threadIdx.x] = A.bucket_off[(uint64_t)blockIdx.x * kBuckets + threadIdx.x];
     __syncthreads();
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -156,16 +172,24 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
     const uint8_t* p = A.arena + A.off[r];
     const uint32_t init = A.init ? A.init[r] : A.init_scalar;
     const uint32_t h = head_register(lds, 0, 1024, p, u.g, init);
-    const uint64_t ub = A.unit_bytes;
-    const uint8_t* fstart = u.g.a + (u.part ? u.span0 : 0u);
-    if (u.part) {
-        const uint64_t slot = atomicAdd(&cnt[u.c0], 1ull);
-        A.pslot[r] = slot;
-        if (slot < A.unit_cap) A.desc[slot] = UnitDesc{reinterpret_cast<uint64_t>(u.g.a), u.span0, h};
+    const uint64_t U = A.unit_bytes;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
+    const uint64_t A0 = a / U;
+    for (uint64_t j = 0; j < u.k; ++j) {
+        const uintptr_t us = (A0 + j) * U > a ? (A0 + j) * U : a;
+        const uintptr_t ue = (A0 + j + 1) * U < b ? (A0 + j + 1) * U : b;
+        uint64_t slot;
+        if (j == 0 && u.part0) {
+            slot = atomicAdd(&cnt[u.c0], 1ull);
+            A.pslot[2 * r] = slot;
+        } else if (j == u.k - 1 && u.part1) {
+            slot = atomicAdd(&cnt[u.c1], 1ull);
+            A.pslot[2 * r + 1] = slot;
+        } else {
+            slot = fb + j - u.part0;
+        }
+        if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)us, (uint32_t)(ue - us), j == 0 ? h : 0u};
     }
-    for (uint64_t i = 0; i < u.full && fb + i < A.unit_cap; ++i)
-        A.desc[fb + i] = UnitDesc{reinterpret_cast<uint64_t>(fstart + i * ub), (uint32_t)ub,
-                                  (!u.part && i == 0) ? h : 0u};
 }
 
 // Descriptor load through address space 1 (global_load_dwordx4, vmcnt only): a
@@ -201,47 +225,59 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     }
 }
 
-// State of unit j of a record whose full units start at slot fb.
-__device__ __forceinline__ uint64_t unit_slot(uint64_t j, uint64_t fb, uint64_t ps, uint32_t part) {
-    return j == 0 ? (part ? ps : fb) : fb + j - part;
+// Slot of unit j of a record (full units from fb in order, partial ones bucketed).
+__device__ __forceinline__ uint64_t unit_slot(uint64_t j, uint64_t k, uint64_t fb, uint64_t ps0, uint64_t ps1,
+                                              uint32_t part0, uint32_t part1) {
+    if (j == 0 && part0) return ps0;
+    if (j == k - 1 && part1) return ps1;
+    return fb + j - part0;
 }
 
-// One lane per record: Horner fold of the unit contributions (Z_unit), the
-// unaligned tail, ~R.  Records of more than 64 units: the whole wave folds them.
+// Last Horner step over a unit of `last` bytes (== U: the table of Z_U).
+__device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, uint32_t last, uint64_t U) {
+    return last == U ? zmap(lds, 0, x) : zshift16(lds, x, last / 16);
+}
+
+// One lane per record: Horner fold of the unit contributions (Z_U between unit
+// ends, Z_last before the last unit), the unaligned tail, ~R.  Records of more
+// than 64 units: the whole wave folds all but the last unit with the 64-lane tree.
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     __shared__ uint32_t lds[kCombWords];
     load_comb_tables(lds, A.comb_blob);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t U = A.unit_bytes;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t r0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; r0 < A.n_rec;
          r0 += nwaves * 64) {
         const uint64_t r = r0 + lane;
         const bool valid = r < A.n_rec;
         RecUnits u{};
-        uint64_t fb = 0, ps = 0;
+        uint64_t fb = 0, ps0 = 0, ps1 = 0;
         uint32_t init = 0;
         const uint8_t* p = A.arena;
         if (valid) {
             u = rec_units(A, r);
             fb = A.fbase[r];
-            if (u.part) ps = A.pslot[r];
+            if (u.part0) ps0 = A.pslot[2 * r];
+            if (u.part1) ps1 = A.pslot[2 * r + 1];
             init = A.init ? A.init[r] : A.init_scalar;
             p = A.arena + A.off[r];
         }
-        const bool ok = valid && fb + u.full <= A.unit_cap && (!u.part || ps < A.unit_cap);
+        const bool ok = valid && fb + u.full <= A.unit_cap && (!u.part0 || ps0 < A.unit_cap) &&
+                        (!u.part1 || ps1 < A.unit_cap);
         uint32_t acc = 0;
         bool huge = false;
         if (ok && u.k > 0) {
             if (u.k <= 64) {
-                acc = A.partial[unit_slot(0, fb, ps, u.part)];
-                for (uint64_t j = 1; j < u.k; j += 8) {  // 8 loads in flight at a time
+                acc = A.partial[unit_slot(0, u.k, fb, ps0, ps1, u.part0, u.part1)];
+                for (uint64_t j = 1; j + 1 < u.k; j += 8) {  // middle units: Z_U steps, 8 loads in flight
                     uint32_t s[8];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) s[q] = j + q < u.k ? A.partial[fb + j + q - u.part] : 0u;
+                    for (int q = 0; q < 8; ++q) s[q] = j + q + 1 < u.k ? A.partial[fb + j + q - u.part0] : 0u;
 #pragma unroll
                     for (int q = 0; q < 8; ++q)
-                        if (j + q < u.k) acc = zmap(lds, 0, acc) ^ s[q];
+                        if (j + q + 1 < u.k) acc = zmap(lds, 0, acc) ^ s[q];
                 }
             } else {
                 huge = true;
@@ -251,20 +287,24 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
         while (hm) {
             const int h = __ffsll((long long)hm) - 1;
             hm &= hm - 1;
-            const uint64_t hk = __shfl(u.k, h), hfb = __shfl(fb, h), hps = __shfl(ps, h);
-            const uint32_t hpart = __shfl(u.part, h);
+            const uint64_t hk = __shfl(u.k, h) - 1;  // all units but the last
+            const uint64_t hfb = __shfl(fb, h), hps0 = __shfl(ps0, h);
+            const uint32_t hp0 = __shfl(u.part0, h);
             const uint64_t nb = (hk + 63) / 64;
             const int64_t pad = (int64_t)(nb * 64 - hk);
             uint32_t w = 0;
             for (uint64_t blk = 0; blk < nb; ++blk) {
                 const int64_t idx = (int64_t)(blk * 64 + lane) - pad;
-                uint32_t v = idx >= 0 ? A.partial[unit_slot((uint64_t)idx, hfb, hps, hpart)] : 0u;
+                uint32_t v = 0;
+                if (idx >= 0) v = A.partial[idx == 0 && hp0 ? hps0 : hfb + idx - hp0];
                 v = wave_tree(lds, v);
                 w = zmap(lds, 6 * 1024, w) ^ v;
             }
             w = __shfl(w, 0);
             if ((int)lane == h) acc = w;
         }
+        if (ok && u.k >= 2)  // the last unit: shift by its own length
+            acc = shift_last(lds, acc, u.last, U) ^ A.partial[unit_slot(u.k - 1, u.k, fb, ps0, ps1, u.part0, u.part1)];
         if (valid) {
             uint32_t res = 0;
             if (ok) {

@@ -28,12 +28,16 @@ constexpr int kBlobT8 = 5120;      // byte table (one zero byte, low byte index)
 constexpr int kBlobWords = 5376;
 
 // ---- table blob of the combine kernels --------------------------------------
-// maps Z_{D * 2^k}, k = 0..6 (k = 6 is the Horner step of 64 states), then Z4
-// and the byte table (head/tail steps).
+// maps Z_{D * 2^k}, k = 0..6 (k = 6 is the Horner step of 64 states), Z4 and
+// the byte table (head/tail steps), then Z_{16 * 2^i}, i = 0..7, which
+// compose Z_L for any L = 16n < 4096 (the short last unit of a ragged record).
 constexpr int kCombMaps = 7;
 constexpr int kCombZ4 = kCombMaps * 1024;
 constexpr int kCombT8 = kCombZ4 + 1024;
-constexpr int kCombWords = kCombT8 + 256;
+constexpr int kCombCoreWords = kCombT8 + 256;  // what the fixed combine and the head steps need
+constexpr int kCombSmall = kCombT8 + 1024;
+constexpr int kCombSmallMaps = 8;
+constexpr int kCombWords = kCombSmall + kCombSmallMaps * 1024;
 
 // Host builders (gf2.h): fill a blob for stride kChunk / for unit size D.
 void build_stream_blob(uint32_t* out /*kBlobWords*/);
@@ -62,10 +66,11 @@ struct UnitDesc {
 };
 static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
 
-// Ragged batches order their units for balance: all full units
-// (span == unit_bytes) first, in record order, then every record's partial
-// first unit bucketed by chunk count, longest first, so the 8 units a wave
-// streams together have (nearly) equal length.
+// Ragged batches cut record bodies at absolute unit_bytes boundaries (so full
+// units are 4 KiB-aligned and every chunk is a whole cache line) and order the
+// units for balance: all full units first, in record order, then
+// the partial first/last units bucketed by chunk count, longest first, so the
+// 8 units a wave streams together have (nearly) equal length.
 constexpr int kBuckets = 33;  // chunk counts 1..32 of a partial unit (index = chunks)
 static_assert(kDefaultUnit / kChunk < kBuckets, "a partial unit has at most unit/kChunk chunks");
 
@@ -79,7 +84,7 @@ struct RaggedArgs {
     uint64_t unit_bytes;       // kDefaultUnit
     uint64_t* fbase;           // n_rec + 2: slot of the record's first full unit;
                                //   [n_rec] = total units, [n_rec+1] = full units
-    uint64_t* pslot;           // n_rec: slot of the record's partial unit
+    uint64_t* pslot;           // 2 * n_rec: slots of the record's partial first / last unit
     uint64_t* block_sums;      // per scan block: full-unit offset
     uint64_t* bucket_off;      // per scan block x kBuckets: partial-unit offsets
     UnitDesc* desc;            // unit_cap entries

@@ -23,7 +23,9 @@ void build_combine_blob(uint64_t unit_bytes, uint32_t* out) {
         m = Map::compose(m, m);  // Z_{D*2^(k+1)}
     }
     gf2::slicing_tables(Map::zero_bytes(4), out + kCombZ4);
+    for (int i = 0; i < 1024; ++i) out[kCombT8 + i] = 0;
     gf2::byte_table(out + kCombT8);
+    for (int i = 0; i < kCombSmallMaps; ++i) gf2::slicing_tables(Map::zero_bytes(16ull << i), out + kCombSmall + i * 1024);
 }
 
 }  // namespace engine

@@ -15,8 +15,10 @@ import karma_amd as K  # noqa: E402
 variants = [int(v) for v in sys.argv[1:]] or [10, 11, 12, 13, 14, 15, 16, 17, 18, 1]
 dev = torch.device("cuda:0")
 n, rec = 1 << 20, 4096
-buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
-K.fill_splitmix64(buf, 42)
+MIS = int(os.environ.get("MISALIGN", "0"))  # byte offset of the arena (alignment experiments)
+raw = torch.empty(n * rec + 256, dtype=torch.uint8, device=dev)
+K.fill_splitmix64(raw, 42)
+buf = raw[MIS: MIS + n * rec]
 out = torch.empty(n, dtype=torch.uint32, device=dev)
 ref = None
 res = {v: [] for v in variants}
@@ -42,15 +44,16 @@ for v in variants:
     print(f"variant {v}: median {np.median(ms):.4f} ms  min {ms.min():.4f}  -> {n * rec / np.median(ms) / 1e6:.1f} GB/s"
           f"  (best {n * rec / ms.min() / 1e6:.1f})  rounds {' '.join(f'{x:.3f}' for x in ms)}")
 pr = torch.zeros(1, dtype=torch.uint32, device=dev)
+probe_buf = raw[: n * rec]
 for _ in range(3):
-    K.stream_probe(buf, pr)
+    K.stream_probe(probe_buf, pr)
 torch.cuda.synchronize()
 ts = []
 for _ in range(5):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(10):
-        K.stream_probe(buf, pr)
+        K.stream_probe(probe_buf, pr)
     b.record()
     torch.cuda.synchronize()
     ts.append(a.elapsed_time(b) / 10)
