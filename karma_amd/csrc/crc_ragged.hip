@@ -105,7 +105,9 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
     return pre + inc - v;
 }
 
-// Per scan block: exclusive scan of full units, histogram of partial units by chunk count.
+// Per scan block: exclusive scan of full units; partial units counted per
+// bucket (chunk count) into the global bucket totals (one atomic per bucket
+// per block; the totals are zeroed by the launcher).
 __global__ __launch_bounds__(kScanBlock) void k_ragged_scan1(RaggedArgs A) {
     __shared__ uint64_t sm[16];
     __shared__ uint32_t hist[kBuckets];
@@ -122,11 +124,12 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan1(RaggedArgs A) {
     }
     __syncthreads();
     if (threadIdx.x == 0) A.block_sums[blockIdx.x] = total;
-    if (threadIdx.x < kBuckets) A.bucket_off[(uint64_t)blockIdx.x * kBuckets + threadIdx.x] = hist[threadIdx.x];
+    if (threadIdx.x < kBuckets && hist[threadIdx.x])
+        atomicAdd(reinterpret_cast<unsigned long long*>(&A.bucket_off[threadIdx.x]), (unsigned long long)hist[threadIdx.x]);
 }
 
 // Single block: full-unit offsets per scan block (slots [0, F)), then the
-// partial buckets from the longest (31 chunks) down to 1 chunk (slots [F, U)).
+// start of every partial bucket, longest (32 chunks) first (slots [F, U)).
 __global__ __launch_bounds__(kScanBlock) void k_ragged_scan2(RaggedArgs A, uint64_t nblocks) {
     __shared__ uint64_t sm[16];
     uint64_t carry = 0;
@@ -138,34 +141,43 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan2(RaggedArgs A, uint6
         if (i < nblocks) A.block_sums[i] = carry + ex;
         carry += total;
     }
-    const uint64_t F = carry;
-    for (int c = kBuckets - 1; c >= 1; --c) {
-        for (uint64_t base = 0; base < nblocks; base += blockDim.x) {
-            const uint64_t i = base + threadIdx.x;
-            const uint64_t v = i < nblocks ? A.bucket_off[i * kBuckets + c] : 0;
-            uint64_t total;
-            const uint64_t ex = block_excl_scan(v, sm, total);
-            if (i < nblocks) A.bucket_off[i * kBuckets + c] = carry + ex;
-            carry += total;
-        }
-    }
     if (threadIdx.x == 0) {
+        const uint64_t F = carry;
+        for (int c = kBuckets - 1; c >= 1; --c) {  // totals -> cursors
+            const uint64_t t = A.bucket_off[c];
+            A.bucket_off[c] = carry;
+            carry += t;
+        }
         A.fbase[A.n_rec] = carry;  // total units
         A.fbase[A.n_rec + 1] = F;
     }
 }
 
 // One thread per record (block b = scan block b): final slots, the entering
-// register over the unaligned head, and the unit descriptors.
+// register over the unaligned head, and the unit descriptors.  A block
+// reserves its range of every partial bucket with one atomic per bucket.
 __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
     __shared__ uint32_t lds[kCombCoreWords - kCombZ4];  // Z4 then the byte table
     __shared__ unsigned long long cnt[kBuckets];
+    __shared__ uint32_t hist[kBuckets];
     for (int i = threadIdx.x; i < kCombCoreWords - kCombZ4; i += blockDim.x) lds[i] = A.comb_blob[kCombZ4 + i];
-    if (threadIdx.x < kBuckets) cnt[threadIdx.x] = A.bucket_off[(uint64_t)blockIdx.x * kBuckets + threadIdx.x];
+    if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    RecUnits u{};
+    if (r < A.n_rec) {
+        u = rec_units(A, r);
+        if (u.part0) atomicAdd(&hist[u.c0], 1u);
+        if (u.part1) atomicAdd(&hist[u.c1], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kBuckets)
+        cnt[threadIdx.x] = hist[threadIdx.x]
+                               ? atomicAdd(reinterpret_cast<unsigned long long*>(&A.bucket_off[threadIdx.x]),
+                                           (unsigned long long)hist[threadIdx.x])
+                               : 0ull;
+    __syncthreads();
     if (r >= A.n_rec) return;
-    const RecUnits u = rec_units(A, r);
     const uint64_t fb = A.fbase[r] + A.block_sums[blockIdx.x];
     A.fbase[r] = fb;
     if (u.k == 0) return;
@@ -325,6 +337,8 @@ uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock - 1) / 
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
+    hipError_t e = hipMemsetAsync(a.bucket_off, 0, kBuckets * sizeof(uint64_t), s);  // bucket totals
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_ragged_scan1, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     hipLaunchKernelGGL(k_ragged_scan2, dim3(1), dim3(kScanBlock), 0, s, a, nb);
     return hipGetLastError();
