@@ -35,7 +35,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", default="fixed", choices=["fixed", "ragged", "stream", "host"])
     p.add_argument("--records-per-gpu", type=int, default=1 << 20)
     p.add_argument("--rec-bytes", type=int, default=4096)
@@ -119,6 +119,8 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)  # one rank per GPU; several ranks per GPU only for plumbing checks
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -146,7 +148,7 @@ def main():
     wl = args.workload
     n_rec = args.records_per_gpu
     rec = args.rec_bytes
-    info = {}
+    cur = {}  # the output buffer the next crc_step writes (double-buffered for N > 1)
     if wl == "fixed":
         payload = n_rec * rec
         arena = torch.empty(payload, dtype=torch.uint8, device=dev)
@@ -154,7 +156,7 @@ def main():
         out = torch.empty(n_rec, dtype=torch.uint32, device=dev)
 
         def crc_step():
-            st = L.karma_crc32c_batch_fixed(arena.data_ptr(), rec, n_rec, None, 0, out.data_ptr(), sh)
+            st = L.karma_crc32c_batch_fixed(arena.data_ptr(), rec, n_rec, None, 0, cur['out'].data_ptr(), sh)
             if st:
                 _lib.check("batch_fixed", st)
 
@@ -179,7 +181,7 @@ def main():
 
         def crc_step():
             st = L.karma_crc32c_batch_ragged(arena.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), count, total,
-                                             None, 0, out.data_ptr(), sh)
+                                             None, 0, cur['out'].data_ptr(), sh)
             if st:
                 _lib.check("batch_ragged", st)
 
@@ -196,7 +198,7 @@ def main():
         out = torch.empty(nseg, dtype=torch.uint32, device=dev)
 
         def crc_step():
-            st = L.karma_crc32c_batch_fixed(arena.data_ptr(), seg, nseg, None, 0, out.data_ptr(), sh)
+            st = L.karma_crc32c_batch_fixed(arena.data_ptr(), seg, nseg, None, 0, cur['out'].data_ptr(), sh)
             if st:
                 _lib.check("batch_fixed(stream)", st)
 
@@ -221,14 +223,35 @@ def main():
         workload_desc = f"{n_rec} x {rec} B records in pageable host memory -> H2D -> kernel -> D2H (synchronous)"
 
     gather_buf = torch.empty(n_rec * world, dtype=torch.uint32, device=dev) if (comm is not None and rank == 0) else None
+    # N > 1: the CRC gather of step i runs on its own stream while step i+1 computes into the
+    # other output buffer (double-buffered), so the collective overlaps the next kernel.
+    outs = [out, torch.empty_like(out)] if (comm is not None and out is not None) else [out]
+    gstream = torch.cuda.Stream() if comm is not None else None
+    computed = [torch.cuda.Event() for _ in outs]
+    gathered = [torch.cuda.Event() for _ in outs]
+    state = {"i": 0}
+    kernel_step = crc_step
+
+    def crc_step():
+        slot = state["i"] % len(outs)
+        if gstream is not None and state["i"] >= len(outs):
+            stream.wait_event(gathered[slot])  # the gather that last read this buffer is done
+        cur["out"] = outs[slot]
+        kernel_step()
+        state["i"] += 1
 
     def gather_step():
-        if comm is None or out is None:
+        if gstream is None or out is None:
             return
-        st = L.karma_crc32c_gather_u32(comm, out.data_ptr(), n_rec, gather_buf.data_ptr() if gather_buf is not None
-                                       else None, 0, sh)
+        slot = (state["i"] - 1) % len(outs)  # the buffer the last crc_step wrote
+        computed[slot].record(stream)
+        gstream.wait_event(computed[slot])
+        st = L.karma_crc32c_gather_u32(comm, outs[slot].data_ptr(), n_rec,
+                                       gather_buf.data_ptr() if gather_buf is not None else None, 0,
+                                       gstream.cuda_stream)
         if st:
             _lib.check("gather_u32", st)
+        gathered[slot].record(gstream)
 
     # ---- warmup -------------------------------------------------------------------------
     for _ in range(args.warmup):
@@ -265,7 +288,7 @@ def main():
     check = {}
     if out is not None and rank == 0 and wl in ("fixed", "stream"):
         idx = np.unique(np.concatenate([np.arange(min(64, n_rec)), np.random.default_rng(1).integers(0, n_rec, 64)]))
-        got = out.cpu().numpy()
+        got = cur["out"].cpu().numpy()
         bad = 0
         for r in idx[: 16 if wl == "stream" else len(idx)]:
             b = arena[int(r) * rec:(int(r) + 1) * rec].cpu().numpy()

@@ -14,6 +14,8 @@
  *                                   wal::scan_record             karma-store/wal.cc:60
  *   karma_crc32c_stream             crc32c::Extend over one long buffer (a 64 MiB segment image)
  *   karma_crc32c_*_sharded / gather the same, records sharded over GPUs, CRCs gathered over RCCL
+ *   karma_wal_append_batch          sivir::build_sqe + segment_file::append_record   sivir.cc:276-317
+ *   karma_wal_replay                sivir::open's wal::scan_record loop              sivir.cc:31-41, wal.cc:34-87
  *
  * Errors: 0 = success, negative = KARMA_E_* below.  No entry point throws.
  * There is no CPU fallback behind the device entry points: without a usable
@@ -91,6 +93,36 @@ int karma_crc32c_gather_u32(karma_comm_t comm, const uint32_t* d_send, size_t co
 int karma_crc32c_batch_fixed_sharded(karma_comm_t comm, const void* d_local, size_t rec_bytes, size_t n_local,
                                      uint32_t init, uint32_t* d_local_out, uint32_t* d_all_out, int root,
                                      karma_stream_t stream);
+
+/* ---- WAL segment images (karma-store framing) ------------------------------
+ * Record = [crc u32 LE = Value(payload)][len<<8 | type u32 LE][payload]
+ * (segment_file.cc:21-31, common.h:11); type 1 = padding to the segment end
+ * ('0' bytes, crc 0; segment_file.cc:33-49).  The WAL image is a host buffer of
+ * wal_bytes = k * seg_bytes (segments back to back, WAL offset = byte offset). */
+#define KARMA_WAL_END 0      /* replay walked past the last segment */
+#define KARMA_WAL_CORRUPT 1  /* stopped where wal.cc logs "Corrupt record" */
+#define KARMA_WAL_BAD_TYPE 2 /* stopped at a record type other than 0 / 1 */
+
+/* Batched append (sivir::build_sqe + segment_file::append_record / append_footer):
+ * frame payloads i = 0..n-1 (h_src + h_src_off[i], h_len[i]) at WAL offset *h_cursor,
+ * closing a segment with a footer when a record does not fit (can_hold).  The CRCs of
+ * the whole batch come from one GPU batch.  Updates *h_cursor, writes the header offset
+ * of record i to h_rec_off[i] (optional) and the number framed to *h_n_framed (records
+ * that do not fit in the image are left out). */
+int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const uint32_t* h_len, size_t n,
+                           void* h_wal, size_t wal_bytes, size_t seg_bytes, uint64_t* h_cursor, uint64_t* h_rec_off,
+                           size_t* h_n_framed, int device);
+
+/* Batched replay (sivir::open's wal::scan_record loop, wal.cc:34-87) from WAL offset
+ * `start`: headers walked on the host, all payload CRCs verified in one GPU batch
+ * (over d_wal when the caller already holds a device copy, else the image is copied).
+ * Outputs: *h_n_records type-0 records accepted, their header offsets in h_rec_off
+ * (optional, up to rec_cap), *h_stop the WAL offset where replay stops (the writer's
+ * resume point), *h_status KARMA_WAL_*.  Keeps the reference's size-0 quirk (the CRC
+ * of an empty type-0 record is taken over the stale 4-byte len/type word). */
+int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
+                     uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
+                     int device);
 
 /* ---- synthetic data and probes (bench / tests) ---------------------------- */
 /* d_dst[i] = byte (first_byte + i) of the little-endian splitmix64 stream of

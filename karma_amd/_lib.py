@@ -41,6 +41,9 @@ SIGNATURES = {
     "karma_crc32c_comm_destroy": (_i, [_vp]),
     "karma_crc32c_gather_u32": (_i, [_vp, _vp, _sz, _vp, _i, _vp]),
     "karma_crc32c_batch_fixed_sharded": (_i, [_vp, _vp, _sz, _sz, _u32, _vp, _vp, _i, _vp]),
+    "karma_wal_append_batch": (_i, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, _c.POINTER(_u64), _vp, _c.POINTER(_sz), _i]),
+    "karma_wal_replay": (_i, [_vp, _vp, _sz, _sz, _u64, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_i), _vp, _sz,
+                              _i]),
     "karma_fill_splitmix64": (_i, [_vp, _sz, _u64, _u64, _vp]),
     "karma_stream_probe": (_i, [_vp, _sz, _vp, _vp]),
     "karma_device_cu_count": (_i, []),

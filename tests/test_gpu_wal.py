@@ -1,0 +1,112 @@
+"""Batched WAL append / replay (karma_wal_append_batch / karma_wal_replay) against the Python
+restatement of Karma's framing and scan_record loop (tests/wal_model.py)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import synth
+import wal_model
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from karma_amd import _lib  # noqa: E402
+
+SEG = 64 << 10
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return _lib.lib()
+
+
+def _payloads(seed, n, lo, hi):
+    lens = synth.uniform_lengths(seed, n, lo, hi)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(seed + 1, 0, int(lens.sum()) + 16).copy()
+    return src, offs, lens
+
+
+def _append(lib, src, offs, lens, wal, cursor=0):
+    cur = ctypes.c_uint64(cursor)
+    nf = ctypes.c_size_t()
+    rec = np.zeros(lens.size, np.uint64)
+    st = lib.karma_wal_append_batch(src.ctypes.data, offs.ctypes.data, lens.ctypes.data, lens.size, wal.ctypes.data,
+                                    wal.nbytes, SEG, ctypes.byref(cur), rec.ctypes.data, ctypes.byref(nf), 0)
+    _lib.check("karma_wal_append_batch", st)
+    return cur.value, rec[: nf.value]
+
+
+def _replay(lib, wal, start=0, d_wal=None):
+    n, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+    rec = np.zeros(wal.nbytes // 8, np.uint64)
+    st = lib.karma_wal_replay(wal.ctypes.data, d_wal.data_ptr() if d_wal is not None else None, wal.nbytes, SEG, start,
+                              ctypes.byref(n), ctypes.byref(stop), ctypes.byref(status), rec.ctypes.data, rec.size, 0)
+    _lib.check("karma_wal_replay", st)
+    return list(rec[: n.value]), stop.value, status.value
+
+
+def test_append_matches_reference_framing(lib):
+    src, offs, lens = _payloads(3, 3000, 1, 3000)
+    wal = np.zeros(32 * SEG, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal)
+    model = bytearray(32 * SEG)
+    payloads = [src[int(o): int(o) + int(n)] for o, n in zip(offs, lens)]
+    mcur, mrec = wal_model.append(payloads, model, SEG, 0)
+    assert cur == mcur and list(rec) == mrec
+    assert wal.tobytes() == bytes(model)
+
+
+def test_replay_round_trip_and_zero_tail(lib):
+    src, offs, lens = _payloads(5, 4000, 1, 2000)
+    wal = np.zeros(64 * SEG, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal)
+    got = _replay(lib, wal)
+    want = wal_model.replay(wal.tobytes(), SEG)
+    assert got == (list(want[0]), want[1], want[2])
+    # every framed record replays; replay ends at the never-written zero tail, which the
+    # reference reports as "Corrupt record" (size-0 quirk), i.e. the writer resumes at the cursor
+    assert got[0] == list(rec) and got[1] == cur and got[2] == wal_model.CORRUPT
+    # same through a device copy of the image
+    d = torch.from_numpy(wal).cuda()
+    assert _replay(lib, wal, d_wal=d) == got
+
+
+@pytest.mark.parametrize("what", ["payload_bit", "crc_field", "length_past_segment", "bad_type", "empty_record"])
+def test_replay_stops_where_scan_record_does(lib, what):
+    src, offs, lens = _payloads(7, 2500, 1, 2500)
+    wal = np.zeros(48 * SEG, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal)
+    k = 1234
+    h = int(rec[k])
+    if what == "payload_bit":
+        wal[h + 8 + int(lens[k]) // 2] ^= 0x10
+    elif what == "crc_field":
+        wal[h] ^= 0x01
+    elif what == "length_past_segment":
+        wal[h + 4: h + 8] = np.frombuffer(np.uint32(((SEG) << 8) | 0).tobytes(), np.uint8)
+    elif what == "bad_type":
+        wal[h + 4] = 7
+    else:  # an empty record as append_record writes it: crc Value("") = 0, len/type 0
+        wal[h: h + 8] = 0
+    got = _replay(lib, wal)
+    want = wal_model.replay(wal.tobytes(), SEG)
+    assert got == (list(want[0]), want[1], want[2])
+    assert got[1] == h and len(got[0]) == k
+    assert got[2] == (wal_model.BAD_TYPE if what == "bad_type" else wal_model.CORRUPT)
+
+
+def test_replay_from_checkpoint_and_short_segment_tails(lib):
+    # records sized so segments end with < 8 spare bytes (footer = '0' bytes only) and with padding records
+    lens = np.array(([SEG // 2 - 8, SEG // 2 - 12] * 8) + [100] * 50, dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(11, 0, int(lens.sum()) + 16).copy()
+    wal = np.zeros(16 * SEG, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal)
+    for start in [0, int(rec[3]), int(rec[10])]:
+        got = _replay(lib, wal, start=start)
+        want = wal_model.replay(wal.tobytes(), SEG, start)
+        assert got == (list(want[0]), want[1], want[2])
