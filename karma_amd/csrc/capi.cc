@@ -4,7 +4,6 @@
 // returns a KARMA_E_* status; nothing throws across the ABI and nothing falls
 // back to the CPU.
 #include <hip/hip_runtime_api.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstring>
@@ -266,10 +265,10 @@ struct Locked {
 
 }  // namespace
 
-struct karma_comm {
-    ncclComm_t nc = nullptr;
-    int rank = 0, nranks = 1;
-};
+namespace karma::engine {
+// shared with rccl_comm.cc so RCCL failures land in karma_crc32c_last_error()
+int set_last_error(int code, const std::string& what) { return fail(code, what); }
+}  // namespace karma::engine
 
 extern "C" {
 
@@ -437,50 +436,6 @@ int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, cons
     if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
     (void)hipStreamDestroy(s);
     return rc;
-}
-
-// ---- multi-GPU --------------------------------------------------------------------
-int karma_crc32c_get_unique_id(void* uid, size_t uid_bytes) {
-    if (!uid || uid_bytes < sizeof(ncclUniqueId)) return fail(KARMA_E_INVALID, "get_unique_id: buffer too small");
-    ncclUniqueId id;
-    ncclResult_t r = ncclGetUniqueId(&id);
-    if (r != ncclSuccess) return fail(KARMA_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
-    std::memcpy(uid, &id, sizeof(id));
-    return 0;
-}
-
-int karma_crc32c_comm_init(karma_comm_t* comm, int nranks, const void* uid, int rank) {
-    if (!comm || !uid || nranks < 1 || rank < 0 || rank >= nranks) return fail(KARMA_E_INVALID, "comm_init");
-    karma_comm* c = new (std::nothrow) karma_comm;
-    if (!c) return fail(KARMA_E_NOMEM, "comm_init");
-    ncclUniqueId id;
-    std::memcpy(&id, uid, sizeof(id));
-    ncclResult_t r = ncclCommInitRank(&c->nc, nranks, id, rank);
-    if (r != ncclSuccess) {
-        delete c;
-        return fail(KARMA_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-    }
-    c->rank = rank;
-    c->nranks = nranks;
-    *comm = c;
-    return 0;
-}
-
-int karma_crc32c_comm_destroy(karma_comm_t comm) {
-    if (!comm) return 0;
-    ncclResult_t r = ncclCommDestroy(comm->nc);
-    delete comm;
-    if (r != ncclSuccess) return fail(KARMA_E_RCCL, std::string("ncclCommDestroy: ") + ncclGetErrorString(r));
-    return 0;
-}
-
-int karma_crc32c_gather_u32(karma_comm_t comm, const uint32_t* d_send, size_t count, uint32_t* d_recv, int root,
-                            karma_stream_t stream) {
-    if (!comm || (!d_send && count)) return fail(KARMA_E_INVALID, "gather_u32");
-    if (comm->rank == root && !d_recv && count) return fail(KARMA_E_INVALID, "gather_u32: root needs d_recv");
-    ncclResult_t r = ncclGather(d_send, d_recv, count, ncclUint32, root, comm->nc, (hipStream_t)stream);
-    if (r != ncclSuccess) return fail(KARMA_E_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
-    return 0;
 }
 
 int karma_crc32c_batch_fixed_sharded(karma_comm_t comm, const void* d_local, size_t rec_bytes, size_t n_local,

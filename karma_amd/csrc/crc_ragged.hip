@@ -337,7 +337,7 @@ uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock - 1) / 
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
-    hipError_t e = hipMemsetAsync(a.bucket_off, 0, kBuckets * sizeof(uint64_t), s);  // bucket totals
+    hipError_t e = hipMemsetAsync(a.bucket_off, 0, (kBuckets + 1) * sizeof(uint64_t), s);  // bucket totals (padded to 16 B: one fill)
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_ragged_scan1, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     hipLaunchKernelGGL(k_ragged_scan2, dim3(1), dim3(kScanBlock), 0, s, a, nb);

@@ -1,0 +1,160 @@
+// karma_amd/csrc/rccl_comm.cc -- the engine's RCCL communicator (one process
+// per GPU, xGMI) for the multi-GPU path: unique id, init/destroy, and the
+// gather of per-record CRCs to the root.
+//
+// RCCL is bound at run time through ONE library handle.  A process may already
+// hold an RCCL (PyTorch ships its own librccl); linking ours as well would
+// let the dynamic linker resolve each nccl* symbol from whichever copy comes
+// first in scope, mixing two RCCLs on one communicator.  So: reuse an RCCL that
+// is already loaded (RTLD_NOLOAD), else load ROCm's, and take every entry
+// point from that handle.  The gather uses ncclGather when the library has it
+// and a grouped ncclSend/ncclRecv otherwise.
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "karma_crc32c.h"
+
+namespace karma::engine {
+int set_last_error(int code, const std::string& what);  // capi.cc
+}
+
+namespace {
+
+struct Rccl {
+    void* h = nullptr;
+    ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    const char* (*getErrorString)(ncclResult_t) = nullptr;
+    ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*groupStart)() = nullptr;
+    ncclResult_t (*groupEnd)() = nullptr;
+    std::string error;
+};
+
+template <typename F>
+void bind(void* h, F& f, const char* name) {
+    f = reinterpret_cast<F>(dlsym(h, name));
+}
+
+Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* names[] = {"librccl.so.1", "librccl.so"};
+        for (const char* n : names)
+            if ((r.h = dlopen(n, RTLD_NOW | RTLD_NOLOAD))) break;  // an RCCL already in the process
+        if (!r.h) r.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!r.h) r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!r.h) {
+            const char* e = dlerror();
+            r.error = std::string("cannot load librccl: ") + (e ? e : "?");
+            return;
+        }
+        bind(r.h, r.getUniqueId, "ncclGetUniqueId");
+        bind(r.h, r.commInitRank, "ncclCommInitRank");
+        bind(r.h, r.commDestroy, "ncclCommDestroy");
+        bind(r.h, r.getErrorString, "ncclGetErrorString");
+        bind(r.h, r.gather, "ncclGather");
+        bind(r.h, r.send, "ncclSend");
+        bind(r.h, r.recv, "ncclRecv");
+        bind(r.h, r.groupStart, "ncclGroupStart");
+        bind(r.h, r.groupEnd, "ncclGroupEnd");
+        if (!r.getUniqueId || !r.commInitRank || !r.commDestroy || !r.getErrorString ||
+            (!r.gather && !(r.send && r.recv && r.groupStart && r.groupEnd))) {
+            r.error = "librccl lacks a required entry point";
+            r.h = nullptr;
+        }
+    });
+    return r;
+}
+
+int rfail(const std::string& what) { return karma::engine::set_last_error(KARMA_E_RCCL, what); }
+
+}  // namespace
+
+struct karma_comm {
+    ncclComm_t nc = nullptr;
+    int rank = 0, nranks = 1;
+};
+
+extern "C" {
+
+int karma_crc32c_get_unique_id(void* uid, size_t uid_bytes) {
+    if (!uid || uid_bytes < sizeof(ncclUniqueId)) return KARMA_E_INVALID;
+    Rccl& r = rccl();
+    if (!r.h) return rfail(r.error);
+    ncclUniqueId id;
+    const ncclResult_t e = r.getUniqueId(&id);
+    if (e != ncclSuccess) return rfail(std::string("ncclGetUniqueId: ") + r.getErrorString(e));
+    std::memcpy(uid, &id, sizeof(id));
+    return 0;
+}
+
+int karma_crc32c_comm_init(karma_comm_t* comm, int nranks, const void* uid, int rank) {
+    if (!comm || !uid || nranks < 1 || rank < 0 || rank >= nranks) return KARMA_E_INVALID;
+    Rccl& r = rccl();
+    if (!r.h) return rfail(r.error);
+    karma_comm* c = new (std::nothrow) karma_comm;
+    if (!c) return KARMA_E_NOMEM;
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    const ncclResult_t e = r.commInitRank(&c->nc, nranks, id, rank);
+    if (e != ncclSuccess) {
+        delete c;
+        return rfail(std::string("ncclCommInitRank: ") + r.getErrorString(e));
+    }
+    c->rank = rank;
+    c->nranks = nranks;
+    *comm = c;
+    return 0;
+}
+
+int karma_crc32c_comm_destroy(karma_comm_t comm) {
+    if (!comm) return 0;
+    Rccl& r = rccl();
+    const ncclResult_t e = r.h ? r.commDestroy(comm->nc) : ncclSuccess;
+    delete comm;
+    if (e != ncclSuccess) return rfail(std::string("ncclCommDestroy: ") + r.getErrorString(e));
+    return 0;
+}
+
+int karma_crc32c_gather_u32(karma_comm_t comm, const uint32_t* d_send, size_t count, uint32_t* d_recv, int root,
+                            karma_stream_t stream) {
+    if (!comm || (!d_send && count) || root < 0 || root >= comm->nranks) return KARMA_E_INVALID;
+    if (comm->rank == root && !d_recv && count) return KARMA_E_INVALID;
+    Rccl& r = rccl();
+    if (!r.h) return rfail(r.error);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (r.gather) {
+        const ncclResult_t e = r.gather(d_send, d_recv, count, ncclUint32, root, comm->nc, s);
+        if (e != ncclSuccess) return rfail(std::string("ncclGather: ") + r.getErrorString(e));
+        return 0;
+    }
+    // grouped point-to-point form: every rank sends, the root receives each shard in rank order
+    ncclResult_t e = r.groupStart();
+    if (e == ncclSuccess && comm->rank == root) {
+        for (int p = 0; p < comm->nranks && e == ncclSuccess; ++p)
+            if (p != root) e = r.recv(d_recv + (size_t)p * count, count, ncclUint32, p, comm->nc, s);
+    } else if (e == ncclSuccess) {
+        e = r.send(d_send, count, ncclUint32, root, comm->nc, s);
+    }
+    const ncclResult_t e2 = r.groupEnd();
+    if (e != ncclSuccess || e2 != ncclSuccess)
+        return rfail(std::string("ncclSend/ncclRecv: ") + r.getErrorString(e != ncclSuccess ? e : e2));
+    if (comm->rank == root && count &&
+        hipMemcpyAsync(d_recv + (size_t)root * count, d_send, count * sizeof(uint32_t), hipMemcpyDeviceToDevice, s) !=
+            hipSuccess)
+        return KARMA_E_HIP;
+    return 0;
+}
+
+}  // extern "C"
