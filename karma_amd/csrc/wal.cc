@@ -30,6 +30,10 @@
 #include "karma-util/crc32c.h"
 #include "karma_crc32c.h"
 
+namespace karma::engine {
+int set_last_error(int code, const std::string& what);  // capi.cc
+}
+
 namespace {
 
 inline uint32_t le32(const uint8_t* p) {
@@ -92,10 +96,7 @@ int walk_segment(const uint8_t* seg, uint64_t seg_base, uint64_t seg_bytes, uint
     }
 }
 
-int fail(int code, const char* what) {
-    (void)what;
-    return code;
-}
+int fail(int code, const char* what) { return karma::engine::set_last_error(code, what); }
 
 static_assert(KARMA_WAL_CORRUPT == 1 && KARMA_WAL_BAD_TYPE == 2, "walk_segment stop kinds");
 
