@@ -48,26 +48,54 @@ def parse():
 
 
 # ---------------------------------------------------------------------------------------------
-def cpu_baseline(rec_bytes: int, threads: int) -> dict:
+def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
     """Reference crc32c (oracle/_ref, built from /root/reference/karma-util/crc32c.cc) on host cores.
 
-    Bounded sample: 65536 records of rec_bytes of the same splitmix64 stream, repeated for
-    ~2 s on `threads` threads and ~2 s on one thread.
+    Bounded sample of the same workload, ~2 s on `threads` std::threads (records round-robin)
+    and ~2 s on one thread:
+      fixed/host -- 65536 records of rec_bytes of the same splitmix64 stream;
+      ragged     -- the first ~256 MiB of records of the configs[2] layout (same lengths, seed 7);
+      stream     -- 4 distinct 64 MiB segments (one thread per segment at most).
     """
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib  # the CPU checker; only the cpu_baseline leg touches it
     import synth
-    n = 65536 if rec_bytes <= 4096 else max(1, (256 << 20) // rec_bytes)
-    buf = synth.splitmix_np(42, 0, n * rec_bytes).copy()
-    out = np.empty(n, dtype=np.uint32)
     ref = oracle_lib.ref()
     kind = "reference" if ref is not None else "port"
+    if workload == "ragged":
+        lens_all = synth.loguniform_lengths(7, 1 << 20, 64, 65536)
+        k = int(np.searchsorted(np.cumsum(lens_all, dtype=np.uint64), np.uint64(256 << 20)))
+        lens = lens_all[:max(k, 1)].astype(np.uint32)
+        offs, arena_bytes = synth.ragged_layout(lens, header=8)
+        buf = synth.splitmix_np(42, 0, arena_bytes + 16).copy()
+        offs = np.ascontiguousarray(offs.astype(np.uint64))
+        n, nbytes = lens.size, int(lens.sum())
+        out = np.empty(n, dtype=np.uint32)
+        desc = f"{n} ragged records (log-uniform 64 B-64 KiB, configs[2] layout, {nbytes >> 20} MiB payload)"
 
-    def run(nthr):
-        if ref is not None:
-            ref.ref_crc32c_fixed_mt(buf.ctypes.data, rec_bytes, n, out.ctypes.data, nthr)
+        def run(nthr):
+            if ref is not None:
+                ref.ref_crc32c_ragged_mt(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, n,
+                                         out.ctypes.data, nthr)
+            else:
+                oracle_lib.port().oracle_ragged_crcs(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, n,
+                                                     out.ctypes.data, nthr)
+    else:
+        if workload == "stream":
+            rec_bytes, n = 64 << 20, 4
+            threads = min(threads, n)
         else:
-            oracle_lib.port().oracle_fixed_crcs(buf.ctypes.data, rec_bytes, n, out.ctypes.data, nthr)
+            n = 65536 if rec_bytes <= 4096 else max(1, (256 << 20) // rec_bytes)
+        buf = synth.splitmix_np(42, 0, n * rec_bytes).copy()
+        out = np.empty(n, dtype=np.uint32)
+        nbytes = n * rec_bytes
+        desc = f"{n} x {rec_bytes} B splitmix64 records ({nbytes >> 20} MiB)"
+
+        def run(nthr):
+            if ref is not None:
+                ref.ref_crc32c_fixed_mt(buf.ctypes.data, rec_bytes, n, out.ctypes.data, nthr)
+            else:
+                oracle_lib.port().oracle_fixed_crcs(buf.ctypes.data, rec_bytes, n, out.ctypes.data, nthr)
 
     def rate(nthr, budget):
         run(nthr)
@@ -77,7 +105,7 @@ def cpu_baseline(rec_bytes: int, threads: int) -> dict:
             reps += 1
             dt = time.perf_counter() - t0
             if dt > budget:
-                return reps * n * rec_bytes / dt / GIB, reps
+                return reps * nbytes / dt / GIB, reps
 
     multi, reps_m = rate(threads, 2.0)
     single, reps_s = rate(1, 2.0)
@@ -91,8 +119,8 @@ def cpu_baseline(rec_bytes: int, threads: int) -> dict:
     except OSError:
         pass
     return {"value": round(multi, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{n} x {rec_bytes} B splitmix64 records ({n * rec_bytes >> 20} MiB), crc32c::Value per "
-                      f"record, round-robin over {threads} std::threads, repeated {reps_m}x (~2 s)",
+            "sample": f"{desc}, crc32c::Value per record, round-robin over {threads} std::threads, "
+                      f"repeated {reps_m}x (~2 s)",
             "single_thread_value": round(single, 3), "cpu_model": cpu, "host_cores_visible": os.cpu_count()}
 
 
@@ -261,12 +289,22 @@ def main():
 
     # ---- timed region: K steps between barrier + synchronize --------------------------------
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # the dominant kernel alone (k_units_*), bracketed inside the library on the launch stream
+    uev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    timed_units = wl != "host"
+    if timed_units:
+        for a, b in uev:  # materialise the hipEvents so their raw handles exist
+            a.record(stream)
+            b.record(stream)
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
+        if timed_units:
+            L.karma_crc32c_time_next_units(uev[i][0].cuda_event, uev[i][1].cuda_event)
         crc_step()
         ev[i][1].record(stream)
         gather_step()
@@ -275,14 +313,16 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    call_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_ms = [a.elapsed_time(b) for a, b in uev] if timed_units else call_ms
     kern_avg = float(np.mean(kern_ms))
+    call_avg = float(np.mean(call_ms))
     if world > 1:
-        t = torch.tensor([elapsed, kern_avg], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_avg, call_avg], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_max = float(t[0]), float(t[1])
+        elapsed, kern_max, call_max = float(t[0]), float(t[1]), float(t[2])
     else:
-        kern_max = kern_avg
+        kern_max, call_max = kern_avg, call_avg
 
     # ---- self-check: a sample of records against the host crc32c::Extend (product path) ----
     check = {}
@@ -320,16 +360,16 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(algo_bytes),
-                         "kernel_ms_avg": round(kern_avg, 4), "kernel_ms_max_over_ranks": round(kern_max, 4)},
-            "compute_only_gibs": round(payload * world / (kern_max * 1e-3) / GIB, 2),
+                         "kernel_ms_avg": round(kern_avg, 4), "kernel_ms_max_over_ranks": round(kern_max, 4),
+                         "call_ms_avg": round(call_avg, 4),
+                         "call_frac": round(algo_bytes / (call_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "compute_only_gibs": round(payload * world / (call_max * 1e-3) / GIB, 2),
         }
         if check:
             res["self_check"] = check
-        if world == 1 and not args.no_cpu_baseline and wl in ("fixed", "host"):
+        if world == 1 and not args.no_cpu_baseline:
             thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            res["cpu_baseline"] = cpu_baseline(rec, thr)
-        elif world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = None
+            res["cpu_baseline"] = cpu_baseline(wl, rec, thr)
         print(json.dumps(res), flush=True)
 
     if comm is not None:

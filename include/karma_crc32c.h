@@ -16,6 +16,8 @@
  *   karma_crc32c_*_sharded / gather the same, records sharded over GPUs, CRCs gathered over RCCL
  *   karma_wal_append_batch          sivir::build_sqe + segment_file::append_record   sivir.cc:276-317
  *   karma_wal_replay                sivir::open's wal::scan_record loop              sivir.cc:31-41, wal.cc:34-87
+ *   karma_kfp_encode_batch          transport::frame::encode                         frame.cc:41-60
+ *   karma_kfp_parse_batch           connection::read_frame's frame::parse loop       connection.cc:20-27, frame.cc:62-130
  *
  * Errors: 0 = success, negative = KARMA_E_* below.  No entry point throws.
  * There is no CPU fallback behind the device entry points: without a usable
@@ -124,6 +126,41 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                      int device);
 
+/* ---- KFP frames (karma-transport) ------------------------------------------
+ * Frame (frame.cc:29-60): [frame_length u32][magic u8 = 123][operation_code i16][flag u8]
+ * [seq u32][header_length u32][header][payload][crc u32], integers little-endian,
+ * frame_length = 16 + header + payload + 4, crc = Extend(Value(header), payload). */
+#define KARMA_KFP_MAGIC 123                 /* frame.h:20 */
+#define KARMA_KFP_FIXED_HEADER 16           /* frame.h:21 */
+#define KARMA_KFP_MAX_FRAME (4096u * 128u)  /* frame.h:23 */
+#define KARMA_KFP_OK 0              /* every complete frame parsed; the rest is an incomplete frame */
+#define KARMA_KFP_BAD_SIZE 1        /* frame_length > MAX_FRAME_SIZE        (frame.cc:70-73 throws) */
+#define KARMA_KFP_BAD_MAGIC 2       /* magic != 123                          (frame.cc:86-89 throws) */
+#define KARMA_KFP_BAD_HEADER_LEN 3  /* header_length > frame_length - 20     (frame.cc:101-104 throws) */
+#define KARMA_KFP_BAD_CRC 4         /* stored crc != computed                (frame.cc:125-128 throws) */
+#define KARMA_KFP_BAD_LENGTH 5      /* frame_length < 20: undefined behaviour in the reference
+                                       (unsigned wrap at frame.cc:101,111); refused here */
+
+/* Encode frames i = 0..n-1 back to back into h_out (frame::encode): header bytes
+ * h_hdr + h_hdr_off[i] (h_hdr_len[i]), payload h_pay + h_pay_off[i] (h_pay_len[i]),
+ * operation code, flag and seq per frame.  The CRCs of all frames come from one GPU
+ * batch.  Frames that do not fit out_bytes are left for the next call: *h_n_encoded
+ * frames, *h_bytes bytes written; h_frame_off[i] (optional) = offset of frame i. */
+int karma_kfp_encode_batch(const void* h_hdr, const uint64_t* h_hdr_off, const uint32_t* h_hdr_len,
+                           const void* h_pay, const uint64_t* h_pay_off, const uint32_t* h_pay_len,
+                           const int16_t* h_op, const uint8_t* h_flag, const uint32_t* h_seq, size_t n, void* h_out,
+                           size_t out_bytes, uint64_t* h_frame_off, size_t* h_n_encoded, uint64_t* h_bytes,
+                           int device);
+
+/* Parse a receive buffer the way connection::read_frame drains it: frame::parse at the
+ * cursor, advance by frame_length, repeat (at most max_frames).  *h_n_frames frames were
+ * accepted (offsets in h_frame_off, optional, capacity max_frames); *h_consumed = bytes
+ * they occupy = where parsing stopped; *h_status = KARMA_KFP_*.  All frame CRCs are
+ * verified in one GPU batch, from d_buf when a device copy of the buffer is given. */
+int karma_kfp_parse_batch(const void* h_buf, const void* d_buf, size_t buf_bytes, size_t max_frames,
+                          uint64_t* h_frame_off, size_t* h_n_frames, uint64_t* h_consumed, int* h_status,
+                          int device);
+
 /* ---- synthetic data and probes (bench / tests) ---------------------------- */
 /* d_dst[i] = byte (first_byte + i) of the little-endian splitmix64 stream of
  * `seed` (word j = mix(seed + (j+1)*0x9E3779B97F4A7C15)); first_byte % 8 == 0. */
@@ -132,6 +169,12 @@ int karma_fill_splitmix64(void* d_dst, size_t n_bytes, uint64_t seed, uint64_t f
 int karma_stream_probe(const void* d_src, size_t n_bytes, uint32_t* d_out, karma_stream_t stream);
 /* Number of compute units of the current device (grid sizing, reporting). */
 int karma_device_cu_count(void);
+
+/* Instrumentation: arm two hipEvent_t (created by the caller with timing enabled).  The next
+ * batch call on this thread records them on its stream immediately before and after its
+ * dominant kernel (the units kernel: k_units_fixed / k_units_ragged), so a caller can time that
+ * kernel alone.  Passing (NULL, NULL) disarms. */
+int karma_crc32c_time_next_units(void* start_event, void* stop_event);
 
 #ifdef __cplusplus
 }

@@ -44,9 +44,13 @@ SIGNATURES = {
     "karma_wal_append_batch": (_i, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, _c.POINTER(_u64), _vp, _c.POINTER(_sz), _i]),
     "karma_wal_replay": (_i, [_vp, _vp, _sz, _sz, _u64, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_i), _vp, _sz,
                               _i]),
+    "karma_kfp_encode_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _c.POINTER(_sz),
+                                    _c.POINTER(_u64), _i]),
+    "karma_kfp_parse_batch": (_i, [_vp, _vp, _sz, _sz, _vp, _c.POINTER(_sz), _c.POINTER(_u64), _c.POINTER(_i), _i]),
     "karma_fill_splitmix64": (_i, [_vp, _sz, _u64, _u64, _vp]),
     "karma_stream_probe": (_i, [_vp, _sz, _vp, _vp]),
     "karma_device_cu_count": (_i, []),
+    "karma_crc32c_time_next_units": (_i, [_vp, _vp]),
 }
 
 

@@ -266,6 +266,17 @@ struct Locked {
 }  // namespace
 
 namespace karma::engine {
+namespace {
+thread_local hipEvent_t t_units_start = nullptr, t_units_stop = nullptr;
+}
+void units_timer_begin(hipStream_t s) {
+    if (t_units_start) (void)hipEventRecord(t_units_start, s);
+}
+void units_timer_end(hipStream_t s) {
+    if (!t_units_start) return;
+    if (t_units_stop) (void)hipEventRecord(t_units_stop, s);
+    t_units_start = t_units_stop = nullptr;
+}
 // shared with rccl_comm.cc so RCCL failures land in karma_crc32c_last_error()
 int set_last_error(int code, const std::string& what) { return fail(code, what); }
 }  // namespace karma::engine
@@ -287,6 +298,13 @@ const char* karma_crc32c_strerror(int status) {
 }
 
 const char* karma_crc32c_last_error(void) { return g_last.c_str(); }
+
+int karma_crc32c_time_next_units(void* start_event, void* stop_event) {
+    if (!start_event != !stop_event) return fail(KARMA_E_INVALID, "time_next_units: give both events or neither");
+    karma::engine::t_units_start = static_cast<hipEvent_t>(start_event);
+    karma::engine::t_units_stop = static_cast<hipEvent_t>(stop_event);
+    return 0;
+}
 
 int karma_device_cu_count(void) {
     Locked L;

@@ -123,12 +123,14 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     const uint64_t units = a.n_rec * a.units_per_rec;
     const uint64_t need = (units + kGroupsPerWave * kWavesPerBlock - 1) / (kGroupsPerWave * kWavesPerBlock);
     const dim3 grid((unsigned)(need < (uint64_t)grid_blocks ? need : (uint64_t)grid_blocks));
+    units_timer_begin(s);
     switch (fixed_variant()) {
         case 1: hipLaunchKernelGGL((k_units_fixed<4, false>), grid, dim3(kBlockThreads), 0, s, a); break;
         case 2: hipLaunchKernelGGL((k_units_fixed<2, true>), grid, dim3(kBlockThreads), 0, s, a); break;
         case 3: hipLaunchKernelGGL((k_units_fixed<6, true>), grid, dim3(kBlockThreads), 0, s, a); break;
         default: hipLaunchKernelGGL((k_units_fixed<4, true>), grid, dim3(kBlockThreads), 0, s, a); break;
     }
+    units_timer_end(s);
     return hipGetLastError();
 }
 

@@ -348,7 +348,9 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     if (a.n_rec == 0) return hipSuccess;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
     hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+    units_timer_begin(s);
     hipLaunchKernelGGL(k_units_ragged, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    units_timer_end(s);
     uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
     const uint64_t cap = 2 * (uint64_t)grid_blocks;
     if (fblocks > cap) fblocks = cap;

@@ -95,6 +95,11 @@ struct RaggedArgs {
     const uint32_t* comb_blob; // kCombWords for unit_bytes
 };
 
+// Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
+// recorded on `s` immediately around the next units kernel launched by this thread.
+void units_timer_begin(hipStream_t s);
+void units_timer_end(hipStream_t s);
+
 // Launchers (stream-ordered, no allocation, no synchronisation).
 hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s);
 // True when the continuous-stream kernel applies (aligned arena, whole-chunk units).

@@ -1,0 +1,150 @@
+// karma_amd/csrc/kfp.cc -- batched KFP frame encode / parse on top of the GPU
+// CRC batches.
+//
+// Frame layout (karma-transport/frame.cc:29-60, frame.h:20-23), native
+// little-endian integers:
+//   [frame_length u32][magic u8 = 123][operation_code i16][flag u8][seq u32]
+//   [header_length u32][header][payload][crc u32]
+// frame_length = 16 + header + payload + 4, and
+// crc = Extend(Value(header), payload) (frame.cc:56-57).  Header and payload
+// are adjacent in the frame, so crc = Value(frame[16, frame_length - 4)): one
+// span per frame, which is what the ragged batch checksums.
+//
+// karma_kfp_encode_batch = frame::encode for n frames written back to back.
+// karma_kfp_parse_batch  = connection::read_frame's loop over a receive buffer
+//   (connection.cc:20-27): frame::parse at the cursor (frame.cc:62-130), erase
+//   frame->size() bytes, repeat.  It stops where parse returns nullopt
+//   (incomplete frame) or throws (bad size / magic / header length / crc).
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "karma_crc32c.h"
+
+namespace karma::engine {
+int set_last_error(int code, const std::string& what);  // capi.cc
+int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std::vector<uint64_t>& off,
+              const std::vector<uint32_t>& len, std::vector<uint32_t>& out, int device);  // wal.cc
+}  // namespace karma::engine
+
+namespace {
+
+constexpr uint32_t kFixed = KARMA_KFP_FIXED_HEADER;  // frame.h:21
+constexpr uint32_t kCrcLen = 4;                      // frame.h:22
+
+inline uint32_t le32(const uint8_t* p) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;
+}
+
+int fail(int code, const char* what) { return karma::engine::set_last_error(code, what); }
+
+}  // namespace
+
+extern "C" {
+
+int karma_kfp_encode_batch(const void* h_hdr, const uint64_t* h_hdr_off, const uint32_t* h_hdr_len,
+                           const void* h_pay, const uint64_t* h_pay_off, const uint32_t* h_pay_len,
+                           const int16_t* h_op, const uint8_t* h_flag, const uint32_t* h_seq, size_t n, void* h_out,
+                           size_t out_bytes, uint64_t* h_frame_off, size_t* h_n_encoded, uint64_t* h_bytes,
+                           int device) {
+    if (!h_n_encoded || !h_bytes || (n && (!h_hdr_len || !h_pay_len || !h_op || !h_flag || !h_seq || !h_out)))
+        return fail(KARMA_E_INVALID, "kfp_encode_batch: null argument");
+    const uint8_t* hdr = static_cast<const uint8_t*>(h_hdr);
+    const uint8_t* pay = static_cast<const uint8_t*>(h_pay);
+    uint8_t* out = static_cast<uint8_t*>(h_out);
+    std::vector<uint64_t> span_off;
+    std::vector<uint32_t> span_len;
+    uint64_t cur = 0;
+    size_t i = 0;
+    for (; i < n; ++i) {
+        const uint64_t hl = h_hdr_len[i], pl = h_pay_len[i];
+        const uint64_t fl = kFixed + hl + pl + kCrcLen;
+        if (fl > 0xFFFFFFFFull) return fail(KARMA_E_INVALID, "kfp_encode_batch: frame_length overflows u32");
+        if ((hl && (!hdr || !h_hdr_off)) || (pl && (!pay || !h_pay_off)))
+            return fail(KARMA_E_INVALID, "kfp_encode_batch: null header/payload source");
+        if (cur + fl > out_bytes) break;  // the rest does not fit: caller flushes and continues
+        uint8_t* f = out + cur;
+        const uint32_t fl32 = static_cast<uint32_t>(fl), hl32 = static_cast<uint32_t>(hl);
+        std::memcpy(f, &fl32, 4);
+        f[4] = KARMA_KFP_MAGIC;
+        std::memcpy(f + 5, &h_op[i], 2);
+        f[7] = h_flag[i];
+        std::memcpy(f + 8, &h_seq[i], 4);
+        std::memcpy(f + 12, &hl32, 4);
+        if (hl) std::memcpy(f + kFixed, hdr + h_hdr_off[i], hl);
+        if (pl) std::memcpy(f + kFixed + hl, pay + h_pay_off[i], pl);
+        if (h_frame_off) h_frame_off[i] = cur;
+        span_off.push_back(cur + kFixed);
+        span_len.push_back(static_cast<uint32_t>(hl + pl));
+        cur += fl;
+    }
+    // Extend(Value(header), payload) of every frame in one batch over the encoded bytes
+    std::vector<uint32_t> crc;
+    if (const int rc = karma::engine::crc_spans(out, nullptr, cur, span_off, span_len, crc, device)) return rc;
+    for (size_t k = 0; k < crc.size(); ++k) std::memcpy(out + span_off[k] + span_len[k], &crc[k], 4);
+    *h_n_encoded = i;
+    *h_bytes = cur;
+    return 0;
+}
+
+int karma_kfp_parse_batch(const void* h_buf, const void* d_buf, size_t buf_bytes, size_t max_frames,
+                          uint64_t* h_frame_off, size_t* h_n_frames, uint64_t* h_consumed, int* h_status,
+                          int device) {
+    if (!h_n_frames || !h_consumed || !h_status || (buf_bytes && !h_buf))
+        return fail(KARMA_E_INVALID, "kfp_parse_batch: null argument");
+    const uint8_t* b = static_cast<const uint8_t*>(h_buf);
+    // 1. structural walk: parse's checks in its order (frame.cc:64-116)
+    std::vector<uint64_t> frame, span_off;
+    std::vector<uint32_t> span_len, stored;
+    uint64_t cur = 0;
+    int status = KARMA_KFP_OK;
+    while (frame.size() < max_frames) {
+        const uint64_t avail = buf_bytes - cur;
+        if (avail < kFixed + kCrcLen) break;  // nullopt: wait for more bytes (:64-66)
+        const uint32_t fl = le32(b + cur);
+        if (fl > KARMA_KFP_MAX_FRAME) {  // throws "decoded frame size is larger than the limit" (:70-73)
+            status = KARMA_KFP_BAD_SIZE;
+            break;
+        }
+        if (avail < fl) break;                  // nullopt: incomplete frame (:75-77)
+        if (b[cur + 4] != KARMA_KFP_MAGIC) {    // throws "Wrong magic code" (:86-89)
+            status = KARMA_KFP_BAD_MAGIC;
+            break;
+        }
+        if (fl < kFixed + kCrcLen) {  // unsigned wrap in :101 and :111-113: undefined in the reference
+            status = KARMA_KFP_BAD_LENGTH;
+            break;
+        }
+        const uint32_t hl = le32(b + cur + 12);
+        if (hl > fl - kFixed - kCrcLen) {  // throws "Wrong header length" (:101-104)
+            status = KARMA_KFP_BAD_HEADER_LEN;
+            break;
+        }
+        frame.push_back(cur);
+        span_off.push_back(cur + kFixed);
+        span_len.push_back(fl - kFixed - kCrcLen);
+        stored.push_back(le32(b + cur + fl - kCrcLen));
+        cur += fl;  // read_frame erases frame->size() == frame_length bytes (connection.cc:25)
+    }
+    // 2. every frame's crc in one GPU batch; the first mismatch throws "Wrong crc32" (:125-128)
+    std::vector<uint32_t> got;
+    if (const int rc = karma::engine::crc_spans(h_buf, d_buf, buf_bytes, span_off, span_len, got, device)) return rc;
+    size_t ok = frame.size();
+    for (size_t k = 0; k < got.size(); ++k)
+        if (got[k] != stored[k]) {
+            ok = k;
+            status = KARMA_KFP_BAD_CRC;
+            cur = frame[k];
+            break;
+        }
+    if (h_frame_off)
+        for (size_t k = 0; k < ok; ++k) h_frame_off[k] = frame[k];
+    *h_n_frames = ok;
+    *h_consumed = cur;
+    *h_status = status;
+    return 0;
+}
+
+}  // extern "C"

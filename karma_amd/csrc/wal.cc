@@ -32,7 +32,36 @@
 
 namespace karma::engine {
 int set_last_error(int code, const std::string& what);  // capi.cc
+
+int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std::vector<uint64_t>& off,
+              const std::vector<uint32_t>& len, std::vector<uint32_t>& out, int device) {
+    out.resize(off.size());
+    if (off.empty()) return 0;
+    if (!d_buf) return karma_crc32c_batch_ragged_host(h_buf, buf_bytes, off.data(), len.data(), off.size(), 0,
+                                                      out.data(), device);
+    // device copy supplied: stage the offsets/lengths and run the device batch
+    uint64_t total = 0;
+    for (uint32_t l : len) total += l;
+    if (device >= 0 && hipSetDevice(device) != hipSuccess) return set_last_error(KARMA_E_HIP, "hipSetDevice");
+    void *doff = nullptr, *dlen = nullptr, *dout = nullptr;
+    int rc = 0;
+    if (hipMalloc(&doff, off.size() * 8) != hipSuccess || hipMalloc(&dlen, len.size() * 4) != hipSuccess ||
+        hipMalloc(&dout, out.size() * 4) != hipSuccess)
+        rc = set_last_error(KARMA_E_NOMEM, "crc_spans: hipMalloc");
+    else if (hipMemcpy(doff, off.data(), off.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(dlen, len.data(), len.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        rc = set_last_error(KARMA_E_HIP, "crc_spans: hipMemcpy H2D");
+    else if ((rc = karma_crc32c_batch_ragged(d_buf, static_cast<uint64_t*>(doff), static_cast<uint32_t*>(dlen),
+                                             off.size(), total, nullptr, 0, static_cast<uint32_t*>(dout), nullptr)))
+        ;
+    else if (hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = set_last_error(KARMA_E_HIP, "crc_spans: hipMemcpy D2H");
+    (void)hipFree(doff);
+    (void)hipFree(dlen);
+    (void)hipFree(dout);
+    return rc;
 }
+}  // namespace karma::engine
 
 namespace {
 
@@ -216,36 +245,7 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
             idx.push_back(i);
         }
     std::vector<uint32_t> got(off.size());
-    if (!off.empty()) {
-        int rc;
-        if (d_wal) {
-            // device copy supplied: stage the offsets/lengths and run the device batch
-            uint64_t total = 0;
-            for (uint32_t l : len) total += l;
-            void *doff = nullptr, *dlen = nullptr, *dout = nullptr;
-            if (device >= 0 && hipSetDevice(device) != hipSuccess) return KARMA_E_HIP;
-            if (hipMalloc(&doff, off.size() * 8) != hipSuccess || hipMalloc(&dlen, len.size() * 4) != hipSuccess ||
-                hipMalloc(&dout, got.size() * 4) != hipSuccess) {
-                (void)hipFree(doff);
-                (void)hipFree(dlen);
-                return KARMA_E_NOMEM;
-            }
-            rc = (hipMemcpy(doff, off.data(), off.size() * 8, hipMemcpyHostToDevice) == hipSuccess &&
-                  hipMemcpy(dlen, len.data(), len.size() * 4, hipMemcpyHostToDevice) == hipSuccess)
-                     ? karma_crc32c_batch_ragged(d_wal, static_cast<uint64_t*>(doff), static_cast<uint32_t*>(dlen),
-                                                 off.size(), total, nullptr, 0, static_cast<uint32_t*>(dout), nullptr)
-                     : KARMA_E_HIP;
-            if (!rc && hipMemcpy(got.data(), dout, got.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
-                rc = KARMA_E_HIP;
-            (void)hipFree(doff);
-            (void)hipFree(dlen);
-            (void)hipFree(dout);
-        } else {
-            rc = karma_crc32c_batch_ragged_host(wal, wal_bytes, off.data(), len.data(), off.size(), 0, got.data(),
-                                                device);
-        }
-        if (rc) return rc;
-    }
+    if (const int rc = karma::engine::crc_spans(h_wal, d_wal, wal_bytes, off, len, got, device)) return rc;
     // 3. the first mismatch (in WAL order) is where scan_record logs "Corrupt record"
     size_t accepted = all.size();
     for (size_t j = 0; j < idx.size(); ++j)
