@@ -110,7 +110,8 @@ int karma_crc32c_batch_fixed_sharded(karma_comm_t comm, const void* d_local, siz
  * closing a segment with a footer when a record does not fit (can_hold).  The CRCs of
  * the whole batch come from one GPU batch.  Updates *h_cursor, writes the header offset
  * of record i to h_rec_off[i] (optional) and the number framed to *h_n_framed (records
- * that do not fit in the image are left out). */
+ * that do not fit in the image are left out).  On an error *h_cursor is unchanged;
+ * bytes past it may have been written (without valid CRC fields). */
 int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const uint32_t* h_len, size_t n,
                            void* h_wal, size_t wal_bytes, size_t seg_bytes, uint64_t* h_cursor, uint64_t* h_rec_off,
                            size_t* h_n_framed, int device);

@@ -192,7 +192,7 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     L.pslot_off = align256((n_rec + 2) * sizeof(uint64_t));
     L.sums_off = L.pslot_off + align256(2 * n_rec * sizeof(uint64_t));
     L.bucket_off = L.sums_off + align256(nb * sizeof(uint64_t));
-    L.desc_off = L.bucket_off + align256(kBuckets * sizeof(uint64_t));
+    L.desc_off = L.bucket_off + align256((kBuckets + 1) * sizeof(uint64_t));
     L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
     L.total = L.part_off + align256(cap * sizeof(uint32_t));
     return L;

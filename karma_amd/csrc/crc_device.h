@@ -160,8 +160,18 @@ __device__ __forceinline__ uint32_t tail_register(const uint32_t* lds, int z4, i
     return r;
 }
 
+// MODE (timing experiments only, wrong results): bit 0 = main-loop steps without the
+// LDS lookups, bit 1 = group epilogue without lookups.  The shipped kernels use MODE 0.
+template <int MODE = 0>
 __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
                                       uint32_t& a3, const u32x4& v) {
+    if constexpr (MODE & 1) {
+        a0 = ((a0 << 1) | (a0 >> 31)) ^ v.x;
+        a1 = ((a1 << 1) | (a1 >> 31)) ^ v.y;
+        a2 = ((a2 << 1) | (a2 >> 31)) ^ v.z;
+        a3 = ((a3 << 1) | (a3 >> 31)) ^ v.w;
+        return;
+    }
     a0 = stride_step(lds, X, a0, v.x);
     a1 = stride_step(lds, X, a1, v.y);
     a2 = stride_step(lds, X, a2, v.z);
@@ -184,7 +194,7 @@ __device__ __forceinline__ const uint8_t* floor128(const uint8_t* p) {
 // word carries the record's entering register).  PF chunk loads stay in flight
 // per lane.  Every lane of the wave must call this (cross-lane shuffles); the
 // result is valid in group lane 0.
-template <int PF, bool NT>
+template <int PF, bool NT, int MODE = 0>
 __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, uint32_t l, const uint8_t* us,
                                                const uint8_t* ue, const uint8_t* inj_at, uint32_t inj) {
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
@@ -219,13 +229,20 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
 #pragma unroll
             for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
 #pragma unroll
-            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+            for (int q = 0; q < PF; ++q) step4<MODE>(lds, X, a0, a1, a2, a3, cur[q]);
             rem -= PF;
         }
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
-            if (q < rem - 1 || (q == rem - 1 && lok)) step4(lds, X, a0, a1, a2, a3, nb[q]);
+            if (q < rem - 1 || (q == rem - 1 && lok)) step4<MODE>(lds, X, a0, a1, a2, a3, nb[q]);
         }
+    }
+    if constexpr ((MODE & 2) != 0) {
+        uint32_t c = a0 ^ a1 ^ a2 ^ a3;
+        c ^= __shfl_down(c, 1, kGroupLanes);
+        c ^= __shfl_down(c, 2, kGroupLanes);
+        c ^= __shfl_down(c, 4, kGroupLanes);
+        return c;
     }
     // lane fold (crc32c.cc STEP4W order): c = Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0))))
     uint32_t c = zmap(lds, kLZ4, a0);
@@ -245,16 +262,48 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
     return c;
 }
 
-__device__ __forceinline__ void load_stream_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
-    for (int i = threadIdx.x; i < kSmallWords; i += blockDim.x) lds[kSmallBase + i] = blob[1024 + i];
-    // word index = region*16384 + row*64 + half*32 + lane32; table k = region*2 + half
+// Copy WORDS words (WORDS % 4 == 0, both pointers 16-byte aligned) from global
+// memory into LDS with THREADS threads: every thread issues all of its 16-byte
+// loads before its first LDS store, so the copy costs about one memory latency
+// instead of one per loop trip.
+template <int WORDS, int THREADS>
+__device__ __forceinline__ void copy_to_lds(uint32_t* lds, const uint32_t* __restrict__ g) {
+    static_assert(WORDS % 4 == 0, "whole 16-byte vectors");
+    constexpr int N4 = WORDS / 4;
+    constexpr int IT = (N4 + THREADS - 1) / THREADS;
+    const u32x4* g4 = reinterpret_cast<const u32x4*>(g);
     u32x4* l4 = reinterpret_cast<u32x4*>(lds);
-    for (int i = threadIdx.x; i < kRepWords / 4; i += blockDim.x) {
-        const int idx = i * 4;
-        const int region = idx >> 14, row = (idx >> 6) & 255, half = (idx >> 5) & 1;
-        const uint32_t v = blob[kBlobStride + (region * 2 + half) * 256 + row];
-        l4[i] = u32x4{v, v, v, v};
+    u32x4 v[IT];
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int i = (int)threadIdx.x + q * THREADS;
+        if (i < N4) v[q] = *(const gu32x4*)(g4 + i);
     }
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int i = (int)threadIdx.x + q * THREADS;
+        if (i < N4) l4[i] = v[q];
+    }
+}
+
+// The streaming kernels' LDS image (kBlockThreads threads).
+__device__ __forceinline__ void load_stream_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
+    static_assert(kSmallWords % 4 == 0 && (kRepWords / 4) % kBlockThreads == 0, "table copy shape");
+    // word index = region*16384 + row*64 + half*32 + lane32; table k = region*2 + half.
+    // Each 16-byte LDS vector holds 4 copies of one entry; a thread's entries
+    // are blob words 0..1023 (the 4 Z_S tables), read once each.
+    constexpr int IT = kRepWords / 4 / kBlockThreads;
+    uint32_t e[IT];
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int idx = ((int)threadIdx.x + q * kBlockThreads) * 4;
+        const int region = idx >> 14, row = (idx >> 6) & 255, half = (idx >> 5) & 1;
+        e[q] = *(const __attribute__((address_space(1))) uint32_t*)(blob + kBlobStride + (region * 2 + half) * 256 + row);
+    }
+    copy_to_lds<kSmallWords, kBlockThreads>(lds + kSmallBase, blob + 1024);
+    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
+#pragma unroll
+    for (int q = 0; q < IT; ++q) l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e[q], e[q], e[q], e[q]};
 }
 
 // Per-lane constant of the replicated-table address (see the LDS image above).
@@ -264,9 +313,9 @@ __device__ __forceinline__ uint32_t lane_const() {
 }
 
 // ---- combine-blob LDS image: Z_{D*2^k} (k = 0..6), Z4, byte table ----------
-template <int WORDS = kCombWords>
+template <int WORDS = kCombWords, int THREADS = 1024>
 __device__ __forceinline__ void load_comb_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
-    for (int i = threadIdx.x; i < WORDS; i += blockDim.x) lds[i] = blob[i];
+    copy_to_lds<WORDS, THREADS>(lds, blob);
 }
 
 // Z_L for L = 16n, 0 < n < 256 (binary decomposition over Z_{16*2^i}).

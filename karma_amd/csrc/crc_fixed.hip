@@ -19,9 +19,9 @@ namespace {
 
 using namespace dev;
 
-template <int PF, bool NT>
+template <int PF, bool NT, int MODE = 0>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
-    __shared__ uint32_t lds[kLdsWords];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
                 inj = head_register(lds, kLZ4, kLT8, p, g, init);
             }
         }
-        uint32_t R = group_unit<PF, NT>(lds, X, l, us, ue, inj_at, inj);
+        uint32_t R = group_unit<PF, NT, MODE>(lds, X, l, us, ue, inj_at, inj);
         if (valid && l == 0) {
             if (g.is_short) {
                 A.out[r] = short_record(lds, kLZ4, kLT8, p, A.rec_bytes, init);
@@ -80,8 +80,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
 // adds the record tail and writes the CRC.  One wave per output state.
 __global__ __launch_bounds__(256) void k_combine_fixed(FixedArgs A, const uint32_t* in, uint64_t k_in, uint32_t* outs,
                                                       uint64_t k_out, const uint32_t* comb) {
-    __shared__ uint32_t lds[kCombCoreWords];
-    load_comb_tables<kCombCoreWords>(lds, comb);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords];
+    load_comb_tables<kCombCoreWords, 256>(lds, comb);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -128,6 +128,9 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
         case 1: hipLaunchKernelGGL((k_units_fixed<4, false>), grid, dim3(kBlockThreads), 0, s, a); break;
         case 2: hipLaunchKernelGGL((k_units_fixed<2, true>), grid, dim3(kBlockThreads), 0, s, a); break;
         case 3: hipLaunchKernelGGL((k_units_fixed<6, true>), grid, dim3(kBlockThreads), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_units_fixed<4, true, 1>), grid, dim3(kBlockThreads), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((k_units_fixed<4, true, 2>), grid, dim3(kBlockThreads), 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_units_fixed<4, true, 3>), grid, dim3(kBlockThreads), 0, s, a); break;
         default: hipLaunchKernelGGL((k_units_fixed<4, true>), grid, dim3(kBlockThreads), 0, s, a); break;
     }
     units_timer_end(s);

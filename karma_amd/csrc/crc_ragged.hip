@@ -6,7 +6,7 @@
 // body end) so every group of 8 lanes gets at most one unit's worth of work
 // regardless of how skewed the record sizes are:
 //
-//   k_ragged_scan1/2   full units per record -> exclusive scan (record order);
+//   k_ragged_scan      full units per record -> exclusive scan (record order);
 //                      partial first units -> buckets by chunk count, longest
 //                      first, after all full units
 //   k_ragged_desc      one thread per record: entering register over the
@@ -32,6 +32,9 @@ constexpr int kRaggedPF = 4;
 constexpr bool kRaggedNT = true;
 
 constexpr int kScanBlock = 1024;
+constexpr uint64_t kU = kDefaultUnit;  // ragged units: absolute kU-byte boundaries
+constexpr int kUShift = __builtin_ctzll(kDefaultUnit);
+static_assert((kU & (kU - 1)) == 0, "unit size is a power of two");
 
 // Unit layout of one record: the aligned body [a, b) cut at absolute multiples
 // of U = unit_bytes.  Unit j = [max(a, (A0+j)U), min(b, (A0+j+1)U)), A0 = a/U,
@@ -56,9 +59,9 @@ __device__ __forceinline__ RecUnits rec_units(const RaggedArgs& A, uint64_t r) {
     u.k = u.full = 0;
     u.part0 = u.part1 = u.c0 = u.c1 = u.last = 0;
     if (!u.g.is_short) {
-        const uint64_t U = A.unit_bytes;
+        constexpr uint64_t U = kU;
         const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
-        const uint64_t A0 = a / U, A1 = (b + U - 1) / U;
+        const uint64_t A0 = a >> kUShift, A1 = (b + U - 1) >> kUShift;
         u.k = A1 - A0;
         const uintptr_t e0 = (A0 + 1) * U < b ? (A0 + 1) * U : b;
         u.part0 = (e0 - a) < U ? 1u : 0u;
@@ -105,12 +108,20 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
     return pre + inc - v;
 }
 
+__device__ __forceinline__ uint64_t load_agent(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Per scan block: exclusive scan of full units; partial units counted per
 // bucket (chunk count) into the global bucket totals (one atomic per bucket
-// per block; the totals are zeroed by the launcher).
-__global__ __launch_bounds__(kScanBlock) void k_ragged_scan1(RaggedArgs A) {
+// per block; the totals and the done counter bucket_off[kBuckets] are zeroed
+// by the launcher).  The last block to finish then scans the block sums
+// (full-unit offsets, slots [0, F)) and turns the bucket totals into the start
+// of every partial bucket, longest (32 chunks) first (slots [F, U)).
+__global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
     __shared__ uint64_t sm[16];
     __shared__ uint32_t hist[kBuckets];
+    __shared__ bool last;
     if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     RecUnits u{};
@@ -126,25 +137,28 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan1(RaggedArgs A) {
     if (threadIdx.x == 0) A.block_sums[blockIdx.x] = total;
     if (threadIdx.x < kBuckets && hist[threadIdx.x])
         atomicAdd(reinterpret_cast<unsigned long long*>(&A.bucket_off[threadIdx.x]), (unsigned long long)hist[threadIdx.x]);
-}
-
-// Single block: full-unit offsets per scan block (slots [0, F)), then the
-// start of every partial bucket, longest (32 chunks) first (slots [F, U)).
-__global__ __launch_bounds__(kScanBlock) void k_ragged_scan2(RaggedArgs A, uint64_t nblocks) {
-    __shared__ uint64_t sm[16];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();  // this block's sums and totals before its done count
+        last = atomicAdd(reinterpret_cast<unsigned long long*>(&A.bucket_off[kBuckets]), 1ull) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const uint64_t nblocks = gridDim.x;
     uint64_t carry = 0;
     for (uint64_t base = 0; base < nblocks; base += blockDim.x) {
         const uint64_t i = base + threadIdx.x;
-        const uint64_t v = i < nblocks ? A.block_sums[i] : 0;
-        uint64_t total;
-        const uint64_t ex = block_excl_scan(v, sm, total);
-        if (i < nblocks) A.block_sums[i] = carry + ex;
-        carry += total;
+        const uint64_t v = i < nblocks ? load_agent(A.block_sums + i) : 0;
+        uint64_t t;
+        const uint64_t e = block_excl_scan(v, sm, t);
+        if (i < nblocks) A.block_sums[i] = carry + e;
+        carry += t;
     }
     if (threadIdx.x == 0) {
         const uint64_t F = carry;
         for (int c = kBuckets - 1; c >= 1; --c) {  // totals -> cursors
-            const uint64_t t = A.bucket_off[c];
+            const uint64_t t = load_agent(A.bucket_off + c);
             A.bucket_off[c] = carry;
             carry += t;
         }
@@ -155,17 +169,24 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan2(RaggedArgs A, uint6
 
 // One thread per record (block b = scan block b): final slots, the entering
 // register over the unaligned head, and the unit descriptors.  A block
-// reserves its range of every partial bucket with one atomic per bucket.
+// reserves its range of every partial bucket with one atomic per bucket; each
+// lane writes its record's (at most two) partial units.  The full units of a
+// wave's 64 records are consecutive slots: the wave writes them together, lane
+// t taking slot F0 + t and finding its record by a search over the lanes'
+// inclusive unit counts, so the descriptor stores are coalesced and balanced
+// however skewed the record sizes are.
 __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
-    __shared__ uint32_t lds[kCombCoreWords - kCombZ4];  // Z4 then the byte table
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4 then the byte table
     __shared__ unsigned long long cnt[kBuckets];
     __shared__ uint32_t hist[kBuckets];
-    for (int i = threadIdx.x; i < kCombCoreWords - kCombZ4; i += blockDim.x) lds[i] = A.comb_blob[kCombZ4 + i];
+    copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
     if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = r < A.n_rec;
     RecUnits u{};
-    if (r < A.n_rec) {
+    if (valid) {
         u = rec_units(A, r);
         if (u.part0) atomicAdd(&hist[u.c0], 1u);
         if (u.part1) atomicAdd(&hist[u.c1], 1u);
@@ -177,30 +198,44 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
                                            (unsigned long long)hist[threadIdx.x])
                                : 0ull;
     __syncthreads();
-    if (r >= A.n_rec) return;
-    const uint64_t fb = A.fbase[r] + A.block_sums[blockIdx.x];
-    A.fbase[r] = fb;
-    if (u.k == 0) return;
-    const uint8_t* p = A.arena + A.off[r];
-    const uint32_t init = A.init ? A.init[r] : A.init_scalar;
-    const uint32_t h = head_register(lds, 0, 1024, p, u.g, init);
-    const uint64_t U = A.unit_bytes;
+    uint64_t fb = 0;
+    uint32_t h = 0;
     const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
-    const uint64_t A0 = a / U;
-    for (uint64_t j = 0; j < u.k; ++j) {
-        const uintptr_t us = (A0 + j) * U > a ? (A0 + j) * U : a;
-        const uintptr_t ue = (A0 + j + 1) * U < b ? (A0 + j + 1) * U : b;
-        uint64_t slot;
-        if (j == 0 && u.part0) {
-            slot = atomicAdd(&cnt[u.c0], 1ull);
+    const uint64_t A0 = a >> kUShift;
+    if (valid) {
+        fb = A.fbase[r] + A.block_sums[blockIdx.x];
+        A.fbase[r] = fb;
+        if (u.k) h = head_register(lds, 0, 1024, A.arena + A.off[r], u.g, A.init ? A.init[r] : A.init_scalar);
+        if (u.part0) {
+            const uint64_t slot = atomicAdd(&cnt[u.c0], 1ull);
             A.pslot[2 * r] = slot;
-        } else if (j == u.k - 1 && u.part1) {
-            slot = atomicAdd(&cnt[u.c1], 1ull);
-            A.pslot[2 * r + 1] = slot;
-        } else {
-            slot = fb + j - u.part0;
+            const uintptr_t e0 = ((A0 + 1) << kUShift) < b ? ((A0 + 1) << kUShift) : b;
+            if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a), h};
         }
-        if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)us, (uint32_t)(ue - us), j == 0 ? h : 0u};
+        if (u.part1) {
+            const uint64_t slot = atomicAdd(&cnt[u.c1], 1ull);
+            A.pslot[2 * r + 1] = slot;
+            const uintptr_t s1 = (A0 + u.k - 1) << kUShift;
+            if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1), 0u};
+        }
+    }
+    // full units of the wave's records, slot F0 + t for t in [0, T)
+    const uint64_t nfull = valid ? u.full : 0;
+    const uint64_t incl = wave_incl_scan(nfull);
+    const uint64_t T = __shfl(incl, 63);
+    const uint64_t F0 = __shfl(fb, 0);
+    for (uint64_t base = 0; base < T; base += 64) {  // uniform trip count: shuffles see every lane
+        const uint64_t t = base + lane;
+        int o = 0;  // owner: the first lane whose inclusive count exceeds t
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1)
+            if (__shfl(incl, o + s - 1) <= t) o += s;
+        o = o < 63 ? o : 63;
+        const uint64_t incl_o = __shfl(incl, o), full_o = __shfl(nfull, o), A0_o = __shfl(A0, o);
+        const uint32_t part0_o = __shfl(u.part0, o), h_o = __shfl(h, o);
+        const uint64_t j = t - (incl_o - full_o) + part0_o;  // unit index within the owner's record
+        const uint64_t slot = F0 + t;
+        if (t < T && slot < A.unit_cap) A.desc[slot] = UnitDesc{(A0_o + j) << kUShift, (uint32_t)kU, j == 0 ? h_o : 0u};
     }
 }
 
@@ -212,7 +247,7 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
 }
 
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
-    __shared__ uint32_t lds[kLdsWords];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -254,11 +289,11 @@ __device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, 
 // ends, Z_last before the last unit), the unaligned tail, ~R.  Records of more
 // than 64 units: the whole wave folds all but the last unit with the 64-lane tree.
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
-    __shared__ uint32_t lds[kCombWords];
-    load_comb_tables(lds, A.comb_blob);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kCombWords];
+    load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t U = A.unit_bytes;
+    constexpr uint64_t U = kU;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t r0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; r0 < A.n_rec;
          r0 += nwaves * 64) {
@@ -336,11 +371,11 @@ uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock - 1) / 
 
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
+    if (a.unit_bytes != kU) return hipErrorInvalidValue;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
-    hipError_t e = hipMemsetAsync(a.bucket_off, 0, (kBuckets + 1) * sizeof(uint64_t), s);  // bucket totals (padded to 16 B: one fill)
+    hipError_t e = hipMemsetAsync(a.bucket_off, 0, (kBuckets + 1) * sizeof(uint64_t), s);  // bucket totals + done counter
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ragged_scan1, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
-    hipLaunchKernelGGL(k_ragged_scan2, dim3(1), dim3(kScanBlock), 0, s, a, nb);
+    hipLaunchKernelGGL(k_ragged_scan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     return hipGetLastError();
 }
 

