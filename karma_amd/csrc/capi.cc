@@ -338,123 +338,7 @@ int karma_crc32c_stream(uint32_t init, const void* d_data, size_t n, uint32_t* d
 
 }  // extern "C"
 
-// ---- host-memory batches ------------------------------------------------------
-namespace {
-
-struct HostPin {
-    void* p = nullptr;
-    bool registered = false;
-    HostPin(const void* ptr, size_t bytes) {
-        hipPointerAttribute_t attr;
-        if (!ptr || !bytes) return;
-        if (hipPointerGetAttributes(&attr, ptr) == hipSuccess && attr.type == hipMemoryTypeHost) return;  // pinned
-        (void)hipGetLastError();
-        if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) == hipSuccess) {
-            p = const_cast<void*>(ptr);
-            registered = true;
-        } else {
-            (void)hipGetLastError();
-        }
-    }
-    ~HostPin() {
-        if (registered) (void)hipHostUnregister(p);
-    }
-};
-
-struct DevBuf {
-    void* p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-};
-
-int select_device(int device) {
-    if (device >= 0) KARMA_HIP(hipSetDevice(device));
-    return 0;
-}
-
-}  // namespace
-
 extern "C" {
-
-int karma_crc32c_batch_fixed_host(const void* h_data, size_t rec_bytes, size_t n_rec, uint32_t init,
-                                  uint32_t* h_out, int device) {
-    if (n_rec == 0) return KARMA_OK;
-    if (!h_out || (!h_data && rec_bytes)) return fail(KARMA_E_INVALID, "batch_fixed_host: null pointer");
-    KARMA_RC(select_device(device));
-    // Chunks of ~64 MiB alternate over two streams: H2D(i+1) overlaps kernel(i).
-    const size_t chunk_recs = std::max<size_t>(1, rec_bytes ? (size_t(64) << 20) / std::max<size_t>(rec_bytes, 1) : n_rec);
-    const size_t nchunks = (n_rec + chunk_recs - 1) / chunk_recs;
-    const size_t slot_bytes = chunk_recs * rec_bytes;
-    HostPin pin_in(h_data, n_rec * rec_bytes);
-    HostPin pin_out(h_out, n_rec * sizeof(uint32_t));
-    DevBuf din, dout;
-    const int nslots = nchunks > 1 ? 2 : 1;
-    KARMA_HIP(hipMalloc(&din.p, std::max<size_t>(1, slot_bytes * nslots)));
-    KARMA_HIP(hipMalloc(&dout.p, chunk_recs * sizeof(uint32_t) * nslots));
-    hipStream_t st[2] = {nullptr, nullptr};
-    for (int i = 0; i < nslots; ++i) KARMA_HIP(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
-    int rc = 0;
-    for (size_t c = 0; c < nchunks && !rc; ++c) {
-        const int sl = (int)(c % nslots);
-        const size_t r0 = c * chunk_recs;
-        const size_t nr = std::min(chunk_recs, n_rec - r0);
-        char* dslot = static_cast<char*>(din.p) + sl * slot_bytes;
-        uint32_t* oslot = static_cast<uint32_t*>(dout.p) + sl * chunk_recs;
-        hipError_t e = hipMemcpyAsync(dslot, static_cast<const char*>(h_data) + r0 * rec_bytes, nr * rec_bytes,
-                                      hipMemcpyHostToDevice, st[sl]);
-        if (e != hipSuccess) {
-            rc = hip_fail(e, "H2D");
-            break;
-        }
-        rc = karma_crc32c_batch_fixed(dslot, rec_bytes, nr, nullptr, init, oslot, st[sl]);
-        if (rc) break;
-        e = hipMemcpyAsync(h_out + r0, oslot, nr * sizeof(uint32_t), hipMemcpyDeviceToHost, st[sl]);
-        if (e != hipSuccess) rc = hip_fail(e, "D2H");
-    }
-    for (int i = 0; i < nslots; ++i) {
-        hipError_t e = hipStreamSynchronize(st[i]);
-        if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
-        (void)hipStreamDestroy(st[i]);
-    }
-    return rc;
-}
-
-int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, const uint64_t* h_off,
-                                   const uint32_t* h_len, size_t n_rec, uint32_t init, uint32_t* h_out, int device) {
-    if (n_rec == 0) return KARMA_OK;
-    if (!h_out || !h_off || !h_len || (!h_arena && arena_bytes)) return fail(KARMA_E_INVALID, "batch_ragged_host");
-    KARMA_RC(select_device(device));
-    uint64_t total = 0;
-    for (size_t r = 0; r < n_rec; ++r) {
-        if (h_off[r] + h_len[r] > arena_bytes) return fail(KARMA_E_INVALID, "batch_ragged_host: record past arena");
-        total += h_len[r];
-    }
-    HostPin pin(h_arena, arena_bytes);
-    DevBuf da, doff, dlen, dout;
-    KARMA_HIP(hipMalloc(&da.p, std::max<size_t>(arena_bytes, 16)));
-    KARMA_HIP(hipMalloc(&doff.p, n_rec * sizeof(uint64_t)));
-    KARMA_HIP(hipMalloc(&dlen.p, n_rec * sizeof(uint32_t)));
-    KARMA_HIP(hipMalloc(&dout.p, n_rec * sizeof(uint32_t)));
-    hipStream_t s = nullptr;
-    KARMA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    int rc = 0;
-    hipError_t e = hipMemcpyAsync(da.p, h_arena, arena_bytes, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(doff.p, h_off, n_rec * sizeof(uint64_t), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(dlen.p, h_len, n_rec * sizeof(uint32_t), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) rc = hip_fail(e, "H2D");
-    if (!rc)
-        rc = karma_crc32c_batch_ragged(da.p, static_cast<uint64_t*>(doff.p), static_cast<uint32_t*>(dlen.p), n_rec,
-                                       total, nullptr, init, static_cast<uint32_t*>(dout.p), s);
-    if (!rc) {
-        e = hipMemcpyAsync(h_out, dout.p, n_rec * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-        if (e != hipSuccess) rc = hip_fail(e, "D2H");
-    }
-    e = hipStreamSynchronize(s);
-    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
-    (void)hipStreamDestroy(s);
-    return rc;
-}
 
 int karma_crc32c_batch_fixed_sharded(karma_comm_t comm, const void* d_local, size_t rec_bytes, size_t n_local,
                                      uint32_t init, uint32_t* d_local_out, uint32_t* d_all_out, int root,

@@ -6,6 +6,7 @@
 // tests/golden/ and as bench.py's cpu_baseline (kind "reference").  No
 // reference source is copied into this repository.
 #include <cstddef>
+#include <cstring>
 #include <cstdint>
 #include <thread>
 #include <vector>
@@ -45,6 +46,52 @@ int ref_crc32c_ragged_mt(const void* base, const uint64_t* off, const uint32_t* 
         });
     for (auto& x : th) x.join();
     return 0;
+}
+
+// Config 1 harness: segment_file::append_record / append_footer
+// framing (karma-store/segment_file.cc:21-49, can_hold :74-77) with the
+// reference's crc32c::Value, as sivir::build_sqe drives it (sivir.cc:276-317).
+// Thread t frames records [n*t/T, n*(t+1)/T) into its own WAL image
+// wal + t*wal_bytes (each thread its own writer).  Returns records framed.
+uint64_t ref_wal_append_mt(const void* src, const uint64_t* off, const uint32_t* len, uint64_t n, void* wal,
+                           uint64_t wal_bytes, uint64_t seg, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    const char* s = static_cast<const char*>(src);
+    std::vector<uint64_t> done(nthreads, 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+        th.emplace_back([=, &done] {
+            char* w = static_cast<char*>(wal) + (uint64_t)t * wal_bytes;
+            uint64_t cur = 0, cnt = 0;
+            for (uint64_t i = n * t / nthreads; i < n * (t + 1) / nthreads; ++i) {
+                const uint64_t l = len[i];
+                uint64_t seg_end = (cur / seg + 1) * seg;
+                if (cur + 8 + l > seg_end) {  // append_footer
+                    const uint64_t room = seg_end - cur;
+                    if (room < 8) {
+                        std::memset(w + cur, '0', room);
+                    } else {
+                        const uint32_t z = 0, st = uint32_t((room - 8) << 8 | 1u);
+                        std::memcpy(w + cur, &z, 4);
+                        std::memcpy(w + cur + 4, &st, 4);
+                        std::memset(w + cur + 8, '0', room - 8);
+                    }
+                    cur = seg_end;
+                }
+                if (cur + 8 + l > wal_bytes) break;
+                const uint32_t crc = crc32c::Value(s + off[i], l), st = uint32_t(l << 8);
+                std::memcpy(w + cur, &crc, 4);
+                std::memcpy(w + cur + 4, &st, 4);
+                std::memcpy(w + cur + 8, s + off[i], l);
+                cur += 8 + l;
+                ++cnt;
+            }
+            done[t] = cnt;
+        });
+    for (auto& x : th) x.join();
+    uint64_t total = 0;
+    for (uint64_t d : done) total += d;
+    return total;
 }
 
 }  // extern "C"

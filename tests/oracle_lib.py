@@ -55,6 +55,9 @@ def ref():
         L.ref_crc32c_extend.argtypes = [_c.c_uint32, _c.c_void_p, _c.c_size_t]
         L.ref_crc32c_fixed_mt.restype = _c.c_int
         L.ref_crc32c_fixed_mt.argtypes = [_c.c_void_p, _c.c_uint64, _c.c_uint64, _c.c_void_p, _c.c_int]
+        L.ref_wal_append_mt.restype = _c.c_uint64
+        L.ref_wal_append_mt.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_uint64, _c.c_void_p, _c.c_uint64,
+                                        _c.c_uint64, _c.c_int]
         L.ref_crc32c_ragged_mt.restype = _c.c_int
         L.ref_crc32c_ragged_mt.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_uint64,
                                            _c.c_void_p, _c.c_int]

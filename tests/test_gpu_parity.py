@@ -253,6 +253,23 @@ def test_host_memory_paths(raw):
     _eq(got, oracle_lib.ragged_crcs(host, offs, lens, np.full(lens.size, 0x77, np.uint32)))
 
 
+def test_ragged_host_chunks_and_order():
+    # > 64 MiB of records: several staged chunks over the two streams; then the same
+    # records in shuffled order (one chunk over the whole arena) and repeated calls
+    # reusing the cached slots
+    lens = synth.loguniform_lengths(9, 24000, 64, 65536)
+    offs, arena = synth.ragged_layout(lens, header=8)
+    buf = synth.splitmix_np(10, 0, arena + 16).copy()
+    want = oracle_lib.ragged_crcs(buf, offs, lens)
+    assert arena > 3 * (64 << 20)
+    _eq(K.extend_batch_ragged_host(buf[:arena], offs, lens), want)
+    perm = np.random.default_rng(3).permutation(lens.size)
+    _eq(K.extend_batch_ragged_host(buf[:arena], offs[perm], lens[perm]), want[perm])
+    few = slice(100, 140)
+    _eq(K.extend_batch_ragged_host(buf[:arena], offs[few], lens[few]), want[few])
+    _eq(K.extend_batch_ragged_host(buf[:arena], offs[:0], lens[:0]), want[:0])
+
+
 def test_rejects_bad_arguments(dev):
     L = _lib.lib()
     buf = torch.zeros(64, dtype=torch.uint8, device=dev)

@@ -33,3 +33,22 @@ def test_model_footer_kinds():
     wal = bytearray(2 * SEG)
     cur, offs = wal_model.append([b"a" * 100, b"b" * (SEG - 50)], wal, SEG, 0)
     assert offs == [0, SEG] and wal[108] == 0 and wal[112] == 1  # padding record: crc 0, type 1
+
+
+def test_reference_append_harness_matches_model():
+    """The config-1 CPU harness (oracle/ref_shim.cc, reference crc32c::Value) frames byte-for-byte
+    what the model frames; bench.py times it as the wal_append cpu_baseline."""
+    import oracle_lib
+    ref = oracle_lib.ref()
+    if ref is None:
+        import pytest
+        pytest.skip("oracle/_ref not built")
+    lens = synth.uniform_lengths(3, 500, 1, 3000).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(4, 0, int(lens.sum()) + 8).copy()
+    wal = np.zeros(64 * SEG, np.uint8)
+    n = ref.ref_wal_append_mt(src.ctypes.data, offs.ctypes.data, lens.ctypes.data, lens.size, wal.ctypes.data,
+                              wal.nbytes, SEG, 1)
+    model = bytearray(64 * SEG)
+    _, moffs = wal_model.append([src[int(o): int(o) + int(k)] for o, k in zip(offs, lens)], model, SEG, 0)
+    assert n == len(moffs) and wal.tobytes() == bytes(model)
