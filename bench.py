@@ -36,7 +36,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", default="fixed", choices=["fixed", "ragged", "stream", "host"])
+    p.add_argument("--workload", default="fixed",
+                   choices=["fixed", "ragged", "stream", "host", "wal_append", "wal_replay"])
+    p.add_argument("--wal-record", type=int, default=180, help="wal_* payload bytes (configs[0]: ~180 B)")
     p.add_argument("--records-per-gpu", type=int, default=1 << 20)
     p.add_argument("--rec-bytes", type=int, default=4096)
     p.add_argument("--seed", type=int, default=42)
@@ -136,6 +138,96 @@ def pmc_traffic(path: str, workload: str, n_bytes_per_launch: int):
 
 
 # ---------------------------------------------------------------------------------------------
+def wal_bench(args, L, rank):
+    """configs[0] shape end to end from host memory: karma_wal_append_batch (sivir::build_sqe +
+    append_record framing, CRCs in one GPU batch) or karma_wal_replay (sivir::open's scan_record
+    loop) over n records of --wal-record bytes in 1 MiB segments (options.h:8).  The CPU
+    baseline is the reference's crc32c::Value in the same framing / replay loop
+    (oracle/ref_shim.cc ref_wal_append_mt / ref_wal_replay_mt), 1 thread and 16 independent WALs."""
+    import ctypes
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import synth
+    from karma_amd import _lib
+    n, size, seg = args.records_per_gpu, args.wal_record, 1 << 20
+    lens = np.full(n, size, dtype=np.uint32)
+    offs = (np.arange(n, dtype=np.uint64) * np.uint64(size)).astype(np.uint64)
+    src = synth.splitmix_np(args.seed + rank, 0, n * size + 16).copy()
+    per_seg = seg // (size + 8)
+    wal_bytes = ((n + per_seg - 1) // per_seg + 1) * seg
+    wal = np.zeros(wal_bytes, dtype=np.uint8)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cur, nf = ctypes.c_uint64(0), ctypes.c_size_t()
+
+    def append():
+        cur.value = 0
+        _lib.check("wal_append", L.karma_wal_append_batch(src.ctypes.data, offs.ctypes.data, lens.ctypes.data, n,
+                                                          wal.ctypes.data, wal_bytes, seg, ctypes.byref(cur), None,
+                                                          ctypes.byref(nf), local))
+        assert nf.value == n
+
+    nrec, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+
+    def replay():
+        _lib.check("wal_replay", L.karma_wal_replay(wal.ctypes.data, None, wal_bytes, seg, 0, ctypes.byref(nrec),
+                                                    ctypes.byref(stop), ctypes.byref(status), None, 0, local))
+        assert nrec.value == n
+
+    append()
+    step = append if args.workload == "wal_append" else replay
+    for _ in range(args.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    dt = (time.perf_counter() - t0) / args.steps
+    payload = n * size
+    res = {"metric": METRIC + f" [{args.workload}: host memory end to end]",
+           "value": round(payload / dt / GIB, 3), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u8", "data": "synthetic splitmix64 payloads in pageable host memory",
+           "records_per_s": round(n / dt, 1),
+           "config": {"workload": f"{n} x {size} B WAL records, 1 MiB segments, "
+                                  f"{'karma_wal_append_batch' if step is append else 'karma_wal_replay'} "
+                                  f"(BASELINE configs[0] shape)", "records": n, "record_bytes": size},
+           "roofline": None}
+    if not args.no_cpu_baseline:
+        import oracle_lib
+        ref = oracle_lib.ref()
+        if ref is not None:
+            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+            k = min(n, 1 << 20)
+            img = ((k // thr + per_seg - 1) // per_seg + 2) * seg
+            imgs = np.zeros(img * thr, dtype=np.uint8)
+
+            def rate(nthr, fn):
+                fn(nthr)
+                reps, t1 = 0, time.perf_counter()
+                while True:
+                    got = fn(nthr)
+                    reps += 1
+                    el = time.perf_counter() - t1
+                    if el > 2.0:
+                        return got, reps * got * size / el / GIB, reps
+
+            def app(nthr):
+                return ref.ref_wal_append_mt(src.ctypes.data, offs.ctypes.data, lens.ctypes.data, k, imgs.ctypes.data,
+                                             img, seg, nthr)
+
+            def rep(nthr):
+                return ref.ref_wal_replay_mt(imgs.ctypes.data, img, seg, nthr, nthr)
+
+            app(thr)  # the images the replay baseline reads
+            fn = app if step is append else rep
+            _, multi, reps = rate(thr, fn)
+            _, single, _ = rate(1, fn)
+            res["cpu_baseline"] = {"value": round(multi, 3), "unit": "GiB/s", "cores": thr, "kind": "reference",
+                                   "sample": f"{k} x {size} B records framed ({'append' if fn is app else 'replay'}) "
+                                             f"into {thr} independent WAL images, one per std::thread, reference "
+                                             f"crc32c::Value, repeated {reps}x (~2 s)",
+                                   "single_thread_value": round(single, 3)}
+    return res
+
+
 def main():
     args = parse()
     import torch
@@ -174,6 +266,16 @@ def main():
         _lib.check("comm_init", L.karma_crc32c_comm_init(ctypes.byref(comm), world, uid, rank))
 
     wl = args.workload
+    if wl in ("wal_append", "wal_replay"):
+        res = wal_bench(args, L, rank)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if comm is not None:
+            L.karma_crc32c_comm_destroy(comm)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     n_rec = args.records_per_gpu
     rec = args.rec_bytes
     cur = {}  # the output buffer the next crc_step writes (double-buffered for N > 1)

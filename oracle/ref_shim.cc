@@ -94,4 +94,47 @@ uint64_t ref_wal_append_mt(const void* src, const uint64_t* off, const uint32_t*
     return total;
 }
 
+// Replay harness: sivir::open's loop over wal::scan_record (sivir.cc:31-41,
+// wal.cc:34-87) with the reference's crc32c::Value, over nimg independent WAL
+// images of wal_bytes each, image i on thread i % nthreads.  Returns records
+// accepted over all images.
+uint64_t ref_wal_replay_mt(const void* wal, uint64_t wal_bytes, uint64_t seg, int nimg, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    std::vector<uint64_t> done(nthreads, 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+        th.emplace_back([=, &done] {
+            uint64_t cnt = 0;
+            for (int im = t; im < nimg; im += nthreads) {
+                const unsigned char* w = static_cast<const unsigned char*>(wal) + (uint64_t)im * wal_bytes;
+                uint64_t off = 0;
+                while (off < wal_bytes) {
+                    const uint64_t base = off / seg * seg, pos = off - base;
+                    if (pos + 8 > seg) {
+                        off = base + seg;
+                        continue;
+                    }
+                    uint32_t crc, st;
+                    std::memcpy(&crc, w + off, 4);
+                    std::memcpy(&st, w + off + 4, 4);
+                    const uint32_t type = st & 0xff, size = st >> 8;
+                    if (type == 1) {
+                        off = base + seg;
+                        continue;
+                    }
+                    if (type != 0 || pos + 8 + size > seg) break;
+                    const char* data = reinterpret_cast<const char*>(size ? w + off + 8 : w + off + 4);
+                    if (crc32c::Value(data, size ? size : 4) != crc) break;
+                    ++cnt;
+                    off += 8 + size;
+                }
+            }
+            done[t] = cnt;
+        });
+    for (auto& x : th) x.join();
+    uint64_t total = 0;
+    for (uint64_t d : done) total += d;
+    return total;
+}
+
 }  // extern "C"

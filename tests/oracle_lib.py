@@ -58,6 +58,8 @@ def ref():
         L.ref_wal_append_mt.restype = _c.c_uint64
         L.ref_wal_append_mt.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_uint64, _c.c_void_p, _c.c_uint64,
                                         _c.c_uint64, _c.c_int]
+        L.ref_wal_replay_mt.restype = _c.c_uint64
+        L.ref_wal_replay_mt.argtypes = [_c.c_void_p, _c.c_uint64, _c.c_uint64, _c.c_int, _c.c_int]
         L.ref_crc32c_ragged_mt.restype = _c.c_int
         L.ref_crc32c_ragged_mt.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_uint64,
                                            _c.c_void_p, _c.c_int]

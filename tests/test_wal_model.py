@@ -52,3 +52,6 @@ def test_reference_append_harness_matches_model():
     model = bytearray(64 * SEG)
     _, moffs = wal_model.append([src[int(o): int(o) + int(k)] for o, k in zip(offs, lens)], model, SEG, 0)
     assert n == len(moffs) and wal.tobytes() == bytes(model)
+    # and the replay harness accepts exactly the records the model replays
+    recs, _, _ = wal_model.replay(bytes(model), SEG)
+    assert ref.ref_wal_replay_mt(wal.ctypes.data, wal.nbytes, SEG, 1, 1) == len(recs) == n
