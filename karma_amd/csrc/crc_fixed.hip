@@ -75,6 +75,77 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     }
 }
 
+// Fixed records on the absolute 128-byte grid (arena 128-aligned, unit a
+// multiple of PF chunks, rec_bytes = k * unit): unit u is simply
+// arena + u * unit_bytes, with no head, tail or partial chunk.  Each lane's
+// loads form one continuous stream across the wave's units: the first PF
+// chunks of the group's next unit are issued before the current unit's
+// fold and tree, so no memory bubble opens at unit boundaries.
+template <int PF>
+__global__ __launch_bounds__(kBlockThreads) void k_units_aligned(FixedArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const uint64_t k = A.units_per_rec;
+    const uint64_t U = A.n_rec * k;
+    const uint64_t C = A.unit_bytes / kChunk;  // chunks per unit, a multiple of PF
+    const uint64_t step = (uint64_t)gridDim.x * kWavesPerBlock * kGroupsPerWave;
+    const uint8_t* base = A.arena + 16 * l;
+    const uint64_t ub = A.unit_bytes;
+    auto at = [&](uint64_t uu, uint64_t c) {  // clamped: groups past the end load a valid line
+        return base + (uu < U ? uu : U - 1) * ub + c * kChunk;
+    };
+    uint64_t w0 = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kGroupsPerWave;
+    uint64_t u = w0 + grp;
+    u32x4 nb[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) nb[q] = ldg<true>(at(u, q));
+    for (; w0 < U; w0 += step, u += step) {
+        const bool valid = u < U;
+        uint32_t inj = 0;
+        uint64_t r = u;
+        if (k != 1) r = u / k;
+        if (valid && l == 0 && r * k == u) inj = ~(A.init ? A.init[r] : A.init_scalar);
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        for (uint64_t c = 0; c < C; c += PF) {
+            u32x4 cur[PF];
+#pragma unroll
+            for (int q = 0; q < PF; ++q) cur[q] = nb[q];
+            if (c + PF < C) {
+#pragma unroll
+                for (int q = 0; q < PF; ++q) nb[q] = ldg<true>(at(u, c + PF + q));
+            } else {
+#pragma unroll
+                for (int q = 0; q < PF; ++q) nb[q] = ldg<true>(at(u + step, q));
+            }
+            if (c == 0) cur[0].x ^= inj;
+#pragma unroll
+            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+        }
+        // lane fold (crc32c.cc STEP4W order), then the 8-lane tree (lane 7 holds the last window)
+        uint32_t c = zmap(lds, kLZ4, a0);
+        c = zmap(lds, kLZ4, c ^ a1);
+        c = zmap(lds, kLZ4, c ^ a2);
+        c = zmap(lds, kLZ4, c ^ a3);
+        uint32_t t = __shfl_down(c, 1, kGroupLanes);
+        c = zmap(lds, kLZ16, c) ^ t;
+        t = __shfl_down(c, 2, kGroupLanes);
+        c = zmap(lds, kLZ32, c) ^ t;
+        t = __shfl_down(c, 4, kGroupLanes);
+        c = zmap(lds, kLZ64, c) ^ t;
+        if (valid && l == 0) {
+            if (k == 1)
+                A.out[u] = ~c;
+            else
+                A.partial[u] = c;
+        }
+    }
+}
+
 // One combine level: record r's k_in states (end-aligned, D bytes each) ->
 // k_out = ceil(k_in / 64) states of 64*D bytes; the last level (k_out == 1)
 // adds the record tail and writes the CRC.  One wave per output state.
@@ -113,6 +184,11 @@ int fixed_variant() {
 
 }  // namespace
 
+bool fixed_aligned_ok(const FixedArgs& a) {
+    return (reinterpret_cast<uintptr_t>(a.arena) & (kChunk - 1)) == 0 && a.unit_bytes % (kChunk * 4) == 0 &&
+           a.rec_bytes == a.units_per_rec * a.unit_bytes && a.rec_bytes > 0;
+}
+
 bool fixed_fast_path_ok(const FixedArgs& a) {
     return (reinterpret_cast<uintptr_t>(a.arena) & 15u) == 0 && a.unit_bytes % kChunk == 0 &&
            a.rec_bytes == a.units_per_rec * a.unit_bytes && a.rec_bytes > 0;
@@ -131,6 +207,12 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
         case 4: hipLaunchKernelGGL((k_units_fixed<4, true, 1>), grid, dim3(kBlockThreads), 0, s, a); break;
         case 5: hipLaunchKernelGGL((k_units_fixed<4, true, 2>), grid, dim3(kBlockThreads), 0, s, a); break;
         case 6: hipLaunchKernelGGL((k_units_fixed<4, true, 3>), grid, dim3(kBlockThreads), 0, s, a); break;
+        case 7:
+            if (fixed_aligned_ok(a)) {
+                hipLaunchKernelGGL((k_units_aligned<4>), grid, dim3(kBlockThreads), 0, s, a);
+                break;
+            }
+            [[fallthrough]];
         default: hipLaunchKernelGGL((k_units_fixed<4, true>), grid, dim3(kBlockThreads), 0, s, a); break;
     }
     units_timer_end(s);

@@ -139,3 +139,40 @@ def test_python_batch_api_rejects_host_tensors():
         K.value_batch_fixed(torch.zeros(64, dtype=torch.uint8), 16)
     with pytest.raises(ValueError):
         K.extend_stream(0, torch.zeros(64, dtype=torch.uint8))
+
+
+def test_wal_and_kfp_host_logic_without_gpu(karma_lib):
+    """The structural halves of the WAL / KFP layers run on the host; with nothing to checksum
+    they need no device, and any checksum work refuses with KARMA_E_NO_DEVICE (no CPU fallback)."""
+    import struct
+
+    import numpy as np
+
+    u64, sz, i32 = ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int
+    # KFP: a first frame whose size is over MAX_FRAME_SIZE stops before any CRC (frame.cc:70-73)
+    buf = np.frombuffer(b"\xff\xff\xff\xff" + bytes(40), np.uint8).copy()
+    n, used, why = sz(), u64(), i32()
+    st = karma_lib.karma_kfp_parse_batch(buf.ctypes.data, None, buf.nbytes, 16, None, ctypes.byref(n),
+                                         ctypes.byref(used), ctypes.byref(why), -1)
+    assert st == 0 and (n.value, used.value, why.value) == (0, 0, 1)  # KARMA_KFP_BAD_SIZE
+    # fewer than 20 bytes: wait for more (nullopt)
+    st = karma_lib.karma_kfp_parse_batch(buf.ctypes.data, None, 19, 16, None, ctypes.byref(n), ctypes.byref(used),
+                                         ctypes.byref(why), -1)
+    assert st == 0 and (n.value, used.value, why.value) == (0, 0, 0)
+    # a complete frame needs its CRC: refused without a device
+    frame = struct.pack("<IBhBII", 24, 123, 1, 0, 0, 0) + b"abcd" + b"\0\0\0\0"
+    fb = np.frombuffer(frame, np.uint8).copy()
+    st = karma_lib.karma_kfp_parse_batch(fb.ctypes.data, None, fb.nbytes, 16, None, ctypes.byref(n),
+                                         ctypes.byref(used), ctypes.byref(why), -1)
+    assert st == _lib.KARMA_E_NO_DEVICE
+    # WAL replay of an image whose first header has an unknown type: BAD_TYPE at 0, no CRC needed
+    seg = 4096
+    wal = np.zeros(2 * seg, np.uint8)
+    wal[4] = 7
+    nr, stop, status = u64(), u64(), i32()
+    st = karma_lib.karma_wal_replay(wal.ctypes.data, None, wal.nbytes, seg, 0, ctypes.byref(nr), ctypes.byref(stop),
+                                    ctypes.byref(status), None, 0, -1)
+    assert st == 0 and (nr.value, stop.value, status.value) == (0, 0, 2)
+    # invalid geometry is rejected before any device work
+    assert karma_lib.karma_wal_replay(wal.ctypes.data, None, wal.nbytes, 3000, 0, ctypes.byref(nr),
+                                      ctypes.byref(stop), ctypes.byref(status), None, 0, -1) == _lib.KARMA_E_INVALID
