@@ -262,6 +262,102 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
     return c;
 }
 
+// ---- pipelined form of group_unit: the next unit's first loads are issued
+// before the current unit's last chunks and epilogue, so a group's load stream
+// has no gap at unit boundaries.  Same arithmetic and result as group_unit.
+struct LaneUnit {
+    const uint8_t* us;      // unit span [us, ue)
+    const uint8_t* ue;
+    const uint8_t* w;       // this lane's window in chunk 0
+    const uint8_t* lclamp;  // last address this lane may prefetch
+    int64_t nch;            // 128-byte chunks on the absolute grid (0: empty unit)
+    uint32_t m;             // lane holding the unit's last window
+    bool lok;               // this lane's window in the last chunk lies inside the unit
+};
+
+__device__ __forceinline__ LaneUnit lane_unit(const uint8_t* us, const uint8_t* ue, uint32_t l) {
+    LaneUnit L;
+    L.us = us;
+    L.ue = ue;
+    L.nch = 0;
+    L.m = kGroupLanes - 1;
+    L.lok = false;
+    L.w = us;
+    L.lclamp = us;
+    if (ue > us) {
+        const uint8_t* base = floor128(us);
+        L.nch = (ue - base + kChunk - 1) / kChunk;
+        L.m = (uint32_t)((reinterpret_cast<uintptr_t>(ue) - 16) >> 4) & (kGroupLanes - 1);
+        L.w = base + 16 * l;
+        const uint8_t* wl = base + (L.nch - 1) * kChunk + 16 * l;
+        L.lok = wl < ue;
+        L.lclamp = L.lok ? wl : ue - 16;
+    }
+    return L;
+}
+
+// First loads of a unit: chunk 0 (kept only where the window is inside the
+// span: ok0) and chunks 1..PF (clamped to the lane's last valid window).
+template <int PF, bool NT>
+__device__ __forceinline__ void unit_first_loads(const LaneUnit& L, u32x4& v0, bool& ok0, u32x4 (&nb)[PF]) {
+    ok0 = false;
+    if (L.nch == 0) return;
+    ok0 = L.w >= L.us && L.w < L.ue;
+    v0 = ldg<NT>(ok0 ? L.w : L.lclamp);
+#pragma unroll
+    for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(L.w + (q + 1) * kChunk, L.lclamp));
+}
+
+// Streams unit L (its first loads already in v0/ok0/nb), issuing unit N's first
+// loads into v0n/ok0n/nb on the way.  Every lane of the wave must call this.
+template <int PF, bool NT>
+__device__ __forceinline__ uint32_t group_unit_pipe(const uint32_t* lds, uint32_t X, uint32_t l, const LaneUnit& L,
+                                                    u32x4 v0, bool ok0, u32x4 (&nb)[PF], const uint8_t* inj_at,
+                                                    uint32_t inj, const LaneUnit& N, u32x4& v0n, bool& ok0n) {
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    if (L.nch > 0) {
+        u32x4 v = ok0 ? v0 : u32x4{0u, 0u, 0u, 0u};
+        if (L.w == inj_at) v.x ^= inj;
+        a0 = v.x;
+        a1 = v.y;
+        a2 = v.z;
+        a3 = v.w;
+    }
+    int64_t rem = L.nch - 1;
+    const uint8_t* w = L.w + kChunk;
+    while (rem > PF) {
+        u32x4 cur[PF];
+#pragma unroll
+        for (int q = 0; q < PF; ++q) cur[q] = nb[q];
+        w += PF * kChunk;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, L.lclamp));
+#pragma unroll
+        for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+        rem -= PF;
+    }
+    u32x4 cur[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) cur[q] = nb[q];
+    unit_first_loads<PF, NT>(N, v0n, ok0n, nb);
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+        if (q < rem - 1 || (q == rem - 1 && L.lok)) step4(lds, X, a0, a1, a2, a3, cur[q]);
+    uint32_t c = zmap(lds, kLZ4, a0);
+    c = zmap(lds, kLZ4, c ^ a1);
+    c = zmap(lds, kLZ4, c ^ a2);
+    c = zmap(lds, kLZ4, c ^ a3);
+    const uint32_t lane = threadIdx.x & 63u;
+    c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + L.m + 1) & (kGroupLanes - 1))), 64);
+    uint32_t t = __shfl_down(c, 1, kGroupLanes);
+    c = zmap(lds, kLZ16, c) ^ t;
+    t = __shfl_down(c, 2, kGroupLanes);
+    c = zmap(lds, kLZ32, c) ^ t;
+    t = __shfl_down(c, 4, kGroupLanes);
+    c = zmap(lds, kLZ64, c) ^ t;
+    return c;
+}
+
 // Copy WORDS words (WORDS % 4 == 0, both pointers 16-byte aligned) from global
 // memory into LDS with THREADS threads: every thread issues all of its 16-byte
 // loads before its first LDS store, so the copy costs about one memory latency

@@ -19,6 +19,8 @@
 //                      records with > 64 units are folded by the whole wave
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "crc_device.h"
 #include "engine.h"
 
@@ -272,6 +274,50 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     }
 }
 
+// k_units_ragged with the group_unit_pipe load stream (next unit's first
+// loads issued before the current unit's tail and epilogue).
+__global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const uint64_t U_all = A.fbase[A.n_rec];
+    const uint64_t U = U_all < A.unit_cap ? U_all : A.unit_cap;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t step = nwaves * kGroupsPerWave;
+    uint64_t wb = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    uint64_t u = wb * kGroupsPerWave + grp;
+    UnitDesc d = u < U ? load_desc(A.desc + u) : UnitDesc{0, 0, 0};
+    UnitDesc dn = u + step < U ? load_desc(A.desc + u + step) : UnitDesc{0, 0, 0};
+    LaneUnit L = lane_unit(reinterpret_cast<const uint8_t*>(d.us), reinterpret_cast<const uint8_t*>(d.us) + d.span, l);
+    u32x4 v0 = u32x4{0u, 0u, 0u, 0u}, nb[kRaggedPF];
+    bool ok0 = false;
+    unit_first_loads<kRaggedPF, kRaggedNT>(L, v0, ok0, nb);
+    for (; wb * kGroupsPerWave < U; wb += nwaves, u += step) {
+        const bool valid = u < U;
+        const uint8_t* nus = reinterpret_cast<const uint8_t*>(dn.us);
+        const LaneUnit N = lane_unit(nus, nus + dn.span, l);
+        const UnitDesc dnn = u + 2 * step < U ? load_desc(A.desc + u + 2 * step) : UnitDesc{0, 0, 0};
+        u32x4 v0n = u32x4{0u, 0u, 0u, 0u};
+        bool ok0n = false;
+        const uint32_t R = group_unit_pipe<kRaggedPF, kRaggedNT>(lds, X, l, L, v0, ok0, nb, L.us, d.inj, N, v0n, ok0n);
+        if (valid && l == 0) A.partial[u] = R;
+        d = dn;
+        dn = dnn;
+        L = N;
+        v0 = v0n;
+        ok0 = ok0n;
+    }
+}
+
+int ragged_variant() {
+    const char* e = getenv("KARMA_RAGGED_VARIANT");
+    return e ? atoi(e) : 0;
+}
+
 // Slot of unit j of a record (full units from fb in order, partial ones bucketed).
 __device__ __forceinline__ uint64_t unit_slot(uint64_t j, uint64_t k, uint64_t fb, uint64_t ps0, uint64_t ps1,
                                               uint32_t part0, uint32_t part1) {
@@ -384,7 +430,10 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
     hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     units_timer_begin(s);
-    hipLaunchKernelGGL(k_units_ragged, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    if (ragged_variant() == 1)
+        hipLaunchKernelGGL(k_units_ragged_pipe, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_units_ragged, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
     const uint64_t cap = 2 * (uint64_t)grid_blocks;

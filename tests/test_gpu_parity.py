@@ -277,3 +277,24 @@ def test_rejects_bad_arguments(dev):
     assert L.karma_fill_splitmix64(buf.data_ptr(), 32, 1, 3, None) == _lib.KARMA_E_INVALID
     with pytest.raises(ValueError):
         K.value_batch_fixed(buf, 7)
+
+
+@pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", "7"), ("KARMA_RAGGED_VARIANT", "1")])
+def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
+    """The A/B kernel builds (tools/variant_bench.py) are held to the same parity as the default."""
+    monkeypatch.setenv(env, val)
+    host, dbuf = raw
+    for rec, n in [(4096, 2000), (512, 5000), (1 << 16, 100), (3 << 20, 2)]:
+        got = K.value_batch_fixed(dbuf[: n * rec], rec).cpu().numpy()
+        _eq(got, oracle_lib.fixed_crcs(host[: n * rec], rec))
+    got = K.value_batch_fixed(dbuf[: 1000 * 4096], 4096, init=0x1234).cpu().numpy()
+    offs4 = np.arange(1000, dtype=np.uint64) * 4096
+    _eq(got, oracle_lib.ragged_crcs(host, offs4, np.full(1000, 4096, np.uint32), np.full(1000, 0x1234, np.uint32)))
+    lens = synth.loguniform_lengths(4, 3000, 1, 65536)
+    offs, arena = synth.ragged_layout(lens, header=8)
+    ini = np.arange(lens.size, dtype=np.uint32) * 2654435761 % (1 << 32)
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    d_ini = torch.from_numpy(ini.astype(np.uint32).view(np.int32)).to(dev)
+    got = K.extend_batch_ragged(dbuf[:arena], d_off, d_len, init=d_ini, total_len=int(lens.sum())).cpu().numpy()
+    _eq(got, oracle_lib.ragged_crcs(host, offs, lens, ini.astype(np.uint32)))
