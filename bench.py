@@ -34,8 +34,8 @@ METRIC = "CRC32C GiB/s device-resident, batched WAL records, 1/2/4/8 MI355X"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="fixed",
                    choices=["fixed", "ragged", "stream", "host", "wal_append", "wal_replay"])
     p.add_argument("--wal-record", type=int, default=180, help="wal_* payload bytes (configs[0]: ~180 B)")
@@ -124,6 +124,15 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
             "sample": f"{desc}, crc32c::Value per record, round-robin over {threads} std::threads, "
                       f"repeated {reps_m}x (~2 s)",
             "single_thread_value": round(single, 3), "cpu_model": cpu, "host_cores_visible": os.cpu_count()}
+
+
+def units_kernel_name(wl: str, arena, rec: int, n_rec: int) -> str:
+    """The dominant kernel a batch runs (capi.cc planning; crc_fixed.hip fixed_aligned_ok)."""
+    if wl == "ragged":
+        return "k_units_ragged_pipe" if os.environ.get("KARMA_RAGGED_VARIANT") == "1" else "k_units_ragged"
+    variant = os.environ.get("KARMA_CRC_VARIANT", "0")
+    aligned = arena.data_ptr() % 128 == 0 and rec % 512 == 0
+    return "k_units_aligned" if (aligned and variant == "7") else "k_units_fixed"
 
 
 def pmc_traffic(path: str, workload: str, n_bytes_per_launch: int):
@@ -457,8 +466,8 @@ def main():
             "data": "synthetic: little-endian splitmix64 byte stream generated on the device before timing",
             "config": {"workload": workload_desc, "records_per_gpu": int(n_rec), "rec_bytes": int(rec),
                        "parallelism": f"record-sharded x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
-                       "kernel": "k_units_fixed" if wl in ("fixed", "stream") else
-                                 ("k_units_ragged" if wl == "ragged" else "host->device pipeline")},
+                       "kernel": units_kernel_name(wl, arena, rec, n_rec) if out is not None else
+                                 "host->device pipeline"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(algo_bytes),

@@ -109,8 +109,15 @@ int comb_blob(DevState& d, uint64_t unit_bytes, const uint32_t** out) {
     return 0;
 }
 
-int workspace(int dev, hipStream_t s, size_t bytes, void** out) {
+// A per-(device, stream) workspace: a kWsHeader-byte header that persists across
+// calls (the ragged scan's bucket starts and done counter, which must stay at a fixed
+// place and start at zero) followed by `bytes` of scratch returned in *out.
+constexpr size_t kWsHeader = 512;
+static_assert((kBuckets + 1) * sizeof(uint64_t) <= kWsHeader, "ragged header fits");
+
+int workspace(int dev, hipStream_t s, size_t bytes, void** out, uint64_t** header = nullptr) {
     Workspace& w = g_ws[{dev, (void*)s}];
+    bytes += kWsHeader;
     if (w.bytes < bytes) {
         if (w.ptr) {
             KARMA_HIP(hipStreamSynchronize(s));
@@ -121,8 +128,10 @@ int workspace(int dev, hipStream_t s, size_t bytes, void** out) {
         const size_t want = align256(bytes + bytes / 4);
         KARMA_HIP(hipMalloc(&w.ptr, want));
         w.bytes = want;
+        KARMA_HIP(hipMemsetAsync(w.ptr, 0, kWsHeader, s));  // the done counter starts at 0
     }
-    *out = w.ptr;
+    *out = static_cast<char*>(w.ptr) + kWsHeader;
+    if (header) *header = static_cast<uint64_t*>(w.ptr);
     return 0;
 }
 
@@ -182,28 +191,29 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 
 // ---- ragged records -------------------------------------------------------
 struct RaggedLayout {
-    size_t fbase_off, pslot_off, sums_off, bucket_off, desc_off, part_off, total;
+    size_t fbase_off, pslot_off, sums_off, bhist_off, desc_off, part_off, total;
 };
 
 RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     RaggedLayout L;
     const uint64_t nb = ragged_scan_blocks(n_rec);
     L.fbase_off = 0;
-    L.pslot_off = align256((n_rec + 2) * sizeof(uint64_t));
+    L.pslot_off = L.fbase_off + align256((n_rec + 2) * sizeof(uint64_t));
     L.sums_off = L.pslot_off + align256(2 * n_rec * sizeof(uint64_t));
-    L.bucket_off = L.sums_off + align256(nb * sizeof(uint64_t));
-    L.desc_off = L.bucket_off + align256((kBuckets + 1) * sizeof(uint64_t));
+    L.bhist_off = L.sums_off + align256(nb * sizeof(uint64_t));
+    L.desc_off = L.bhist_off + align256(nb * kBuckets * sizeof(uint32_t));
     L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
     L.total = L.part_off + align256(cap * sizeof(uint32_t));
     return L;
 }
 
-void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
+void bind_ragged(RaggedArgs& a, void* ws, uint64_t* header, const RaggedLayout& L, uint64_t cap) {
     char* b = static_cast<char*>(ws);
     a.fbase = reinterpret_cast<uint64_t*>(b + L.fbase_off);
     a.pslot = reinterpret_cast<uint64_t*>(b + L.pslot_off);
     a.block_sums = reinterpret_cast<uint64_t*>(b + L.sums_off);
-    a.bucket_off = reinterpret_cast<uint64_t*>(b + L.bucket_off);
+    a.bucket_off = header;
+    a.bhist = reinterpret_cast<uint32_t*>(b + L.bhist_off);
     a.desc = reinterpret_cast<UnitDesc*>(b + L.desc_off);
     a.partial = reinterpret_cast<uint32_t*>(b + L.part_off);
     a.unit_cap = cap;
@@ -228,15 +238,17 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
     if (total_len > 0) {
         cap = 2 * n_rec + ceil_div(total_len, kDefaultUnit);
         const RaggedLayout L = ragged_layout(n_rec, cap);
-        KARMA_RC(workspace(dev, s, L.total, &ws));
-        bind_ragged(a, ws, L, cap);
+        uint64_t* hdr = nullptr;
+        KARMA_RC(workspace(dev, s, L.total, &ws, &hdr));
+        bind_ragged(a, ws, hdr, L, cap);
         KARMA_HIP(launch_ragged_scan(a, s));
     } else {
         // Unknown total: scan, read the unit count back, size the table, rescan if it moved.
         cap = n_rec;
         RaggedLayout L = ragged_layout(n_rec, cap);
-        KARMA_RC(workspace(dev, s, L.total, &ws));
-        bind_ragged(a, ws, L, cap);
+        uint64_t* hdr = nullptr;
+        KARMA_RC(workspace(dev, s, L.total, &ws, &hdr));
+        bind_ragged(a, ws, hdr, L, cap);
         KARMA_HIP(launch_ragged_scan(a, s));
         uint64_t units = 0;
         KARMA_HIP(hipMemcpyAsync(&units, a.fbase + n_rec, sizeof(units), hipMemcpyDeviceToHost, s));
@@ -244,8 +256,8 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         cap = std::max<uint64_t>(units, 1);
         L = ragged_layout(n_rec, cap);
         void* ws2 = nullptr;
-        KARMA_RC(workspace(dev, s, L.total, &ws2));
-        bind_ragged(a, ws2, L, cap);
+        KARMA_RC(workspace(dev, s, L.total, &ws2, &hdr));
+        bind_ragged(a, ws2, hdr, L, cap);
         if (ws2 != ws) KARMA_HIP(launch_ragged_scan(a, s));
     }
     KARMA_HIP(launch_ragged_main(a, ds.cu, s));

@@ -113,16 +113,23 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
 __device__ __forceinline__ uint64_t load_agent(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ uint32_t load_agent(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-// Per scan block: exclusive scan of full units; partial units counted per
-// bucket (chunk count) into the global bucket totals (one atomic per bucket
-// per block; the totals and the done counter bucket_off[kBuckets] are zeroed
-// by the launcher).  The last block to finish then scans the block sums
-// (full-unit offsets, slots [0, F)) and turns the bucket totals into the start
-// of every partial bucket, longest (32 chunks) first (slots [F, U)).
+// Per scan block: exclusive scan of full units (record order) and the block's
+// count of partial units per bucket (chunk count), stored to bhist[block][bucket].
+// The last block to finish (done counter bucket_off[kBuckets], which it resets
+// for the next call) then
+//   * scans the block sums: full-unit offsets, slots [0, F);
+//   * scans every bucket's column of bhist in place: each block's first slot
+//     within the bucket (a wave per bucket, no global atomics anywhere);
+//   * places the buckets after the full units, longest (32 chunks) first, and
+//     writes their starts to bucket_off[bucket] (slots [F, U)).
 __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
     __shared__ uint64_t sm[16];
     __shared__ uint32_t hist[kBuckets];
+    __shared__ uint64_t tot[kBuckets];
     __shared__ bool last;
     if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -137,13 +144,11 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
     }
     __syncthreads();
     if (threadIdx.x == 0) A.block_sums[blockIdx.x] = total;
-    if (threadIdx.x < kBuckets && hist[threadIdx.x])
-        atomicAdd(reinterpret_cast<unsigned long long*>(&A.bucket_off[threadIdx.x]), (unsigned long long)hist[threadIdx.x]);
+    if (threadIdx.x < kBuckets) A.bhist[blockIdx.x * kBuckets + threadIdx.x] = hist[threadIdx.x];
+    __threadfence();  // every thread's results before the block's done count
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();  // this block's sums and totals before its done count
+    if (threadIdx.x == 0)
         last = atomicAdd(reinterpret_cast<unsigned long long*>(&A.bucket_off[kBuckets]), 1ull) == gridDim.x - 1;
-    }
     __syncthreads();
     if (!last) return;
     __threadfence();
@@ -157,22 +162,35 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
         if (i < nblocks) A.block_sums[i] = carry + e;
         carry += t;
     }
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (uint32_t bk = wave; bk < (uint32_t)kBuckets; bk += nw) {
+        uint64_t c = 0;
+        for (uint64_t base = 0; base < nblocks; base += 64) {
+            const uint64_t i = base + lane;
+            const uint64_t v = i < nblocks ? load_agent(A.bhist + i * kBuckets + bk) : 0u;
+            const uint64_t inc = wave_incl_scan(v);
+            if (i < nblocks) A.bhist[i * kBuckets + bk] = (uint32_t)(c + inc - v);
+            c += __shfl(inc, 63);
+        }
+        if (lane == 0) tot[bk] = c;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         const uint64_t F = carry;
-        for (int c = kBuckets - 1; c >= 1; --c) {  // totals -> cursors
-            const uint64_t t = load_agent(A.bucket_off + c);
+        for (int c = kBuckets - 1; c >= 1; --c) {  // totals -> bucket starts
             A.bucket_off[c] = carry;
-            carry += t;
+            carry += tot[c];
         }
         A.fbase[A.n_rec] = carry;  // total units
         A.fbase[A.n_rec + 1] = F;
+        A.bucket_off[kBuckets] = 0;  // done counter, ready for the next call
     }
 }
 
 // One thread per record (block b = scan block b): final slots, the entering
-// register over the unaligned head, and the unit descriptors.  A block
-// reserves its range of every partial bucket with one atomic per bucket; each
-// lane writes its record's (at most two) partial units.  The full units of a
+// register over the unaligned head, and the unit descriptors.  The block's
+// range of every partial bucket comes from k_ragged_scan; lanes take slots in
+// it with LDS atomics and write their record's (at most two) partial units.  The full units of a
 // wave's 64 records are consecutive slots: the wave writes them together, lane
 // t taking slot F0 + t and finding its record by a search over the lanes'
 // inclusive unit counts, so the descriptor stores are coalesced and balanced
@@ -180,25 +198,14 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
 __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4 then the byte table
     __shared__ unsigned long long cnt[kBuckets];
-    __shared__ uint32_t hist[kBuckets];
     copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
-    if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
-    __syncthreads();
+    if (threadIdx.x < kBuckets)  // this block's first slot in every bucket (k_ragged_scan)
+        cnt[threadIdx.x] = A.bucket_off[threadIdx.x] + A.bhist[blockIdx.x * kBuckets + threadIdx.x];
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = r < A.n_rec;
     RecUnits u{};
-    if (valid) {
-        u = rec_units(A, r);
-        if (u.part0) atomicAdd(&hist[u.c0], 1u);
-        if (u.part1) atomicAdd(&hist[u.c1], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < kBuckets)
-        cnt[threadIdx.x] = hist[threadIdx.x]
-                               ? atomicAdd(reinterpret_cast<unsigned long long*>(&A.bucket_off[threadIdx.x]),
-                                           (unsigned long long)hist[threadIdx.x])
-                               : 0ull;
+    if (valid) u = rec_units(A, r);
     __syncthreads();
     uint64_t fb = 0;
     uint32_t h = 0;
@@ -419,8 +426,6 @@ hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     if (a.unit_bytes != kU) return hipErrorInvalidValue;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
-    hipError_t e = hipMemsetAsync(a.bucket_off, 0, (kBuckets + 1) * sizeof(uint64_t), s);  // bucket totals + done counter
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_ragged_scan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     return hipGetLastError();
 }

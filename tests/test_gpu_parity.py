@@ -290,9 +290,10 @@ def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
     got = K.value_batch_fixed(dbuf[: 1000 * 4096], 4096, init=0x1234).cpu().numpy()
     offs4 = np.arange(1000, dtype=np.uint64) * 4096
     _eq(got, oracle_lib.ragged_crcs(host, offs4, np.full(1000, 4096, np.uint32), np.full(1000, 0x1234, np.uint32)))
-    lens = synth.loguniform_lengths(4, 3000, 1, 65536)
+    lens = synth.loguniform_lengths(4, 1500, 1, 16384)
     offs, arena = synth.ragged_layout(lens, header=8)
-    ini = np.arange(lens.size, dtype=np.uint32) * 2654435761 % (1 << 32)
+    assert arena <= host.size
+    ini = (np.arange(lens.size, dtype=np.uint64) * 2654435761 % (1 << 32)).astype(np.uint32)
     d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
     d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
     d_ini = torch.from_numpy(ini.astype(np.uint32).view(np.int32)).to(dev)

@@ -32,17 +32,17 @@ def main():
     src = os.path.join(ROOT, "gpurun_out", "prof")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
-    kernel = {"fixed": "k_units_fixed", "stream": "k_units_fixed", "ragged": "k_units_ragged"}.get(wl, "k_units_fixed")
     fetch, nf = per_kernel(os.path.join(src, f"pmc_fetch_{rnd}_{wl}", "run_counter_collection.csv"), "FETCH_SIZE")
     write, nw = per_kernel(os.path.join(src, f"pmc_write_{rnd}_{wl}", "run_counter_collection.csv"), "WRITE_SIZE")
-    kf = [k for k in fetch if kernel in k][0]
     bench = json.load(open(os.path.join(src, f"bench_{rnd}_{wl}.json")))
+    kernel = bench["config"]["kernel"]  # the dominant kernel bench.py timed
     payload = bench["config"]["records_per_gpu"] * bench["config"]["rec_bytes"] if wl != "ragged" else None
     stats = {}
     for r in csv.DictReader(open(os.path.join(src, f"trace_{rnd}_{wl}", "run_kernel_stats.csv"))):
         stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
                             "max_ns": float(r["MaxNs"])}
     ks = [v for k, v in stats.items() if kernel in k][0]
+    kf = [k for k in fetch if kernel in k][0]
     fetch_b = fetch[kf] * 1024 * 2
     write_b = write.get(kf, 0.0) * 1024
     out = {
