@@ -115,9 +115,11 @@ int comb_blob(DevState& d, uint64_t unit_bytes, const uint32_t** out) {
 constexpr size_t kWsHeader = 512;
 static_assert((kBuckets + 1) * sizeof(uint64_t) <= kWsHeader, "ragged header fits");
 
-int workspace(int dev, hipStream_t s, size_t bytes, void** out, uint64_t** header = nullptr) {
+int workspace(int dev, hipStream_t s, size_t bytes, void** out, uint64_t** header = nullptr,
+              bool* reallocated = nullptr) {
     Workspace& w = g_ws[{dev, (void*)s}];
     bytes += kWsHeader;
+    if (reallocated) *reallocated = w.bytes < bytes;
     if (w.bytes < bytes) {
         if (w.ptr) {
             KARMA_HIP(hipStreamSynchronize(s));
@@ -191,7 +193,7 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 
 // ---- ragged records -------------------------------------------------------
 struct RaggedLayout {
-    size_t fbase_off, pslot_off, sums_off, bhist_off, desc_off, part_off, total;
+    size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off, total;
 };
 
 RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
@@ -200,8 +202,8 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     L.fbase_off = 0;
     L.pslot_off = L.fbase_off + align256((n_rec + 2) * sizeof(uint64_t));
     L.sums_off = L.pslot_off + align256(2 * n_rec * sizeof(uint64_t));
-    L.bhist_off = L.sums_off + align256(nb * sizeof(uint64_t));
-    L.desc_off = L.bhist_off + align256(nb * kBuckets * sizeof(uint32_t));
+    L.psums_off = L.sums_off + align256(nb * sizeof(uint64_t));
+    L.desc_off = L.psums_off + align256(nb * sizeof(uint64_t));
     L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
     L.total = L.part_off + align256(cap * sizeof(uint32_t));
     return L;
@@ -213,7 +215,7 @@ void bind_ragged(RaggedArgs& a, void* ws, uint64_t* header, const RaggedLayout& 
     a.pslot = reinterpret_cast<uint64_t*>(b + L.pslot_off);
     a.block_sums = reinterpret_cast<uint64_t*>(b + L.sums_off);
     a.bucket_off = header;
-    a.bhist = reinterpret_cast<uint32_t*>(b + L.bhist_off);
+    a.block_psums = reinterpret_cast<uint64_t*>(b + L.psums_off);
     a.desc = reinterpret_cast<UnitDesc*>(b + L.desc_off);
     a.partial = reinterpret_cast<uint32_t*>(b + L.part_off);
     a.unit_cap = cap;
@@ -255,10 +257,11 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         KARMA_HIP(hipStreamSynchronize(s));
         cap = std::max<uint64_t>(units, 1);
         L = ragged_layout(n_rec, cap);
-        void* ws2 = nullptr;
-        KARMA_RC(workspace(dev, s, L.total, &ws2, &hdr));
-        bind_ragged(a, ws2, hdr, L, cap);
-        if (ws2 != ws) KARMA_HIP(launch_ragged_scan(a, s));
+        // a new allocation (possibly at the same address) holds none of the scan's results
+        bool fresh = false;
+        KARMA_RC(workspace(dev, s, L.total, &ws, &hdr, &fresh));
+        bind_ragged(a, ws, hdr, L, cap);
+        if (fresh) KARMA_HIP(launch_ragged_scan(a, s));
     }
     KARMA_HIP(launch_ragged_main(a, ds.cu, s));
     return 0;

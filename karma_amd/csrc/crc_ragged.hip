@@ -113,38 +113,27 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
 __device__ __forceinline__ uint64_t load_agent(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t load_agent(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
-// Per scan block: exclusive scan of full units (record order) and the block's
-// count of partial units per bucket (chunk count), stored to bhist[block][bucket].
-// The last block to finish (done counter bucket_off[kBuckets], which it resets
-// for the next call) then
-//   * scans the block sums: full-unit offsets, slots [0, F);
-//   * scans every bucket's column of bhist in place: each block's first slot
-//     within the bucket (a wave per bucket, no global atomics anywhere);
-//   * places the buckets after the full units, longest (32 chunks) first, and
-//     writes their starts to bucket_off[bucket] (slots [F, U)).
+// Per scan block: exclusive scan of full units (record order) and the
+// block's count of partial units.  The last block to finish (done counter
+// bucket_off[kBuckets], which it resets for the next call) scans both block
+// arrays: full units take slots [0, F) in record order; block b's partial
+// units take the run [F + P_b, F + P_b + parts_b), which k_ragged_desc sorts by
+// chunk count, longest first (a wave's 8 units then have nearly equal length).
 __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
     __shared__ uint64_t sm[16];
-    __shared__ uint32_t hist[kBuckets];
-    __shared__ uint64_t tot[kBuckets];
     __shared__ bool last;
-    if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     RecUnits u{};
     if (r < A.n_rec) u = rec_units(A, r);
-    uint64_t total;
+    uint64_t total, parts;
     const uint64_t ex = block_excl_scan(r < A.n_rec ? u.full : 0, sm, total);  // has barriers
-    if (r < A.n_rec) {
-        A.fbase[r] = ex;
-        if (u.part0) atomicAdd(&hist[u.c0], 1u);
-        if (u.part1) atomicAdd(&hist[u.c1], 1u);
+    (void)block_excl_scan(r < A.n_rec ? u.part0 + u.part1 : 0, sm, parts);
+    if (r < A.n_rec) A.fbase[r] = ex;
+    if (threadIdx.x == 0) {
+        A.block_sums[blockIdx.x] = total;
+        A.block_psums[blockIdx.x] = parts;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) A.block_sums[blockIdx.x] = total;
-    if (threadIdx.x < kBuckets) A.bhist[blockIdx.x * kBuckets + threadIdx.x] = hist[threadIdx.x];
     __threadfence();  // every thread's results before the block's done count
     __syncthreads();
     if (threadIdx.x == 0)
@@ -153,35 +142,26 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
     if (!last) return;
     __threadfence();
     const uint64_t nblocks = gridDim.x;
-    uint64_t carry = 0;
+    uint64_t F = 0;
     for (uint64_t base = 0; base < nblocks; base += blockDim.x) {
         const uint64_t i = base + threadIdx.x;
         const uint64_t v = i < nblocks ? load_agent(A.block_sums + i) : 0;
         uint64_t t;
         const uint64_t e = block_excl_scan(v, sm, t);
-        if (i < nblocks) A.block_sums[i] = carry + e;
-        carry += t;
+        if (i < nblocks) A.block_sums[i] = F + e;
+        F += t;
     }
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (uint32_t bk = wave; bk < (uint32_t)kBuckets; bk += nw) {
-        uint64_t c = 0;
-        for (uint64_t base = 0; base < nblocks; base += 64) {
-            const uint64_t i = base + lane;
-            const uint64_t v = i < nblocks ? load_agent(A.bhist + i * kBuckets + bk) : 0u;
-            const uint64_t inc = wave_incl_scan(v);
-            if (i < nblocks) A.bhist[i * kBuckets + bk] = (uint32_t)(c + inc - v);
-            c += __shfl(inc, 63);
-        }
-        if (lane == 0) tot[bk] = c;
+    uint64_t P = F;
+    for (uint64_t base = 0; base < nblocks; base += blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t v = i < nblocks ? load_agent(A.block_psums + i) : 0;
+        uint64_t t;
+        const uint64_t e = block_excl_scan(v, sm, t);
+        if (i < nblocks) A.block_psums[i] = P + e;
+        P += t;
     }
-    __syncthreads();
     if (threadIdx.x == 0) {
-        const uint64_t F = carry;
-        for (int c = kBuckets - 1; c >= 1; --c) {  // totals -> bucket starts
-            A.bucket_off[c] = carry;
-            carry += tot[c];
-        }
-        A.fbase[A.n_rec] = carry;  // total units
+        A.fbase[A.n_rec] = P;  // total units
         A.fbase[A.n_rec + 1] = F;
         A.bucket_off[kBuckets] = 0;  // done counter, ready for the next call
     }
@@ -189,8 +169,8 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
 
 // One thread per record (block b = scan block b): final slots, the entering
 // register over the unaligned head, and the unit descriptors.  The block's
-// range of every partial bucket comes from k_ragged_scan; lanes take slots in
-// it with LDS atomics and write their record's (at most two) partial units.  The full units of a
+// partial units fill its run from k_ragged_scan sorted by chunk count (a
+// counting sort in LDS); each lane writes its record's (at most two).  The full units of a
 // wave's 64 records are consecutive slots: the wave writes them together, lane
 // t taking slot F0 + t and finding its record by a search over the lanes'
 // inclusive unit counts, so the descriptor stores are coalesced and balanced
@@ -198,14 +178,27 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
 __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4 then the byte table
     __shared__ unsigned long long cnt[kBuckets];
+    __shared__ uint32_t hist[kBuckets];
     copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
-    if (threadIdx.x < kBuckets)  // this block's first slot in every bucket (k_ragged_scan)
-        cnt[threadIdx.x] = A.bucket_off[threadIdx.x] + A.bhist[blockIdx.x * kBuckets + threadIdx.x];
+    if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = r < A.n_rec;
     RecUnits u{};
-    if (valid) u = rec_units(A, r);
+    if (valid) {
+        u = rec_units(A, r);
+        if (u.part0) atomicAdd(&hist[u.c0], 1u);
+        if (u.part1) atomicAdd(&hist[u.c1], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // the block's partial run, longest bucket first
+        unsigned long long s = A.block_psums[blockIdx.x];
+        for (int c = kBuckets - 1; c >= 0; --c) {
+            cnt[c] = s;
+            s += hist[c];
+        }
+    }
     __syncthreads();
     uint64_t fb = 0;
     uint32_t h = 0;

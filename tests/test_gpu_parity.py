@@ -299,3 +299,19 @@ def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
     d_ini = torch.from_numpy(ini.astype(np.uint32).view(np.int32)).to(dev)
     got = K.extend_batch_ragged(dbuf[:arena], d_off, d_len, init=d_ini, total_len=int(lens.sum())).cpu().numpy()
     _eq(got, oracle_lib.ragged_crcs(host, offs, lens, ini.astype(np.uint32)))
+
+
+def test_ragged_unknown_total_workspace_growth(raw, dev):
+    """Without total_len the batch is scanned, sized and, when its workspace had to grow, scanned
+    again; a fresh allocation can land at the old address, so growth (not the pointer) decides."""
+    host, dbuf = raw
+    s = torch.cuda.Stream()  # its own, initially empty workspace
+    for nrec, hi in [(40, 100), (300, 1 << 16), (20, 1 << 21), (2000, 3000), (60, 1 << 22)]:
+        rng = np.random.default_rng(nrec)
+        lens = rng.integers(0, hi, nrec).astype(np.uint32)
+        offs = np.array([int(rng.integers(0, host.size - int(n) + 1)) for n in lens], dtype=np.uint64)
+        with torch.cuda.stream(s):
+            got = K.extend_batch_ragged(dbuf, torch.from_numpy(offs.astype(np.int64)).to(dev),
+                                        torch.from_numpy(lens.astype(np.int32)).to(dev), stream=s)
+        s.synchronize()
+        _eq(got.cpu().numpy(), oracle_lib.ragged_crcs(host, offs, lens))
