@@ -109,16 +109,9 @@ int comb_blob(DevState& d, uint64_t unit_bytes, const uint32_t** out) {
     return 0;
 }
 
-// A per-(device, stream) workspace: a kWsHeader-byte header that persists across
-// calls (the ragged scan's bucket starts and done counter, which must stay at a fixed
-// place and start at zero) followed by `bytes` of scratch returned in *out.
-constexpr size_t kWsHeader = 512;
-static_assert((kBuckets + 1) * sizeof(uint64_t) <= kWsHeader, "ragged header fits");
-
-int workspace(int dev, hipStream_t s, size_t bytes, void** out, uint64_t** header = nullptr,
-              bool* reallocated = nullptr) {
+// A per-(device, stream) scratch buffer, grown on demand (*reallocated: it was).
+int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocated = nullptr) {
     Workspace& w = g_ws[{dev, (void*)s}];
-    bytes += kWsHeader;
     if (reallocated) *reallocated = w.bytes < bytes;
     if (w.bytes < bytes) {
         if (w.ptr) {
@@ -130,10 +123,8 @@ int workspace(int dev, hipStream_t s, size_t bytes, void** out, uint64_t** heade
         const size_t want = align256(bytes + bytes / 4);
         KARMA_HIP(hipMalloc(&w.ptr, want));
         w.bytes = want;
-        KARMA_HIP(hipMemsetAsync(w.ptr, 0, kWsHeader, s));  // the done counter starts at 0
     }
-    *out = static_cast<char*>(w.ptr) + kWsHeader;
-    if (header) *header = static_cast<uint64_t*>(w.ptr);
+    *out = w.ptr;
     return 0;
 }
 
@@ -209,12 +200,11 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     return L;
 }
 
-void bind_ragged(RaggedArgs& a, void* ws, uint64_t* header, const RaggedLayout& L, uint64_t cap) {
+void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
     char* b = static_cast<char*>(ws);
     a.fbase = reinterpret_cast<uint64_t*>(b + L.fbase_off);
     a.pslot = reinterpret_cast<uint64_t*>(b + L.pslot_off);
     a.block_sums = reinterpret_cast<uint64_t*>(b + L.sums_off);
-    a.bucket_off = header;
     a.block_psums = reinterpret_cast<uint64_t*>(b + L.psums_off);
     a.desc = reinterpret_cast<UnitDesc*>(b + L.desc_off);
     a.partial = reinterpret_cast<uint32_t*>(b + L.part_off);
@@ -240,27 +230,30 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
     if (total_len > 0) {
         cap = 2 * n_rec + ceil_div(total_len, kDefaultUnit);
         const RaggedLayout L = ragged_layout(n_rec, cap);
-        uint64_t* hdr = nullptr;
-        KARMA_RC(workspace(dev, s, L.total, &ws, &hdr));
-        bind_ragged(a, ws, hdr, L, cap);
+        KARMA_RC(workspace(dev, s, L.total, &ws));
+        bind_ragged(a, ws, L, cap);
         KARMA_HIP(launch_ragged_scan(a, s));
     } else {
-        // Unknown total: scan, read the unit count back, size the table, rescan if it moved.
+        // Unknown total: scan, read the block totals back, size the unit table, and scan
+        // again if the workspace had to grow (a new allocation holds none of the results,
+        // even when it lands at the old address).
         cap = n_rec;
         RaggedLayout L = ragged_layout(n_rec, cap);
-        uint64_t* hdr = nullptr;
-        KARMA_RC(workspace(dev, s, L.total, &ws, &hdr));
-        bind_ragged(a, ws, hdr, L, cap);
+        KARMA_RC(workspace(dev, s, L.total, &ws));
+        bind_ragged(a, ws, L, cap);
         KARMA_HIP(launch_ragged_scan(a, s));
-        uint64_t units = 0;
-        KARMA_HIP(hipMemcpyAsync(&units, a.fbase + n_rec, sizeof(units), hipMemcpyDeviceToHost, s));
+        const uint64_t nb = ragged_scan_blocks(n_rec);
+        std::vector<uint64_t> sums(2 * nb);
+        KARMA_HIP(hipMemcpyAsync(sums.data(), a.block_sums, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        KARMA_HIP(hipMemcpyAsync(sums.data() + nb, a.block_psums, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
         KARMA_HIP(hipStreamSynchronize(s));
+        uint64_t units = 0;
+        for (uint64_t v : sums) units += v;
         cap = std::max<uint64_t>(units, 1);
         L = ragged_layout(n_rec, cap);
-        // a new allocation (possibly at the same address) holds none of the scan's results
         bool fresh = false;
-        KARMA_RC(workspace(dev, s, L.total, &ws, &hdr, &fresh));
-        bind_ragged(a, ws, hdr, L, cap);
+        KARMA_RC(workspace(dev, s, L.total, &ws, &fresh));
+        bind_ragged(a, ws, L, cap);
         if (fresh) KARMA_HIP(launch_ragged_scan(a, s));
     }
     KARMA_HIP(launch_ragged_main(a, ds.cu, s));

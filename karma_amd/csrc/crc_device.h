@@ -86,13 +86,12 @@ __device__ __forceinline__ const uint8_t* ceil16(const uint8_t* p) {
     return reinterpret_cast<const uint8_t*>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
 }
 
-// Register after bytes [from, to) of the aligned 16-byte block `blk`
-// (0 <= from <= to <= 16): whole aligned words through Z4 (one LDS round trip
-// per word), the rest byte by byte.
-__device__ __forceinline__ uint32_t steps_in_block(const uint32_t* lds, int z4, int t8, uint32_t r, const uint8_t* blk,
-                                                   uint32_t from, uint32_t to) {
+// Register after bytes [from, to) of an aligned 16-byte block already loaded
+// into v (0 <= from <= to <= 16): whole aligned words through Z4 (one LDS
+// round trip per word), the rest byte by byte.
+__device__ __forceinline__ uint32_t steps_in_vec(const uint32_t* lds, int z4, int t8, uint32_t r, const u32x4& v,
+                                                 uint32_t from, uint32_t to) {
     if (from >= to) return r;
-    const u32x4 v = ld16(blk);
     // 128-bit shift register of the block, consumed from byte 0 upwards
     uint64_t lo = v.x | ((uint64_t)v.y << 32), hi = v.z | ((uint64_t)v.w << 32);
     uint32_t i = 0;
@@ -113,6 +112,13 @@ __device__ __forceinline__ uint32_t steps_in_block(const uint32_t* lds, int z4, 
         hi >>= 8;
     }
     return r;
+}
+
+// The same for the block at `blk`, loaded here.
+__device__ __forceinline__ uint32_t steps_in_block(const uint32_t* lds, int z4, int t8, uint32_t r, const uint8_t* blk,
+                                                   uint32_t from, uint32_t to) {
+    if (from >= to) return r;
+    return steps_in_vec(lds, z4, t8, r, ld16(blk), from, to);
 }
 
 // A whole record step by step (records with no aligned 16-byte block inside).

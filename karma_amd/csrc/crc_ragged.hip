@@ -110,19 +110,14 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
     return pre + inc - v;
 }
 
-__device__ __forceinline__ uint64_t load_agent(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Per scan block: exclusive scan of full units (record order) and the
-// block's count of partial units.  The last block to finish (done counter
-// bucket_off[kBuckets], which it resets for the next call) scans both block
-// arrays: full units take slots [0, F) in record order; block b's partial
-// units take the run [F + P_b, F + P_b + parts_b), which k_ragged_desc sorts by
-// chunk count, longest first (a wave's 8 units then have nearly equal length).
+// Per scan block: exclusive scan of full units (record order), and the
+// block's totals of full and partial units (block_sums / block_psums).
+// k_ragged_desc turns the block totals into slots: full units take [0, F) in
+// record order; block b's partial units take the run [F + P_b, F + P_b +
+// parts_b), sorted by chunk count, longest first (a wave's 8 units then have
+// nearly equal length).
 __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
     __shared__ uint64_t sm[16];
-    __shared__ bool last;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     RecUnits u{};
     if (r < A.n_rec) u = rec_units(A, r);
@@ -134,37 +129,43 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
         A.block_sums[blockIdx.x] = total;
         A.block_psums[blockIdx.x] = parts;
     }
-    __threadfence();  // every thread's results before the block's done count
+}
+
+// Block b's full-unit prefix, its partial-unit prefix and the grand totals,
+// reduced from the scan's block totals by every desc block (nb loads per
+// block: cheaper than another launch or a grid-wide fence).
+struct BlockBase {
+    uint64_t full_pre, part_pre, F, P;
+};
+
+__device__ BlockBase block_base(const RaggedArgs& A, uint64_t* sm) {
+    const uint64_t nb = gridDim.x, b = blockIdx.x;
+    uint64_t fp = 0, pp = 0, ft = 0, pt = 0;
+    for (uint64_t i = threadIdx.x; i < nb; i += blockDim.x) {
+        const uint64_t f = A.block_sums[i], p = A.block_psums[i];
+        ft += f;
+        pt += p;
+        if (i < b) {
+            fp += f;
+            pp += p;
+        }
+    }
+    uint64_t v[4] = {fp, pp, ft, pt};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) v[k] += __shfl_xor(v[k], d);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (lane < 4) sm[wave * 4 + lane] = lane == 0 ? v[0] : lane == 1 ? v[1] : lane == 2 ? v[2] : v[3];
     __syncthreads();
-    if (threadIdx.x == 0)
-        last = atomicAdd(reinterpret_cast<unsigned long long*>(&A.bucket_off[kBuckets]), 1ull) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const uint64_t nblocks = gridDim.x;
-    uint64_t F = 0;
-    for (uint64_t base = 0; base < nblocks; base += blockDim.x) {
-        const uint64_t i = base + threadIdx.x;
-        const uint64_t v = i < nblocks ? load_agent(A.block_sums + i) : 0;
-        uint64_t t;
-        const uint64_t e = block_excl_scan(v, sm, t);
-        if (i < nblocks) A.block_sums[i] = F + e;
-        F += t;
+    BlockBase B{0, 0, 0, 0};
+    for (uint32_t w = 0; w < nw; ++w) {
+        B.full_pre += sm[w * 4 + 0];
+        B.part_pre += sm[w * 4 + 1];
+        B.F += sm[w * 4 + 2];
+        B.P += sm[w * 4 + 3];
     }
-    uint64_t P = F;
-    for (uint64_t base = 0; base < nblocks; base += blockDim.x) {
-        const uint64_t i = base + threadIdx.x;
-        const uint64_t v = i < nblocks ? load_agent(A.block_psums + i) : 0;
-        uint64_t t;
-        const uint64_t e = block_excl_scan(v, sm, t);
-        if (i < nblocks) A.block_psums[i] = P + e;
-        P += t;
-    }
-    if (threadIdx.x == 0) {
-        A.fbase[A.n_rec] = P;  // total units
-        A.fbase[A.n_rec + 1] = F;
-        A.bucket_off[kBuckets] = 0;  // done counter, ready for the next call
-    }
+    return B;
 }
 
 // One thread per record (block b = scan block b): final slots, the entering
@@ -179,9 +180,14 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4 then the byte table
     __shared__ unsigned long long cnt[kBuckets];
     __shared__ uint32_t hist[kBuckets];
+    __shared__ uint64_t sm[4 * (kScanBlock / 64)];
     copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
     if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
-    __syncthreads();
+    const BlockBase B = block_base(A, sm);  // has a barrier
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        A.fbase[A.n_rec] = B.F + B.P;  // total units
+        A.fbase[A.n_rec + 1] = B.F;
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = r < A.n_rec;
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
     }
     __syncthreads();
     if (threadIdx.x == 0) {  // the block's partial run, longest bucket first
-        unsigned long long s = A.block_psums[blockIdx.x];
+        unsigned long long s = B.F + B.part_pre;
         for (int c = kBuckets - 1; c >= 0; --c) {
             cnt[c] = s;
             s += hist[c];
@@ -205,7 +211,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
     const uint64_t A0 = a >> kUShift;
     if (valid) {
-        fb = A.fbase[r] + A.block_sums[blockIdx.x];
+        fb = A.fbase[r] + B.full_pre;
         A.fbase[r] = fb;
         if (u.k) h = head_register(lds, 0, 1024, A.arena + A.off[r], u.g, A.init ? A.init[r] : A.init_scalar);
         if (u.part0) {

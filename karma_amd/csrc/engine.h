@@ -86,7 +86,6 @@ struct RaggedArgs {
                                //   [n_rec] = total units, [n_rec+1] = full units
     uint64_t* pslot;           // 2 * n_rec: slots of the record's partial first / last unit
     uint64_t* block_sums;      // per scan block: full-unit offset
-    uint64_t* bucket_off;      // workspace header; [kBuckets] = scan done count (kept 0 between calls)
     uint64_t* block_psums;     // per scan block: partial units, then the block's first partial slot
     UnitDesc* desc;            // unit_cap entries
     uint64_t unit_cap;         // capacity of desc / partial
