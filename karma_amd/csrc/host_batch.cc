@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "host_trace.h"
 #include "karma_crc32c.h"
 
 namespace karma::engine {
@@ -198,6 +199,7 @@ int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, cons
     if (n_rec == 0) return KARMA_OK;
     if (!h_out || !h_off || !h_len || (!h_arena && arena_bytes))
         return karma::engine::set_last_error(KARMA_E_INVALID, "batch_ragged_host: null pointer");
+    karma::engine::PhaseTimer T("ragged_host");
     bool monotone = true;
     for (size_t r = 0; r < n_rec; ++r) {
         if (h_off[r] + h_len[r] > arena_bytes)
@@ -209,7 +211,9 @@ int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, cons
     HostCtx& c = ctx_for(dev);
     std::lock_guard<std::mutex> lk(c.mu);
     if (const int rc = c.init(dev)) return rc;
+    T.mark("validate");
     HostPin pin(h_arena, arena_bytes);
+    T.mark("hipHostRegister");
     const char* src = static_cast<const char*>(h_arena);
     int rc = 0;
     size_t r0 = 0;
@@ -266,7 +270,10 @@ int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, cons
         s.nr = nr;
         r0 = r1;
     }
-    return drain(c, h_out, rc);
+    T.mark("enqueue chunks");
+    rc = drain(c, h_out, rc);
+    T.mark("drain");
+    return rc;
 }
 
 }  // extern "C"

@@ -23,11 +23,14 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "karma-util/crc32c.h"
+#include "host_trace.h"
 #include "karma_crc32c.h"
 
 namespace karma::engine {
@@ -76,6 +79,23 @@ inline void put32(uint8_t* p, uint32_t v) {
 }
 
 constexpr uint64_t kHeader = 8;  // store::RECORD_HEADER_LENGTH (common.h:11)
+
+// body(i) for i in [lo, hi) on up to 16 std::threads, at least `grain` items each.
+template <typename F>
+void parallel_for(uint64_t lo, uint64_t hi, uint64_t grain, F&& body) {
+    const uint64_t n = hi > lo ? hi - lo : 0;
+    const uint64_t nthr = std::min<uint64_t>(16, std::max<uint64_t>(1, n / std::max<uint64_t>(grain, 1)));
+    if (nthr <= 1) {
+        for (uint64_t i = lo; i < hi; ++i) body(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (uint64_t t = 0; t < nthr; ++t)
+        th.emplace_back([&, t] {
+            for (uint64_t i = lo + n * t / nthr; i < lo + n * (t + 1) / nthr; ++i) body(i);
+        });
+    for (auto& x : th) x.join();
+}
 
 // One replay candidate: payload span to checksum and the stored CRC.
 struct Cand {
@@ -129,6 +149,78 @@ int fail(int code, const char* what) { return karma::engine::set_last_error(code
 
 static_assert(KARMA_WAL_CORRUPT == 1 && KARMA_WAL_BAD_TYPE == 2, "walk_segment stop kinds");
 
+// Device copy of a host WAL image, uploaded on a worker thread while the caller
+// walks the headers.  One cached, grow-only device buffer per device; the
+// device's lock is held from the upload until release() (the CRC batch that
+// reads the copy has completed).
+struct ImageCache {
+    std::mutex mu;
+    void* d = nullptr;
+    size_t bytes = 0;
+    hipStream_t st = nullptr;
+};
+std::mutex g_img_mu;
+std::vector<std::unique_ptr<ImageCache>> g_img;
+
+class ImageUpload {
+  public:
+    ImageUpload(const void* h, size_t bytes, int device) {
+        int dev = device;  // resolved here: a new thread starts on device 0
+        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+        th_ = std::thread([=] { rc_ = run(h, bytes, dev); });
+    }
+    ~ImageUpload() { release(); }
+    // Wait for the copy; *d = the device image.
+    int wait(const void** d) {
+        if (th_.joinable()) th_.join();
+        *d = cache_ ? cache_->d : nullptr;
+        return rc_ ? fail(rc_, msg_.c_str()) : 0;  // the worker's error, reported on this thread
+    }
+    void release() {
+        if (th_.joinable()) th_.join();
+        if (lock_.owns_lock()) lock_.unlock();
+    }
+
+  private:
+    int err(int code, const char* what) {
+        msg_ = what;
+        return code;
+    }
+    int run(const void* h, size_t bytes, int dev) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return err(KARMA_E_NO_DEVICE, "no HIP device visible");
+        if (dev >= n || hipSetDevice(dev) != hipSuccess) return err(KARMA_E_INVALID, "wal image: bad device");
+        {
+            std::lock_guard<std::mutex> g(g_img_mu);
+            if ((int)g_img.size() <= dev) g_img.resize(dev + 1);
+            if (!g_img[dev]) g_img[dev] = std::make_unique<ImageCache>();
+            cache_ = g_img[dev].get();
+        }
+        lock_ = std::unique_lock<std::mutex>(cache_->mu);
+        ImageCache& ic = *cache_;
+        if (!ic.st && hipStreamCreateWithFlags(&ic.st, hipStreamNonBlocking) != hipSuccess)
+            return err(KARMA_E_HIP, "hipStreamCreate");
+        if (ic.bytes < bytes) {
+            if (ic.d) (void)hipFree(ic.d);
+            ic.d = nullptr;
+            ic.bytes = 0;
+            if (hipMalloc(&ic.d, bytes) != hipSuccess) return err(KARMA_E_NOMEM, "wal image: hipMalloc");
+            ic.bytes = bytes;
+        }
+        const bool reg = hipHostRegister(const_cast<void*>(h), bytes, hipHostRegisterDefault) == hipSuccess;
+        if (!reg) (void)hipGetLastError();  // already pinned or not registrable: a staged copy still works
+        hipError_t e = hipMemcpyAsync(ic.d, h, bytes, hipMemcpyHostToDevice, ic.st);
+        if (e == hipSuccess) e = hipStreamSynchronize(ic.st);
+        if (reg) (void)hipHostUnregister(const_cast<void*>(h));
+        return e == hipSuccess ? 0 : err(KARMA_E_HIP, "wal image: H2D");
+    }
+    std::thread th_;
+    int rc_ = 0;
+    std::string msg_;
+    ImageCache* cache_ = nullptr;
+    std::unique_lock<std::mutex> lock_;
+};
+
 }  // namespace
 
 extern "C" {
@@ -141,15 +233,29 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
         return fail(KARMA_E_INVALID, "wal_append_batch");
     uint8_t* wal = static_cast<uint8_t*>(h_wal);
     const uint8_t* src = static_cast<const uint8_t*>(h_src);
-    // 1. placement (sequential, cheap): can_hold or footer + next segment
+    karma::engine::PhaseTimer T("wal_append");
+    // 1. CRCs of every payload: one GPU batch over the source buffer, on its own
+    //    thread while the host places and frames the records (2, 3) around it.
+    //    Records that end up not framed (image full) cost only their checksum.
+    uint64_t extent = 0;  // source bytes the batch reads
+    for (size_t i = 0; i < n; ++i) extent = std::max<uint64_t>(extent, h_src_off[i] + h_len[i]);
+    std::vector<uint32_t> crc(n);
+    int crc_rc = 0;
+    std::thread gpu;
+    if (n)
+        gpu = std::thread([&, extent] {
+            crc_rc = karma_crc32c_batch_ragged_host(src, extent, h_src_off, h_len, n, 0, crc.data(), device);
+        });
+    // 2. placement (sequential, cheap): can_hold or footer + next segment
     std::vector<uint64_t> at(n);
     uint64_t cur = *h_cursor;
     size_t framed = 0;
     std::vector<std::pair<uint64_t, uint64_t>> footers;  // (wal offset, segment end)
+    uint64_t seg_end = (cur / seg_bytes + 1) * seg_bytes;  // end of the segment holding cur
     for (; framed < n; ++framed) {
         const uint64_t len = h_len[framed];
         if (len + kHeader > seg_bytes || (len >> 24)) break;  // never fits / 3-byte size field
-        uint64_t seg_end = (cur / seg_bytes + 1) * seg_bytes;
+        if (cur == seg_end) seg_end += seg_bytes;             // the last record filled its segment
         if (cur + kHeader + len > seg_end) {  // !can_hold -> append_footer, next segment
             footers.emplace_back(cur, seg_end);
             cur = seg_end;
@@ -159,18 +265,7 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
         at[framed] = cur;
         cur += kHeader + len;
     }
-    // 2. CRCs of the framed payloads: one GPU batch over the source buffer, on its
-    //    own thread while the host threads frame the records (3) around it
-    std::vector<uint32_t> crc(framed);
-    int crc_rc = 0;
-    std::thread gpu;
-    if (framed) {
-        uint64_t extent = 0;
-        for (size_t i = 0; i < framed; ++i) extent = std::max<uint64_t>(extent, h_src_off[i] + h_len[i]);
-        gpu = std::thread([&, extent] {
-            crc_rc = karma_crc32c_batch_ragged_host(src, extent, h_src_off, h_len, framed, 0, crc.data(), device);
-        });
-    }
+    T.mark("placement");
     // 3. framing (segment_file::append_record / append_footer); the CRC fields last
     for (const auto& f : footers) {
         const uint64_t room = f.second - f.first;
@@ -195,7 +290,9 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
             std::memcpy(p + kHeader, src + h_src_off[i], h_len[i]);
         }
     });
+    T.mark("framing (payloads, lengths, footers)");
     if (gpu.joinable()) gpu.join();
+    T.mark("wait for the CRC batch");
     if (crc_rc) return crc_rc;  // payloads and length fields are written; no CRC field is
     parallel([&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) put32(wal + at[i], crc[i]);
@@ -214,59 +311,99 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
         return fail(KARMA_E_INVALID, "wal_replay");
     const uint8_t* wal = static_cast<const uint8_t*>(h_wal);
     const uint64_t nseg = wal_bytes / seg_bytes;
-    const uint64_t s0 = start / seg_bytes;
+    const uint64_t s0 = std::min<uint64_t>(start / seg_bytes, nseg);
+    const uint64_t nwork = nseg - s0;
+    karma::engine::PhaseTimer T("wal_replay");
+    // 0. no device copy given: upload the image while the headers are walked
+    std::unique_ptr<ImageUpload> up;
+    if (!d_wal && nwork) up = std::make_unique<ImageUpload>(wal + s0 * seg_bytes, nwork * seg_bytes, device);
     // 1. walk every segment from where replay would enter it, in parallel
     std::vector<std::vector<Cand>> cands(nseg);
     std::vector<uint64_t> stop(nseg);
     std::vector<int> kind(nseg);
-    auto walk = [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t s = lo; s < hi; ++s) {
-            const uint64_t base = s * seg_bytes;
-            const uint64_t pos = s == s0 ? start - base : 0;
-            kind[s] = walk_segment(wal + base, base, seg_bytes, pos, cands[s], &stop[s]);
-        }
-    };
-    const uint64_t nwork = nseg - std::min(nseg, s0);
-    const uint64_t nthr = std::min<uint64_t>(16, std::max<uint64_t>(1, nwork / 4));
-    std::vector<std::thread> th;
-    for (uint64_t t = 0; t < nthr; ++t) th.emplace_back(walk, s0 + nwork * t / nthr, s0 + nwork * (t + 1) / nthr);
-    for (auto& x : th) x.join();
+    parallel_for(s0, nseg, 4, [&](uint64_t s) {
+        const uint64_t base = s * seg_bytes;
+        const uint64_t pos = s == s0 ? start - base : 0;
+        kind[s] = walk_segment(wal + base, base, seg_bytes, pos, cands[s], &stop[s]);
+    });
+    T.mark("header walk");
     // replay enters segment s+1 only if segment s ended cleanly
-    std::vector<Cand> all;
     int status = 0;
-    uint64_t end = wal_bytes;
-    for (uint64_t s = s0; s < nseg; ++s) {
-        all.insert(all.end(), cands[s].begin(), cands[s].end());
+    uint64_t end = nwork ? wal_bytes : start;
+    uint64_t s1 = nseg;  // one past the last segment replay reads
+    for (uint64_t s = s0; s < nseg; ++s)
         if (kind[s] != 0) {
             status = kind[s];
             end = stop[s];
+            s1 = s + 1;
             break;
         }
+    // candidate slots: gb = all candidates before segment s, nb = those with a payload
+    std::vector<uint64_t> gb(nseg + 1, 0), nb(nseg + 1, 0);
+    for (uint64_t s = s0; s < s1; ++s) {
+        uint64_t nz = 0;
+        for (const Cand& x : cands[s]) nz += x.len != 0;
+        gb[s + 1] = gb[s] + cands[s].size();
+        nb[s + 1] = nb[s] + nz;
     }
-    if (s0 >= nseg) end = start;
+    const uint64_t n_all = gb[s1], n_nz = nb[s1];
     // 2. payload CRCs in one GPU batch (size-0 records were checked on the host)
-    std::vector<uint64_t> off;
-    std::vector<uint32_t> len;
-    std::vector<size_t> idx;
-    for (size_t i = 0; i < all.size(); ++i)
-        if (all[i].len) {
-            off.push_back(all[i].off);
-            len.push_back(all[i].len);
-            idx.push_back(i);
-        }
-    std::vector<uint32_t> got(off.size());
-    if (const int rc = karma::engine::crc_spans(h_wal, d_wal, wal_bytes, off, len, got, device)) return rc;
+    std::vector<uint64_t> off(n_nz);
+    std::vector<uint32_t> len(n_nz);
+    parallel_for(s0, s1, 8, [&](uint64_t s) {
+        uint64_t j = nb[s];
+        for (const Cand& x : cands[s])
+            if (x.len) {
+                off[j] = x.off;
+                len[j] = x.len;
+                ++j;
+            }
+    });
+    T.mark("span lists");
+    std::vector<uint32_t> got;
+    if (up && off.empty()) {
+        up->release();  // nothing to checksum: the upload (and any device error) does not matter
+    } else if (up) {  // spans are WAL offsets; the uploaded copy starts at segment s0
+        const void* d = nullptr;
+        if (const int rc = up->wait(&d)) return rc;
+        T.mark("image upload (rest of it)");
+        const uint64_t base = s0 * seg_bytes;
+        parallel_for(0, off.size(), 1 << 16, [&](uint64_t j) { off[j] -= base; });
+        const int rc = karma::engine::crc_spans(wal + base, d, nwork * seg_bytes, off, len, got, device);
+        up->release();
+        if (rc) return rc;
+    } else if (const int rc = karma::engine::crc_spans(h_wal, d_wal, wal_bytes, off, len, got, device)) {
+        return rc;
+    }
+    T.mark("CRC batch");
     // 3. the first mismatch (in WAL order) is where scan_record logs "Corrupt record"
-    size_t accepted = all.size();
-    for (size_t j = 0; j < idx.size(); ++j)
-        if (got[j] != all[idx[j]].stored) {
-            accepted = idx[j];
+    std::vector<uint64_t> bad(nseg, UINT64_MAX);
+    parallel_for(s0, s1, 8, [&](uint64_t s) {
+        uint64_t j = nb[s];
+        for (size_t i = 0; i < cands[s].size(); ++i) {
+            const Cand& x = cands[s][i];
+            if (x.len && got[j++] != x.stored) {
+                bad[s] = gb[s] + i;
+                return;
+            }
+        }
+    });
+    uint64_t accepted = n_all;
+    for (uint64_t s = s0; s < s1; ++s)
+        if (bad[s] != UINT64_MAX) {
+            accepted = bad[s];
             status = KARMA_WAL_CORRUPT;
-            end = all[idx[j]].rec;
+            end = cands[s][bad[s] - gb[s]].rec;
             break;
         }
     if (h_rec_off)
-        for (size_t i = 0; i < accepted && i < rec_cap; ++i) h_rec_off[i] = all[i].rec;
+        parallel_for(s0, s1, 8, [&](uint64_t s) {
+            for (size_t i = 0; i < cands[s].size(); ++i) {
+                const uint64_t g = gb[s] + i;
+                if (g < accepted && g < rec_cap) h_rec_off[g] = cands[s][i].rec;
+            }
+        });
+    T.mark("compare + offsets");
     *h_n_records = accepted;
     *h_stop = end;
     *h_status = status;
