@@ -126,13 +126,11 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
             "single_thread_value": round(single, 3), "cpu_model": cpu, "host_cores_visible": os.cpu_count()}
 
 
-def units_kernel_name(wl: str, arena, rec: int, n_rec: int) -> str:
-    """The dominant kernel a batch runs (capi.cc planning; crc_fixed.hip fixed_aligned_ok)."""
+def units_kernel_name(wl: str) -> str:
+    """The dominant kernel a batch runs (capi.cc planning, crc_fixed.hip / crc_ragged.hip launchers)."""
     if wl == "ragged":
         return "k_units_ragged_pipe" if os.environ.get("KARMA_RAGGED_VARIANT") == "1" else "k_units_ragged"
-    variant = os.environ.get("KARMA_CRC_VARIANT", "0")
-    aligned = arena.data_ptr() % 128 == 0 and rec % 512 == 0
-    return "k_units_aligned" if (aligned and variant == "7") else "k_units_fixed"
+    return "k_units_fixed_v1" if os.environ.get("KARMA_CRC_VARIANT") == "1" else "k_units_fixed"
 
 
 def pmc_traffic(path: str, workload: str, n_bytes_per_launch: int):
@@ -466,7 +464,7 @@ def main():
             "data": "synthetic: little-endian splitmix64 byte stream generated on the device before timing",
             "config": {"workload": workload_desc, "records_per_gpu": int(n_rec), "rec_bytes": int(rec),
                        "parallelism": f"record-sharded x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
-                       "kernel": units_kernel_name(wl, arena, rec, n_rec) if out is not None else
+                       "kernel": units_kernel_name(wl) if out is not None else
                                  "host->device pipeline"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -268,9 +268,7 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
     return c;
 }
 
-// ---- pipelined form of group_unit: the next unit's first loads are issued
-// before the current unit's last chunks and epilogue, so a group's load stream
-// has no gap at unit boundaries.  Same arithmetic and result as group_unit.
+// ---- one unit as seen by one lane of its group
 struct LaneUnit {
     const uint8_t* us;      // unit span [us, ue)
     const uint8_t* ue;
@@ -302,53 +300,66 @@ __device__ __forceinline__ LaneUnit lane_unit(const uint8_t* us, const uint8_t* 
     return L;
 }
 
-// First loads of a unit: chunk 0 (kept only where the window is inside the
-// span: ok0) and chunks 1..PF (clamped to the lane's last valid window).
+// ---- software-pipelined unit stream ----------------------------------------
+// The loads a lane has in flight for one unit: its chunk-0 window and chunks
+// 1..PF (clamped to its last valid window).  Every address is valid whatever
+// the unit (empty and out-of-range units point at a safe 16-byte block), so
+// the loads are issued without branches and their results are first used one
+// unit later: the compiler never has to wait for a just-issued load
+// (s_waitcnt vmcnt(0)), and a group's load stream has no gap at unit
+// boundaries.
+template <int PF>
+struct UnitLoads {
+    u32x4 v0;
+    u32x4 nb[PF];
+};
+
 template <int PF, bool NT>
-__device__ __forceinline__ void unit_first_loads(const LaneUnit& L, u32x4& v0, bool& ok0, u32x4 (&nb)[PF]) {
-    ok0 = false;
-    if (L.nch == 0) return;
-    ok0 = L.w >= L.us && L.w < L.ue;
-    v0 = ldg<NT>(ok0 ? L.w : L.lclamp);
+__device__ __forceinline__ void issue_unit_loads(const LaneUnit& L, UnitLoads<PF>& Ld) {
+    const bool ok0 = L.nch > 0 && L.w >= L.us && L.w < L.ue;
+    Ld.v0 = ldg<NT>(ok0 ? L.w : L.lclamp);
 #pragma unroll
-    for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(L.w + (q + 1) * kChunk, L.lclamp));
+    for (int q = 0; q < PF; ++q) Ld.nb[q] = ldg<NT>(pmin(L.w + (q + 1) * kChunk, L.lclamp));
 }
 
-// Streams unit L (its first loads already in v0/ok0/nb), issuing unit N's first
-// loads into v0n/ok0n/nb on the way.  Every lane of the wave must call this.
-template <int PF, bool NT>
-__device__ __forceinline__ uint32_t group_unit_pipe(const uint32_t* lds, uint32_t X, uint32_t l, const LaneUnit& L,
-                                                    u32x4 v0, bool ok0, u32x4 (&nb)[PF], const uint8_t* inj_at,
-                                                    uint32_t inj, const LaneUnit& N, u32x4& v0n, bool& ok0n) {
-    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    if (L.nch > 0) {
-        u32x4 v = ok0 ? v0 : u32x4{0u, 0u, 0u, 0u};
-        if (L.w == inj_at) v.x ^= inj;
-        a0 = v.x;
-        a1 = v.y;
-        a2 = v.z;
-        a3 = v.w;
-    }
-    int64_t rem = L.nch - 1;
+// Streams unit L whose first loads are in Ld; `issue_next(Ld)` is called once,
+// before the unit's last PF chunks are consumed, to put the next unit's first
+// loads in flight.  `inj` is xored into the word at `inj_at` (nullptr: none).
+// One batch of PF chunks is in flight while the previous one is stepped (a
+// two-bank ring that never runs dry measured no faster: DESIGN.md §4).
+// Every lane of the wave must call this (cross-lane shuffles); the result is
+// valid in group lane 0.
+template <int PF, bool NT, int MODE = 0, typename IssueNext>
+__device__ __forceinline__ uint32_t stream_unit(const uint32_t* lds, uint32_t X, uint32_t l, const LaneUnit& L,
+                                                UnitLoads<PF>& Ld, const uint8_t* inj_at, uint32_t inj,
+                                                IssueNext&& issue_next) {
+    const bool ok0 = L.nch > 0 && L.w >= L.us && L.w < L.ue;
+    u32x4 v = ok0 ? Ld.v0 : u32x4{0u, 0u, 0u, 0u};
+    if (ok0 && L.w == inj_at) v.x ^= inj;
+    uint32_t a0 = v.x, a1 = v.y, a2 = v.z, a3 = v.w;
+    int64_t rem = L.nch - 1;  // chunks after chunk 0; the final one is masked per lane
     const uint8_t* w = L.w + kChunk;
     while (rem > PF) {
         u32x4 cur[PF];
 #pragma unroll
-        for (int q = 0; q < PF; ++q) cur[q] = nb[q];
+        for (int q = 0; q < PF; ++q) cur[q] = Ld.nb[q];
         w += PF * kChunk;
 #pragma unroll
-        for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, L.lclamp));
+        for (int q = 0; q < PF; ++q) Ld.nb[q] = ldg<NT>(pmin(w + q * kChunk, L.lclamp));
 #pragma unroll
-        for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+        for (int q = 0; q < PF; ++q) step4<MODE>(lds, X, a0, a1, a2, a3, cur[q]);
         rem -= PF;
     }
-    u32x4 cur[PF];
+    constexpr int D = PF;
+    u32x4 cur[D];
 #pragma unroll
-    for (int q = 0; q < PF; ++q) cur[q] = nb[q];
-    unit_first_loads<PF, NT>(N, v0n, ok0n, nb);
+    for (int q = 0; q < D; ++q) cur[q] = Ld.nb[q];
+    issue_next(Ld);
 #pragma unroll
-    for (int q = 0; q < PF; ++q)
-        if (q < rem - 1 || (q == rem - 1 && L.lok)) step4(lds, X, a0, a1, a2, a3, cur[q]);
+    for (int q = 0; q < D; ++q)
+        if (q < rem - 1 || (q == rem - 1 && L.lok)) step4<MODE>(lds, X, a0, a1, a2, a3, cur[q]);
+    // lane fold (crc32c.cc STEP4W order), then the 8-lane tree with the lane
+    // holding the unit's last window rotated to the end
     uint32_t c = zmap(lds, kLZ4, a0);
     c = zmap(lds, kLZ4, c ^ a1);
     c = zmap(lds, kLZ4, c ^ a2);

@@ -19,8 +19,101 @@ namespace {
 
 using namespace dev;
 
-template <int PF, bool NT, int MODE = 0>
+// Per-lane plan of unit u of a fixed-layout batch (arithmetic only, no memory
+// access).  Records hold an aligned 16-byte block (rec_bytes >= 31), so the
+// body start g.a is a safe address for every load of an empty or out-of-range
+// unit.
+struct FixedPlan {
+    LaneUnit L;
+    const uint8_t* hblk;  // 16-byte block with the unaligned head bytes [hfrom, 16)
+    const uint8_t* tblk;  // 16-byte block with the unaligned tail bytes [0, tto)
+    const uint8_t* inj_at;  // the body start when this unit holds it, else nullptr
+    uint64_t r;
+    uint32_t hfrom, tto;
+    bool valid;
+};
+
+__device__ __forceinline__ FixedPlan fixed_plan(const FixedArgs& A, uint64_t u, uint64_t U, uint32_t l) {
+    FixedPlan P;
+    const uint64_t k = A.units_per_rec;
+    P.valid = u < U;
+    const uint64_t uu = P.valid ? u : 0;
+    P.r = k == 1 ? uu : uu / k;
+    const uint64_t j = uu - P.r * k;
+    const uint8_t* p = A.arena + P.r * A.rec_bytes;
+    const Geom g = geom(p, A.rec_bytes);
+    // unit j of the body [a, b), end-aligned at b: [b - (k-j)*U, b - (k-1-j)*U) clipped to a
+    const uint8_t* ue = g.b - (int64_t)((k - 1 - j) * A.unit_bytes);
+    const uint8_t* us_raw = ue - (int64_t)A.unit_bytes;
+    const uint8_t* us = pmax(us_raw, g.a);
+    const bool first = P.valid && g.a >= us_raw && g.a < ue;
+    if (!P.valid || ue <= g.a) us = ue = g.a;  // empty: safe addresses, no steps
+    P.L = lane_unit(us, ue, l);
+    P.inj_at = first ? g.a : nullptr;
+    const bool head = first && p < g.a;
+    P.hblk = head ? g.a - 16 : g.a;
+    P.hfrom = head ? (uint32_t)(p - (g.a - 16)) : 16u;
+    const bool tail = P.valid && j == k - 1 && g.e > g.b;
+    P.tblk = tail ? g.b : g.a;
+    P.tto = tail ? (uint32_t)(g.e - g.b) : 0u;
+    return P;
+}
+
+// Fixed records with rec_bytes >= 31: every lane streams its groups' units
+// back to back; the loads of unit u + step (chunk 0, PF chunks, the head and
+// tail blocks, the init value) are issued before unit u's last chunks are
+// consumed (stream_unit), so no wave waits on a fresh load at a unit boundary.
+template <int PF, bool NT, bool HAS_INIT, int MODE = 0>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const uint64_t k = A.units_per_rec;
+    const uint64_t U = A.n_rec * k;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t step = nwaves * kGroupsPerWave;
+    uint64_t wb = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    uint64_t u = wb * kGroupsPerWave + grp;
+    // unit u's head block and init value, then its chunk loads
+    FixedPlan P = fixed_plan(A, u, U, l);
+    u32x4 hv = ld16(P.hblk), tv = ld16(P.tblk);
+    uint32_t iv = HAS_INIT ? *(const __attribute__((address_space(1))) uint32_t*)(A.init + P.r) : A.init_scalar;
+    UnitLoads<PF> Ld;
+    issue_unit_loads<PF, NT>(P.L, Ld);
+    for (; wb * kGroupsPerWave < U; wb += nwaves, u += step) {
+        uint32_t inj = 0;
+        if (P.inj_at) inj = P.hfrom < 16 ? steps_in_vec(lds, kLZ4, kLT8, ~iv, hv, P.hfrom, 16u) : ~iv;
+        // Every load is issued ahead of unit boundaries, with the next unit's
+        // chunks (a load issued just before the main loop would be waited on by
+        // its first batch: vmcnt counts in order).
+        const u32x4 tcur = tv;
+        FixedPlan N;
+        const uint32_t R = stream_unit<PF, NT, MODE>(lds, X, l, P.L, Ld, P.inj_at, inj, [&](UnitLoads<PF>& nx) {
+            N = fixed_plan(A, u + step, U, l);
+            hv = ld16(N.hblk);
+            tv = ld16(N.tblk);
+            if constexpr (HAS_INIT) iv = *(const __attribute__((address_space(1))) uint32_t*)(A.init + N.r);
+            issue_unit_loads<PF, NT>(N.L, nx);
+        });
+        if (P.valid && l == 0) {
+            if (k == 1)
+                A.out[P.r] = ~steps_in_vec(lds, kLZ4, kLT8, R, tcur, 0u, P.tto);
+            else
+                A.partial[u] = R;
+        }
+        P = N;
+    }
+}
+
+// Records of fewer than 31 bytes may hold no aligned 16-byte block (and tiny
+// batches need no streaming): the general kernel, one unit per group, each
+// unit's loads issued when the unit starts.  Also the A/B baseline (variant 1).
+template <int PF, bool NT, int MODE = 0>
+__global__ __launch_bounds__(kBlockThreads) void k_units_fixed_v1(FixedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
     __syncthreads();
@@ -75,77 +168,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     }
 }
 
-// Fixed records on the absolute 128-byte grid (arena 128-aligned, unit a
-// multiple of PF chunks, rec_bytes = k * unit): unit u is simply
-// arena + u * unit_bytes, with no head, tail or partial chunk.  Each lane's
-// loads form one continuous stream across the wave's units: the first PF
-// chunks of the group's next unit are issued before the current unit's
-// fold and tree, so no memory bubble opens at unit boundaries.
-template <int PF>
-__global__ __launch_bounds__(kBlockThreads) void k_units_aligned(FixedArgs A) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
-    load_stream_tables(lds, A.blob);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t l = lane & (kGroupLanes - 1);
-    const uint32_t grp = lane / kGroupLanes;
-    const uint32_t X = lane_const();
-    const uint64_t k = A.units_per_rec;
-    const uint64_t U = A.n_rec * k;
-    const uint64_t C = A.unit_bytes / kChunk;  // chunks per unit, a multiple of PF
-    const uint64_t step = (uint64_t)gridDim.x * kWavesPerBlock * kGroupsPerWave;
-    const uint8_t* base = A.arena + 16 * l;
-    const uint64_t ub = A.unit_bytes;
-    auto at = [&](uint64_t uu, uint64_t c) {  // clamped: groups past the end load a valid line
-        return base + (uu < U ? uu : U - 1) * ub + c * kChunk;
-    };
-    uint64_t w0 = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kGroupsPerWave;
-    uint64_t u = w0 + grp;
-    u32x4 nb[PF];
-#pragma unroll
-    for (int q = 0; q < PF; ++q) nb[q] = ldg<true>(at(u, q));
-    for (; w0 < U; w0 += step, u += step) {
-        const bool valid = u < U;
-        uint32_t inj = 0;
-        uint64_t r = u;
-        if (k != 1) r = u / k;
-        if (valid && l == 0 && r * k == u) inj = ~(A.init ? A.init[r] : A.init_scalar);
-        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-        for (uint64_t c = 0; c < C; c += PF) {
-            u32x4 cur[PF];
-#pragma unroll
-            for (int q = 0; q < PF; ++q) cur[q] = nb[q];
-            if (c + PF < C) {
-#pragma unroll
-                for (int q = 0; q < PF; ++q) nb[q] = ldg<true>(at(u, c + PF + q));
-            } else {
-#pragma unroll
-                for (int q = 0; q < PF; ++q) nb[q] = ldg<true>(at(u + step, q));
-            }
-            if (c == 0) cur[0].x ^= inj;
-#pragma unroll
-            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
-        }
-        // lane fold (crc32c.cc STEP4W order), then the 8-lane tree (lane 7 holds the last window)
-        uint32_t c = zmap(lds, kLZ4, a0);
-        c = zmap(lds, kLZ4, c ^ a1);
-        c = zmap(lds, kLZ4, c ^ a2);
-        c = zmap(lds, kLZ4, c ^ a3);
-        uint32_t t = __shfl_down(c, 1, kGroupLanes);
-        c = zmap(lds, kLZ16, c) ^ t;
-        t = __shfl_down(c, 2, kGroupLanes);
-        c = zmap(lds, kLZ32, c) ^ t;
-        t = __shfl_down(c, 4, kGroupLanes);
-        c = zmap(lds, kLZ64, c) ^ t;
-        if (valid && l == 0) {
-            if (k == 1)
-                A.out[u] = ~c;
-            else
-                A.partial[u] = c;
-        }
-    }
-}
-
 // One combine level: record r's k_in states (end-aligned, D bytes each) ->
 // k_out = ceil(k_in / 64) states of 64*D bytes; the last level (k_out == 1)
 // adds the record tail and writes the CRC.  One wave per output state.
@@ -184,36 +206,28 @@ int fixed_variant() {
 
 }  // namespace
 
-bool fixed_aligned_ok(const FixedArgs& a) {
-    return (reinterpret_cast<uintptr_t>(a.arena) & (kChunk - 1)) == 0 && a.unit_bytes % (kChunk * 4) == 0 &&
-           a.rec_bytes == a.units_per_rec * a.unit_bytes && a.rec_bytes > 0;
-}
-
-bool fixed_fast_path_ok(const FixedArgs& a) {
-    return (reinterpret_cast<uintptr_t>(a.arena) & 15u) == 0 && a.unit_bytes % kChunk == 0 &&
-           a.rec_bytes == a.units_per_rec * a.unit_bytes && a.rec_bytes > 0;
-}
-
 hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     const uint64_t units = a.n_rec * a.units_per_rec;
     const uint64_t need = (units + kGroupsPerWave * kWavesPerBlock - 1) / (kGroupsPerWave * kWavesPerBlock);
     const dim3 grid((unsigned)(need < (uint64_t)grid_blocks ? need : (uint64_t)grid_blocks));
     units_timer_begin(s);
-    switch (fixed_variant()) {
-        case 1: hipLaunchKernelGGL((k_units_fixed<4, false>), grid, dim3(kBlockThreads), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_units_fixed<2, true>), grid, dim3(kBlockThreads), 0, s, a); break;
-        case 3: hipLaunchKernelGGL((k_units_fixed<6, true>), grid, dim3(kBlockThreads), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_units_fixed<4, true, 1>), grid, dim3(kBlockThreads), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((k_units_fixed<4, true, 2>), grid, dim3(kBlockThreads), 0, s, a); break;
-        case 6: hipLaunchKernelGGL((k_units_fixed<4, true, 3>), grid, dim3(kBlockThreads), 0, s, a); break;
-        case 7:
-            if (fixed_aligned_ok(a)) {
-                hipLaunchKernelGGL((k_units_aligned<4>), grid, dim3(kBlockThreads), 0, s, a);
+    const dim3 blk(kBlockThreads);
+    if (a.rec_bytes < 31) {  // records may hold no aligned 16-byte block
+        hipLaunchKernelGGL((k_units_fixed_v1<4, true>), grid, blk, 0, s, a);
+    } else {
+        switch (fixed_variant()) {
+            case 1: hipLaunchKernelGGL((k_units_fixed_v1<4, true>), grid, blk, 0, s, a); break;
+            case 2:
+                if (a.init) hipLaunchKernelGGL((k_units_fixed<2, true, true>), grid, blk, 0, s, a);
+                else hipLaunchKernelGGL((k_units_fixed<2, true, false>), grid, blk, 0, s, a);
                 break;
-            }
-            [[fallthrough]];
-        default: hipLaunchKernelGGL((k_units_fixed<4, true>), grid, dim3(kBlockThreads), 0, s, a); break;
+            case 6: hipLaunchKernelGGL((k_units_fixed<4, true, false, 1>), grid, blk, 0, s, a); break;  // timing only
+            default:
+                if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true>), grid, blk, 0, s, a);
+                else hipLaunchKernelGGL((k_units_fixed<4, true, false>), grid, blk, 0, s, a);
+                break;
+        }
     }
     units_timer_end(s);
     return hipGetLastError();

@@ -102,11 +102,6 @@ void units_timer_end(hipStream_t s);
 
 // Launchers (stream-ordered, no allocation, no synchronisation).
 hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s);
-// True when the continuous-stream kernel applies (aligned arena, whole-chunk units).
-bool fixed_fast_path_ok(const FixedArgs& a);
-// True when k_units_aligned applies: 128-byte aligned arena, unit a multiple of 4 chunks,
-// records made of whole units.
-bool fixed_aligned_ok(const FixedArgs& a);
 // One combine level for the fixed layout: k_in states per record -> k_out = ceil(k_in / 64).
 hipError_t launch_combine_fixed(const FixedArgs& a, const uint32_t* in_states, uint64_t k_in, uint32_t* out_states,
                                 uint64_t k_out, const uint32_t* comb_blob, hipStream_t s);

@@ -279,7 +279,7 @@ def test_rejects_bad_arguments(dev):
         K.value_batch_fixed(buf, 7)
 
 
-@pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", "7"), ("KARMA_RAGGED_VARIANT", "1")])
+@pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", v) for v in "12"] + [("KARMA_RAGGED_VARIANT", "1")])
 def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
     """The A/B kernel builds (tools/variant_bench.py) are held to the same parity as the default."""
     monkeypatch.setenv(env, val)

@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import karma_amd as K  # noqa: E402
 
-variants = [int(v) for v in sys.argv[1:]] or [10, 11, 12, 13, 14, 15, 16, 17, 18, 1]
+variants = [int(v) for v in sys.argv[1:]] or [0, 1, 2, 6]
 dev = torch.device("cuda:0")
 n, rec = 1 << 20, 4096
 MIS = int(os.environ.get("MISALIGN", "0"))  # byte offset of the arena (alignment experiments)
@@ -38,7 +38,7 @@ for rnd in range(int(os.environ.get('ROUNDS', '8'))):
         got = out.cpu().numpy()
         if ref is None:
             ref = got.copy()
-        if v < 4:  # variants 4-6 are timing experiments with wrong results by design
+        if v != 6:  # variant 6 is a timing experiment with wrong results by design
             assert np.array_equal(got, ref), f"variant {v} differs"
 for v in variants:
     ms = np.array(res[v])
