@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="fixed",
-                   choices=["fixed", "ragged", "stream", "host", "wal_append", "wal_replay"])
+                   choices=["fixed", "ragged", "stream", "segment", "host", "wal_append", "wal_replay"])
     p.add_argument("--wal-record", type=int, default=180, help="wal_* payload bytes (configs[0]: ~180 B)")
     p.add_argument("--records-per-gpu", type=int, default=1 << 20)
     p.add_argument("--rec-bytes", type=int, default=4096)
@@ -83,7 +83,7 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
                 oracle_lib.port().oracle_ragged_crcs(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, n,
                                                      out.ctypes.data, nthr)
     else:
-        if workload == "stream":
+        if workload in ("stream", "segment"):
             rec_bytes, n = 64 << 20, 4
             threads = min(threads, n)
         else:
@@ -181,6 +181,23 @@ def wal_bench(args, L, rank):
 
     append()
     step = append if args.workload == "wal_append" else replay
+    dev_rate = None
+    if args.workload == "wal_replay":  # the same replay over a copy already in HBM (no upload)
+        import torch
+        d_wal = torch.from_numpy(wal).to(torch.device("cuda", local))
+
+        def replay_dev():
+            _lib.check("wal_replay", L.karma_wal_replay(None, d_wal.data_ptr(), wal_bytes, seg, 0, ctypes.byref(nrec),
+                                                        ctypes.byref(stop), ctypes.byref(status), None, 0, local))
+            assert nrec.value == n
+
+        for _ in range(args.warmup):
+            replay_dev()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            replay_dev()
+        dev_rate = n * size / ((time.perf_counter() - t0) / args.steps) / GIB
+        del d_wal
     for _ in range(args.warmup):
         step()
     t0 = time.perf_counter()
@@ -193,6 +210,7 @@ def wal_bench(args, L, rank):
            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "u8", "data": "synthetic splitmix64 payloads in pageable host memory",
            "records_per_s": round(n / dt, 1),
+           "device_resident_value": round(dev_rate, 3) if dev_rate is not None else None,
            "config": {"workload": f"{n} x {size} B WAL records, 1 MiB segments, "
                                   f"{'karma_wal_append_batch' if step is append else 'karma_wal_replay'} "
                                   f"(BASELINE configs[0] shape)", "records": n, "record_bytes": size},
@@ -342,6 +360,27 @@ def main():
         algo_bytes = payload + nseg * 4
         workload_desc = f"{nseg} distinct 64 MiB segment scans per step (chunked CRC + polynomial combine, " \
                         f"BASELINE configs[3])"
+    elif wl == "segment":
+        # configs[3] as latency: one 64 MiB segment -> one Value per step (karma_crc32c_stream),
+        # rotating over 64 distinct segments so every step reads HBM, not the 256 MB MALL
+        seg, nseg = 64 << 20, 64
+        arena = torch.empty(nseg * seg, dtype=torch.uint8, device=dev)
+        K.fill_splitmix64(arena, args.seed, first_byte=rank * nseg * seg)
+        n_rec, rec = 1, seg
+        payload = seg
+        out = torch.empty(nseg, dtype=torch.uint32, device=dev)
+        seg_i = {"i": 0}
+
+        def crc_step():
+            i = seg_i["i"] % nseg
+            seg_i["i"] += 1
+            st = L.karma_crc32c_stream(0, arena.data_ptr() + i * seg, seg, cur['out'].data_ptr() + 4 * i, sh)
+            if st:
+                _lib.check("stream", st)
+
+        algo_bytes = seg + 4
+        workload_desc = "one 64 MiB segment scan per step (karma_crc32c_stream: chunked CRC + polynomial combine), " \
+                        "64 distinct segments in rotation (BASELINE configs[3], latency)"
     else:  # host: PCIe-inclusive end-to-end from pageable host memory
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import synth
@@ -433,8 +472,26 @@ def main():
     else:
         kern_max, call_max = kern_avg, call_avg
 
+    # ---- single-segment latency: isolated calls, each waited for ------------------------------
+    extra = {}
+    if wl == "segment" and rank == 0:
+        lat = []
+        for _ in range(20):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            crc_step()
+            b.record(stream)
+            torch.cuda.synchronize()
+            lat.append(a.elapsed_time(b))
+        extra["single_segment_latency_us"] = round(float(np.median(lat)) * 1e3, 2)
+        extra["single_segment_latency_gibs"] = round(payload / (float(np.median(lat)) * 1e-3) / GIB, 1)
+
     # ---- self-check: a sample of records against the host crc32c::Extend (product path) ----
     check = {}
+    if wl == "segment" and rank == 0:
+        got = cur["out"].cpu().numpy()
+        bad = sum(int(K.Value(arena[i * rec:(i + 1) * rec].cpu().numpy()) != int(got[i])) for i in range(4))
+        check = {"sampled_records": 4, "mismatches": bad}
     if out is not None and rank == 0 and wl in ("fixed", "stream"):
         idx = np.unique(np.concatenate([np.arange(min(64, n_rec)), np.random.default_rng(1).integers(0, n_rec, 64)]))
         got = cur["out"].cpu().numpy()
@@ -474,6 +531,7 @@ def main():
                          "call_frac": round(algo_bytes / (call_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "compute_only_gibs": round(payload * world / (call_max * 1e-3) / GIB, 2),
         }
+        res.update(extra)
         if check:
             res["self_check"] = check
         if world == 1 and not args.no_cpu_baseline:

@@ -111,6 +111,35 @@ uint64_t ragged_scan_blocks(uint64_t n_rec);
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 
+// ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
+struct WalSegMeta {
+    uint32_t count;  // type-0 records (candidates) the walk found
+    uint32_t kind;   // KARMA_WAL_END / _CORRUPT / _BAD_TYPE
+    uint64_t stop;   // WAL offset where the segment's walk stopped (segment end for END)
+};
+static_assert(sizeof(WalSegMeta) == 16, "one 16-byte record per segment");
+
+struct WalArgs {
+    const uint8_t* wal;        // first byte of segment s0 (WAL offset base0)
+    uint64_t base0;            // s0 * seg_bytes
+    uint64_t seg_bytes;        // < 2^32
+    uint64_t first_pos;        // where replay enters segment s0 (start - base0)
+    uint32_t* cand_rec;        // per segment: cand_cap header offsets within the segment
+    uint32_t* cand_len;        //              and payload lengths
+    uint64_t cand_cap;         // seg_bytes / 8 + 1
+    WalSegMeta* meta;          // per segment
+    const uint64_t* cand_base; // per segment: first slot in the contiguous lists
+    uint64_t* off;             // header offset relative to wal, per candidate
+    uint32_t* len;
+    uint32_t* stored;          // CRC field of the header
+    const uint32_t* crc;       // payload CRC from the ragged batch
+    uint64_t* first_bad;       // min candidate index with crc != stored
+};
+uint32_t wal_walk_tile();
+hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, hipStream_t s);
+hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s);
+hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);
+
 // Synthetic data: bytes of the counter-based splitmix64 stream.
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n_bytes, uint64_t seed, uint64_t first_byte, hipStream_t s);
 // Read-only streaming probe (achievable-HBM reference): xor-reduces n_bytes.

@@ -12,9 +12,11 @@
 //   segment with append_footer and move on; then append_record.  The
 //   payload CRCs of the whole batch are computed in one GPU ragged batch.
 // karma_wal_replay        = sivir::open's loop over wal::scan_record
-//   (sivir.cc:31-41, wal.cc:34-87): headers are walked on the host, every
-//   payload CRC is verified in one GPU ragged batch, and replay stops where
-//   scan_record would return false.  The reference's quirk for a type-0
+//   (sivir.cc:31-41, wal.cc:34-87), entirely on the device over an image in
+//   HBM (wal_device.hip): segment-parallel header walk, one ragged CRC batch
+//   over every payload, first mismatch; replay stops where scan_record would
+//   return false.  A host image is first streamed into HBM through pinned
+//   staging buffers filled by several threads.  The reference's quirk for a type-0
 //   record of size 0 is kept: read_exact_at returns early for size 0
 //   (segment_file.cc:8) so the CRC is taken over the stale 4-byte len/type
 //   word just read (wal.cc:50-60).  It is load-bearing: it is what ends replay
@@ -29,7 +31,7 @@
 #include <thread>
 #include <vector>
 
-#include "karma-util/crc32c.h"
+#include "engine.h"
 #include "host_trace.h"
 #include "karma_crc32c.h"
 
@@ -97,129 +99,114 @@ void parallel_for(uint64_t lo, uint64_t hi, uint64_t grain, F&& body) {
     for (auto& x : th) x.join();
 }
 
-// One replay candidate: payload span to checksum and the stored CRC.
-struct Cand {
-    uint64_t rec;      // WAL offset of the header
-    uint64_t off;      // checksummed span (payload, or the len/type word for size 0)
-    uint32_t len;
-    uint32_t stored;
-};
-
-// Walk one segment's headers from `pos` (scan_record's structural checks).
-// Returns the stop kind: 0 = reached the segment end (padding / short tail),
-// 1 = corrupt (length past the segment end, or a size-0 record whose stale
-// 4-byte CRC mismatches), 2 = unknown record type.
-int walk_segment(const uint8_t* seg, uint64_t seg_base, uint64_t seg_bytes, uint64_t pos, std::vector<Cand>& out,
-                 uint64_t* stop) {
-    while (true) {
-        if (pos + kHeader > seg_bytes) {  // wal.cc:40-45: the rest of the segment is skipped
-            *stop = seg_base + seg_bytes;
-            return 0;
-        }
-        const uint32_t crc = le32(seg + pos);
-        const uint32_t st = le32(seg + pos + 4);
-        const uint32_t type = st & 0xffu, size = st >> 8;
-        if (type == 0) {
-            if (pos + kHeader + size > seg_bytes) {  // wal.cc:71-74
-                *stop = seg_base + pos;
-                return 1;
-            }
-            if (size == 0) {  // stale len/type word (wal.cc:50, segment_file.cc:8)
-                if (crc32c::Value(reinterpret_cast<const char*>(seg + pos + 4), 4) != crc) {
-                    *stop = seg_base + pos;
-                    return 1;
-                }
-                out.push_back(Cand{seg_base + pos, 0, 0, crc});
-                pos += kHeader;
-                continue;
-            }
-            out.push_back(Cand{seg_base + pos, seg_base + pos + kHeader, size, crc});
-            pos += kHeader + size;
-        } else if (type == 1) {  // padding: skip to the segment end (wal.cc:76-82)
-            *stop = seg_base + seg_bytes;
-            return 0;
-        } else {
-            *stop = seg_base + pos;
-            return 2;
-        }
-    }
-}
-
 int fail(int code, const char* what) { return karma::engine::set_last_error(code, what); }
 
-static_assert(KARMA_WAL_CORRUPT == 1 && KARMA_WAL_BAD_TYPE == 2, "walk_segment stop kinds");
-
-// Device copy of a host WAL image, uploaded on a worker thread while the caller
-// walks the headers.  One cached, grow-only device buffer per device; the
-// device's lock is held from the upload until release() (the CRC batch that
-// reads the copy has completed).
-struct ImageCache {
-    std::mutex mu;
-    void* d = nullptr;
+// Per-device replay context: a stream, the device image buffer (host images
+// are streamed into it), the walk's candidate tables, the contiguous lists and
+// the pinned staging ring of the upload.  Grow-only; one replay at a time per
+// device (the context's lock).
+struct DevBuf {
+    void* p = nullptr;
     size_t bytes = 0;
+    bool host = false;
+    int ensure(size_t want, bool pinned_host = false) {
+        if (p && bytes >= want) return 0;
+        if (p) (void)(host ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        bytes = 0;
+        want = std::max<size_t>(want + want / 8, 256);
+        const hipError_t e = pinned_host ? hipHostMalloc(&p, want, hipHostMallocDefault) : hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(e == hipErrorOutOfMemory ? KARMA_E_NOMEM : KARMA_E_HIP, "wal_replay: allocation");
+        }
+        bytes = want;
+        host = pinned_host;
+        return 0;
+    }
+    template <typename T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+constexpr int kUpThreads = 8;                   // upload workers
+constexpr size_t kUpChunk = size_t(8) << 20;    // bytes per staging buffer
+struct ReplayCtx {
+    std::mutex mu;
+    bool ready = false;
+    int cu = 1;
     hipStream_t st = nullptr;
-};
-std::mutex g_img_mu;
-std::vector<std::unique_ptr<ImageCache>> g_img;
-
-class ImageUpload {
-  public:
-    ImageUpload(const void* h, size_t bytes, int device) {
-        int dev = device;  // resolved here: a new thread starts on device 0
-        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
-        th_ = std::thread([=] { rc_ = run(h, bytes, dev); });
-    }
-    ~ImageUpload() { release(); }
-    // Wait for the copy; *d = the device image.
-    int wait(const void** d) {
-        if (th_.joinable()) th_.join();
-        *d = cache_ ? cache_->d : nullptr;
-        return rc_ ? fail(rc_, msg_.c_str()) : 0;  // the worker's error, reported on this thread
-    }
-    void release() {
-        if (th_.joinable()) th_.join();
-        if (lock_.owns_lock()) lock_.unlock();
-    }
-
-  private:
-    int err(int code, const char* what) {
-        msg_ = what;
-        return code;
-    }
-    int run(const void* h, size_t bytes, int dev) {
-        int n = 0;
-        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return err(KARMA_E_NO_DEVICE, "no HIP device visible");
-        if (dev >= n || hipSetDevice(dev) != hipSuccess) return err(KARMA_E_INVALID, "wal image: bad device");
-        {
-            std::lock_guard<std::mutex> g(g_img_mu);
-            if ((int)g_img.size() <= dev) g_img.resize(dev + 1);
-            if (!g_img[dev]) g_img[dev] = std::make_unique<ImageCache>();
-            cache_ = g_img[dev].get();
+    DevBuf img, crec, clen, meta, cbase, off, len, stored, crc, bad;
+    DevBuf h_meta, h_small;                     // pinned readbacks
+    hipStream_t up_st[kUpThreads] = {};
+    hipEvent_t up_ev[kUpThreads][2] = {};
+    DevBuf stage[kUpThreads][2];
+    int init(int dev) {
+        if (ready) return 0;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(KARMA_E_HIP, "hipGetDeviceProperties");
+        cu = std::max(1, prop.multiProcessorCount);
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return fail(KARMA_E_HIP, "stream");
+        for (int t = 0; t < kUpThreads; ++t) {
+            if (hipStreamCreateWithFlags(&up_st[t], hipStreamNonBlocking) != hipSuccess) return fail(KARMA_E_HIP, "stream");
+            for (auto& e : up_ev[t])
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(KARMA_E_HIP, "event");
         }
-        lock_ = std::unique_lock<std::mutex>(cache_->mu);
-        ImageCache& ic = *cache_;
-        if (!ic.st && hipStreamCreateWithFlags(&ic.st, hipStreamNonBlocking) != hipSuccess)
-            return err(KARMA_E_HIP, "hipStreamCreate");
-        if (ic.bytes < bytes) {
-            if (ic.d) (void)hipFree(ic.d);
-            ic.d = nullptr;
-            ic.bytes = 0;
-            if (hipMalloc(&ic.d, bytes) != hipSuccess) return err(KARMA_E_NOMEM, "wal image: hipMalloc");
-            ic.bytes = bytes;
-        }
-        const bool reg = hipHostRegister(const_cast<void*>(h), bytes, hipHostRegisterDefault) == hipSuccess;
-        if (!reg) (void)hipGetLastError();  // already pinned or not registrable: a staged copy still works
-        hipError_t e = hipMemcpyAsync(ic.d, h, bytes, hipMemcpyHostToDevice, ic.st);
-        if (e == hipSuccess) e = hipStreamSynchronize(ic.st);
-        if (reg) (void)hipHostUnregister(const_cast<void*>(h));
-        return e == hipSuccess ? 0 : err(KARMA_E_HIP, "wal image: H2D");
+        ready = true;
+        return 0;
     }
-    std::thread th_;
-    int rc_ = 0;
-    std::string msg_;
-    ImageCache* cache_ = nullptr;
-    std::unique_lock<std::mutex> lock_;
 };
+std::mutex g_rctx_mu;
+std::vector<std::unique_ptr<ReplayCtx>> g_rctx;
+
+ReplayCtx& replay_ctx(int dev) {
+    std::lock_guard<std::mutex> g(g_rctx_mu);
+    if ((int)g_rctx.size() <= dev) g_rctx.resize(dev + 1);
+    if (!g_rctx[dev]) g_rctx[dev] = std::make_unique<ReplayCtx>();
+    return *g_rctx[dev];
+}
+
+// Host image -> device buffer without page-locking the caller's memory: worker t
+// copies chunks t, t + T, ... into its two pinned staging buffers (alternating)
+// and DMAs each one on its own stream, so the memcpy of one chunk overlaps the
+// DMA of the previous and T copies run at once.
+int upload_staged(ReplayCtx& c, void* d_dst, const uint8_t* h_src, size_t bytes, int dev) {
+    const size_t nchunk = (bytes + kUpChunk - 1) / kUpChunk;
+    const int nthr = (int)std::min<size_t>(kUpThreads, std::max<size_t>(1, nchunk));
+    for (int t = 0; t < nthr; ++t)
+        for (auto& b : c.stage[t])
+            if (const int rc = b.ensure(kUpChunk, true)) return rc;
+    std::vector<int> rcs(nthr, 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthr; ++t)
+        th.emplace_back([&, t] {
+            if (hipSetDevice(dev) != hipSuccess) {
+                rcs[t] = KARMA_E_HIP;
+                return;
+            }
+            int k = 0;
+            for (size_t i = t; i < nchunk; i += nthr, k ^= 1) {
+                const size_t o = i * kUpChunk, n = std::min(kUpChunk, bytes - o);
+                if (hipEventSynchronize(c.up_ev[t][k]) != hipSuccess) {  // the buffer's previous DMA
+                    rcs[t] = KARMA_E_HIP;
+                    return;
+                }
+                std::memcpy(c.stage[t][k].p, h_src + o, n);
+                if (hipMemcpyAsync(static_cast<uint8_t*>(d_dst) + o, c.stage[t][k].p, n, hipMemcpyHostToDevice,
+                                   c.up_st[t]) != hipSuccess ||
+                    hipEventRecord(c.up_ev[t][k], c.up_st[t]) != hipSuccess) {
+                    rcs[t] = KARMA_E_HIP;
+                    return;
+                }
+            }
+            if (hipStreamSynchronize(c.up_st[t]) != hipSuccess) rcs[t] = KARMA_E_HIP;
+        });
+    for (auto& x : th) x.join();
+    for (int rc : rcs)
+        if (rc) return fail(rc, "wal_replay: image upload");
+    return 0;
+}
 
 }  // namespace
 
@@ -307,103 +294,119 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
 int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                      int device) {
-    if (!h_wal || !h_n_records || !h_stop || !h_status || seg_bytes < 1 || wal_bytes % seg_bytes || start > wal_bytes)
+    if ((!h_wal && !d_wal) || !h_n_records || !h_stop || !h_status || seg_bytes < 1 || wal_bytes % seg_bytes ||
+        start > wal_bytes || seg_bytes >= (uint64_t(1) << 32))
         return fail(KARMA_E_INVALID, "wal_replay");
-    const uint8_t* wal = static_cast<const uint8_t*>(h_wal);
+    using namespace karma::engine;
     const uint64_t nseg = wal_bytes / seg_bytes;
     const uint64_t s0 = std::min<uint64_t>(start / seg_bytes, nseg);
     const uint64_t nwork = nseg - s0;
-    karma::engine::PhaseTimer T("wal_replay");
-    // 0. no device copy given: upload the image while the headers are walked
-    std::unique_ptr<ImageUpload> up;
-    if (!d_wal && nwork) up = std::make_unique<ImageUpload>(wal + s0 * seg_bytes, nwork * seg_bytes, device);
-    // 1. walk every segment from where replay would enter it, in parallel
-    std::vector<std::vector<Cand>> cands(nseg);
-    std::vector<uint64_t> stop(nseg);
-    std::vector<int> kind(nseg);
-    parallel_for(s0, nseg, 4, [&](uint64_t s) {
-        const uint64_t base = s * seg_bytes;
-        const uint64_t pos = s == s0 ? start - base : 0;
-        kind[s] = walk_segment(wal + base, base, seg_bytes, pos, cands[s], &stop[s]);
-    });
-    T.mark("header walk");
+    if (!nwork) {  // nothing past start: replay is already at the end
+        *h_n_records = 0;
+        *h_stop = start;
+        *h_status = KARMA_WAL_END;
+        return 0;
+    }
+    int n = 0, dev = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(KARMA_E_NO_DEVICE, "no HIP device visible");
+    if (device >= n) return fail(KARMA_E_INVALID, "wal_replay: device index out of range");
+    if (device >= 0 && hipSetDevice(device) != hipSuccess) return fail(KARMA_E_HIP, "hipSetDevice");
+    if (hipGetDevice(&dev) != hipSuccess) return fail(KARMA_E_HIP, "hipGetDevice");
+    ReplayCtx& c = replay_ctx(dev);
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (const int rc = c.init(dev)) return rc;
+    PhaseTimer T("wal_replay");
+    const uint64_t base0 = s0 * seg_bytes, img_bytes = nwork * seg_bytes;
+    WalArgs A{};
+    // 0. the image in HBM: the caller's copy, or the host image streamed in
+    if (d_wal) {
+        A.wal = static_cast<const uint8_t*>(d_wal) + base0;
+    } else {
+        if (const int rc = c.img.ensure(img_bytes)) return rc;
+        if (const int rc = upload_staged(c, c.img.p, static_cast<const uint8_t*>(h_wal) + base0, img_bytes, dev))
+            return rc;
+        A.wal = c.img.as<const uint8_t>();
+        T.mark("image upload");
+    }
+    A.base0 = base0;
+    A.seg_bytes = seg_bytes;
+    A.first_pos = start - base0;
+    A.cand_cap = seg_bytes / 8 + 1;
+    // 1. segment-parallel header walk
+    if (const int rc = c.crec.ensure(nwork * A.cand_cap * 4)) return rc;
+    if (const int rc = c.clen.ensure(nwork * A.cand_cap * 4)) return rc;
+    if (const int rc = c.meta.ensure(nwork * sizeof(WalSegMeta))) return rc;
+    if (const int rc = c.h_meta.ensure(nwork * sizeof(WalSegMeta), true)) return rc;
+    A.cand_rec = c.crec.as<uint32_t>();
+    A.cand_len = c.clen.as<uint32_t>();
+    A.meta = c.meta.as<WalSegMeta>();
+    if (launch_wal_walk(A, nwork, c.st) != hipSuccess ||
+        hipMemcpyAsync(c.h_meta.p, A.meta, nwork * sizeof(WalSegMeta), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+        hipStreamSynchronize(c.st) != hipSuccess)
+        return fail(KARMA_E_HIP, "wal_replay: header walk");
+    T.mark("header walk (device)");
     // replay enters segment s+1 only if segment s ended cleanly
-    int status = 0;
-    uint64_t end = nwork ? wal_bytes : start;
-    uint64_t s1 = nseg;  // one past the last segment replay reads
-    for (uint64_t s = s0; s < nseg; ++s)
-        if (kind[s] != 0) {
-            status = kind[s];
-            end = stop[s];
-            s1 = s + 1;
+    const WalSegMeta* M = c.h_meta.as<WalSegMeta>();
+    int status = KARMA_WAL_END;
+    uint64_t end = wal_bytes, w1 = nwork;  // segments [0, w1) relative to s0 are read
+    for (uint64_t w = 0; w < nwork; ++w)
+        if (M[w].kind != KARMA_WAL_END) {
+            status = (int)M[w].kind;
+            end = M[w].stop;
+            w1 = w + 1;
             break;
         }
-    // candidate slots: gb = all candidates before segment s, nb = those with a payload
-    std::vector<uint64_t> gb(nseg + 1, 0), nb(nseg + 1, 0);
-    for (uint64_t s = s0; s < s1; ++s) {
-        uint64_t nz = 0;
-        for (const Cand& x : cands[s]) nz += x.len != 0;
-        gb[s + 1] = gb[s] + cands[s].size();
-        nb[s + 1] = nb[s] + nz;
+    if (const int rc = c.cbase.ensure(w1 * 8)) return rc;
+    if (const int rc = c.h_small.ensure(std::max<size_t>(w1 * 8, 64), true)) return rc;
+    uint64_t* cb = c.h_small.as<uint64_t>();
+    uint64_t n_all = 0;
+    for (uint64_t w = 0; w < w1; ++w) {
+        cb[w] = n_all;
+        n_all += M[w].count;
     }
-    const uint64_t n_all = gb[s1], n_nz = nb[s1];
-    // 2. payload CRCs in one GPU batch (size-0 records were checked on the host)
-    std::vector<uint64_t> off(n_nz);
-    std::vector<uint32_t> len(n_nz);
-    parallel_for(s0, s1, 8, [&](uint64_t s) {
-        uint64_t j = nb[s];
-        for (const Cand& x : cands[s])
-            if (x.len) {
-                off[j] = x.off;
-                len[j] = x.len;
-                ++j;
-            }
-    });
-    T.mark("span lists");
-    std::vector<uint32_t> got;
-    if (up && off.empty()) {
-        up->release();  // nothing to checksum: the upload (and any device error) does not matter
-    } else if (up) {  // spans are WAL offsets; the uploaded copy starts at segment s0
-        const void* d = nullptr;
-        if (const int rc = up->wait(&d)) return rc;
-        T.mark("image upload (rest of it)");
-        const uint64_t base = s0 * seg_bytes;
-        parallel_for(0, off.size(), 1 << 16, [&](uint64_t j) { off[j] -= base; });
-        const int rc = karma::engine::crc_spans(wal + base, d, nwork * seg_bytes, off, len, got, device);
-        up->release();
-        if (rc) return rc;
-    } else if (const int rc = karma::engine::crc_spans(h_wal, d_wal, wal_bytes, off, len, got, device)) {
-        return rc;
-    }
-    T.mark("CRC batch");
-    // 3. the first mismatch (in WAL order) is where scan_record logs "Corrupt record"
-    std::vector<uint64_t> bad(nseg, UINT64_MAX);
-    parallel_for(s0, s1, 8, [&](uint64_t s) {
-        uint64_t j = nb[s];
-        for (size_t i = 0; i < cands[s].size(); ++i) {
-            const Cand& x = cands[s][i];
-            if (x.len && got[j++] != x.stored) {
-                bad[s] = gb[s] + i;
-                return;
-            }
-        }
-    });
     uint64_t accepted = n_all;
-    for (uint64_t s = s0; s < s1; ++s)
-        if (bad[s] != UINT64_MAX) {
-            accepted = bad[s];
+    if (n_all) {
+        // 2. contiguous candidate lists, one ragged CRC batch, first mismatch
+        if (const int rc = c.off.ensure(n_all * 8)) return rc;
+        if (const int rc = c.len.ensure(n_all * 4)) return rc;
+        if (const int rc = c.stored.ensure(n_all * 4)) return rc;
+        if (const int rc = c.crc.ensure(n_all * 4)) return rc;
+        if (const int rc = c.bad.ensure(8)) return rc;
+        A.cand_base = c.cbase.as<uint64_t>();
+        A.off = c.off.as<uint64_t>();
+        A.len = c.len.as<uint32_t>();
+        A.stored = c.stored.as<uint32_t>();
+        A.crc = c.crc.as<uint32_t>();
+        A.first_bad = c.bad.as<uint64_t>();
+        if (hipMemcpyAsync(c.cbase.p, cb, w1 * 8, hipMemcpyHostToDevice, c.st) != hipSuccess ||
+            launch_wal_gather(A, w1, c.st) != hipSuccess)
+            return fail(KARMA_E_HIP, "wal_replay: gather");
+        // payload = header + 8: the arena is the image shifted by the header
+        if (const int rc = karma_crc32c_batch_ragged(A.wal + 8, A.off, A.len, n_all, w1 * seg_bytes, nullptr, 0,
+                                                     c.crc.as<uint32_t>(), c.st))
+            return rc;
+        uint64_t* hb = c.h_small.as<uint64_t>();  // cb was consumed by the H2D above (stream-ordered)
+        if (hipMemsetAsync(A.first_bad, 0xff, 8, c.st) != hipSuccess ||
+            launch_wal_compare(A, n_all, c.cu, c.st) != hipSuccess ||
+            hipMemcpyAsync(hb, A.first_bad, 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+            hipStreamSynchronize(c.st) != hipSuccess)
+            return fail(KARMA_E_HIP, "wal_replay: CRC check");
+        T.mark("CRC batch + compare");
+        if (hb[0] < n_all) {  // the first mismatch in WAL order is where scan_record logs "Corrupt record"
+            accepted = hb[0];
             status = KARMA_WAL_CORRUPT;
-            end = cands[s][bad[s] - gb[s]].rec;
-            break;
+            if (hipMemcpy(hb, A.off + accepted, 8, hipMemcpyDeviceToHost) != hipSuccess)
+                return fail(KARMA_E_HIP, "wal_replay: D2H");
+            end = base0 + hb[0];
         }
-    if (h_rec_off)
-        parallel_for(s0, s1, 8, [&](uint64_t s) {
-            for (size_t i = 0; i < cands[s].size(); ++i) {
-                const uint64_t g = gb[s] + i;
-                if (g < accepted && g < rec_cap) h_rec_off[g] = cands[s][i].rec;
-            }
-        });
-    T.mark("compare + offsets");
+        if (h_rec_off && rec_cap && accepted) {
+            const uint64_t k = std::min<uint64_t>(accepted, rec_cap);
+            if (hipMemcpy(h_rec_off, A.off, k * 8, hipMemcpyDeviceToHost) != hipSuccess)
+                return fail(KARMA_E_HIP, "wal_replay: D2H offsets");
+            parallel_for(0, k, 1 << 16, [&](uint64_t i) { h_rec_off[i] += base0; });
+        }
+        T.mark("offsets");
+    }
     *h_n_records = accepted;
     *h_stop = end;
     *h_status = status;

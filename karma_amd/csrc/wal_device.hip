@@ -1,0 +1,183 @@
+// karma_amd/csrc/wal_device.hip -- WAL replay on the device.
+//
+// sivir::open's loop over wal::scan_record (sivir.cc:31-41, wal.cc:34-87) over a
+// WAL image held in HBM, in three kernels around one ragged CRC batch:
+//
+//   k_wal_walk     one workgroup per segment: the segment is staged through LDS
+//                  in 32 KiB tiles and one lane walks its [crc][len<<8|type]
+//                  headers with scan_record's structural checks, writing the
+//                  header offset and payload length of every type-0 record
+//                  (the candidates) and the segment's stop kind / offset.  The
+//                  header chain is serial inside a segment; segments walk in
+//                  parallel, replacing the host's per-record pread loop.
+//   k_wal_gather   candidates of the segments replay enters, in WAL order,
+//                  into contiguous (header offset, length) lists + stored CRCs
+//   (ragged batch) payload CRCs: the arena is the image shifted by the 8-byte
+//                  header, so the list of header offsets is the offset list
+//   k_wal_compare  the first candidate whose payload CRC differs (atomicMin)
+//
+// The size-0 quirk is kept: read_exact_at returns early for size 0
+// (segment_file.cc:8), so the CRC compared is that of the stale 4-byte len/type
+// word (wal.cc:50-60); the walk checks it in place.
+#include <hip/hip_runtime.h>
+
+#include "engine.h"
+#include "karma_crc32c.h"
+
+namespace karma {
+namespace engine {
+namespace {
+
+constexpr int kWalkThreads = 256;
+constexpr uint32_t kTile = 32768;          // LDS tile of the walk
+constexpr uint32_t kTileLoad = kTile + 16;  // + one header's slack (16-byte multiple)
+static_assert(kTileLoad % 16 == 0, "tile of whole vectors");
+
+// crc32c::Value of 4 bytes (the stale len/type word of a size-0 record), bitwise.
+__device__ __forceinline__ uint32_t crc_word(uint32_t w) {
+    uint32_t l = 0xFFFFFFFFu ^ w;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) l = (l >> 1) ^ (0x82F63B78u & (0u - (l & 1u)));
+    return l ^ 0xFFFFFFFFu;
+}
+
+// The walker (thread 0) keeps its position in 32 bits (seg_bytes < 2^32), reads
+// each header as three aligned LDS words funnel-shifted into place, and appends
+// the tile's candidates to an LDS list that the whole block writes out
+// coalesced after the tile: a lane issuing two global stores per header would
+// stall on the vmcnt limit of outstanding stores.
+__global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t tile[kTileLoad / 4 + 4];
+    __shared__ uint32_t lrec[kTile / 8 + 1], llen[kTile / 8 + 1];
+    __shared__ uint32_t sh_pos, sh_done, sh_n;
+    const uint32_t seg = (uint32_t)A.seg_bytes;
+    const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;  // segment s0 + blockIdx.x, relative to A.wal
+    const uint64_t base = A.base0 + rel;                      // its WAL offset
+    const uint8_t* img = A.wal + rel;
+    uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
+    uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
+    const bool vec = ((reinterpret_cast<uintptr_t>(img)) & 15u) == 0;
+    // uniform: every thread follows the walker through sh_pos
+    uint32_t pos = blockIdx.x == 0 ? (uint32_t)A.first_pos : 0u;
+    uint32_t count = 0, kind = 0, stop = seg;  // stop: segment-relative
+    uint8_t* tb = reinterpret_cast<uint8_t*>(tile);
+    while ((uint64_t)pos + 8 <= seg) {  // wal.cc:40-45: a shorter rest is skipped (kind 0)
+        const uint32_t t0 = pos / kTile * kTile;
+        const uint32_t n = (uint64_t)t0 + kTileLoad < seg ? kTileLoad : seg - t0;
+        if (vec) {  // whole 16-byte vectors, then the tail bytes
+            const uint32_t nv = n / 16;
+            for (uint32_t i = threadIdx.x; i < nv; i += kWalkThreads)
+                reinterpret_cast<uint4*>(tile)[i] = reinterpret_cast<const uint4*>(img + t0)[i];
+            for (uint32_t i = nv * 16 + threadIdx.x; i < n; i += kWalkThreads) tb[i] = img[t0 + i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < n; i += kWalkThreads) tb[i] = img[t0 + i];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t done = 0, nc = 0;
+            const uint32_t tend = t0 + kTile;
+            while (pos + 8 <= seg && pos < tend) {  // 64-bit safe: pos + 8 <= seg < 2^32 is checked first
+                const uint32_t h = pos - t0, q = h >> 2, sh = h & 3u;
+                const uint32_t w0 = tile[q], w1 = tile[q + 1], w2 = tile[q + 2];
+                const uint32_t crc = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                const uint32_t st = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                const uint32_t type = st & 0xffu, size = st >> 8;
+                if (type == 0) {
+                    if ((uint64_t)pos + 8 + size > seg || (size == 0 && crc_word(st) != crc)) {
+                        kind = KARMA_WAL_CORRUPT;  // wal.cc:71-74; size 0: stale len/type word (wal.cc:50-60)
+                        stop = pos;
+                        done = 1;
+                        break;
+                    }
+                    lrec[nc] = pos;
+                    llen[nc] = size;
+                    ++nc;
+                    pos += 8 + size;
+                } else {
+                    done = 1;
+                    if (type == 1) {  // padding: skip to the segment end (wal.cc:76-82)
+                        pos = seg;
+                    } else {
+                        kind = KARMA_WAL_BAD_TYPE;
+                        stop = pos;
+                    }
+                    break;
+                }
+            }
+            sh_pos = pos;
+            sh_done = done;
+            sh_n = nc;
+        }
+        __syncthreads();
+        pos = sh_pos;
+        const uint32_t done = sh_done, nc = sh_n;
+        for (uint32_t i = threadIdx.x; i < nc; i += kWalkThreads) {  // the tile's candidates, coalesced
+            if (count + i < A.cand_cap) {
+                crec[count + i] = lrec[i];
+                clen[count + i] = llen[i];
+            }
+        }
+        count += nc;
+        __syncthreads();  // the tile and the candidate list are refilled next
+        if (done) break;
+    }
+    if (threadIdx.x == 0) A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg)};
+}
+
+// Candidates of segment s0 + blockIdx.x (one block per segment) into the
+// contiguous lists at slot A.cand_base[blockIdx.x]: header offset (relative to
+// A.wal), length and the CRC field stored in the header.
+__global__ __launch_bounds__(256) void k_wal_gather(WalArgs A) {
+    const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;
+    const uint32_t count = A.meta[blockIdx.x].count;
+    const uint64_t g0 = A.cand_base[blockIdx.x];
+    const uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
+    const uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
+    for (uint32_t j = threadIdx.x; j < count; j += blockDim.x) {
+        const uint64_t rec = rel + crec[j];
+        const uint8_t* h = A.wal + rec;
+        A.off[g0 + j] = rec;
+        A.len[g0 + j] = clen[j];
+        A.stored[g0 + j] = uint32_t(h[0]) | uint32_t(h[1]) << 8 | uint32_t(h[2]) << 16 | uint32_t(h[3]) << 24;
+    }
+}
+
+// The first candidate (in WAL order) whose payload CRC differs from the stored
+// one; size-0 records were checked by the walk.
+__global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t first = ~0ull;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += stride)
+        if (A.len[g] && A.crc[g] != A.stored[g]) {
+            first = g;
+            break;  // later g of this thread are larger
+        }
+    if (first != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(A.first_bad), (unsigned long long)first);
+}
+
+}  // namespace
+
+uint32_t wal_walk_tile() { return kTile; }
+
+hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, hipStream_t s) {
+    if (!nseg) return hipSuccess;
+    hipLaunchKernelGGL(k_wal_walk, dim3((unsigned)nseg), dim3(kWalkThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s) {
+    if (!nseg) return hipSuccess;
+    hipLaunchKernelGGL(k_wal_gather, dim3((unsigned)nseg), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s) {
+    if (!n) return hipSuccess;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > (uint64_t)cu * 8) blocks = (uint64_t)cu * 8;
+    hipLaunchKernelGGL(k_wal_compare, dim3((unsigned)blocks), dim3(256), 0, s, a, n);
+    return hipGetLastError();
+}
+
+}  // namespace engine
+}  // namespace karma

@@ -30,21 +30,23 @@ def _payloads(seed, n, lo, hi):
     return src, offs, lens
 
 
-def _append(lib, src, offs, lens, wal, cursor=0):
+def _append(lib, src, offs, lens, wal, cursor=0, seg=SEG):
     cur = ctypes.c_uint64(cursor)
     nf = ctypes.c_size_t()
     rec = np.zeros(lens.size, np.uint64)
     st = lib.karma_wal_append_batch(src.ctypes.data, offs.ctypes.data, lens.ctypes.data, lens.size, wal.ctypes.data,
-                                    wal.nbytes, SEG, ctypes.byref(cur), rec.ctypes.data, ctypes.byref(nf), 0)
+                                    wal.nbytes, seg, ctypes.byref(cur), rec.ctypes.data, ctypes.byref(nf), 0)
     _lib.check("karma_wal_append_batch", st)
     return cur.value, rec[: nf.value]
 
 
-def _replay(lib, wal, start=0, d_wal=None):
+def _replay(lib, wal, start=0, d_wal=None, seg=SEG, host=True):
+    """karma_wal_replay over the host image, or (host=False) over the device copy d_wal only."""
     n, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
     rec = np.zeros(wal.nbytes // 8, np.uint64)
-    st = lib.karma_wal_replay(wal.ctypes.data, d_wal.data_ptr() if d_wal is not None else None, wal.nbytes, SEG, start,
-                              ctypes.byref(n), ctypes.byref(stop), ctypes.byref(status), rec.ctypes.data, rec.size, 0)
+    st = lib.karma_wal_replay(wal.ctypes.data if host else None, d_wal.data_ptr() if d_wal is not None else None,
+                              wal.nbytes, seg, start, ctypes.byref(n), ctypes.byref(stop), ctypes.byref(status),
+                              rec.ctypes.data, rec.size, 0)
     _lib.check("karma_wal_replay", st)
     return list(rec[: n.value]), stop.value, status.value
 
@@ -70,9 +72,10 @@ def test_replay_round_trip_and_zero_tail(lib):
     # every framed record replays; replay ends at the never-written zero tail, which the
     # reference reports as "Corrupt record" (size-0 quirk), i.e. the writer resumes at the cursor
     assert got[0] == list(rec) and got[1] == cur and got[2] == wal_model.CORRUPT
-    # same through a device copy of the image
+    # same through a device copy of the image, with and without the host image
     d = torch.from_numpy(wal).cuda()
     assert _replay(lib, wal, d_wal=d) == got
+    assert _replay(lib, wal, d_wal=d, host=False) == got
 
 
 @pytest.mark.parametrize("what", ["payload_bit", "crc_field", "length_past_segment", "bad_type", "empty_record"])
@@ -110,3 +113,33 @@ def test_replay_from_checkpoint_and_short_segment_tails(lib):
         got = _replay(lib, wal, start=start)
         want = wal_model.replay(wal.tobytes(), SEG, start)
         assert got == (list(want[0]), want[1], want[2])
+
+
+@pytest.mark.parametrize("seg", [(1 << 20), (64 << 10) + 12, 4096 + 4])
+def test_replay_segment_sizes_tiles_and_misaligned_segments(lib, seg):
+    """1 MiB segments (32 LDS tiles of the device walk), and segment sizes that are not a
+    multiple of 16 (every segment but the first is misaligned in the image: byte-wise tile loads)."""
+    n = 6000 if seg >= (64 << 10) else 600
+    src, offs, lens = _payloads(13, n, 1, min(3000, seg - 8))
+    nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 3
+    wal = np.zeros(nseg * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    want = wal_model.replay(wal.tobytes(), seg)
+    d = torch.from_numpy(wal).cuda()
+    for kw in ({}, {"d_wal": d, "host": False}):
+        got = _replay(lib, wal, seg=seg, **kw)
+        assert got == (list(want[0]), want[1], want[2])
+    assert want[0] == list(rec)
+    # a flipped payload byte deep in the image: replay stops at that record
+    k = len(rec) * 3 // 4
+    wal[int(rec[k]) + 8] ^= 0x40
+    got = _replay(lib, wal, seg=seg)
+    assert got[2] == wal_model.CORRUPT and got[1] == int(rec[k]) and len(got[0]) == k
+
+
+def test_replay_empty_and_start_at_end(lib):
+    wal = np.zeros(4 * SEG, np.uint8)
+    got = _replay(lib, wal)
+    want = wal_model.replay(wal.tobytes(), SEG)
+    assert got == (list(want[0]), want[1], want[2])
+    assert _replay(lib, wal, start=wal.nbytes) == ([], wal.nbytes, wal_model.END)

@@ -142,8 +142,9 @@ def test_python_batch_api_rejects_host_tensors():
 
 
 def test_wal_and_kfp_host_logic_without_gpu(karma_lib):
-    """The structural halves of the WAL / KFP layers run on the host; with nothing to checksum
-    they need no device, and any checksum work refuses with KARMA_E_NO_DEVICE (no CPU fallback)."""
+    """The structural half of the KFP layer runs on the host; with nothing to checksum it needs
+    no device, and any device work (checksums, the WAL replay walk) refuses with
+    KARMA_E_NO_DEVICE (no CPU fallback)."""
     import struct
 
     import numpy as np
@@ -165,14 +166,18 @@ def test_wal_and_kfp_host_logic_without_gpu(karma_lib):
     st = karma_lib.karma_kfp_parse_batch(fb.ctypes.data, None, fb.nbytes, 16, None, ctypes.byref(n),
                                          ctypes.byref(used), ctypes.byref(why), -1)
     assert st == _lib.KARMA_E_NO_DEVICE
-    # WAL replay of an image whose first header has an unknown type: BAD_TYPE at 0, no CRC needed
+    # WAL replay walks the headers on the device too: refused without one (no host walk)
     seg = 4096
     wal = np.zeros(2 * seg, np.uint8)
     wal[4] = 7
     nr, stop, status = u64(), u64(), i32()
     st = karma_lib.karma_wal_replay(wal.ctypes.data, None, wal.nbytes, seg, 0, ctypes.byref(nr), ctypes.byref(stop),
                                     ctypes.byref(status), None, 0, -1)
-    assert st == 0 and (nr.value, stop.value, status.value) == (0, 0, 2)
+    assert st == _lib.KARMA_E_NO_DEVICE
+    # replay from the end of the image has nothing to walk
+    st = karma_lib.karma_wal_replay(wal.ctypes.data, None, wal.nbytes, seg, wal.nbytes, ctypes.byref(nr),
+                                    ctypes.byref(stop), ctypes.byref(status), None, 0, -1)
+    assert st == 0 and (nr.value, stop.value, status.value) == (0, wal.nbytes, 0)
     # invalid geometry is rejected before any device work
     assert karma_lib.karma_wal_replay(wal.ctypes.data, None, wal.nbytes, 3000, 0, ctypes.byref(nr),
                                       ctypes.byref(stop), ctypes.byref(status), None, 0, -1) == _lib.KARMA_E_INVALID
