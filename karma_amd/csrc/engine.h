@@ -122,7 +122,7 @@ static_assert(sizeof(WalSegMeta) == 16, "one 16-byte record per segment");
 struct WalArgs {
     const uint8_t* wal;        // first byte of segment s0 (WAL offset base0)
     uint64_t base0;            // s0 * seg_bytes
-    uint64_t seg_bytes;        // < 2^32
+    uint64_t seg_bytes;        // < 2^31
     uint64_t first_pos;        // where replay enters segment s0 (start - base0)
     uint32_t* cand_rec;        // per segment: cand_cap header offsets within the segment
     uint32_t* cand_len;        //              and payload lengths

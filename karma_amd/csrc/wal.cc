@@ -295,7 +295,7 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                      int device) {
     if ((!h_wal && !d_wal) || !h_n_records || !h_stop || !h_status || seg_bytes < 1 || wal_bytes % seg_bytes ||
-        start > wal_bytes || seg_bytes >= (uint64_t(1) << 32))
+        start > wal_bytes || seg_bytes >= (uint64_t(1) << 31))
         return fail(KARMA_E_INVALID, "wal_replay");
     using namespace karma::engine;
     const uint64_t nseg = wal_bytes / seg_bytes;

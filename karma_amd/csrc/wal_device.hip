@@ -4,7 +4,7 @@
 // WAL image held in HBM, in three kernels around one ragged CRC batch:
 //
 //   k_wal_walk     one workgroup per segment: the segment is staged through LDS
-//                  in 32 KiB tiles and one lane walks its [crc][len<<8|type]
+//                  in 16 KiB tiles and one lane walks its [crc][len<<8|type]
 //                  headers with scan_record's structural checks, writing the
 //                  header offset and payload length of every type-0 record
 //                  (the candidates) and the segment's stop kind / offset.  The
@@ -29,7 +29,7 @@ namespace engine {
 namespace {
 
 constexpr int kWalkThreads = 256;
-constexpr uint32_t kTile = 32768;          // LDS tile of the walk
+constexpr uint32_t kTile = 16384;          // LDS tile of the walk (two buffers)
 constexpr uint32_t kTileLoad = kTile + 16;  // + one header's slack (16-byte multiple)
 static_assert(kTileLoad % 16 == 0, "tile of whole vectors");
 
@@ -41,14 +41,16 @@ __device__ __forceinline__ uint32_t crc_word(uint32_t w) {
     return l ^ 0xFFFFFFFFu;
 }
 
-// The walker (thread 0) keeps its position in 32 bits (seg_bytes < 2^32), reads
-// each header as three aligned LDS words funnel-shifted into place, and appends
-// the tile's candidates to an LDS list that the whole block writes out
-// coalesced after the tile: a lane issuing two global stores per header would
-// stall on the vmcnt limit of outstanding stores.
+// The walker (thread 0) keeps its position in 32 bits (seg_bytes < 2^31) and
+// reads each header as three aligned LDS words funnel-shifted into place; the
+// common header (type 0, payload that fits) costs one branch.  Its candidates
+// go to an LDS list.  While it walks tile t, waves 1-3 write the previous
+// tile's list out to global memory (coalesced) and load tile t + 1 into the
+// other buffer, so the walker waits neither on tile loads nor on stores; a
+// payload that jumps past tile t + 1 costs one synchronous tile load.
 __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
-    __shared__ __attribute__((aligned(16))) uint32_t tile[kTileLoad / 4 + 4];
-    __shared__ uint32_t lrec[kTile / 8 + 1], llen[kTile / 8 + 1];
+    __shared__ __attribute__((aligned(16))) uint32_t tile[2][kTileLoad / 4 + 4];
+    __shared__ uint32_t lrec[2][kTile / 8 + 1], llen[2][kTile / 8 + 1];
     __shared__ uint32_t sh_pos, sh_done, sh_n;
     const uint32_t seg = (uint32_t)A.seg_bytes;
     const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;  // segment s0 + blockIdx.x, relative to A.wal
@@ -57,45 +59,71 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
     uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
     uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
     const bool vec = ((reinterpret_cast<uintptr_t>(img)) & 15u) == 0;
-    // uniform: every thread follows the walker through sh_pos
-    uint32_t pos = blockIdx.x == 0 ? (uint32_t)A.first_pos : 0u;
-    uint32_t count = 0, kind = 0, stop = seg;  // stop: segment-relative
-    uint8_t* tb = reinterpret_cast<uint8_t*>(tile);
-    while ((uint64_t)pos + 8 <= seg) {  // wal.cc:40-45: a shorter rest is skipped (kind 0)
-        const uint32_t t0 = pos / kTile * kTile;
+    auto load = [&](int b, uint32_t t0, uint32_t tid, uint32_t nthr) {  // [t0, t0 + kTileLoad) clipped to seg
         const uint32_t n = (uint64_t)t0 + kTileLoad < seg ? kTileLoad : seg - t0;
+        uint8_t* tb = reinterpret_cast<uint8_t*>(tile[b]);
+        uint32_t i0 = 0;
         if (vec) {  // whole 16-byte vectors, then the tail bytes
             const uint32_t nv = n / 16;
-            for (uint32_t i = threadIdx.x; i < nv; i += kWalkThreads)
-                reinterpret_cast<uint4*>(tile)[i] = reinterpret_cast<const uint4*>(img + t0)[i];
-            for (uint32_t i = nv * 16 + threadIdx.x; i < n; i += kWalkThreads) tb[i] = img[t0 + i];
-        } else {
-            for (uint32_t i = threadIdx.x; i < n; i += kWalkThreads) tb[i] = img[t0 + i];
+            for (uint32_t i = tid; i < nv; i += nthr)
+                reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(img + t0)[i];
+            i0 = nv * 16;
         }
+        for (uint32_t i = i0 + tid; i < n; i += nthr) tb[i] = img[t0 + i];
+    };
+    auto flush = [&](int b, uint32_t nc, uint32_t at, uint32_t tid, uint32_t nthr) {
+        for (uint32_t i = tid; i < nc; i += nthr)
+            if (at + i < A.cand_cap) {
+                crec[at + i] = lrec[b][i];
+                clen[at + i] = llen[b][i];
+            }
+    };
+    // uniform: every thread follows the walker through sh_pos
+    uint32_t pos = blockIdx.x == 0 ? (uint32_t)A.first_pos : 0u;
+    uint32_t count = 0, kind = 0, stop = seg;  // stop: segment-relative (thread 0's)
+    uint32_t pend_n = 0, pend_at = 0;          // the list of the previous tile, not yet written out
+    int b = 0;
+    if ((uint64_t)pos + 8 <= seg) {  // wal.cc:40-45: a shorter rest is skipped (kind 0)
+        load(0, pos / kTile * kTile, threadIdx.x, kWalkThreads);
         __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t done = 0, nc = 0;
-            const uint32_t tend = t0 + kTile;
-            while (pos + 8 <= seg && pos < tend) {  // 64-bit safe: pos + 8 <= seg < 2^32 is checked first
-                const uint32_t h = pos - t0, q = h >> 2, sh = h & 3u;
-                const uint32_t w0 = tile[q], w1 = tile[q + 1], w2 = tile[q + 2];
-                const uint32_t crc = __builtin_amdgcn_alignbyte(w1, w0, sh);
-                const uint32_t st = __builtin_amdgcn_alignbyte(w2, w1, sh);
-                const uint32_t type = st & 0xffu, size = st >> 8;
-                if (type == 0) {
-                    if ((uint64_t)pos + 8 + size > seg || (size == 0 && crc_word(st) != crc)) {
-                        kind = KARMA_WAL_CORRUPT;  // wal.cc:71-74; size 0: stale len/type word (wal.cc:50-60)
-                        stop = pos;
-                        done = 1;
-                        break;
+        while (true) {
+            const uint32_t t0 = pos / kTile * kTile;
+            if (threadIdx.x == 0) {
+                const uint32_t* tl = tile[b];
+                uint32_t done = 0, nc = 0;
+                const uint32_t tend = t0 + kTile, lim = seg - 8;  // a header at pos needs pos <= lim
+                while (pos <= lim && pos < tend) {
+                    // fast path: type-0 records with a payload that fits, one branch per header
+                    uint32_t crc, st, size, npos;
+                    while (true) {
+                        const uint32_t h = pos - t0, q = h >> 2, sh = h & 3u;
+                        const uint32_t w0 = tl[q], w1 = tl[q + 1], w2 = tl[q + 2];
+                        crc = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                        st = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                        size = st >> 8;
+                        npos = pos + 8 + size;  // < 2^32: seg_bytes < 2^31, size < 2^24
+                        if ((st & 0xffu) != 0 || size == 0 || npos > seg) break;
+                        lrec[b][nc] = pos;
+                        llen[b][nc] = size;
+                        ++nc;
+                        pos = npos;
+                        if (pos > lim || pos >= tend) break;
                     }
-                    lrec[nc] = pos;
-                    llen[nc] = size;
-                    ++nc;
-                    pos += 8 + size;
-                } else {
+                    if (pos > lim || pos >= tend) break;  // left the segment / tile on the fast path
+                    // the header at pos is special (scan_record's other branches)
+                    const uint32_t type = st & 0xffu;
+                    if (type == 0 && npos <= seg && crc_word(st) == crc) {  // size 0: stale word (wal.cc:50-60)
+                        lrec[b][nc] = pos;
+                        llen[b][nc] = 0;
+                        ++nc;
+                        pos = npos;
+                        continue;
+                    }
                     done = 1;
-                    if (type == 1) {  // padding: skip to the segment end (wal.cc:76-82)
+                    if (type == 0) {  // wal.cc:71-74 (length past the segment), or the stale-word mismatch
+                        kind = KARMA_WAL_CORRUPT;
+                        stop = pos;
+                    } else if (type == 1) {  // padding: skip to the segment end (wal.cc:76-82)
                         pos = seg;
                     } else {
                         kind = KARMA_WAL_BAD_TYPE;
@@ -103,23 +131,30 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
                     }
                     break;
                 }
+                sh_pos = pos;
+                sh_done = done;
+                sh_n = nc;
+            } else if (threadIdx.x >= 64) {  // waves 1-3: the previous list out, the next tile in
+                flush(b ^ 1, pend_n, pend_at, threadIdx.x - 64, kWalkThreads - 64);
+                if ((uint64_t)t0 + kTile < seg) load(b ^ 1, t0 + kTile, threadIdx.x - 64, kWalkThreads - 64);
             }
-            sh_pos = pos;
-            sh_done = done;
-            sh_n = nc;
-        }
-        __syncthreads();
-        pos = sh_pos;
-        const uint32_t done = sh_done, nc = sh_n;
-        for (uint32_t i = threadIdx.x; i < nc; i += kWalkThreads) {  // the tile's candidates, coalesced
-            if (count + i < A.cand_cap) {
-                crec[count + i] = lrec[i];
-                clen[count + i] = llen[i];
+            __syncthreads();
+            pos = sh_pos;
+            const uint32_t done = sh_done, nc = sh_n;
+            pend_n = nc;
+            pend_at = count;
+            count += nc;
+            if (done || (uint64_t)pos + 8 > seg) {
+                flush(b, nc, pend_at, threadIdx.x, kWalkThreads);
+                break;
             }
+            const uint32_t nt0 = pos / kTile * kTile;
+            if (nt0 != t0 + kTile) {  // jumped past the prefetched tile
+                load(b ^ 1, nt0, threadIdx.x, kWalkThreads);
+            }
+            __syncthreads();  // sh_* are read by everyone before the walker rewrites them
+            b ^= 1;
         }
-        count += nc;
-        __syncthreads();  // the tile and the candidate list are refilled next
-        if (done) break;
     }
     if (threadIdx.x == 0) A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg)};
 }
