@@ -26,16 +26,19 @@ typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 // so one v_perm_b32 builds it from the register (entry = byte k) and a
 // per-lane constant, and the 32 lanes of each ds_read_b32 half-wave hit 32
 // distinct banks (no conflicts on random data).
-// [128 KiB, +17 KiB): Z4, Z16, Z32, Z64 slicing tables and the byte table.
+// [128 KiB, +25 KiB): Z4, Z16, Z32, Z64 slicing tables, the byte table, Z8, Z12.
 constexpr int kRepWords = 32768;
 constexpr int kSmallBase = kRepWords;
 constexpr int kSmallWords = kBlobWords - 1024;
-constexpr int kLdsWords = kRepWords + kSmallWords;  // 148,480 bytes
+constexpr int kLdsWords = kRepWords + kSmallWords;  // 156,672 bytes
 constexpr int kLZ4 = kSmallBase + (kBlobZ4 - 1024);
 constexpr int kLZ16 = kSmallBase + (kBlobZ16 - 1024);
 constexpr int kLZ32 = kSmallBase + (kBlobZ32 - 1024);
 constexpr int kLZ64 = kSmallBase + (kBlobZ64 - 1024);
 constexpr int kLT8 = kSmallBase + (kBlobT8 - 1024);
+constexpr int kLZ8 = kSmallBase + (kBlobZ8 - 1024);
+constexpr int kLZ12 = kSmallBase + (kBlobZ12 - 1024);
+
 
 constexpr uint32_t kSel0 = 0x0c0c0004u;  // {X.b0, acc.b0, 0, 0}
 constexpr uint32_t kSel1 = 0x0c0c0105u;  // {X.b1, acc.b1, 0, 0}
@@ -59,6 +62,15 @@ __device__ __forceinline__ uint32_t stride_step(const uint32_t* lds, uint32_t X,
 __device__ __forceinline__ uint32_t zmap(const uint32_t* lds, int base, uint32_t x) {
     return lds[base + (x & 255u)] ^ lds[base + 256 + ((x >> 8) & 255u)] ^ lds[base + 512 + ((x >> 16) & 255u)] ^
            lds[base + 768 + (x >> 24)];
+}
+
+// Lane fold of the four word slots in the reference's STEP4W order
+// (crc32c.cc:312-319): Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0)))) expanded into four
+// independent lookups, Z16(a0) ^ Z12(a1) ^ Z8(a2) ^ Z4(a3) (one LDS round trip
+// instead of four dependent ones).
+__device__ __forceinline__ uint32_t lane_fold(const uint32_t* lds, uint32_t a0, uint32_t a1, uint32_t a2,
+                                              uint32_t a3) {
+    return zmap(lds, kLZ16, a0) ^ zmap(lds, kLZ12, a1) ^ zmap(lds, kLZ8, a2) ^ zmap(lds, kLZ4, a3);
 }
 
 // One data byte (STEP1).
@@ -250,11 +262,7 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
         c ^= __shfl_down(c, 4, kGroupLanes);
         return c;
     }
-    // lane fold (crc32c.cc STEP4W order): c = Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0))))
-    uint32_t c = zmap(lds, kLZ4, a0);
-    c = zmap(lds, kLZ4, c ^ a1);
-    c = zmap(lds, kLZ4, c ^ a2);
-    c = zmap(lds, kLZ4, c ^ a3);
+    uint32_t c = lane_fold(lds, a0, a1, a2, a3);
     // rotate so the lane holding the last window comes last (identity when m == 7)
     const uint32_t lane = threadIdx.x & 63u;
     c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + m + 1) & (kGroupLanes - 1))), 64);
@@ -360,10 +368,7 @@ __device__ __forceinline__ uint32_t stream_unit(const uint32_t* lds, uint32_t X,
         if (q < rem - 1 || (q == rem - 1 && L.lok)) step4<MODE>(lds, X, a0, a1, a2, a3, cur[q]);
     // lane fold (crc32c.cc STEP4W order), then the 8-lane tree with the lane
     // holding the unit's last window rotated to the end
-    uint32_t c = zmap(lds, kLZ4, a0);
-    c = zmap(lds, kLZ4, c ^ a1);
-    c = zmap(lds, kLZ4, c ^ a2);
-    c = zmap(lds, kLZ4, c ^ a3);
+    uint32_t c = lane_fold(lds, a0, a1, a2, a3);
     const uint32_t lane = threadIdx.x & 63u;
     c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + L.m + 1) & (kGroupLanes - 1))), 64);
     uint32_t t = __shfl_down(c, 1, kGroupLanes);

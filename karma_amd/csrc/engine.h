@@ -25,7 +25,9 @@ constexpr int kBlobZ16 = 2048;     // Z_16  (group tree, level 0)
 constexpr int kBlobZ32 = 3072;     // Z_32  (level 1)
 constexpr int kBlobZ64 = 4096;     // Z_64  (level 2)
 constexpr int kBlobT8 = 5120;      // byte table (one zero byte, low byte index)
-constexpr int kBlobWords = 5376;
+constexpr int kBlobZ8 = 5376;      // Z_8   (in-lane fold, parallel form)
+constexpr int kBlobZ12 = 6400;     // Z_12
+constexpr int kBlobWords = 7424;
 
 // ---- table blob of the combine kernels --------------------------------------
 // maps Z_{D * 2^k}, k = 0..6 (k = 6 is the Horner step of 64 states), Z4 and

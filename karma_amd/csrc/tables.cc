@@ -13,6 +13,8 @@ void build_stream_blob(uint32_t* out) {
     gf2::slicing_tables(Map::zero_bytes(32), out + kBlobZ32);
     gf2::slicing_tables(Map::zero_bytes(64), out + kBlobZ64);
     gf2::byte_table(out + kBlobT8);
+    gf2::slicing_tables(Map::zero_bytes(8), out + kBlobZ8);
+    gf2::slicing_tables(Map::zero_bytes(12), out + kBlobZ12);
 }
 
 void build_combine_blob(uint64_t unit_bytes, uint32_t* out) {

@@ -64,6 +64,8 @@ for rec in (4096, 2048, 1024):
 for rec in (4096, 2048):
     n = GB // rec
     cases[f"ragged aligned {rec}"] = ragged_case(np.full(n, rec, np.uint32), np.arange(n, dtype=np.uint64) * rec)
+    for v in RV:
+        cases[f"ragged aligned {rec} v{v}"] = ragged_case(np.full(n, rec, np.uint32), np.arange(n, dtype=np.uint64) * rec, v)
 count = int(GB / (((65536 - 64) / np.log(1024)) + 8))
 lens = synth.loguniform_lengths(7, count, 64, 65536)
 offs, _ = synth.ragged_layout(lens, header=8)
