@@ -117,8 +117,10 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
                            size_t* h_n_framed, int device);
 
 /* Batched replay (sivir::open's wal::scan_record loop, wal.cc:34-87) from WAL offset
- * `start`: headers walked on the host, all payload CRCs verified in one GPU batch
- * (over d_wal when the caller already holds a device copy, else the image is copied).
+ * `start`, entirely on the device: segment-parallel header walk, all payload CRCs in one
+ * GPU batch, first mismatch.  The image is d_wal when the caller already holds a device
+ * copy (h_wal may then be NULL), else h_wal is streamed into HBM (pinned staging, no
+ * page-locking of the caller's buffer).  seg_bytes < 2^31.
  * Outputs: *h_n_records type-0 records accepted, their header offsets in h_rec_off
  * (optional, up to rec_cap), *h_stop the WAL offset where replay stops (the writer's
  * resume point), *h_status KARMA_WAL_*.  Keeps the reference's size-0 quirk (the CRC
