@@ -57,6 +57,7 @@ struct DevState {
     int cu = 0;
     uint32_t* blob = nullptr;
     std::map<uint64_t, uint32_t*> comb;  // unit bytes -> combine blob
+    std::map<std::pair<uint64_t, uint64_t>, uint32_t*> bcomb;  // (unit bytes, states per thread) -> block blob
 };
 
 struct Workspace {
@@ -109,6 +110,21 @@ int comb_blob(DevState& d, uint64_t unit_bytes, const uint32_t** out) {
     return 0;
 }
 
+int block_comb_blob(DevState& d, uint64_t unit_bytes, uint64_t per_thread, const uint32_t** out) {
+    const auto key = std::make_pair(unit_bytes, per_thread);
+    auto it = d.bcomb.find(key);
+    if (it == d.bcomb.end()) {
+        std::vector<uint32_t> host(kBlockCombWords);
+        build_block_combine_blob(unit_bytes, per_thread, host.data());
+        uint32_t* p = nullptr;
+        KARMA_HIP(hipMalloc(&p, kBlockCombWords * sizeof(uint32_t)));
+        KARMA_HIP(hipMemcpy(p, host.data(), kBlockCombWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+        it = d.bcomb.emplace(key, p).first;
+    }
+    *out = it->second;
+    return 0;
+}
+
 // A per-(device, stream) scratch buffer, grown on demand (*reallocated: it was).
 int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocated = nullptr) {
     Workspace& w = g_ws[{dev, (void*)s}];
@@ -142,6 +158,9 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
         unit = std::max<uint64_t>(kMinSplitUnit, round_up(ceil_div(rec_bytes, k_ideal), kChunk));
         k = ceil_div(rec_bytes, unit);
         if (k == 1) unit = round_up(rec_bytes, kChunk);
+        // a whole number of waves per record (the leading units are then empty: the
+        // units are end-aligned), so each wave folds its 8 units (k_units_fixed WAVE_COMB)
+        if (k > 1) k = round_up(k, kGroupsPerWave);
     }
     FixedArgs a;
     a.arena = static_cast<const uint8_t*>(d_data);
@@ -154,10 +173,12 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
     a.out = d_out;
     a.partial = nullptr;
     a.blob = ds.blob;
+    a.comb_maps = nullptr;
     if (k == 1) {
         KARMA_HIP(launch_fixed(a, ds.cu, s));
         return 0;
     }
+    KARMA_RC(comb_blob(ds, unit, &a.comb_maps));  // Z_U, Z_2U, Z_4U lead the unit's combine blob
     const size_t part_bytes = align256(n_rec * k * sizeof(uint32_t));
     const size_t lvl_bytes = align256(n_rec * ceil_div(k, 64) * sizeof(uint32_t));
     void* ws = nullptr;
@@ -166,8 +187,16 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
     uint32_t* bufs[2] = {reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + part_bytes),
                          reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + part_bytes + lvl_bytes)};
     KARMA_HIP(launch_fixed(a, ds.cu, s));
-    const uint32_t* in = a.partial;
-    uint64_t k_in = k, d = unit;
+    const uint32_t* in = a.partial;  // one state per wave of 8 units
+    uint64_t k_in = k / kGroupsPerWave, d = unit * kGroupsPerWave;
+    // few records: every state of a record in one launch, one block per record
+    if (n_rec <= 4 * (uint64_t)ds.cu && k_in <= kBlockCombMaxPerThread * 1024) {
+        const uint64_t m = ceil_div(k_in, 1024);
+        const uint32_t* bb = nullptr;
+        KARMA_RC(block_comb_blob(ds, d, m, &bb));
+        KARMA_HIP(launch_combine_block(a, in, k_in, m, bb, s));
+        return 0;
+    }
     for (int which = 0;; which ^= 1) {
         const uint64_t k_out = ceil_div(k_in, 64);
         const uint32_t* cb = nullptr;

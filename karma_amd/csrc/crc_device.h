@@ -26,18 +26,20 @@ typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 // so one v_perm_b32 builds it from the register (entry = byte k) and a
 // per-lane constant, and the 32 lanes of each ds_read_b32 half-wave hit 32
 // distinct banks (no conflicts on random data).
-// [128 KiB, +25 KiB): Z4, Z16, Z32, Z64 slicing tables, the byte table, Z8, Z12.
+// [128 KiB, +17 KiB): Z4, Z16, Z32, Z64 slicing tables and the byte table.
+// [145 KiB, +12 KiB): Z_U, Z_2U, Z_4U of the batch's unit size U (the cross-group
+//   combine of k_units_fixed; loaded only when a wave's 8 units belong to one record).
 constexpr int kRepWords = 32768;
 constexpr int kSmallBase = kRepWords;
 constexpr int kSmallWords = kBlobWords - 1024;
-constexpr int kLdsWords = kRepWords + kSmallWords;  // 156,672 bytes
+constexpr int kCombLdsBase = kRepWords + kSmallWords;
+constexpr int kLdsWords = kRepWords + kSmallWords;       // 148,480 bytes
+constexpr int kLdsWordsComb = kLdsWords + 3 * 1024;      // 160,768 bytes
 constexpr int kLZ4 = kSmallBase + (kBlobZ4 - 1024);
 constexpr int kLZ16 = kSmallBase + (kBlobZ16 - 1024);
 constexpr int kLZ32 = kSmallBase + (kBlobZ32 - 1024);
 constexpr int kLZ64 = kSmallBase + (kBlobZ64 - 1024);
 constexpr int kLT8 = kSmallBase + (kBlobT8 - 1024);
-constexpr int kLZ8 = kSmallBase + (kBlobZ8 - 1024);
-constexpr int kLZ12 = kSmallBase + (kBlobZ12 - 1024);
 
 
 constexpr uint32_t kSel0 = 0x0c0c0004u;  // {X.b0, acc.b0, 0, 0}
@@ -65,12 +67,15 @@ __device__ __forceinline__ uint32_t zmap(const uint32_t* lds, int base, uint32_t
 }
 
 // Lane fold of the four word slots in the reference's STEP4W order
-// (crc32c.cc:312-319): Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0)))) expanded into four
-// independent lookups, Z16(a0) ^ Z12(a1) ^ Z8(a2) ^ Z4(a3) (one LDS round trip
-// instead of four dependent ones).
+// (crc32c.cc:312-319): Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0)))).  (The expanded form
+// Z16(a0)^Z12(a1)^Z8(a2)^Z4(a3), one LDS round trip instead of four, measured
+// no faster and costs 8 KiB of LDS: DESIGN.md §4.)
 __device__ __forceinline__ uint32_t lane_fold(const uint32_t* lds, uint32_t a0, uint32_t a1, uint32_t a2,
                                               uint32_t a3) {
-    return zmap(lds, kLZ16, a0) ^ zmap(lds, kLZ12, a1) ^ zmap(lds, kLZ8, a2) ^ zmap(lds, kLZ4, a3);
+    uint32_t c = zmap(lds, kLZ4, a0);
+    c = zmap(lds, kLZ4, c ^ a1);
+    c = zmap(lds, kLZ4, c ^ a2);
+    return zmap(lds, kLZ4, c ^ a3);
 }
 
 // One data byte (STEP1).

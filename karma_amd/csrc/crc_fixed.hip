@@ -63,11 +63,14 @@ __device__ __forceinline__ FixedPlan fixed_plan(const FixedArgs& A, uint64_t u, 
 // back to back; the loads of unit u + step (chunk 0, PF chunks, the head and
 // tail blocks, the init value) are issued before unit u's last chunks are
 // consumed (stream_unit), so no wave waits on a fresh load at a unit boundary.
-template <int PF, bool NT, bool HAS_INIT, int MODE = 0>
+// The first unit's loads are issued before the LDS table fill, which then
+// costs no separate memory round trip.  WAVE_COMB (k % 8 == 0): the 8 groups of
+// a wave hold units 8i..8i+7 of one record, end-aligned; a 3-level tree over
+// the groups (Z_U, Z_2U, Z_4U) leaves one state per 8 units, so the combine
+// kernels start one level up (a 64 MiB segment: 32768 -> 4096 states here).
+template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
-    load_stream_tables(lds, A.blob);
-    __syncthreads();
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVE_COMB ? kLdsWordsComb : kLdsWords];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & (kGroupLanes - 1);
     const uint32_t grp = lane / kGroupLanes;
@@ -78,12 +81,15 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     const uint64_t step = nwaves * kGroupsPerWave;
     uint64_t wb = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     uint64_t u = wb * kGroupsPerWave + grp;
-    // unit u's head block and init value, then its chunk loads
+    // unit u's head block and init value, then its chunk loads, then the tables
     FixedPlan P = fixed_plan(A, u, U, l);
     u32x4 hv = ld16(P.hblk), tv = ld16(P.tblk);
     uint32_t iv = HAS_INIT ? *(const __attribute__((address_space(1))) uint32_t*)(A.init + P.r) : A.init_scalar;
     UnitLoads<PF> Ld;
     issue_unit_loads<PF, NT>(P.L, Ld);
+    load_stream_tables(lds, A.blob);
+    if constexpr (WAVE_COMB) copy_to_lds<3 * 1024, kBlockThreads>(lds + kCombLdsBase, A.comb_maps);
+    __syncthreads();
     for (; wb * kGroupsPerWave < U; wb += nwaves, u += step) {
         uint32_t inj = 0;
         if (P.inj_at) inj = P.hfrom < 16 ? steps_in_vec(lds, kLZ4, kLT8, ~iv, hv, P.hfrom, 16u) : ~iv;
@@ -92,14 +98,22 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
         // its first batch: vmcnt counts in order).
         const u32x4 tcur = tv;
         FixedPlan N;
-        const uint32_t R = stream_unit<PF, NT, MODE>(lds, X, l, P.L, Ld, P.inj_at, inj, [&](UnitLoads<PF>& nx) {
+        uint32_t R = stream_unit<PF, NT, MODE>(lds, X, l, P.L, Ld, P.inj_at, inj, [&](UnitLoads<PF>& nx) {
             N = fixed_plan(A, u + step, U, l);
             hv = ld16(N.hblk);
             tv = ld16(N.tblk);
             if constexpr (HAS_INIT) iv = *(const __attribute__((address_space(1))) uint32_t*)(A.init + N.r);
             issue_unit_loads<PF, NT>(N.L, nx);
         });
-        if (P.valid && l == 0) {
+        if constexpr (WAVE_COMB) {  // unit states sit in lanes 8g; fold g = 0..7 (g = 7 ends last)
+            uint32_t t = __shfl_down(R, 8, 64);
+            R = zmap(lds, kCombLdsBase, R) ^ t;
+            t = __shfl_down(R, 16, 64);
+            R = zmap(lds, kCombLdsBase + 1024, R) ^ t;
+            t = __shfl_down(R, 32, 64);
+            R = zmap(lds, kCombLdsBase + 2048, R) ^ t;
+            if (P.valid && lane == 0) A.partial[wb] = R;  // state wb = units 8wb .. 8wb+7
+        } else if (P.valid && l == 0) {
             if (k == 1)
                 A.out[P.r] = ~steps_in_vec(lds, kLZ4, kLT8, R, tcur, 0u, P.tto);
             else
@@ -197,6 +211,51 @@ __global__ __launch_bounds__(256) void k_combine_fixed(FixedArgs A, const uint32
     }
 }
 
+// Every state of one record (blockIdx.x) folded in one block: thread t folds
+// states [t*m, t*m + m) (leading zero states pad k_in to 1024 m) with Z_D, the
+// 64-lane tree (Z_{mD*2^d}) folds each wave, thread 0 folds the 16 wave
+// results with Z_{64mD}, adds the record tail and writes the CRC.
+__global__ __launch_bounds__(1024) void k_combine_block(FixedArgs A, const uint32_t* in, uint64_t k_in, uint64_t m,
+                                                        const uint32_t* bc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kBlockCombWords];
+    __shared__ uint32_t wv[16];
+    const uint64_t r = blockIdx.x;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const int64_t pad = (int64_t)(m * 1024 - k_in);
+    const int64_t i0 = (int64_t)(threadIdx.x * m) - pad;
+    const uint32_t* rs = in + r * k_in;
+    uint32_t first[8];  // the first states are issued before the table fill
+#pragma unroll
+    for (int q = 0; q < 8; ++q) first[q] = (uint64_t)q < m && i0 + q >= 0 ? rs[i0 + q] : 0u;
+    copy_to_lds<kBlockCombWords, 1024>(lds, bc);
+    __syncthreads();
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if ((uint64_t)q < m) acc = zmap(lds, kBcZD, acc) ^ first[q];
+    for (uint64_t i = 8; i < m; i += 8) {
+        uint32_t sv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sv[q] = i + q < m && i0 + (int64_t)(i + q) >= 0 ? rs[i0 + i + q] : 0u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (i + q < m) acc = zmap(lds, kBcZD, acc) ^ sv[q];
+    }
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        const uint32_t t = __shfl_down(acc, 1u << d, 64);
+        acc = zmap(lds, kBcTree + d * 1024, acc) ^ t;
+    }
+    if (lane == 0) wv[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t v = wv[0];
+        for (int w = 1; w < 16; ++w) v = zmap(lds, kBcWave, v) ^ wv[w];
+        const uint8_t* p = A.arena + r * A.rec_bytes;
+        A.out[r] = ~tail_register(lds, kBcZ4, kBcT8, v, geom(p, A.rec_bytes));
+    }
+}
+
 // KARMA_CRC_VARIANT selects an alternative build of the streaming kernel for
 // in-process A/B measurements (tools/variant_bench.py); 0 = shipped default.
 int fixed_variant() {
@@ -216,19 +275,22 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     // Records of < 31 bytes may hold no aligned 16-byte block.  Units under 2 KiB:
     // the pipelined kernel's extra per-unit work outweighs its hidden latency
     // (1 KiB units: 0.700 vs 0.669 ms per 4 GiB; 4 KiB: 0.628 vs 0.641).
-    if (a.rec_bytes < 31 || a.unit_bytes < 2048) {
+    if (a.comb_maps) {  // k % 8 == 0, units >= 2 KiB (planner)
+        if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_units_fixed<4, true, false, true>), grid, blk, 0, s, a);
+    } else if (a.rec_bytes < 31 || a.unit_bytes < 2048) {
         hipLaunchKernelGGL((k_units_fixed_v1<4, true>), grid, blk, 0, s, a);
     } else {
         switch (fixed_variant()) {
             case 1: hipLaunchKernelGGL((k_units_fixed_v1<4, true>), grid, blk, 0, s, a); break;
             case 2:
-                if (a.init) hipLaunchKernelGGL((k_units_fixed<2, true, true>), grid, blk, 0, s, a);
-                else hipLaunchKernelGGL((k_units_fixed<2, true, false>), grid, blk, 0, s, a);
+                if (a.init) hipLaunchKernelGGL((k_units_fixed<2, true, true, false>), grid, blk, 0, s, a);
+                else hipLaunchKernelGGL((k_units_fixed<2, true, false, false>), grid, blk, 0, s, a);
                 break;
-            case 6: hipLaunchKernelGGL((k_units_fixed<4, true, false, 1>), grid, blk, 0, s, a); break;  // timing only
+            case 6: hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 1>), grid, blk, 0, s, a); break;  // timing only
             default:
-                if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true>), grid, blk, 0, s, a);
-                else hipLaunchKernelGGL((k_units_fixed<4, true, false>), grid, blk, 0, s, a);
+                if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false>), grid, blk, 0, s, a);
+                else hipLaunchKernelGGL((k_units_fixed<4, true, false, false>), grid, blk, 0, s, a);
                 break;
         }
     }
@@ -243,6 +305,14 @@ hipError_t launch_combine_fixed(const FixedArgs& a, const uint32_t* in_states, u
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_combine_fixed, dim3((unsigned)blocks), dim3(256), 0, s, a, in_states, k_in, out_states,
                        k_out, comb_blob);
+    return hipGetLastError();
+}
+
+hipError_t launch_combine_block(const FixedArgs& a, const uint32_t* in_states, uint64_t k_in, uint64_t m,
+                                const uint32_t* block_blob, hipStream_t s) {
+    if (a.n_rec == 0) return hipSuccess;
+    if (m == 0 || m > kBlockCombMaxPerThread || k_in > m * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_combine_block, dim3((unsigned)a.n_rec), dim3(1024), 0, s, a, in_states, k_in, m, block_blob);
     return hipGetLastError();
 }
 

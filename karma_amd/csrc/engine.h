@@ -25,9 +25,7 @@ constexpr int kBlobZ16 = 2048;     // Z_16  (group tree, level 0)
 constexpr int kBlobZ32 = 3072;     // Z_32  (level 1)
 constexpr int kBlobZ64 = 4096;     // Z_64  (level 2)
 constexpr int kBlobT8 = 5120;      // byte table (one zero byte, low byte index)
-constexpr int kBlobZ8 = 5376;      // Z_8   (in-lane fold, parallel form)
-constexpr int kBlobZ12 = 6400;     // Z_12
-constexpr int kBlobWords = 7424;
+constexpr int kBlobWords = 5376;
 
 // ---- table blob of the combine kernels --------------------------------------
 // maps Z_{D * 2^k}, k = 0..6 (k = 6 is the Horner step of 64 states), Z4 and
@@ -41,9 +39,22 @@ constexpr int kCombSmall = kCombT8 + 1024;
 constexpr int kCombSmallMaps = 8;
 constexpr int kCombWords = kCombSmall + kCombSmallMaps * 1024;
 
+// ---- table blob of the one-block combine (k_combine_block) -----------------
+// For states of D bytes folded m per thread: Z_D (the in-thread Horner step),
+// Z_{mD*2^d} for d = 0..5 (the 64-lane tree), Z_{64mD} (the fold of the 16
+// wave results), Z4 and the byte table (the record tail).
+constexpr int kBcZD = 0;
+constexpr int kBcTree = 1024;
+constexpr int kBcWave = 7 * 1024;
+constexpr int kBcZ4 = 8 * 1024;
+constexpr int kBcT8 = 9 * 1024;
+constexpr int kBlockCombWords = 9 * 1024 + 256;
+constexpr uint64_t kBlockCombMaxPerThread = 64;  // one launch folds up to 64 Ki states per record
+
 // Host builders (gf2.h): fill a blob for stride kChunk / for unit size D.
 void build_stream_blob(uint32_t* out /*kBlobWords*/);
 void build_combine_blob(uint64_t unit_bytes, uint32_t* out /*kCombWords*/);
+void build_block_combine_blob(uint64_t unit_bytes, uint64_t per_thread, uint32_t* out /*kBlockCombWords*/);
 
 struct FixedArgs {
     const uint8_t* arena;      // record r at arena + r * rec_bytes
@@ -54,8 +65,10 @@ struct FixedArgs {
     uint64_t unit_bytes;       // multiple of kChunk
     uint64_t units_per_rec;    // k (same for every record)
     uint32_t* out;             // final crc per record (written when k == 1)
-    uint32_t* partial;         // per-unit register contributions (k > 1)
+    uint32_t* partial;         // per-unit register contributions (k > 1); with comb_maps, one per 8 units
     const uint32_t* blob;      // kBlobWords, device
+    const uint32_t* comb_maps; // k % 8 == 0: Z_U, Z_2U, Z_4U (3 x 1024 words): the 8 groups of a
+                               // wave fold their 8 consecutive units into one state (else nullptr)
 };
 
 // One unit of a ragged batch: the 16-aligned span [us, us + span) of a record
@@ -107,6 +120,10 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s);
 // One combine level for the fixed layout: k_in states per record -> k_out = ceil(k_in / 64).
 hipError_t launch_combine_fixed(const FixedArgs& a, const uint32_t* in_states, uint64_t k_in, uint32_t* out_states,
                                 uint64_t k_out, const uint32_t* comb_blob, hipStream_t s);
+// All of a record's k_in states (D bytes each, end-aligned) -> its CRC in one
+// launch: one 1024-thread block per record, m = ceil(k_in / 1024) states per thread.
+hipError_t launch_combine_block(const FixedArgs& a, const uint32_t* in_states, uint64_t k_in, uint64_t m,
+                                const uint32_t* block_blob, hipStream_t s);
 uint64_t ragged_scan_blocks(uint64_t n_rec);
 // Ragged: scan (full-unit offsets + partial-unit buckets; total units at
 // fbase[n_rec]), then descriptors, the unit kernel and the per-record finalize.

@@ -13,8 +13,19 @@ void build_stream_blob(uint32_t* out) {
     gf2::slicing_tables(Map::zero_bytes(32), out + kBlobZ32);
     gf2::slicing_tables(Map::zero_bytes(64), out + kBlobZ64);
     gf2::byte_table(out + kBlobT8);
-    gf2::slicing_tables(Map::zero_bytes(8), out + kBlobZ8);
-    gf2::slicing_tables(Map::zero_bytes(12), out + kBlobZ12);
+}
+
+void build_block_combine_blob(uint64_t unit_bytes, uint64_t per_thread, uint32_t* out) {
+    using gf2::Map;
+    gf2::slicing_tables(Map::zero_bytes(unit_bytes), out + kBcZD);
+    Map m = Map::zero_bytes(unit_bytes * per_thread);
+    for (int d = 0; d < 6; ++d) {
+        gf2::slicing_tables(m, out + kBcTree + d * 1024);
+        m = Map::compose(m, m);
+    }
+    gf2::slicing_tables(m, out + kBcWave);  // Z_{64 m D}
+    gf2::slicing_tables(Map::zero_bytes(4), out + kBcZ4);
+    gf2::byte_table(out + kBcT8);
 }
 
 void build_combine_blob(uint64_t unit_bytes, uint32_t* out) {
