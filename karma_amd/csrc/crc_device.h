@@ -184,7 +184,7 @@ __device__ __forceinline__ uint32_t tail_register(const uint32_t* lds, int z4, i
 }
 
 // MODE (timing experiments only, wrong results): bit 0 = main-loop steps without the
-// LDS lookups, bit 1 = group epilogue without lookups.  The shipped kernels use MODE 0.
+// LDS lookups (KARMA_CRC_VARIANT=6).  The shipped kernels use MODE 0.
 template <int MODE = 0>
 __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
                                       uint32_t& a3, const u32x4& v) {
@@ -217,7 +217,7 @@ __device__ __forceinline__ const uint8_t* floor128(const uint8_t* p) {
 // word carries the record's entering register).  PF chunk loads stay in flight
 // per lane.  Every lane of the wave must call this (cross-lane shuffles); the
 // result is valid in group lane 0.
-template <int PF, bool NT, int MODE = 0>
+template <int PF, bool NT>
 __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, uint32_t l, const uint8_t* us,
                                                const uint8_t* ue, const uint8_t* inj_at, uint32_t inj) {
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
@@ -252,20 +252,13 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
 #pragma unroll
             for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
 #pragma unroll
-            for (int q = 0; q < PF; ++q) step4<MODE>(lds, X, a0, a1, a2, a3, cur[q]);
+            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
             rem -= PF;
         }
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
-            if (q < rem - 1 || (q == rem - 1 && lok)) step4<MODE>(lds, X, a0, a1, a2, a3, nb[q]);
+            if (q < rem - 1 || (q == rem - 1 && lok)) step4(lds, X, a0, a1, a2, a3, nb[q]);
         }
-    }
-    if constexpr ((MODE & 2) != 0) {
-        uint32_t c = a0 ^ a1 ^ a2 ^ a3;
-        c ^= __shfl_down(c, 1, kGroupLanes);
-        c ^= __shfl_down(c, 2, kGroupLanes);
-        c ^= __shfl_down(c, 4, kGroupLanes);
-        return c;
     }
     uint32_t c = lane_fold(lds, a0, a1, a2, a3);
     // rotate so the lane holding the last window comes last (identity when m == 7)

@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
 // Records of fewer than 31 bytes may hold no aligned 16-byte block (and tiny
 // batches need no streaming): the general kernel, one unit per group, each
 // unit's loads issued when the unit starts.  Also the A/B baseline (variant 1).
-template <int PF, bool NT, int MODE = 0>
+template <int PF, bool NT>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed_v1(FixedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed_v1(FixedArgs A) {
                 inj = head_register(lds, kLZ4, kLT8, p, g, init);
             }
         }
-        uint32_t R = group_unit<PF, NT, MODE>(lds, X, l, us, ue, inj_at, inj);
+        uint32_t R = group_unit<PF, NT>(lds, X, l, us, ue, inj_at, inj);
         if (valid && l == 0) {
             if (g.is_short) {
                 A.out[r] = short_record(lds, kLZ4, kLT8, p, A.rec_bytes, init);

@@ -15,6 +15,8 @@
 //   (connection.cc:20-27): frame::parse at the cursor (frame.cc:62-130), erase
 //   frame->size() bytes, repeat.  It stops where parse returns nullopt
 //   (incomplete frame) or throws (bad size / magic / header length / crc).
+#include <hip/hip_runtime_api.h>
+
 #include <cstring>
 #include <string>
 #include <vector>
@@ -23,8 +25,37 @@
 
 namespace karma::engine {
 int set_last_error(int code, const std::string& what);  // capi.cc
+
+// CRCs of the spans (off[i], len[i]) of a buffer in one ragged GPU batch: from host
+// memory (batch_ragged_host), or over the caller's device copy d_buf.
 int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std::vector<uint64_t>& off,
-              const std::vector<uint32_t>& len, std::vector<uint32_t>& out, int device);  // wal.cc
+              const std::vector<uint32_t>& len, std::vector<uint32_t>& out, int device) {
+    out.resize(off.size());
+    if (off.empty()) return 0;
+    if (!d_buf) return karma_crc32c_batch_ragged_host(h_buf, buf_bytes, off.data(), len.data(), off.size(), 0,
+                                                      out.data(), device);
+    // device copy supplied: stage the offsets/lengths and run the device batch
+    uint64_t total = 0;
+    for (uint32_t l : len) total += l;
+    if (device >= 0 && hipSetDevice(device) != hipSuccess) return set_last_error(KARMA_E_HIP, "hipSetDevice");
+    void *doff = nullptr, *dlen = nullptr, *dout = nullptr;
+    int rc = 0;
+    if (hipMalloc(&doff, off.size() * 8) != hipSuccess || hipMalloc(&dlen, len.size() * 4) != hipSuccess ||
+        hipMalloc(&dout, out.size() * 4) != hipSuccess)
+        rc = set_last_error(KARMA_E_NOMEM, "crc_spans: hipMalloc");
+    else if (hipMemcpy(doff, off.data(), off.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(dlen, len.data(), len.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        rc = set_last_error(KARMA_E_HIP, "crc_spans: hipMemcpy H2D");
+    else if ((rc = karma_crc32c_batch_ragged(d_buf, static_cast<uint64_t*>(doff), static_cast<uint32_t*>(dlen),
+                                             off.size(), total, nullptr, 0, static_cast<uint32_t*>(dout), nullptr)))
+        ;
+    else if (hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = set_last_error(KARMA_E_HIP, "crc_spans: hipMemcpy D2H");
+    (void)hipFree(doff);
+    (void)hipFree(dlen);
+    (void)hipFree(dout);
+    return rc;
+}
 }  // namespace karma::engine
 
 namespace {
