@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--workload", default="fixed",
                    choices=["fixed", "ragged", "stream", "segment", "host", "wal_append", "wal_replay"])
     p.add_argument("--wal-record", type=int, default=180, help="wal_* payload bytes (configs[0]: ~180 B)")
+    p.add_argument("--wal-mix", default="fixed", choices=["fixed", "config3"],
+                   help="wal_*: every payload --wal-record bytes, or configs[2]'s log-uniform 64 B-64 KiB mix (~4 GiB)")
     p.add_argument("--records-per-gpu", type=int, default=1 << 20)
     p.add_argument("--rec-bytes", type=int, default=4096)
     p.add_argument("--seed", type=int, default=42)
@@ -155,14 +157,31 @@ def wal_bench(args, L, rank):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import synth
     from karma_amd import _lib
-    n, size, seg = args.records_per_gpu, args.wal_record, 1 << 20
-    lens = np.full(n, size, dtype=np.uint32)
-    offs = (np.arange(n, dtype=np.uint64) * np.uint64(size)).astype(np.uint64)
-    src = synth.splitmix_np(args.seed + rank, 0, n * size + 16).copy()
-    per_seg = seg // (size + 8)
-    wal_bytes = ((n + per_seg - 1) // per_seg + 1) * seg
-    wal = np.zeros(wal_bytes, dtype=np.uint8)
+    seg = 1 << 20
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.wal_mix == "config3":  # configs[2]'s replay mix framed into 1 MiB segments
+        import torch
+        import karma_amd as K
+        count = int((4 << 30) / (((65536 - 64) / np.log(1024)) + 8))
+        lens = synth.loguniform_lengths(7, count, 64, 65536).astype(np.uint32)
+        n, size = count, None
+        offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+        total = int(lens.sum())
+        d_src = torch.empty(total + 16, dtype=torch.uint8, device=torch.device("cuda", local))
+        K.fill_splitmix64(d_src, args.seed + rank)
+        src = d_src.cpu().numpy()
+        del d_src
+        # every segment loses at most one record's header + payload to its footer
+        wal_bytes = ((total + 8 * n) // (seg - 65544) + 2) * seg
+    else:
+        n, size = args.records_per_gpu, args.wal_record
+        lens = np.full(n, size, dtype=np.uint32)
+        offs = (np.arange(n, dtype=np.uint64) * np.uint64(size)).astype(np.uint64)
+        src = synth.splitmix_np(args.seed + rank, 0, n * size + 16).copy()
+        per_seg = seg // (size + 8)
+        wal_bytes = ((n + per_seg - 1) // per_seg + 1) * seg
+    payload = int(lens.sum())
+    wal = np.zeros(wal_bytes, dtype=np.uint8)
     cur, nf = ctypes.c_uint64(0), ctypes.c_size_t()
 
     def append():
@@ -196,7 +215,7 @@ def wal_bench(args, L, rank):
         t0 = time.perf_counter()
         for _ in range(args.steps):
             replay_dev()
-        dev_rate = n * size / ((time.perf_counter() - t0) / args.steps) / GIB
+        dev_rate = payload / ((time.perf_counter() - t0) / args.steps) / GIB
         del d_wal
     for _ in range(args.warmup):
         step()
@@ -204,18 +223,19 @@ def wal_bench(args, L, rank):
     for _ in range(args.steps):
         step()
     dt = (time.perf_counter() - t0) / args.steps
-    payload = n * size
+    mix = f"{n} x {size} B" if size else f"{n} log-uniform 64 B-64 KiB ({payload / GIB:.2f} GiB)"
     res = {"metric": METRIC + f" [{args.workload}: host memory end to end]",
            "value": round(payload / dt / GIB, 3), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "u8", "data": "synthetic splitmix64 payloads in pageable host memory",
            "records_per_s": round(n / dt, 1),
            "device_resident_value": round(dev_rate, 3) if dev_rate is not None else None,
-           "config": {"workload": f"{n} x {size} B WAL records, 1 MiB segments, "
+           "config": {"workload": f"{mix} WAL records, 1 MiB segments, "
                                   f"{'karma_wal_append_batch' if step is append else 'karma_wal_replay'} "
-                                  f"(BASELINE configs[0] shape)", "records": n, "record_bytes": size},
+                                  f"(BASELINE {'configs[0]' if size else 'configs[2]'} records)", "records": n,
+                      "record_bytes": size},
            "roofline": None}
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and size:
         import oracle_lib
         ref = oracle_lib.ref()
         if ref is not None:
