@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--rec-bytes", type=int, default=4096)
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--call-events", choices=["auto", "on", "off"], default="auto",
+                   help="bracket every call with its own events too (auto: when a call is more than one kernel)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_fixed_4k.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/profile.sh)")
@@ -469,20 +471,26 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    # a fixed batch of one-unit records is one kernel: its call events would only add two
+    # records to the stream per step, so the call time is the kernel time there
+    call_events = {"on": True, "off": False}.get(args.call_events, not (wl == "fixed" and n_rec >= 4 * 32768))
     for i in range(args.steps):
-        ev[i][0].record(stream)
+        if call_events:
+            ev[i][0].record(stream)
         if timed_units:
             L.karma_crc32c_time_next_units(uev[i][0].cuda_event, uev[i][1].cuda_event)
         crc_step()
-        ev[i][1].record(stream)
+        if call_events:
+            ev[i][1].record(stream)
         gather_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    call_ms = [a.elapsed_time(b) for a, b in ev]
-    kern_ms = [a.elapsed_time(b) for a, b in uev] if timed_units else call_ms
+    kern_ms = [a.elapsed_time(b) for a, b in uev] if timed_units else None
+    call_ms = [a.elapsed_time(b) for a, b in ev] if call_events else kern_ms
+    kern_ms = kern_ms if kern_ms is not None else call_ms
     kern_avg = float(np.mean(kern_ms))
     call_avg = float(np.mean(call_ms))
     if world > 1:
