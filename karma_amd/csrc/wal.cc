@@ -24,6 +24,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -193,8 +194,13 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
     // 1. CRCs of every payload: one GPU batch over the source buffer, on its own
     //    thread while the host places and frames the records (2, 3) around it.
     //    Records that end up not framed (image full) cost only their checksum.
-    uint64_t extent = 0;  // source bytes the batch reads
-    for (size_t i = 0; i < n; ++i) extent = std::max<uint64_t>(extent, h_src_off[i] + h_len[i]);
+    const uint64_t nt = n >= (1u << 16) ? 16 : 1;  // source bytes the batch reads, by nt threads
+    std::vector<uint64_t> ext(nt, 0);
+    parallel_for(0, nt, 1, [&](uint64_t t) {
+        for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i)
+            ext[t] = std::max<uint64_t>(ext[t], h_src_off[i] + h_len[i]);
+    });
+    const uint64_t extent = *std::max_element(ext.begin(), ext.end());
     std::vector<uint32_t> crc(n);
     int crc_rc = 0;
     std::thread gpu;
@@ -202,8 +208,34 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
         gpu = std::thread([&, extent] {
             crc_rc = karma_crc32c_batch_ragged_host(src, extent, h_src_off, h_len, n, 0, crc.data(), device);
         });
-    // 2. placement (sequential, cheap): can_hold or footer + next segment
+    // 2. placement (sequential: can_hold, else footer + next segment), published in
+    //    blocks; 3. framing workers write each block's length fields and payloads
+    //    (segment_file::append_record) as soon as it is placed
+    constexpr size_t kBlock = 16384;
     std::vector<uint64_t> at(n);
+    std::atomic<size_t> placed{0}, next_block{0};
+    std::atomic<bool> placing{true};
+    const size_t nwork = std::min<size_t>(15, std::max<size_t>(1, n / kBlock));
+    std::vector<std::thread> framers;
+    for (size_t t = 0; t < nwork; ++t)
+        framers.emplace_back([&] {
+            while (true) {
+                const size_t lo = next_block.fetch_add(1) * kBlock;
+                size_t avail;
+                while ((avail = placed.load(std::memory_order_acquire)) < lo + kBlock &&
+                       placing.load(std::memory_order_acquire))
+                    std::this_thread::yield();
+                avail = placed.load(std::memory_order_acquire);
+                if (lo >= avail) return;  // placement ended before this block
+                const size_t hi = std::min(lo + kBlock, avail);
+                for (size_t i = lo; i < hi; ++i) {
+                    uint8_t* p = wal + at[i];
+                    put32(p + 4, h_len[i] << 8 | 0u);
+                    std::memcpy(p + kHeader, src + h_src_off[i], h_len[i]);
+                    if (h_rec_off) h_rec_off[i] = at[i];
+                }
+            }
+        });
     uint64_t cur = *h_cursor;
     size_t framed = 0;
     std::vector<std::pair<uint64_t, uint64_t>> footers;  // (wal offset, segment end)
@@ -220,10 +252,12 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
         if (cur + kHeader + len > wal_bytes) break;
         at[framed] = cur;
         cur += kHeader + len;
+        if ((framed + 1) % kBlock == 0) placed.store(framed + 1, std::memory_order_release);
     }
+    placed.store(framed, std::memory_order_release);
+    placing.store(false, std::memory_order_release);
     T.mark("placement");
-    // 3. framing (segment_file::append_record / append_footer); the CRC fields last
-    for (const auto& f : footers) {
+    for (const auto& f : footers) {  // segment_file::append_footer
         const uint64_t room = f.second - f.first;
         if (room < kHeader) {
             std::memset(wal + f.first, '0', room);
@@ -233,28 +267,12 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
             std::memset(wal + f.first + kHeader, '0', room - kHeader);
         }
     }
-    const size_t nthr = std::min<size_t>(16, std::max<size_t>(1, framed / 4096));
-    auto parallel = [&](auto&& body) {
-        std::vector<std::thread> th;
-        for (size_t t = 0; t < nthr; ++t) th.emplace_back(body, framed * t / nthr, framed * (t + 1) / nthr);
-        for (auto& x : th) x.join();
-    };
-    parallel([&](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; ++i) {
-            uint8_t* p = wal + at[i];
-            put32(p + 4, h_len[i] << 8 | 0u);
-            std::memcpy(p + kHeader, src + h_src_off[i], h_len[i]);
-        }
-    });
+    for (auto& x : framers) x.join();
     T.mark("framing (payloads, lengths, footers)");
     if (gpu.joinable()) gpu.join();
     T.mark("wait for the CRC batch");
     if (crc_rc) return crc_rc;  // payloads and length fields are written; no CRC field is
-    parallel([&](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; ++i) put32(wal + at[i], crc[i]);
-    });
-    if (h_rec_off)
-        for (size_t i = 0; i < framed; ++i) h_rec_off[i] = at[i];
+    parallel_for(0, framed, 1 << 16, [&](uint64_t i) { put32(wal + at[i], crc[i]); });
     *h_cursor = cur;
     *h_n_framed = framed;
     return 0;
