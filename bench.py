@@ -37,7 +37,8 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="fixed",
-                   choices=["fixed", "ragged", "stream", "segment", "host", "wal_append", "wal_replay"])
+                   choices=["fixed", "ragged", "stream", "segment", "host", "wal_append", "wal_replay", "kfp_encode",
+                            "kfp_parse"])
     p.add_argument("--wal-record", type=int, default=180, help="wal_* payload bytes (configs[0]: ~180 B)")
     p.add_argument("--wal-mix", default="fixed", choices=["fixed", "config3"],
                    help="wal_*: every payload --wal-record bytes, or configs[2]'s log-uniform 64 B-64 KiB mix (~4 GiB)")
@@ -275,6 +276,63 @@ def wal_bench(args, L, rank):
     return res
 
 
+def kfp_bench(args, L, rank):
+    """KFP frame batches from host memory (frame::encode / connection::read_frame's parse loop,
+    frame.cc:29-130): --records-per-gpu frames (default 256 Ki here) of a 64-byte header and a
+    --rec-bytes payload; all frame CRCs of a call in one GPU batch."""
+    import ctypes
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import synth
+    from karma_amd import _lib
+    n = args.records_per_gpu if args.records_per_gpu != (1 << 20) else (1 << 18)
+    hl = np.full(n, 64, np.uint32)
+    pl = np.full(n, args.rec_bytes, np.uint32)
+    hsrc = synth.splitmix_np(args.seed + 2 * rank, 0, 64 * n + 8).copy()
+    psrc = synth.splitmix_np(args.seed + 2 * rank + 1, 0, args.rec_bytes * n + 8).copy()
+    hoff = (np.arange(n, dtype=np.uint64) * np.uint64(64)).astype(np.uint64)
+    poff = (np.arange(n, dtype=np.uint64) * np.uint64(args.rec_bytes)).astype(np.uint64)
+    op = np.ones(n, np.int16)
+    flag = np.zeros(n, np.uint8)
+    seq = np.arange(n, dtype=np.uint32)
+    frame = 16 + 64 + args.rec_bytes + 4
+    out = np.zeros(n * frame, np.uint8)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ne, nb = ctypes.c_size_t(), ctypes.c_uint64()
+
+    def encode():
+        _lib.check("kfp_encode", L.karma_kfp_encode_batch(hsrc.ctypes.data, hoff.ctypes.data, hl.ctypes.data,
+                                                          psrc.ctypes.data, poff.ctypes.data, pl.ctypes.data,
+                                                          op.ctypes.data, flag.ctypes.data, seq.ctypes.data, n,
+                                                          out.ctypes.data, out.nbytes, None, ctypes.byref(ne),
+                                                          ctypes.byref(nb), local))
+        assert ne.value == n and nb.value == out.nbytes
+
+    nf, used, why = ctypes.c_size_t(), ctypes.c_uint64(), ctypes.c_int()
+
+    def parse():
+        _lib.check("kfp_parse", L.karma_kfp_parse_batch(out.ctypes.data, None, out.nbytes, n, None, ctypes.byref(nf),
+                                                        ctypes.byref(used), ctypes.byref(why), local))
+        assert nf.value == n and why.value == 0
+
+    encode()
+    step = encode if args.workload == "kfp_encode" else parse
+    for _ in range(args.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    dt = (time.perf_counter() - t0) / args.steps
+    return {"metric": METRIC + f" [{args.workload}: host memory end to end]",
+            "value": round(out.nbytes / dt / GIB, 3), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic splitmix64 headers and payloads in pageable host memory",
+            "frames_per_s": round(n / dt, 1),
+            "config": {"workload": f"{n} KFP frames of a 64 B header + {args.rec_bytes} B payload "
+                                   f"({'karma_kfp_encode_batch' if step is encode else 'karma_kfp_parse_batch'})",
+                       "frames": n, "frame_bytes": frame},
+            "roofline": None}
+
+
 def main():
     args = parse()
     import torch
@@ -313,8 +371,8 @@ def main():
         _lib.check("comm_init", L.karma_crc32c_comm_init(ctypes.byref(comm), world, uid, rank))
 
     wl = args.workload
-    if wl in ("wal_append", "wal_replay"):
-        res = wal_bench(args, L, rank)
+    if wl in ("wal_append", "wal_replay", "kfp_encode", "kfp_parse"):
+        res = wal_bench(args, L, rank) if wl.startswith("wal") else kfp_bench(args, L, rank)
         if rank == 0:
             print(json.dumps(res), flush=True)
         if comm is not None:

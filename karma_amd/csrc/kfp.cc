@@ -17,8 +17,11 @@
 //   (incomplete frame) or throws (bad size / magic / header length / crc).
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "karma_crc32c.h"
@@ -85,37 +88,73 @@ int karma_kfp_encode_batch(const void* h_hdr, const uint64_t* h_hdr_off, const u
     const uint8_t* hdr = static_cast<const uint8_t*>(h_hdr);
     const uint8_t* pay = static_cast<const uint8_t*>(h_pay);
     uint8_t* out = static_cast<uint8_t*>(h_out);
-    std::vector<uint64_t> span_off;
-    std::vector<uint32_t> span_len;
+    // 1. frame offsets (frame::encode writes frames back to back) and argument checks
+    std::vector<uint64_t> at;
+    at.reserve(n);
     uint64_t cur = 0;
-    size_t i = 0;
-    for (; i < n; ++i) {
-        const uint64_t hl = h_hdr_len[i], pl = h_pay_len[i];
+    size_t ne = 0;
+    for (; ne < n; ++ne) {
+        const uint64_t hl = h_hdr_len[ne], pl = h_pay_len[ne];
         const uint64_t fl = kFixed + hl + pl + kCrcLen;
         if (fl > 0xFFFFFFFFull) return fail(KARMA_E_INVALID, "kfp_encode_batch: frame_length overflows u32");
         if ((hl && (!hdr || !h_hdr_off)) || (pl && (!pay || !h_pay_off)))
             return fail(KARMA_E_INVALID, "kfp_encode_batch: null header/payload source");
         if (cur + fl > out_bytes) break;  // the rest does not fit: caller flushes and continues
-        uint8_t* f = out + cur;
-        const uint32_t fl32 = static_cast<uint32_t>(fl), hl32 = static_cast<uint32_t>(hl);
-        std::memcpy(f, &fl32, 4);
-        f[4] = KARMA_KFP_MAGIC;
-        std::memcpy(f + 5, &h_op[i], 2);
-        f[7] = h_flag[i];
-        std::memcpy(f + 8, &h_seq[i], 4);
-        std::memcpy(f + 12, &hl32, 4);
-        if (hl) std::memcpy(f + kFixed, hdr + h_hdr_off[i], hl);
-        if (pl) std::memcpy(f + kFixed + hl, pay + h_pay_off[i], pl);
-        if (h_frame_off) h_frame_off[i] = cur;
-        span_off.push_back(cur + kFixed);
-        span_len.push_back(static_cast<uint32_t>(hl + pl));
+        at.push_back(cur);
         cur += fl;
     }
-    // Extend(Value(header), payload) of every frame in one batch over the encoded bytes
-    std::vector<uint32_t> crc;
-    if (const int rc = karma::engine::crc_spans(out, nullptr, cur, span_off, span_len, crc, device)) return rc;
-    for (size_t k = 0; k < crc.size(); ++k) std::memcpy(out + span_off[k] + span_len[k], &crc[k], 4);
-    *h_n_encoded = i;
+    // 2. frames written by 16 threads, piece by piece; 3. each written piece's
+    //    CRCs, Extend(Value(header), payload) = Value(frame[16, 16 + hl + pl)), in one
+    //    GPU batch on a worker thread while the next piece is written
+    constexpr size_t kPieces = 4;
+    const size_t npc = ne >= 4 * 4096 ? kPieces : 1;
+    const bool pinned = cur && hipHostRegister(out, cur, hipHostRegisterDefault) == hipSuccess;
+    if (!pinned) (void)hipGetLastError();  // pageable copies still work
+    std::atomic<size_t> written{0};
+    int crc_rc = 0;
+    std::thread gpu([&] {
+        for (size_t p = 0; p < npc && !crc_rc; ++p) {
+            const size_t lo = ne * p / npc, hi = ne * (p + 1) / npc;
+            while (written.load(std::memory_order_acquire) <= p) std::this_thread::yield();
+            if (lo == hi) continue;
+            std::vector<uint64_t> so(hi - lo);
+            std::vector<uint32_t> sl(hi - lo), crc;
+            for (size_t k = lo; k < hi; ++k) {
+                so[k - lo] = at[k] + kFixed;
+                sl[k - lo] = h_hdr_len[k] + h_pay_len[k];
+            }
+            if ((crc_rc = karma::engine::crc_spans(out, nullptr, cur, so, sl, crc, device))) break;
+            for (size_t k = 0; k < crc.size(); ++k) std::memcpy(out + so[k] + sl[k], &crc[k], 4);
+        }
+    });
+    for (size_t p = 0; p < npc; ++p) {
+        const size_t lo = ne * p / npc, hi = ne * (p + 1) / npc;
+        const size_t nthr = std::min<size_t>(16, std::max<size_t>(1, (hi - lo) / 1024));
+        std::vector<std::thread> th;
+        for (size_t t = 0; t < nthr; ++t)
+            th.emplace_back([&, t] {
+                for (size_t i = lo + (hi - lo) * t / nthr; i < lo + (hi - lo) * (t + 1) / nthr; ++i) {
+                    const uint32_t hl = h_hdr_len[i], pl = h_pay_len[i];
+                    const uint32_t fl = kFixed + hl + pl + kCrcLen;
+                    uint8_t* f = out + at[i];
+                    std::memcpy(f, &fl, 4);
+                    f[4] = KARMA_KFP_MAGIC;
+                    std::memcpy(f + 5, &h_op[i], 2);
+                    f[7] = h_flag[i];
+                    std::memcpy(f + 8, &h_seq[i], 4);
+                    std::memcpy(f + 12, &hl, 4);
+                    if (hl) std::memcpy(f + kFixed, hdr + h_hdr_off[i], hl);
+                    if (pl) std::memcpy(f + kFixed + hl, pay + h_pay_off[i], pl);
+                    if (h_frame_off) h_frame_off[i] = at[i];
+                }
+            });
+        for (auto& x : th) x.join();
+        written.store(p + 1, std::memory_order_release);
+    }
+    gpu.join();
+    if (pinned) (void)hipHostUnregister(out);
+    if (crc_rc) return crc_rc;
+    *h_n_encoded = ne;
     *h_bytes = cur;
     return 0;
 }

@@ -20,4 +20,6 @@ run wal_append --workload wal_append
 run wal_replay --workload wal_replay
 run wal_append_mix --workload wal_append --wal-mix config3 --steps 10 --warmup 2
 run wal_replay_mix --workload wal_replay --wal-mix config3 --steps 10 --warmup 2
+run kfp_encode --workload kfp_encode
+run kfp_parse --workload kfp_parse
 run config5_slice --records-per-gpu 33554432 --steps 5 --warmup 1 --no-cpu-baseline
