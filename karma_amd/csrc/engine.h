@@ -154,8 +154,7 @@ struct WalArgs {
     const uint32_t* crc;       // payload CRC from the ragged batch
     uint64_t* first_bad;       // min candidate index with crc != stored
 };
-uint32_t wal_walk_tile();
-hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, hipStream_t s);
+hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, int cu, hipStream_t s);
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s);
 hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);
 

@@ -327,7 +327,7 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
     A.cand_rec = c.crec.as<uint32_t>();
     A.cand_len = c.clen.as<uint32_t>();
     A.meta = c.meta.as<WalSegMeta>();
-    if (launch_wal_walk(A, nwork, c.st) != hipSuccess ||
+    if (launch_wal_walk(A, nwork, c.cu, c.st) != hipSuccess ||
         hipMemcpyAsync(c.h_meta.p, A.meta, nwork * sizeof(WalSegMeta), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
         hipStreamSynchronize(c.st) != hipSuccess)
         return fail(KARMA_E_HIP, "wal_replay: header walk");

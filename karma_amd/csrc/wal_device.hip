@@ -21,6 +21,8 @@
 // word (wal.cc:50-60); the walk checks it in place.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "engine.h"
 #include "karma_crc32c.h"
 
@@ -159,6 +161,130 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
     if (threadIdx.x == 0) A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg)};
 }
 
+// One wave per segment (64 threads, ~8.5 KiB of LDS: many segments walk at
+// once).  The segment passes through one 4 KiB LDS tile; every lane holds 64
+// bytes of the NEXT tile in registers, loaded while lane 0 walks the current
+// one, so dense headers never wait on a load and a payload that jumps past the
+// next tile costs one 4 KiB load (instead of streaming the whole segment).
+template <uint32_t kWTile>
+__global__ __launch_bounds__(64) void k_wal_walk_wave(WalArgs A) {
+    constexpr int QV = kWTile / 1024;  // 16-byte vectors per lane per tile
+    __shared__ __attribute__((aligned(16))) uint32_t tile[kWTile / 4 + 4];  // + a header's slack
+    __shared__ uint32_t lrec[kWTile / 8 + 1], llen[kWTile / 8 + 1];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t seg = (uint32_t)A.seg_bytes;
+    const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;
+    const uint64_t base = A.base0 + rel;
+    const uint8_t* img = A.wal + rel;
+    uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
+    uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
+    const bool vec = ((reinterpret_cast<uintptr_t>(img)) & 15u) == 0;
+    // this lane's share of the tile at t: vectors lane + 64 q (q < QV) and the slack vector.
+    // The fast case is branch-free: a per-lane branch around a load makes the compiler wait
+    // for every outstanding load at the join (vmcnt counts in order), and the prefetch
+    // would no longer overlap the walk.
+    auto fetch = [&](uint32_t t, uint4 (&r)[QV + 1]) {
+        if (vec && (uint64_t)t + kWTile + 16 <= seg) {  // uniform: whole vectors
+#pragma unroll
+            for (int q = 0; q < QV; ++q) r[q] = *reinterpret_cast<const uint4*>(img + t + (lane + 64u * q) * 16u);
+            r[QV] = *reinterpret_cast<const uint4*>(img + t + kWTile);  // the slack (every lane, one line)
+            return;
+        }
+        // the segment's last tile, or a misaligned segment: bytes inside the segment, zeros past it
+#pragma unroll
+        for (int q = 0; q <= QV; ++q) {
+            const uint32_t o = q < QV ? (lane + 64u * q) * 16u : kWTile;
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (uint32_t b = 0; b < 16; ++b)
+                if ((uint64_t)t + o + b < seg) w[b >> 2] |= uint32_t(img[t + o + b]) << (8 * (b & 3));
+            r[q] = uint4{w[0], w[1], w[2], w[3]};
+        }
+    };
+    auto store = [&](const uint4 (&r)[QV + 1]) {
+#pragma unroll
+        for (int q = 0; q < QV; ++q) reinterpret_cast<uint4*>(tile)[lane + 64u * q] = r[q];
+        if (lane == 0) reinterpret_cast<uint4*>(tile)[kWTile / 16] = r[QV];
+        __syncthreads();  // one wave: orders the tile writes before the walker's reads
+    };
+    uint32_t pos = blockIdx.x == 0 ? (uint32_t)A.first_pos : 0u;
+    uint32_t count = 0, kind = 0, stop = seg;
+    if ((uint64_t)pos + 8 <= seg) {  // wal.cc:40-45: a shorter rest is skipped (kind 0)
+        uint32_t t0 = pos / kWTile * kWTile;
+        uint4 r[QV + 1];  // this lane's share of the next tile
+        fetch(t0, r);
+        store(r);
+        while (true) {
+            const bool more = (uint64_t)t0 + kWTile < seg;
+            if (more) fetch(t0 + kWTile, r);  // in flight while lane 0 walks
+            // Every lane runs the walk on identical values (uniform control flow, so the
+            // compiler keeps the header chain in scalar registers); lane 0 writes the list.
+            uint32_t done = 0, nc = 0;
+            {
+                const uint32_t tend = t0 + kWTile, lim = seg - 8;
+                while (pos <= lim && pos < tend) {
+                    uint32_t crc, st, size, npos;
+                    while (true) {  // fast path: type-0 records with a payload that fits
+                        const uint32_t h = pos - t0, q = h >> 2, sh = h & 3u;
+                        const uint32_t w0 = tile[q], w1 = tile[q + 1], w2 = tile[q + 2];
+                        crc = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbyte(w1, w0, sh));
+                        st = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbyte(w2, w1, sh));
+                        size = st >> 8;
+                        npos = pos + 8 + size;
+                        if ((st & 0xffu) != 0 || size == 0 || npos > seg) break;
+                        if (lane == 0) {
+                            lrec[nc] = pos;
+                            llen[nc] = size;
+                        }
+                        ++nc;
+                        pos = npos;
+                        if (pos > lim || pos >= tend) break;
+                    }
+                    if (pos > lim || pos >= tend) break;
+                    const uint32_t type = st & 0xffu;
+                    if (type == 0 && npos <= seg && crc_word(st) == crc) {  // size 0: stale word (wal.cc:50-60)
+                        if (lane == 0) {
+                            lrec[nc] = pos;
+                            llen[nc] = 0;
+                        }
+                        ++nc;
+                        pos = npos;
+                        continue;
+                    }
+                    done = 1;
+                    if (type == 0) {
+                        kind = KARMA_WAL_CORRUPT;
+                        stop = pos;
+                    } else if (type == 1) {
+                        pos = seg;
+                    } else {
+                        kind = KARMA_WAL_BAD_TYPE;
+                        stop = pos;
+                    }
+                    break;
+                }
+            }
+            __syncthreads();  // lane 0's list writes before the others read them
+            for (uint32_t i = lane; i < nc; i += 64)
+                if (count + i < A.cand_cap) {
+                    crec[count + i] = lrec[i];
+                    clen[count + i] = llen[i];
+                }
+            count += nc;
+            if (done || (uint64_t)pos + 8 > seg) break;
+            const uint32_t nt0 = pos / kWTile * kWTile;
+            __syncthreads();  // everyone has read the list and the tile
+            if (more && nt0 == t0 + kWTile) {
+                store(r);  // the prefetched tile
+            } else {
+                fetch(nt0, r);  // jumped past it
+                store(r);
+            }
+            t0 = nt0;
+        }
+    }
+    if (lane == 0) A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg)};
+}
+
 // Candidates of segment s0 + blockIdx.x (one block per segment) into the
 // contiguous lists at slot A.cand_base[blockIdx.x]: header offset (relative to
 // A.wal), length and the CRC field stored in the header.
@@ -192,11 +318,20 @@ __global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n) {
 
 }  // namespace
 
-uint32_t wal_walk_tile() { return kTile; }
-
-hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, hipStream_t s) {
+// Few segments (no more than two per CU): a workgroup per segment, whose helper
+// waves keep the walking lane fed (1M x 180 B records in 188 segments: 0.75 ms
+// against 0.94 ms for the one-wave walker). Many segments: one wave per segment
+// with 4 KiB tiles, many segments per CU (configs[2]'s mix in 4,300 segments:
+// 0.44 ms against 1.55 ms; 8 or 16 KiB tiles measured 0.60 and 0.84 ms).
+// KARMA_WALK_VARIANT=1 / 2 forces the workgroup / the one-wave walker (tests).
+hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, int cu, hipStream_t s) {
     if (!nseg) return hipSuccess;
-    hipLaunchKernelGGL(k_wal_walk, dim3((unsigned)nseg), dim3(kWalkThreads), 0, s, a);
+    const char* e = getenv("KARMA_WALK_VARIANT");
+    const int v = e && *e ? atoi(e) : (nseg <= 2 * (uint64_t)cu ? 1 : 2);
+    if (v == 1)
+        hipLaunchKernelGGL(k_wal_walk, dim3((unsigned)nseg), dim3(kWalkThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_wal_walk_wave<4096>, dim3((unsigned)nseg), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -115,10 +115,13 @@ def test_replay_from_checkpoint_and_short_segment_tails(lib):
         assert got == (list(want[0]), want[1], want[2])
 
 
+@pytest.mark.parametrize("walk", ["1", "2"])
 @pytest.mark.parametrize("seg", [(1 << 20), (64 << 10) + 12, 4096 + 4])
-def test_replay_segment_sizes_tiles_and_misaligned_segments(lib, seg):
-    """1 MiB segments (32 LDS tiles of the device walk), and segment sizes that are not a
-    multiple of 16 (every segment but the first is misaligned in the image: byte-wise tile loads)."""
+def test_replay_segment_sizes_tiles_and_misaligned_segments(lib, seg, walk, monkeypatch):
+    """1 MiB segments (many LDS tiles of the device walk), and segment sizes that are not a
+    multiple of 16 (every segment but the first is misaligned in the image: byte-wise tile loads);
+    both walk kernels (KARMA_WALK_VARIANT=1: workgroup per segment, 2: one wave per segment)."""
+    monkeypatch.setenv("KARMA_WALK_VARIANT", walk)
     n = 6000 if seg >= (64 << 10) else 600
     src, offs, lens = _payloads(13, n, 1, min(3000, seg - 8))
     nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 3
