@@ -138,13 +138,20 @@ struct WalSegMeta {
 };
 static_assert(sizeof(WalSegMeta) == 16, "one 16-byte record per segment");
 
+// One sub-range walker's result: where it started (a header it found, or the
+// sub-range end: none), its list length, its stop kind / offset and where it left
+// the sub-range (segment-relative).
+struct WalSubMeta {
+    uint32_t first, count, kind, stop, exit, pad[3];
+};
 struct WalArgs {
     const uint8_t* wal;        // first byte of segment s0 (WAL offset base0)
     uint64_t base0;            // s0 * seg_bytes
     uint64_t seg_bytes;        // < 2^31
     uint64_t first_pos;        // where replay enters segment s0 (start - base0)
     uint32_t* cand_rec;        // per segment: cand_cap header offsets within the segment
-    uint32_t* cand_len;        //              and payload lengths
+    uint32_t* cand_len;        //              payload lengths
+    uint32_t* cand_crc;        //              and the CRC fields of their headers
     uint64_t cand_cap;         // seg_bytes / 8 + 1
     WalSegMeta* meta;          // per segment
     const uint64_t* cand_base; // per segment: first slot in the contiguous lists
@@ -153,8 +160,19 @@ struct WalArgs {
     uint32_t* stored;          // CRC field of the header
     const uint32_t* crc;       // payload CRC from the ragged batch
     uint64_t* first_bad;       // min candidate index with crc != stored
+    // The walk splits each segment into nsub sub-ranges of sub_bytes (wal_walk_plan).
+    uint64_t nsub;
+    uint64_t sub_bytes;        // a multiple of the walker's 4 KiB tile
+    uint64_t sub_cap;          // list slots per sub-range: sub_bytes / 8 + 1 (cand_cap = nsub * sub_cap)
+    WalSubMeta* sub;           // per (segment, sub-range) walker
+    uint32_t* span;            // per (segment, sub-range): first list slot of the accepted run, candidates before it
 };
-hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, int cu, hipStream_t s);
+struct WalWalkPlan {
+    uint64_t nsub, sub_bytes, sub_cap, cand_cap;
+    int kernel;  // 0: sub-range walkers (+ resolve when nsub > 1), 1: one workgroup per segment
+};
+WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu);
+hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s);
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s);
 hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);
 

@@ -107,7 +107,7 @@ struct ReplayCtx {
     bool ready = false;
     int cu = 1;
     hipStream_t st = nullptr;
-    DevBuf img, crec, clen, meta, cbase, off, len, stored, crc, bad;
+    DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, bad;
     DevBuf h_meta, h_small;                     // pinned readbacks
     hipStream_t up_st[kUpThreads] = {};
     hipEvent_t up_ev[kUpThreads][2] = {};
@@ -318,16 +318,26 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
     A.base0 = base0;
     A.seg_bytes = seg_bytes;
     A.first_pos = start - base0;
-    A.cand_cap = seg_bytes / 8 + 1;
-    // 1. segment-parallel header walk
+    // 1. segment-parallel header walk (sub-range walkers when there are few segments)
+    const WalWalkPlan plan = wal_walk_plan(seg_bytes, nwork, c.cu);
+    A.nsub = plan.nsub;
+    A.sub_bytes = plan.sub_bytes;
+    A.sub_cap = plan.sub_cap;
+    A.cand_cap = plan.cand_cap;
     if (const int rc = c.crec.ensure(nwork * A.cand_cap * 4)) return rc;
     if (const int rc = c.clen.ensure(nwork * A.cand_cap * 4)) return rc;
+    if (const int rc = c.ccrc.ensure(nwork * A.cand_cap * 4)) return rc;
     if (const int rc = c.meta.ensure(nwork * sizeof(WalSegMeta))) return rc;
     if (const int rc = c.h_meta.ensure(nwork * sizeof(WalSegMeta), true)) return rc;
+    if (const int rc = c.sub.ensure(nwork * plan.nsub * sizeof(WalSubMeta))) return rc;
+    if (const int rc = c.span.ensure(nwork * plan.nsub * 2 * sizeof(uint32_t))) return rc;
     A.cand_rec = c.crec.as<uint32_t>();
     A.cand_len = c.clen.as<uint32_t>();
+    A.cand_crc = c.ccrc.as<uint32_t>();
     A.meta = c.meta.as<WalSegMeta>();
-    if (launch_wal_walk(A, nwork, c.cu, c.st) != hipSuccess ||
+    A.sub = c.sub.as<WalSubMeta>();
+    A.span = c.span.as<uint32_t>();
+    if (launch_wal_walk(A, nwork, plan, c.st) != hipSuccess ||
         hipMemcpyAsync(c.h_meta.p, A.meta, nwork * sizeof(WalSegMeta), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
         hipStreamSynchronize(c.st) != hipSuccess)
         return fail(KARMA_E_HIP, "wal_replay: header walk");

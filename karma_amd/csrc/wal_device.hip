@@ -1,26 +1,29 @@
 // karma_amd/csrc/wal_device.hip -- WAL replay on the device.
 //
 // sivir::open's loop over wal::scan_record (sivir.cc:31-41, wal.cc:34-87) over a
-// WAL image held in HBM, in three kernels around one ragged CRC batch:
+// WAL image held in HBM, in a few kernels around one ragged CRC batch:
 //
-//   k_wal_walk     one workgroup per segment: the segment is staged through LDS
-//                  in 16 KiB tiles and one lane walks its [crc][len<<8|type]
-//                  headers with scan_record's structural checks, writing the
-//                  header offset and payload length of every type-0 record
-//                  (the candidates) and the segment's stop kind / offset.  The
-//                  header chain is serial inside a segment; segments walk in
-//                  parallel, replacing the host's per-record pread loop.
-//   k_wal_gather   candidates of the segments replay enters, in WAL order,
-//                  into contiguous (header offset, length) lists + stored CRCs
-//   (ragged batch) payload CRCs: the arena is the image shifted by the 8-byte
-//                  header, so the list of header offsets is the offset list
-//   k_wal_compare  the first candidate whose payload CRC differs (atomicMin)
+//   k_wal_walk_sub  the header walk: one wave per segment, or (few segments) one
+//                   wave per sub-range of a segment, walking the [crc][len<<8|type]
+//                   headers with scan_record's structural checks through a 4 KiB
+//                   LDS tile, and writing the header offset, payload length and
+//                   stored CRC of every type-0 record (the candidates) and the stop
+//                   kind / offset.  The header chain is serial; segments and
+//                   sub-ranges walk in parallel, replacing the host's pread loop.
+//   k_wal_resolve   (sub-ranges) stitches the walkers' lists along the real chain
+//   k_wal_walk      the same walk with one workgroup per segment (A/B, tests)
+//   k_wal_gather    candidates of the segments replay enters, in WAL order, into
+//                   contiguous (header offset, length, stored CRC) lists
+//   (ragged batch)  payload CRCs: the arena is the image shifted by the 8-byte
+//                   header, so the list of header offsets is the offset list
+//   k_wal_compare   the first candidate whose payload CRC differs (atomicMin)
 //
 // The size-0 quirk is kept: read_exact_at returns early for size 0
 // (segment_file.cc:8), so the CRC compared is that of the stale 4-byte len/type
 // word (wal.cc:50-60); the walk checks it in place.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "engine.h"
@@ -35,13 +38,15 @@ constexpr uint32_t kTile = 16384;          // LDS tile of the walk (two buffers)
 constexpr uint32_t kTileLoad = kTile + 16;  // + one header's slack (16-byte multiple)
 static_assert(kTileLoad % 16 == 0, "tile of whole vectors");
 
-// crc32c::Value of 4 bytes (the stale len/type word of a size-0 record), bitwise.
-__device__ __forceinline__ uint32_t crc_word(uint32_t w) {
+// crc32c::Value of the stale len/type word of a size-0 record.  A type-0 record
+// of size 0 has the word 0, so the value is a constant: Value("\0\0\0\0").
+constexpr uint32_t crc_word_host(uint32_t w) {
     uint32_t l = 0xFFFFFFFFu ^ w;
-#pragma unroll
     for (int i = 0; i < 32; ++i) l = (l >> 1) ^ (0x82F63B78u & (0u - (l & 1u)));
     return l ^ 0xFFFFFFFFu;
 }
+constexpr uint32_t kStaleZero = crc_word_host(0);
+static_assert(kStaleZero == 0x48674BC7u, "crc32c::Value of four zero bytes");
 
 // The walker (thread 0) keeps its position in 32 bits (seg_bytes < 2^31) and
 // reads each header as three aligned LDS words funnel-shifted into place; the
@@ -52,7 +57,7 @@ __device__ __forceinline__ uint32_t crc_word(uint32_t w) {
 // payload that jumps past tile t + 1 costs one synchronous tile load.
 __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t tile[2][kTileLoad / 4 + 4];
-    __shared__ uint32_t lrec[2][kTile / 8 + 1], llen[2][kTile / 8 + 1];
+    __shared__ uint32_t lrec[2][kTile / 8 + 1], llen[2][kTile / 8 + 1], lcrc[2][kTile / 8 + 1];
     __shared__ uint32_t sh_pos, sh_done, sh_n;
     const uint32_t seg = (uint32_t)A.seg_bytes;
     const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;  // segment s0 + blockIdx.x, relative to A.wal
@@ -60,6 +65,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
     const uint8_t* img = A.wal + rel;
     uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
     uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
+    uint32_t* ccrc = A.cand_crc + blockIdx.x * A.cand_cap;
     const bool vec = ((reinterpret_cast<uintptr_t>(img)) & 15u) == 0;
     auto load = [&](int b, uint32_t t0, uint32_t tid, uint32_t nthr) {  // [t0, t0 + kTileLoad) clipped to seg
         const uint32_t n = (uint64_t)t0 + kTileLoad < seg ? kTileLoad : seg - t0;
@@ -78,6 +84,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
             if (at + i < A.cand_cap) {
                 crec[at + i] = lrec[b][i];
                 clen[at + i] = llen[b][i];
+                ccrc[at + i] = lcrc[b][i];
             }
     };
     // uniform: every thread follows the walker through sh_pos
@@ -107,6 +114,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
                         if ((st & 0xffu) != 0 || size == 0 || npos > seg) break;
                         lrec[b][nc] = pos;
                         llen[b][nc] = size;
+                        lcrc[b][nc] = crc;
                         ++nc;
                         pos = npos;
                         if (pos > lim || pos >= tend) break;
@@ -114,9 +122,10 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
                     if (pos > lim || pos >= tend) break;  // left the segment / tile on the fast path
                     // the header at pos is special (scan_record's other branches)
                     const uint32_t type = st & 0xffu;
-                    if (type == 0 && npos <= seg && crc_word(st) == crc) {  // size 0: stale word (wal.cc:50-60)
+                    if (type == 0 && npos <= seg && crc == kStaleZero) {  // size 0: stale word (wal.cc:50-60)
                         lrec[b][nc] = pos;
                         llen[b][nc] = 0;
+                        lcrc[b][nc] = crc;
                         ++nc;
                         pos = npos;
                         continue;
@@ -158,148 +167,364 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
             b ^= 1;
         }
     }
-    if (threadIdx.x == 0) A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg)};
+    if (threadIdx.x == 0) {
+        A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg)};
+        A.span[2 * blockIdx.x] = 0;
+        A.span[2 * blockIdx.x + 1] = 0;
+    }
 }
 
-// One wave per segment (64 threads, ~8.5 KiB of LDS: many segments walk at
-// once).  The segment passes through one 4 KiB LDS tile; every lane holds 64
-// bytes of the NEXT tile in registers, loaded while lane 0 walks the current
-// one, so dense headers never wait on a load and a payload that jumps past the
-// next tile costs one 4 KiB load (instead of streaming the whole segment).
-template <uint32_t kWTile>
-__global__ __launch_bounds__(64) void k_wal_walk_wave(WalArgs A) {
-    constexpr int QV = kWTile / 1024;  // 16-byte vectors per lane per tile
-    __shared__ __attribute__((aligned(16))) uint32_t tile[kWTile / 4 + 4];  // + a header's slack
-    __shared__ uint32_t lrec[kWTile / 8 + 1], llen[kWTile / 8 + 1];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t seg = (uint32_t)A.seg_bytes;
-    const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;
-    const uint64_t base = A.base0 + rel;
-    const uint8_t* img = A.wal + rel;
-    uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
-    uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
-    const bool vec = ((reinterpret_cast<uintptr_t>(img)) & 15u) == 0;
-    // this lane's share of the tile at t: vectors lane + 64 q (q < QV) and the slack vector.
-    // The fast case is branch-free: a per-lane branch around a load makes the compiler wait
-    // for every outstanding load at the join (vmcnt counts in order), and the prefetch
-    // would no longer overlap the walk.
-    auto fetch = [&](uint32_t t, uint4 (&r)[QV + 1]) {
-        if (vec && (uint64_t)t + kWTile + 16 <= seg) {  // uniform: whole vectors
+// ---- one-wave walkers -------------------------------------------------------
+// A wave walks through one 4 KiB LDS tile (4 KiB of LDS: many walkers per CU).  Every lane holds 64 bytes of the NEXT tile in registers,
+// loaded while the walk runs on the current one, so dense headers never wait on
+// a load and a payload that jumps past the next tile costs one 4 KiB load
+// (instead of streaming the whole segment).  The walk runs on every lane with
+// identical values (uniform control flow keeps the header chain in scalar
+// registers).
+constexpr uint32_t kWTile = 4096;
+constexpr int kWQV = kWTile / 1024;  // 16-byte vectors per lane per tile
+constexpr uint32_t kChainCheck = 4;  // headers a sub-range walker's start must chain through
+constexpr uint32_t kMaxSub = 4096;   // sub-ranges per segment (k_wal_gather stages their runs in LDS)
+
+struct WaveLds {
+    uint32_t tile[kWTile / 4 + 4];  // + a header's slack
+};
+
+struct Seg {  // one segment as a walker sees it
+    const uint8_t* img;
+    uint32_t seg;
+    bool vec;  // img 16-byte aligned
+};
+
+// This lane's share of the tile at t: vectors lane + 64 q (q < kWQV) and the slack
+// vector.  The fast case is branch-free: a per-lane branch around a load makes the
+// compiler wait for every outstanding load at the join (vmcnt counts in order), and
+// the prefetch would no longer overlap the walk.
+__device__ __forceinline__ void wtile_fetch(const Seg& S, uint32_t lane, uint32_t t, uint4 (&r)[kWQV + 1]) {
+    if (S.vec && (uint64_t)t + kWTile + 16 <= S.seg) {  // uniform: whole vectors
 #pragma unroll
-            for (int q = 0; q < QV; ++q) r[q] = *reinterpret_cast<const uint4*>(img + t + (lane + 64u * q) * 16u);
-            r[QV] = *reinterpret_cast<const uint4*>(img + t + kWTile);  // the slack (every lane, one line)
-            return;
-        }
-        // the segment's last tile, or a misaligned segment: bytes inside the segment, zeros past it
-#pragma unroll
-        for (int q = 0; q <= QV; ++q) {
-            const uint32_t o = q < QV ? (lane + 64u * q) * 16u : kWTile;
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
-            for (uint32_t b = 0; b < 16; ++b)
-                if ((uint64_t)t + o + b < seg) w[b >> 2] |= uint32_t(img[t + o + b]) << (8 * (b & 3));
-            r[q] = uint4{w[0], w[1], w[2], w[3]};
-        }
-    };
-    auto store = [&](const uint4 (&r)[QV + 1]) {
-#pragma unroll
-        for (int q = 0; q < QV; ++q) reinterpret_cast<uint4*>(tile)[lane + 64u * q] = r[q];
-        if (lane == 0) reinterpret_cast<uint4*>(tile)[kWTile / 16] = r[QV];
-        __syncthreads();  // one wave: orders the tile writes before the walker's reads
-    };
-    uint32_t pos = blockIdx.x == 0 ? (uint32_t)A.first_pos : 0u;
-    uint32_t count = 0, kind = 0, stop = seg;
-    if ((uint64_t)pos + 8 <= seg) {  // wal.cc:40-45: a shorter rest is skipped (kind 0)
-        uint32_t t0 = pos / kWTile * kWTile;
-        uint4 r[QV + 1];  // this lane's share of the next tile
-        fetch(t0, r);
-        store(r);
-        while (true) {
-            const bool more = (uint64_t)t0 + kWTile < seg;
-            if (more) fetch(t0 + kWTile, r);  // in flight while lane 0 walks
-            // Every lane runs the walk on identical values (uniform control flow, so the
-            // compiler keeps the header chain in scalar registers); lane 0 writes the list.
-            uint32_t done = 0, nc = 0;
-            {
-                const uint32_t tend = t0 + kWTile, lim = seg - 8;
-                while (pos <= lim && pos < tend) {
-                    uint32_t crc, st, size, npos;
-                    while (true) {  // fast path: type-0 records with a payload that fits
-                        const uint32_t h = pos - t0, q = h >> 2, sh = h & 3u;
-                        const uint32_t w0 = tile[q], w1 = tile[q + 1], w2 = tile[q + 2];
-                        crc = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbyte(w1, w0, sh));
-                        st = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbyte(w2, w1, sh));
-                        size = st >> 8;
-                        npos = pos + 8 + size;
-                        if ((st & 0xffu) != 0 || size == 0 || npos > seg) break;
-                        if (lane == 0) {
-                            lrec[nc] = pos;
-                            llen[nc] = size;
-                        }
-                        ++nc;
-                        pos = npos;
-                        if (pos > lim || pos >= tend) break;
-                    }
-                    if (pos > lim || pos >= tend) break;
-                    const uint32_t type = st & 0xffu;
-                    if (type == 0 && npos <= seg && crc_word(st) == crc) {  // size 0: stale word (wal.cc:50-60)
-                        if (lane == 0) {
-                            lrec[nc] = pos;
-                            llen[nc] = 0;
-                        }
-                        ++nc;
-                        pos = npos;
-                        continue;
-                    }
-                    done = 1;
-                    if (type == 0) {
-                        kind = KARMA_WAL_CORRUPT;
-                        stop = pos;
-                    } else if (type == 1) {
-                        pos = seg;
-                    } else {
-                        kind = KARMA_WAL_BAD_TYPE;
-                        stop = pos;
-                    }
-                    break;
-                }
-            }
-            __syncthreads();  // lane 0's list writes before the others read them
-            for (uint32_t i = lane; i < nc; i += 64)
-                if (count + i < A.cand_cap) {
-                    crec[count + i] = lrec[i];
-                    clen[count + i] = llen[i];
-                }
-            count += nc;
-            if (done || (uint64_t)pos + 8 > seg) break;
-            const uint32_t nt0 = pos / kWTile * kWTile;
-            __syncthreads();  // everyone has read the list and the tile
-            if (more && nt0 == t0 + kWTile) {
-                store(r);  // the prefetched tile
-            } else {
-                fetch(nt0, r);  // jumped past it
-                store(r);
-            }
-            t0 = nt0;
-        }
+        for (int q = 0; q < kWQV; ++q) r[q] = *reinterpret_cast<const uint4*>(S.img + t + (lane + 64u * q) * 16u);
+        r[kWQV] = *reinterpret_cast<const uint4*>(S.img + t + kWTile);  // the slack (every lane, one line)
+        return;
     }
-    if (lane == 0) A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg)};
+    // the segment's last tile, or a misaligned segment: bytes inside the segment, zeros past it
+#pragma unroll
+    for (int q = 0; q <= kWQV; ++q) {
+        const uint32_t o = q < kWQV ? (lane + 64u * q) * 16u : kWTile;
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t b = 0; b < 16; ++b)
+            if ((uint64_t)t + o + b < S.seg) w[b >> 2] |= uint32_t(S.img[t + o + b]) << (8 * (b & 3));
+        r[q] = uint4{w[0], w[1], w[2], w[3]};
+    }
+}
+
+__device__ __forceinline__ void wtile_store(WaveLds& W, uint32_t lane, const uint4 (&r)[kWQV + 1]) {
+#pragma unroll
+    for (int q = 0; q < kWQV; ++q) reinterpret_cast<uint4*>(W.tile)[lane + 64u * q] = r[q];
+    if (lane == 0) reinterpret_cast<uint4*>(W.tile)[kWTile / 16] = r[kWQV];
+    __syncthreads();  // one wave: orders the tile writes before the walker's reads
+}
+
+// The header at segment offset c, read from the tile at t0 (c - t0 < kWTile).
+__device__ __forceinline__ void tile_header(const WaveLds& W, uint32_t c, uint32_t t0, uint32_t& crc, uint32_t& st) {
+    const uint32_t h = c - t0, q = h >> 2, sh = h & 3u;
+    const uint32_t w0 = W.tile[q], w1 = W.tile[q + 1], w2 = W.tile[q + 2];
+    crc = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    st = __builtin_amdgcn_alignbyte(w2, w1, sh);
+}
+
+struct WalkEnd {
+    uint32_t count;  // candidates written
+    uint32_t kind;   // KARMA_WAL_CORRUPT / _BAD_TYPE, or 0
+    uint32_t stop;   // where kind was found
+    uint32_t pos;    // where the walk left off (seg after a type-1 padding record)
+};
+
+// Walk the header chain from pos while pos < hi, with scan_record's checks (wal.cc:34-87):
+// a rest shorter than a header ends the segment, type 0 with a payload that fits
+// is a candidate, a size-0 record compares the stored CRC with Value of the stale
+// len/type word (wal.cc:50-60), type 1 skips to the segment end, anything else
+// stops the walk.  Candidates go to crec / clen (cap slots).
+__device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t pos, uint32_t hi, uint32_t* crec,
+                              uint32_t* clen, uint32_t* ccrc, uint64_t cap) {
+    const uint32_t seg = S.seg;
+    WalkEnd E{0u, 0u, seg, pos};
+    if ((uint64_t)pos + 8 > seg || pos >= hi) return E;  // wal.cc:40-45: a shorter rest is skipped
+    // The list is built in registers, entry i of each run of 64 in lane i, and written
+    // out 64 entries at a time (coalesced): no LDS traffic besides the header reads.
+    uint32_t myrec = 0, mylen = 0, mycrc = 0, k = 0;
+    auto push = [&](uint32_t p, uint32_t n, uint32_t c) {
+        if (lane == k) {
+            myrec = p;
+            mylen = n;
+            mycrc = c;
+        }
+        if (++k == 64) {
+            if (E.count + lane < cap) {
+                crec[E.count + lane] = myrec;
+                clen[E.count + lane] = mylen;
+                ccrc[E.count + lane] = mycrc;
+            }
+            E.count += 64;
+            k = 0;
+        }
+    };
+    const uint32_t tlim = hi < seg ? hi : seg;  // tiles from here on hold no header before hi
+    uint32_t t0 = pos / kWTile * kWTile;
+    uint4 r[kWQV + 1];
+    wtile_fetch(S, lane, t0, r);
+    wtile_store(W, lane, r);
+    while (true) {
+        const bool more = (uint64_t)t0 + kWTile < tlim;
+        if (more) wtile_fetch(S, lane, t0 + kWTile, r);  // in flight while the walk runs
+        uint32_t done = 0;
+        {
+            const uint32_t tend = t0 + kWTile < hi ? t0 + kWTile : hi, lim = seg - 8;
+            while (pos <= lim && pos < tend) {
+                uint32_t crc, st, size, npos;
+                while (true) {  // fast path: type-0 records with a payload that fits
+                    tile_header(W, pos, t0, crc, st);
+                    crc = __builtin_amdgcn_readfirstlane(crc);
+                    st = __builtin_amdgcn_readfirstlane(st);
+                    size = st >> 8;
+                    npos = pos + 8 + size;  // < 2^32: seg < 2^31, size < 2^24
+                    if ((st & 0xffu) != 0 || size == 0 || npos > seg) break;
+                    push(pos, size, crc);
+                    pos = npos;
+                    if (pos > lim || pos >= tend) break;
+                }
+                if (pos > lim || pos >= tend) break;
+                const uint32_t type = st & 0xffu;
+                if (type == 0 && npos <= seg && crc == kStaleZero) {  // size 0: the stale word
+                    push(pos, 0u, crc);
+                    pos = npos;
+                    continue;
+                }
+                done = 1;
+                if (type == 0) {  // wal.cc:71-74 (length past the segment), or the stale-word mismatch
+                    E.kind = KARMA_WAL_CORRUPT;
+                    E.stop = pos;
+                } else if (type == 1) {  // padding: skip to the segment end (wal.cc:76-82)
+                    pos = seg;
+                } else {
+                    E.kind = KARMA_WAL_BAD_TYPE;
+                    E.stop = pos;
+                }
+                break;
+            }
+        }
+        if (done || (uint64_t)pos + 8 > seg || pos >= hi) break;
+        const uint32_t nt0 = pos / kWTile * kWTile;
+        __syncthreads();  // the walk's tile reads are done before the next tile is stored
+        if (!(more && nt0 == t0 + kWTile)) wtile_fetch(S, lane, nt0, r);  // jumped past the prefetched tile
+        wtile_store(W, lane, r);
+        t0 = nt0;
+    }
+    if (lane < k && E.count + lane < cap) {  // the last, partial run
+        crec[E.count + lane] = myrec;
+        clen[E.count + lane] = mylen;
+        ccrc[E.count + lane] = mycrc;
+    }
+    E.count += k;
+    E.pos = pos;
+    return E;
+}
+
+// Is the header (crc, st) at c one scan_record accepts?  Type 0 with a payload that
+// fits, size 0 with the stale-word CRC, or a padding record (CRC field 0,
+// segment_file.cc:33-49).  *next: the following header.
+__device__ __forceinline__ bool header_ok(uint32_t crc, uint32_t st, uint32_t c, uint32_t seg, uint32_t* next,
+                                          bool* last) {
+    const uint32_t type = st & 0xffu, size = st >> 8;
+    *last = false;
+    *next = c + 8 + size;
+    if (type == 1) {
+        *last = true;
+        return crc == 0;
+    }
+    if (type != 0 || (uint64_t)c + 8 + size > seg) return false;
+    return size != 0 || crc == kStaleZero;
+}
+
+// The first offset c in [lo, lo + 4 KiB) where a chain of kChainCheck headers
+// scan_record accepts starts (ending early at padding or at the segment's short
+// rest also counts), or hi.  64 candidates per step, one per lane, from the tile;
+// the rare lanes whose first header passes follow the chain in global memory.
+// One tile is enough: where headers are further apart, k_wal_resolve walks the
+// sub-range itself in a few steps.  A wrong start only costs time: k_wal_resolve
+// accepts a walker's list only where the authoritative chain meets it.
+__device__ uint32_t find_start(WaveLds& W, const Seg& S, uint32_t lane, uint32_t lo, uint32_t hi) {
+    const uint32_t seg = S.seg;
+    uint4 r[kWQV + 1];
+    for (uint32_t t0 = lo; t0 < hi && t0 < lo + kWTile; t0 += kWTile) {  // lo is tile-aligned
+        wtile_fetch(S, lane, t0, r);
+        wtile_store(W, lane, r);
+        const uint32_t tend = t0 + kWTile < hi ? t0 + kWTile : hi;
+        for (uint32_t c0 = t0; c0 < tend; c0 += 64) {
+            const uint32_t c = c0 + lane;
+            bool ok = false;
+            if (c < tend && (uint64_t)c + 8 <= seg) {
+                uint32_t crc, st, next;
+                bool last;
+                tile_header(W, c, t0, crc, st);
+                // The first hop must stay close: a random "header" whose size happens to land
+                // exactly on a real header far ahead would pass the chain check.  Starts with
+                // longer records are left to k_wal_resolve (few headers there).
+                ok = header_ok(crc, st, c, seg, &next, &last) && (last || next < t0 + 2 * kWTile);
+                for (uint32_t k = 1; ok && !last && k < kChainCheck && (uint64_t)next + 8 <= seg; ++k) {
+                    if (next < t0 + kWTile) {  // still in the tile (+ its slack): from LDS
+                        tile_header(W, next, t0, crc, st);
+                    } else {
+                        const uint8_t* h = S.img + next;
+                        crc = uint32_t(h[0]) | uint32_t(h[1]) << 8 | uint32_t(h[2]) << 16 | uint32_t(h[3]) << 24;
+                        st = uint32_t(h[4]) | uint32_t(h[5]) << 8 | uint32_t(h[6]) << 16 | uint32_t(h[7]) << 24;
+                    }
+                    const uint32_t at = next;
+                    ok = header_ok(crc, st, at, seg, &next, &last);
+                }
+            }
+            const uint64_t m = __ballot(ok);
+            if (m) return c0 + (uint32_t)(__ffsll((long long)m) - 1);
+        }
+        __syncthreads();  // everyone is done with the tile before the next store
+    }
+    return hi;
+}
+
+// One wave per (segment, sub-range): segment s0 + blockIdx.x / nsub, sub-range
+// j = blockIdx.x % nsub, [j sub_bytes, min(seg, (j + 1) sub_bytes)).  The walker
+// of the sub-range holding replay's start walks from the start; later ones find
+// a start (find_start); earlier ones have nothing to do.  Each walks until it
+// leaves its sub-range and reports to A.sub; with one sub-range per segment the
+// walk is the whole segment's and goes straight to A.meta / A.span.
+__global__ __launch_bounds__(64) void k_wal_walk_sub(WalArgs A) {
+    __shared__ __attribute__((aligned(16))) WaveLds W;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t P = A.nsub, s = blockIdx.x / P, j = blockIdx.x % P;
+    const uint64_t rel = s * A.seg_bytes;
+    const Seg S{A.wal + rel, (uint32_t)A.seg_bytes, ((reinterpret_cast<uintptr_t>(A.wal + rel)) & 15u) == 0};
+    const uint32_t lo = (uint32_t)(j * A.sub_bytes);
+    const uint32_t hi = (uint64_t)lo + A.sub_bytes < S.seg ? lo + (uint32_t)A.sub_bytes : S.seg;
+    const uint32_t start = s == 0 ? (uint32_t)A.first_pos : 0u;
+    uint32_t first;
+    if (start >= hi)
+        first = hi;  // before replay's start
+    else if (start >= lo)
+        first = start;
+    else
+        first = find_start(W, S, lane, lo, hi);
+    const uint64_t slot = s * A.cand_cap + j * A.sub_cap;
+    const WalkEnd E = walk_range(W, S, lane, first, hi, A.cand_rec + slot, A.cand_len + slot, A.cand_crc + slot, A.sub_cap);
+    if (lane != 0) return;
+    if (P == 1) {
+        A.meta[s] = WalSegMeta{E.count, E.kind, A.base0 + rel + (E.kind ? E.stop : S.seg)};
+        A.span[2 * s] = 0;
+        A.span[2 * s + 1] = 0;
+    } else {
+        A.sub[blockIdx.x] = WalSubMeta{first, E.count, E.kind, E.stop, E.pos, {0u, 0u, 0u}};
+    }
+}
+
+// One wave per segment: follow the authoritative chain through the sub-ranges.
+// Entering sub-range j at pos, the chain continues exactly as walker j's list
+// from the entry equal to pos on (the walk is a function of the position), so
+// that run is accepted; when pos is not in the list (walker j started on a wrong
+// header, or none), this wave walks the sub-range itself from pos, into the same
+// slots.  Writes the segment's count / stop and the accepted run per sub-range.
+__global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
+    __shared__ __attribute__((aligned(16))) WaveLds W;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t P = A.nsub, s = blockIdx.x;
+    const uint64_t rel = s * A.seg_bytes;
+    const Seg S{A.wal + rel, (uint32_t)A.seg_bytes, ((reinterpret_cast<uintptr_t>(A.wal + rel)) & 15u) == 0};
+    const uint32_t seg = S.seg;
+    const WalSubMeta* M = A.sub + s * P;
+    uint32_t* crec = A.cand_rec + s * A.cand_cap;
+    uint32_t* clen = A.cand_len + s * A.cand_cap;
+    uint32_t* ccrc = A.cand_crc + s * A.cand_cap;
+    uint32_t pos = s == 0 ? (uint32_t)A.first_pos : 0u;
+    uint32_t count = 0, kind = 0, stop = seg;
+    WalSubMeta mine{};  // lane l holds walker j0 + l's report: 64 loads at once, not one per step
+    for (uint64_t j = 0; j < P; ++j) {
+        if (j % 64 == 0 && j + lane < P) mine = M[j + lane];
+        const uint32_t lo = (uint32_t)(j * A.sub_bytes);
+        const uint32_t hi = (uint64_t)lo + A.sub_bytes < seg ? lo + (uint32_t)A.sub_bytes : seg;
+        uint32_t st = (uint32_t)(j * A.sub_cap), n = 0;
+        if (!kind && pos < hi && (uint64_t)pos + 8 <= seg) {
+            const int src = (int)(j % 64);
+            WalSubMeta m;
+            m.first = __builtin_amdgcn_readlane(mine.first, src);  // uniform lane: v_readlane, no LDS
+            m.count = __builtin_amdgcn_readlane(mine.count, src);
+            m.kind = __builtin_amdgcn_readlane(mine.kind, src);
+            m.stop = __builtin_amdgcn_readlane(mine.stop, src);
+            m.exit = __builtin_amdgcn_readlane(mine.exit, src);
+            int64_t idx = -1;
+            if (m.first == pos) {
+                idx = 0;
+            } else if (m.first < pos && m.count > 1) {  // pos among the list's later entries?
+                uint32_t a = 1, b = m.count;             // search [a, b)
+                while (a < b) {
+                    const uint32_t mid = (a + b) / 2;
+                    if (crec[st + mid] < pos) a = mid + 1;
+                    else b = mid;
+                }
+                if (a < m.count && crec[st + a] == pos) idx = a;
+            }
+            if (idx >= 0) {
+                st += (uint32_t)idx;
+                n = m.count - (uint32_t)idx;
+                pos = m.exit;
+                if (m.kind) {
+                    kind = m.kind;
+                    stop = m.stop;
+                }
+            } else {
+                const WalkEnd E = walk_range(W, S, lane, pos, hi, crec + st, clen + st, ccrc + st, A.sub_cap);
+                n = E.count;
+                pos = E.pos;
+                if (E.kind) {
+                    kind = E.kind;
+                    stop = E.stop;
+                }
+            }
+        }
+        if (lane == 0) {
+            A.span[2 * (s * P + j)] = st;
+            A.span[2 * (s * P + j) + 1] = count;  // candidates before the run
+        }
+        count += n;
+    }
+    if (lane == 0) A.meta[s] = WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg)};
 }
 
 // Candidates of segment s0 + blockIdx.x (one block per segment) into the
 // contiguous lists at slot A.cand_base[blockIdx.x]: header offset (relative to
-// A.wal), length and the CRC field stored in the header.
-__global__ __launch_bounds__(256) void k_wal_gather(WalArgs A) {
+// A.wal), length and the CRC field stored in the header (the walk kept it).  The segment's list is
+// its accepted runs in order (A.span: first slot, candidates before the run);
+// candidate i finds its run by a binary search over the runs staged in LDS.
+__global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
+    __shared__ uint2 spans[kMaxSub];
     const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;
-    const uint32_t count = A.meta[blockIdx.x].count;
-    const uint64_t g0 = A.cand_base[blockIdx.x];
     const uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
     const uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
-    for (uint32_t j = threadIdx.x; j < count; j += blockDim.x) {
-        const uint64_t rec = rel + crec[j];
-        const uint8_t* h = A.wal + rec;
-        A.off[g0 + j] = rec;
-        A.len[g0 + j] = clen[j];
-        A.stored[g0 + j] = uint32_t(h[0]) | uint32_t(h[1]) << 8 | uint32_t(h[2]) << 16 | uint32_t(h[3]) << 24;
+    const uint32_t* ccrc = A.cand_crc + blockIdx.x * A.cand_cap;
+    const uint32_t P = (uint32_t)A.nsub;
+    const uint2* sp = reinterpret_cast<const uint2*>(A.span) + blockIdx.x * A.nsub;
+    for (uint32_t j = threadIdx.x; j < P; j += blockDim.x) spans[j] = sp[j];
+    __syncthreads();
+    const uint32_t count = A.meta[blockIdx.x].count;
+    const uint64_t g0 = A.cand_base[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < count; i += blockDim.x) {
+        uint32_t a = 0, b = P;  // the last run whose prefix is <= i: [a, b)
+        while (b - a > 1) {
+            const uint32_t mid = (a + b) / 2;
+            if (spans[mid].y <= i) a = mid;
+            else b = mid;
+        }
+        const uint32_t slot = spans[a].x + (i - spans[a].y);
+        A.off[g0 + i] = rel + crec[slot];
+        A.len[g0 + i] = clen[slot];
+        A.stored[g0 + i] = ccrc[slot];
     }
 }
 
@@ -318,26 +543,53 @@ __global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n) {
 
 }  // namespace
 
-// Few segments (no more than two per CU): a workgroup per segment, whose helper
-// waves keep the walking lane fed (1M x 180 B records in 188 segments: 0.75 ms
-// against 0.94 ms for the one-wave walker). Many segments: one wave per segment
-// with 4 KiB tiles, many segments per CU (configs[2]'s mix in 4,300 segments:
-// 0.44 ms against 1.55 ms; 8 or 16 KiB tiles measured 0.60 and 0.84 ms).
-// KARMA_WALK_VARIANT=1 / 2 forces the workgroup / the one-wave walker (tests).
-hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, int cu, hipStream_t s) {
+// How the walk splits the segments.  The header chain is serial inside a
+// segment, so few segments leave most of the GPU idle: each segment is then cut
+// into sub-ranges (at least 16 KiB) so that about 16 walkers per CU run, and
+// k_wal_resolve stitches their lists.  Many segments: one walker per segment.
+// KARMA_WALK_VARIANT=1 forces one workgroup per segment (k_wal_walk);
+// KARMA_WALK_SUB=<bytes> forces the sub-range size (tests).
+WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu) {
+    WalWalkPlan p{1, 0, 0, 0, 0};
+    const char* v = getenv("KARMA_WALK_VARIANT");
+    const char* fs = getenv("KARMA_WALK_SUB");
+    const uint64_t tiles = (seg_bytes + kWTile - 1) / kWTile;
+    uint64_t sub_tiles = tiles;
+    if (v && atoi(v) == 1) {
+        p.kernel = 1;
+    } else if (fs && *fs) {
+        sub_tiles = std::max<uint64_t>(1, (uint64_t)atoll(fs) / kWTile);
+    } else {
+        const uint64_t want = 16 * (uint64_t)(cu > 0 ? cu : 1);  // walkers
+        if (nseg > 0 && nseg < want) {
+            const uint64_t per = (want + nseg - 1) / nseg;  // sub-ranges per segment
+            sub_tiles = std::max<uint64_t>(4, (tiles + per - 1) / per);
+        }
+    }
+    sub_tiles = std::min(sub_tiles, tiles);
+    sub_tiles = std::max(sub_tiles, (tiles + kMaxSub - 1) / kMaxSub);
+    p.sub_bytes = sub_tiles * kWTile;
+    p.nsub = p.kernel == 1 ? 1 : (seg_bytes + p.sub_bytes - 1) / p.sub_bytes;
+    if (p.nsub == 1) p.sub_bytes = seg_bytes;
+    p.sub_cap = p.sub_bytes / 8 + 1;
+    p.cand_cap = p.nsub * p.sub_cap;
+    return p;
+}
+
+hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s) {
     if (!nseg) return hipSuccess;
-    const char* e = getenv("KARMA_WALK_VARIANT");
-    const int v = e && *e ? atoi(e) : (nseg <= 2 * (uint64_t)cu ? 1 : 2);
-    if (v == 1)
+    if (plan.kernel == 1) {
         hipLaunchKernelGGL(k_wal_walk, dim3((unsigned)nseg), dim3(kWalkThreads), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_wal_walk_wave<4096>, dim3((unsigned)nseg), dim3(64), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_wal_walk_sub, dim3((unsigned)(nseg * plan.nsub)), dim3(64), 0, s, a);
+        if (plan.nsub > 1) hipLaunchKernelGGL(k_wal_resolve, dim3((unsigned)nseg), dim3(64), 0, s, a);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s) {
     if (!nseg) return hipSuccess;
-    hipLaunchKernelGGL(k_wal_gather, dim3((unsigned)nseg), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_wal_gather, dim3((unsigned)nseg), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

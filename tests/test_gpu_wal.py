@@ -115,13 +115,28 @@ def test_replay_from_checkpoint_and_short_segment_tails(lib):
         assert got == (list(want[0]), want[1], want[2])
 
 
-@pytest.mark.parametrize("walk", ["1", "2"])
+WALKS = {
+    "workgroup": {"KARMA_WALK_VARIANT": "1"},         # k_wal_walk, one workgroup per segment
+    "whole": {"KARMA_WALK_SUB": str(1 << 30)},        # k_wal_walk_sub, one walker per segment
+    "split": {},                                      # the plan: few segments -> sub-range walkers
+    "split4k": {"KARMA_WALK_SUB": "4096"},            # one-tile sub-ranges + k_wal_resolve
+}
+
+
+def _walk_env(monkeypatch, walk):
+    for k in ("KARMA_WALK_VARIANT", "KARMA_WALK_SUB"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in WALKS[walk].items():
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("walk", list(WALKS))
 @pytest.mark.parametrize("seg", [(1 << 20), (64 << 10) + 12, 4096 + 4])
 def test_replay_segment_sizes_tiles_and_misaligned_segments(lib, seg, walk, monkeypatch):
     """1 MiB segments (many LDS tiles of the device walk), and segment sizes that are not a
     multiple of 16 (every segment but the first is misaligned in the image: byte-wise tile loads);
-    both walk kernels (KARMA_WALK_VARIANT=1: workgroup per segment, 2: one wave per segment)."""
-    monkeypatch.setenv("KARMA_WALK_VARIANT", walk)
+    every walk kernel and sub-range split."""
+    _walk_env(monkeypatch, walk)
     n = 6000 if seg >= (64 << 10) else 600
     src, offs, lens = _payloads(13, n, 1, min(3000, seg - 8))
     nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 3
@@ -133,11 +148,62 @@ def test_replay_segment_sizes_tiles_and_misaligned_segments(lib, seg, walk, monk
         got = _replay(lib, wal, seg=seg, **kw)
         assert got == (list(want[0]), want[1], want[2])
     assert want[0] == list(rec)
+    # replay from checkpoints that fall in different sub-ranges of a segment
+    for k in (1, len(rec) // 3, len(rec) // 2 + 7):
+        got = _replay(lib, wal, start=int(rec[k]), seg=seg)
+        w = wal_model.replay(wal.tobytes(), seg, int(rec[k]))
+        assert got == (list(w[0]), w[1], w[2])
     # a flipped payload byte deep in the image: replay stops at that record
     k = len(rec) * 3 // 4
     wal[int(rec[k]) + 8] ^= 0x40
     got = _replay(lib, wal, seg=seg)
     assert got[2] == wal_model.CORRUPT and got[1] == int(rec[k]) and len(got[0]) == k
+    # a broken length field: a structural stop inside a later sub-range
+    wal[int(rec[k]) + 8] ^= 0x40
+    j = len(rec) * 5 // 6
+    wal[int(rec[j]) + 7] = 0x7F
+    got = _replay(lib, wal, seg=seg)
+    w = wal_model.replay(wal.tobytes(), seg)
+    assert got == (list(w[0]), w[1], w[2])
+
+
+@pytest.mark.parametrize("walk", ["split", "split4k"])
+def test_replay_payloads_that_look_like_wal_records(lib, walk, monkeypatch):
+    """Payloads that are themselves WAL images (valid header chains inside records): a sub-range
+    walker can start on a header inside a payload, and the resolver must then walk the sub-range
+    itself.  The result must still be scan_record's."""
+    _walk_env(monkeypatch, walk)
+    seg = 256 << 10
+    inner_src, inner_offs, inner_lens = _payloads(31, 400, 1, 200)
+    inner = np.zeros(64 << 10, np.uint8)
+    _append(lib, inner_src, inner_offs, inner_lens, inner, seg=64 << 10)
+    rng = np.random.default_rng(3)
+    chunks, lens = [], []
+    for i in range(300):  # alternate fake-WAL payloads (slices of the inner image) and random ones
+        if i % 2 == 0:
+            a = int(rng.integers(0, 4096))
+            n = int(rng.integers(2000, 12000))
+            chunks.append(inner[a: a + n])
+        else:
+            n = int(rng.integers(1, 3000))
+            chunks.append(rng.integers(0, 256, n, dtype=np.uint8))
+        lens.append(n)
+    lens = np.array(lens, np.uint32)
+    src = np.concatenate(chunks + [np.zeros(16, np.uint8)])
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 2
+    wal = np.zeros(nseg * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    want = wal_model.replay(wal.tobytes(), seg)
+    assert want[0] == list(rec)
+    d = torch.from_numpy(wal).cuda()
+    for kw in ({}, {"d_wal": d, "host": False}):
+        got = _replay(lib, wal, seg=seg, **kw)
+        assert got == (list(want[0]), want[1], want[2])
+    for k in (5, 101, 222):
+        got = _replay(lib, wal, start=int(rec[k]), seg=seg)
+        w = wal_model.replay(wal.tobytes(), seg, int(rec[k]))
+        assert got == (list(w[0]), w[1], w[2])
 
 
 def test_replay_empty_and_start_at_end(lib):
