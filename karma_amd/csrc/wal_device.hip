@@ -225,6 +225,31 @@ __device__ __forceinline__ void wtile_store(WaveLds& W, uint32_t lane, const uin
     __syncthreads();  // one wave: orders the tile writes before the walker's reads
 }
 
+// A 1 KiB window at t (16-byte aligned): one vector per lane + the slack, for a
+// walk that jumps (one header per window: a 4 KiB tile and its prefetch would
+// read 8 KiB per header).
+constexpr uint32_t kWSmall = 1024;
+__device__ __forceinline__ void wsmall_fetch(const Seg& S, uint32_t lane, uint32_t t, uint4& v, uint4& slack) {
+    if (S.vec && (uint64_t)t + kWSmall + 16 <= S.seg) {
+        v = *reinterpret_cast<const uint4*>(S.img + t + lane * 16u);
+        slack = *reinterpret_cast<const uint4*>(S.img + t + kWSmall);
+        return;
+    }
+    uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    for (uint32_t b = 0; b < 16; ++b) {
+        if ((uint64_t)t + lane * 16u + b < S.seg) w[b >> 2] |= uint32_t(S.img[t + lane * 16u + b]) << (8 * (b & 3));
+        if ((uint64_t)t + kWSmall + b < S.seg) w[4 + (b >> 2)] |= uint32_t(S.img[t + kWSmall + b]) << (8 * (b & 3));
+    }
+    v = uint4{w[0], w[1], w[2], w[3]};
+    slack = uint4{w[4], w[5], w[6], w[7]};
+}
+
+__device__ __forceinline__ void wsmall_store(WaveLds& W, uint32_t lane, const uint4& v, const uint4& slack) {
+    reinterpret_cast<uint4*>(W.tile)[lane] = v;
+    if (lane == 0) reinterpret_cast<uint4*>(W.tile)[kWSmall / 16] = slack;
+    __syncthreads();
+}
+
 // The header at segment offset c, read from the tile at t0 (c - t0 < kWTile).
 __device__ __forceinline__ void tile_header(const WaveLds& W, uint32_t c, uint32_t t0, uint32_t& crc, uint32_t& st) {
     const uint32_t h = c - t0, q = h >> 2, sh = h & 3u;
@@ -270,16 +295,19 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
         }
     };
     const uint32_t tlim = hi < seg ? hi : seg;  // tiles from here on hold no header before hi
-    uint32_t t0 = pos / kWTile * kWTile;
+    // Sequential headers go through 4 KiB tiles with the next one prefetched; after a
+    // jump past the prefetched tile the walk reads a 1 KiB window at the header, and
+    // goes back to tiles when it leaves a window for the next one.
+    uint32_t t0 = pos / kWTile * kWTile, tsz = kWTile;
     uint4 r[kWQV + 1];
     wtile_fetch(S, lane, t0, r);
     wtile_store(W, lane, r);
     while (true) {
-        const bool more = (uint64_t)t0 + kWTile < tlim;
+        const bool more = tsz == kWTile && (uint64_t)t0 + kWTile < tlim;
         if (more) wtile_fetch(S, lane, t0 + kWTile, r);  // in flight while the walk runs
         uint32_t done = 0;
         {
-            const uint32_t tend = t0 + kWTile < hi ? t0 + kWTile : hi, lim = seg - 8;
+            const uint32_t tend = t0 + tsz < hi ? t0 + tsz : hi, lim = seg - 8;
             while (pos <= lim && pos < tend) {
                 uint32_t crc, st, size, npos;
                 while (true) {  // fast path: type-0 records with a payload that fits
@@ -316,9 +344,21 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
         if (done || (uint64_t)pos + 8 > seg || pos >= hi) break;
         const uint32_t nt0 = pos / kWTile * kWTile;
         __syncthreads();  // the walk's tile reads are done before the next tile is stored
-        if (!(more && nt0 == t0 + kWTile)) wtile_fetch(S, lane, nt0, r);  // jumped past the prefetched tile
-        wtile_store(W, lane, r);
-        t0 = nt0;
+        if (more && nt0 == t0 + kWTile) {  // the prefetched tile
+            wtile_store(W, lane, r);
+            t0 = nt0;
+        } else if (pos - t0 < 2 * tsz) {  // just past a window (or a tile at the segment end): tiles again
+            wtile_fetch(S, lane, nt0, r);
+            wtile_store(W, lane, r);
+            t0 = nt0;
+            tsz = kWTile;
+        } else {  // a jump: the window at the header
+            uint4 v, sl;
+            t0 = pos & ~15u;
+            wsmall_fetch(S, lane, t0, v, sl);
+            wsmall_store(W, lane, v, sl);
+            tsz = kWSmall;
+        }
     }
     if (lane < k && E.count + lane < cap) {  // the last, partial run
         crec[E.count + lane] = myrec;

@@ -167,6 +167,31 @@ def test_replay_segment_sizes_tiles_and_misaligned_segments(lib, seg, walk, monk
     assert got == (list(w[0]), w[1], w[2])
 
 
+@pytest.mark.parametrize("walk", list(WALKS))
+@pytest.mark.parametrize("seg", [(1 << 20), (256 << 10) + 4])
+def test_replay_large_records_jumps(lib, seg, walk, monkeypatch):
+    """configs[2]-like payloads (log-uniform 1 B-60 KiB): the walk jumps past its prefetched
+    tile and reads 1 KiB windows at the headers (byte-wise in misaligned segments), and goes
+    back to tiles where records are short."""
+    _walk_env(monkeypatch, walk)
+    lens = synth.loguniform_lengths(17, 900, 1, 60000)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(18, 0, int(lens.sum()) + 16).copy()
+    nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 3
+    wal = np.zeros(nseg * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    want = wal_model.replay(wal.tobytes(), seg)
+    assert want[0] == list(rec)
+    d = torch.from_numpy(wal).cuda()
+    for kw in ({}, {"d_wal": d, "host": False}):
+        got = _replay(lib, wal, seg=seg, **kw)
+        assert got == (list(want[0]), want[1], want[2])
+    for k in (3, len(rec) // 2):
+        got = _replay(lib, wal, start=int(rec[k]), seg=seg)
+        w = wal_model.replay(wal.tobytes(), seg, int(rec[k]))
+        assert got == (list(w[0]), w[1], w[2])
+
+
 @pytest.mark.parametrize("walk", ["split", "split4k"])
 def test_replay_payloads_that_look_like_wal_records(lib, walk, monkeypatch):
     """Payloads that are themselves WAL images (valid header chains inside records): a sub-range
