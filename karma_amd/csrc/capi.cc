@@ -303,6 +303,23 @@ struct Locked {
 }  // namespace
 
 namespace karma::engine {
+int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
+                       uint32_t* d_out, hipStream_t s) {
+    if (n_rec == 0) return KARMA_OK;
+    Locked L;
+    if (L.rc) return L.rc;
+    RaggedArgs a{};
+    a.arena = static_cast<const uint8_t*>(d_arena);
+    a.off = d_off;
+    a.len = d_len;
+    a.n_rec = n_rec;
+    a.init = nullptr;
+    a.init_scalar = 0;
+    a.out = d_out;
+    a.blob = L.ds->blob;
+    KARMA_HIP(launch_ragged_direct(a, L.ds->cu, s));
+    return KARMA_OK;
+}
 namespace {
 thread_local hipEvent_t t_units_start = nullptr, t_units_stop = nullptr;
 }

@@ -429,7 +429,65 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     }
 }
 
+// Batches of small records (WAL replay of short records): one record per group,
+// its whole body one unit, no plan kernels (scan, descriptors and finalize cost
+// more than the CRCs of 180-byte records).  The head and tail byte steps are
+// serial LDS lookups with a per-record trip count, so a wave does them for 64
+// records at once (lane i: record base + i), then streams the 64 bodies in 8
+// rounds of 8 groups, passing each record's entering register in and its body
+// register out by shuffles.  Correct for any length; balanced when every record
+// is small.
+__global__ __launch_bounds__(kBlockThreads) void k_ragged_direct(RaggedArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; base < A.n_rec;
+         base += nwaves * 64) {
+        // lane i: record base + i -- its extent and entering register
+        const uint64_t ri = base + lane;
+        const bool vi = ri < A.n_rec;
+        const uint8_t* pi = vi ? A.arena + A.off[ri] : A.arena;
+        const uint32_t ni = vi ? A.len[ri] : 0u;
+        const uint32_t initi = vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
+        const Geom gi = geom(pi, ni);
+        const bool body = vi && !gi.is_short;
+        const uint32_t hi = body ? head_register(lds, kLZ4, kLT8, pi, gi, initi) : 0u;
+        const uint64_t ai = reinterpret_cast<uintptr_t>(gi.a), bi = reinterpret_cast<uintptr_t>(gi.b);
+        uint32_t Ri = 0;
+#pragma unroll 1
+        for (uint32_t round = 0; round < 8; ++round) {  // 8 records per round, one per group
+            // shuffles with every lane active (a source lane outside EXEC would read as 0)
+            const int src = (int)(round * kGroupsPerWave + grp);
+            const bool has = __shfl((int)body, src) != 0;
+            const uint64_t sa = (uint64_t)__shfl((long long)ai, src), sb = (uint64_t)__shfl((long long)bi, src);
+            const uint32_t sh = __shfl(hi, src);
+            const uint8_t* us = has ? reinterpret_cast<const uint8_t*>((uintptr_t)sa) : nullptr;
+            const uint8_t* ue = has ? reinterpret_cast<const uint8_t*>((uintptr_t)sb) : nullptr;
+            const uint8_t* inj_at = us;
+            const uint32_t inj = has ? sh : 0u;
+            const uint32_t R = group_unit<kRaggedPF, kRaggedNT>(lds, X, l, us, ue, inj_at, inj);
+            const uint32_t Rr = __shfl(R, (int)((lane & 7u) * kGroupLanes));  // group (lane & 7)'s register
+            if (lane / kGroupsPerWave == round) Ri = Rr;
+        }
+        if (vi)
+            A.out[ri] = gi.is_short ? short_record(lds, kLZ4, kLT8, pi, ni, initi) : ~tail_register(lds, kLZ4, kLT8, Ri, gi);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
+    if (a.n_rec == 0) return hipSuccess;
+    units_timer_begin(s);
+    hipLaunchKernelGGL(k_ragged_direct, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    units_timer_end(s);
+    return hipGetLastError();
+}
 
 uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock - 1) / kScanBlock; }
 

@@ -129,20 +129,28 @@ uint64_t ragged_scan_blocks(uint64_t n_rec);
 // fbase[n_rec]), then descriptors, the unit kernel and the per-record finalize.
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s);
+// One record per group, no plan kernels (uses arena, off, len, n_rec, init, out, blob).
+hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s);
+// Library-internal entry (capi.cc) for callers that know every record is small
+// (WAL replay): CRCs of arena[off[r], off[r] + len[r]) with Value's init.
+int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
+                       uint32_t* d_out, hipStream_t s);
 
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {
     uint32_t count;  // type-0 records (candidates) the walk found
     uint32_t kind;   // KARMA_WAL_END / _CORRUPT / _BAD_TYPE
     uint64_t stop;   // WAL offset where the segment's walk stopped (segment end for END)
+    uint32_t max_len;  // an upper bound of the candidates' payload lengths
+    uint32_t pad;
 };
-static_assert(sizeof(WalSegMeta) == 16, "one 16-byte record per segment");
+static_assert(sizeof(WalSegMeta) == 24, "one 24-byte record per segment");
 
 // One sub-range walker's result: where it started (a header it found, or the
 // sub-range end: none), its list length, its stop kind / offset and where it left
 // the sub-range (segment-relative).
 struct WalSubMeta {
-    uint32_t first, count, kind, stop, exit, pad[3];
+    uint32_t first, count, kind, stop, exit, max_len, pad[2];
 };
 struct WalArgs {
     const uint8_t* wal;        // first byte of segment s0 (WAL offset base0)

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -101,6 +102,7 @@ struct DevBuf {
 };
 
 constexpr int kUpThreads = 8;                   // upload workers
+constexpr uint32_t kSmallRecordMax = 1024;      // payloads up to this take the one-record-per-group batch
 constexpr size_t kUpChunk = size_t(8) << 20;    // bytes per staging buffer
 struct ReplayCtx {
     std::mutex mu;
@@ -357,9 +359,11 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
     if (const int rc = c.h_small.ensure(std::max<size_t>(w1 * 8, 64), true)) return rc;
     uint64_t* cb = c.h_small.as<uint64_t>();
     uint64_t n_all = 0;
+    uint32_t max_len = 0;
     for (uint64_t w = 0; w < w1; ++w) {
         cb[w] = n_all;
         n_all += M[w].count;
+        max_len = std::max(max_len, M[w].max_len);
     }
     uint64_t accepted = n_all;
     if (n_all) {
@@ -378,9 +382,14 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
         if (hipMemcpyAsync(c.cbase.p, cb, w1 * 8, hipMemcpyHostToDevice, c.st) != hipSuccess ||
             launch_wal_gather(A, w1, c.st) != hipSuccess)
             return fail(KARMA_E_HIP, "wal_replay: gather");
-        // payload = header + 8: the arena is the image shifted by the header
-        if (const int rc = karma_crc32c_batch_ragged(A.wal + 8, A.off, A.len, n_all, w1 * seg_bytes, nullptr, 0,
-                                                     c.crc.as<uint32_t>(), c.st))
+        // payload = header + 8: the arena is the image shifted by the header.  Small records
+        // only: one record per group, without the ragged plan kernels.
+        const char* sm = getenv("KARMA_WAL_SMALL_MAX");  // tests: force either batch
+        const uint64_t small_max = sm && *sm ? strtoull(sm, nullptr, 10) : kSmallRecordMax;
+        if (const int rc = max_len <= small_max
+                               ? ragged_small_batch(A.wal + 8, A.off, A.len, n_all, c.crc.as<uint32_t>(), c.st)
+                               : karma_crc32c_batch_ragged(A.wal + 8, A.off, A.len, n_all, w1 * seg_bytes, nullptr,
+                                                           0, c.crc.as<uint32_t>(), c.st))
             return rc;
         uint64_t* hb = c.h_small.as<uint64_t>();  // cb was consumed by the H2D above (stream-ordered)
         if (hipMemsetAsync(A.first_bad, 0xff, 8, c.st) != hipSuccess ||

@@ -90,6 +90,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
     // uniform: every thread follows the walker through sh_pos
     uint32_t pos = blockIdx.x == 0 ? (uint32_t)A.first_pos : 0u;
     uint32_t count = 0, kind = 0, stop = seg;  // stop: segment-relative (thread 0's)
+    uint32_t mx = 0;                            // thread 0's largest payload
     uint32_t pend_n = 0, pend_at = 0;          // the list of the previous tile, not yet written out
     int b = 0;
     if ((uint64_t)pos + 8 <= seg) {  // wal.cc:40-45: a shorter rest is skipped (kind 0)
@@ -115,6 +116,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
                         lrec[b][nc] = pos;
                         llen[b][nc] = size;
                         lcrc[b][nc] = crc;
+                        mx = size > mx ? size : mx;
                         ++nc;
                         pos = npos;
                         if (pos > lim || pos >= tend) break;
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
         }
     }
     if (threadIdx.x == 0) {
-        A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg)};
+        A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg), mx, 0u};
         A.span[2 * blockIdx.x] = 0;
         A.span[2 * blockIdx.x + 1] = 0;
     }
@@ -260,6 +262,7 @@ __device__ __forceinline__ void tile_header(const WaveLds& W, uint32_t c, uint32
 
 struct WalkEnd {
     uint32_t count;  // candidates written
+    uint32_t max_len;  // their largest payload
     uint32_t kind;   // KARMA_WAL_CORRUPT / _BAD_TYPE, or 0
     uint32_t stop;   // where kind was found
     uint32_t pos;    // where the walk left off (seg after a type-1 padding record)
@@ -273,12 +276,13 @@ struct WalkEnd {
 __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t pos, uint32_t hi, uint32_t* crec,
                               uint32_t* clen, uint32_t* ccrc, uint64_t cap) {
     const uint32_t seg = S.seg;
-    WalkEnd E{0u, 0u, seg, pos};
+    WalkEnd E{0u, 0u, 0u, seg, pos};
     if ((uint64_t)pos + 8 > seg || pos >= hi) return E;  // wal.cc:40-45: a shorter rest is skipped
     // The list is built in registers, entry i of each run of 64 in lane i, and written
     // out 64 entries at a time (coalesced): no LDS traffic besides the header reads.
     uint32_t myrec = 0, mylen = 0, mycrc = 0, k = 0;
     auto push = [&](uint32_t p, uint32_t n, uint32_t c) {
+        E.max_len = n > E.max_len ? n : E.max_len;
         if (lane == k) {
             myrec = p;
             mylen = n;
@@ -457,11 +461,11 @@ __global__ __launch_bounds__(64) void k_wal_walk_sub(WalArgs A) {
     const WalkEnd E = walk_range(W, S, lane, first, hi, A.cand_rec + slot, A.cand_len + slot, A.cand_crc + slot, A.sub_cap);
     if (lane != 0) return;
     if (P == 1) {
-        A.meta[s] = WalSegMeta{E.count, E.kind, A.base0 + rel + (E.kind ? E.stop : S.seg)};
+        A.meta[s] = WalSegMeta{E.count, E.kind, A.base0 + rel + (E.kind ? E.stop : S.seg), E.max_len, 0u};
         A.span[2 * s] = 0;
         A.span[2 * s + 1] = 0;
     } else {
-        A.sub[blockIdx.x] = WalSubMeta{first, E.count, E.kind, E.stop, E.pos, {0u, 0u, 0u}};
+        A.sub[blockIdx.x] = WalSubMeta{first, E.count, E.kind, E.stop, E.pos, E.max_len, {0u, 0u}};
     }
 }
 
@@ -483,7 +487,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
     uint32_t* clen = A.cand_len + s * A.cand_cap;
     uint32_t* ccrc = A.cand_crc + s * A.cand_cap;
     uint32_t pos = s == 0 ? (uint32_t)A.first_pos : 0u;
-    uint32_t count = 0, kind = 0, stop = seg;
+    uint32_t count = 0, kind = 0, stop = seg, mx = 0;
     WalSubMeta mine{};  // lane l holds walker j0 + l's report: 64 loads at once, not one per step
     for (uint64_t j = 0; j < P; ++j) {
         if (j % 64 == 0 && j + lane < P) mine = M[j + lane];
@@ -498,6 +502,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
             m.kind = __builtin_amdgcn_readlane(mine.kind, src);
             m.stop = __builtin_amdgcn_readlane(mine.stop, src);
             m.exit = __builtin_amdgcn_readlane(mine.exit, src);
+            m.max_len = __builtin_amdgcn_readlane(mine.max_len, src);
             int64_t idx = -1;
             if (m.first == pos) {
                 idx = 0;
@@ -514,6 +519,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
                 st += (uint32_t)idx;
                 n = m.count - (uint32_t)idx;
                 pos = m.exit;
+                mx = m.max_len > mx ? m.max_len : mx;  // of the walker's whole list: an upper bound
                 if (m.kind) {
                     kind = m.kind;
                     stop = m.stop;
@@ -522,6 +528,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
                 const WalkEnd E = walk_range(W, S, lane, pos, hi, crec + st, clen + st, ccrc + st, A.sub_cap);
                 n = E.count;
                 pos = E.pos;
+                mx = E.max_len > mx ? E.max_len : mx;
                 if (E.kind) {
                     kind = E.kind;
                     stop = E.stop;
@@ -534,7 +541,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
         }
         count += n;
     }
-    if (lane == 0) A.meta[s] = WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg)};
+    if (lane == 0) A.meta[s] = WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg), mx, 0u};
 }
 
 // Candidates of segment s0 + blockIdx.x (one block per segment) into the

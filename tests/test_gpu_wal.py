@@ -119,12 +119,13 @@ WALKS = {
     "workgroup": {"KARMA_WALK_VARIANT": "1"},         # k_wal_walk, one workgroup per segment
     "whole": {"KARMA_WALK_SUB": str(1 << 30)},        # k_wal_walk_sub, one walker per segment
     "split": {},                                      # the plan: few segments -> sub-range walkers
-    "split4k": {"KARMA_WALK_SUB": "4096"},            # one-tile sub-ranges + k_wal_resolve
+    "split4k": {"KARMA_WALK_SUB": "4096",             # one-tile sub-ranges + k_wal_resolve,
+                "KARMA_WAL_SMALL_MAX": str(1 << 24)},  # and every batch one record per group
 }
 
 
 def _walk_env(monkeypatch, walk):
-    for k in ("KARMA_WALK_VARIANT", "KARMA_WALK_SUB"):
+    for k in ("KARMA_WALK_VARIANT", "KARMA_WALK_SUB", "KARMA_WAL_SMALL_MAX"):
         monkeypatch.delenv(k, raising=False)
     for k, v in WALKS[walk].items():
         monkeypatch.setenv(k, v)
