@@ -434,7 +434,7 @@ __device__ __forceinline__ void load_comb_tables(uint32_t* lds, const uint32_t* 
     copy_to_lds<WORDS, THREADS>(lds, blob);
 }
 
-// Z_L for L = 16n, 0 < n < 256 (binary decomposition over Z_{16*2^i}).
+// Z_L for L = 16n, 0 < n < 2^kCombSmallMaps (binary decomposition over Z_{16*2^i}).
 __device__ __forceinline__ uint32_t zshift16(const uint32_t* lds, uint32_t x, uint32_t n) {
 #pragma unroll
     for (int i = 0; i < kCombSmallMaps; ++i)

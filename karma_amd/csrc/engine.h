@@ -16,7 +16,7 @@ constexpr int kChunk = 16 * kGroupLanes;       // bytes a group consumes per ste
 constexpr int kBlockThreads = 1024;            // one workgroup per CU
 constexpr int kWavesPerBlock = kBlockThreads / 64;
 constexpr int kGroupsPerWave = 64 / kGroupLanes;
-constexpr uint64_t kDefaultUnit = 4096;        // unit size for ragged batches
+constexpr uint64_t kDefaultUnit = 8192;        // unit size for ragged batches (4 KiB: 1.9 % slower calls, 16 KiB: 3.5 %)
 
 // ---- table blob of the streaming kernel (uint32 words) ---------------------
 constexpr int kBlobStride = 0;     // Z_S slicing tables, 4 x 256
@@ -36,7 +36,7 @@ constexpr int kCombZ4 = kCombMaps * 1024;
 constexpr int kCombT8 = kCombZ4 + 1024;
 constexpr int kCombCoreWords = kCombT8 + 256;  // what the fixed combine and the head steps need
 constexpr int kCombSmall = kCombT8 + 1024;
-constexpr int kCombSmallMaps = 8;
+constexpr int kCombSmallMaps = 9;
 constexpr int kCombWords = kCombSmall + kCombSmallMaps * 1024;
 
 // ---- table blob of the one-block combine (k_combine_block) -----------------
@@ -86,7 +86,7 @@ static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
 // units for balance: all full units first, in record order, then
 // the partial first/last units bucketed by chunk count, longest first, so the
 // 8 units a wave streams together have (nearly) equal length.
-constexpr int kBuckets = 33;  // chunk counts 1..32 of a partial unit (index = chunks)
+constexpr int kBuckets = 65;  // chunk counts 1..64 of a partial unit (index = chunks)
 static_assert(kDefaultUnit / kChunk < kBuckets, "a partial unit has at most unit/kChunk chunks");
 
 struct RaggedArgs {
