@@ -117,7 +117,8 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
                            size_t* h_n_framed, int device);
 
 /* Batched replay (sivir::open's wal::scan_record loop, wal.cc:34-87) from WAL offset
- * `start`, entirely on the device: segment-parallel header walk, all payload CRCs in one
+ * `start`, entirely on the device: segment-parallel header walk (sub-range walkers
+ * stitched along the real chain when there are few segments), all payload CRCs in one
  * GPU batch, first mismatch.  The image is d_wal when the caller already holds a device
  * copy (h_wal may then be NULL), else h_wal is streamed into HBM (pinned staging, no
  * page-locking of the caller's buffer).  seg_bytes < 2^31.
