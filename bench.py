@@ -203,7 +203,7 @@ def wal_bench(args, L, rank):
 
     append()
     step = append if args.workload == "wal_append" else replay
-    dev_rate = None
+    dev_rate = dir_rate = None
     if args.workload == "wal_replay":  # the same replay over a copy already in HBM (no upload)
         import torch
         d_wal = torch.from_numpy(wal).to(torch.device("cuda", local))
@@ -220,6 +220,30 @@ def wal_bench(args, L, rank):
             replay_dev()
         dev_rate = payload / ((time.perf_counter() - t0) / args.steps) / GIB
         del d_wal
+        # the same replay from segment files named by their WAL offsets (karma_wal_replay_dir),
+        # page-cached: the files are read straight into the pinned staging buffers
+        import shutil
+        import tempfile
+        tmp = tempfile.mkdtemp(prefix="karma_wal_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        try:
+            for i in range(wal_bytes // seg):
+                wal[i * seg:(i + 1) * seg].tofile(os.path.join(tmp, str(i * seg)))
+            base = ctypes.c_uint64()
+
+            def replay_dir():
+                _lib.check("wal_replay_dir", L.karma_wal_replay_dir(tmp.encode(), seg, 0, ctypes.byref(base),
+                                                                    ctypes.byref(nrec), ctypes.byref(stop),
+                                                                    ctypes.byref(status), None, 0, local))
+                assert nrec.value == n
+
+            for _ in range(args.warmup):
+                replay_dir()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                replay_dir()
+            dir_rate = payload / ((time.perf_counter() - t0) / args.steps) / GIB
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
     for _ in range(args.warmup):
         step()
     t0 = time.perf_counter()
@@ -233,6 +257,7 @@ def wal_bench(args, L, rank):
            "vs_baseline": None, "dtype": "u8", "data": "synthetic splitmix64 payloads in pageable host memory",
            "records_per_s": round(n / dt, 1),
            "device_resident_value": round(dev_rate, 3) if dev_rate is not None else None,
+           "segment_files_value": round(dir_rate, 3) if dir_rate is not None else None,
            "config": {"workload": f"{mix} WAL records, 1 MiB segments, "
                                   f"{'karma_wal_append_batch' if step is append else 'karma_wal_replay'} "
                                   f"(BASELINE {'configs[0]' if size else 'configs[2]'} records)", "records": n,

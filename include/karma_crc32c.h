@@ -16,6 +16,7 @@
  *   karma_crc32c_*_sharded / gather the same, records sharded over GPUs, CRCs gathered over RCCL
  *   karma_wal_append_batch          sivir::build_sqe + segment_file::append_record   sivir.cc:276-317
  *   karma_wal_replay                sivir::open's wal::scan_record loop              sivir.cc:31-41, wal.cc:34-87
+ *   karma_wal_replay_dir            wal::load_from_path + the same loop              wal.cc:9-27
  *   karma_kfp_encode_batch          transport::frame::encode                         frame.cc:41-60
  *   karma_kfp_parse_batch           connection::read_frame's frame::parse loop       connection.cc:20-27, frame.cc:62-130
  *
@@ -41,6 +42,7 @@ extern "C" {
 #define KARMA_E_HIP (-3)        /* a HIP runtime call failed */
 #define KARMA_E_NOMEM (-4)      /* device or host allocation failed */
 #define KARMA_E_RCCL (-5)       /* an RCCL call failed */
+#define KARMA_E_IO (-6)         /* reading a file failed (karma_wal_replay_dir) */
 
 typedef void* karma_stream_t;         /* hipStream_t */
 typedef struct karma_comm* karma_comm_t;
@@ -129,6 +131,16 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
 int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                      int device);
+
+/* Replay of a segment directory (wal::load_from_path + sivir::open, wal.cc:9-27): the
+ * regular files of `dir` named by the decimal WAL offset of their first byte, equal
+ * sizes (seg_bytes, or 0 = the first file's size), no gaps.  The files are read by the
+ * staging threads straight into pinned buffers and streamed into HBM; then the same
+ * device replay as karma_wal_replay.  `start`, *h_stop and h_rec_off are WAL offsets;
+ * *h_base = the first segment's offset.  An empty directory replays nothing (END).
+ * KARMA_E_IO when a file cannot be opened or read. */
+int karma_wal_replay_dir(const char* dir, size_t seg_bytes, uint64_t start, uint64_t* h_base, uint64_t* h_n_records,
+                         uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap, int device);
 
 /* ---- KFP frames (karma-transport) ------------------------------------------
  * Frame (frame.cc:29-60): [frame_length u32][magic u8 = 123][operation_code i16][flag u8]

@@ -18,6 +18,7 @@ KARMA_E_NO_DEVICE = -2
 KARMA_E_HIP = -3
 KARMA_E_NOMEM = -4
 KARMA_E_RCCL = -5
+KARMA_E_IO = -6
 UNIQUE_ID_BYTES = 128
 
 _c = ctypes
@@ -44,6 +45,8 @@ SIGNATURES = {
     "karma_wal_append_batch": (_i, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, _c.POINTER(_u64), _vp, _c.POINTER(_sz), _i]),
     "karma_wal_replay": (_i, [_vp, _vp, _sz, _sz, _u64, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_i), _vp, _sz,
                               _i]),
+    "karma_wal_replay_dir": (_i, [_c.c_char_p, _sz, _u64, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_u64),
+                                  _c.POINTER(_i), _vp, _sz, _i]),
     "karma_kfp_encode_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _c.POINTER(_sz),
                                     _c.POINTER(_u64), _i]),
     "karma_kfp_parse_batch": (_i, [_vp, _vp, _sz, _sz, _vp, _c.POINTER(_sz), _c.POINTER(_u64), _c.POINTER(_i), _i]),

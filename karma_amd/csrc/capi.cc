@@ -347,6 +347,7 @@ const char* karma_crc32c_strerror(int status) {
         case KARMA_E_HIP: return "HIP runtime error";
         case KARMA_E_NOMEM: return "out of memory";
         case KARMA_E_RCCL: return "RCCL error";
+        case KARMA_E_IO: return "file I/O error";
         default: return "unknown status";
     }
 }

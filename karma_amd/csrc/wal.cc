@@ -22,11 +22,16 @@
 //   word just read (wal.cc:50-60).  It is load-bearing: it is what ends replay
 //   at the zero-filled, never-written part of the last segment.
 #include <hip/hip_runtime_api.h>
+#include <unistd.h>
+#include <sys/stat.h>
+#include <fcntl.h>
+#include <dirent.h>
 
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -71,6 +76,7 @@ void parallel_for(uint64_t lo, uint64_t hi, uint64_t grain, F&& body) {
 }
 
 int fail(int code, const char* what) { return karma::engine::set_last_error(code, what); }
+int fail(int code, const std::string& what) { return karma::engine::set_last_error(code, what); }
 
 // Per-device replay context: a stream, the device image buffer (host images
 // are streamed into it), the walk's candidate tables, the contiguous lists and
@@ -143,7 +149,12 @@ ReplayCtx& replay_ctx(int dev) {
 // copies chunks t, t + T, ... into its two pinned staging buffers (alternating)
 // and DMAs each one on its own stream, so the memcpy of one chunk overlaps the
 // DMA of the previous and T copies run at once.
-int upload_staged(ReplayCtx& c, void* d_dst, const uint8_t* h_src, size_t bytes, int dev) {
+// Fills dst with image bytes [off, off + n) (offsets relative to the image start).
+using ImageFill = std::function<int(uint8_t* dst, uint64_t off, size_t n)>;
+
+// Streams image bytes [src_off, src_off + bytes) into d_dst through the pinned staging
+// buffers: kUpThreads threads each fill one buffer (fill) while the other's DMA runs.
+int upload_staged(ReplayCtx& c, void* d_dst, const ImageFill& fill, uint64_t src_off, size_t bytes, int dev) {
     const size_t nchunk = (bytes + kUpChunk - 1) / kUpChunk;
     const int nthr = (int)std::min<size_t>(kUpThreads, std::max<size_t>(1, nchunk));
     for (int t = 0; t < nthr; ++t)
@@ -164,7 +175,10 @@ int upload_staged(ReplayCtx& c, void* d_dst, const uint8_t* h_src, size_t bytes,
                     rcs[t] = KARMA_E_HIP;
                     return;
                 }
-                std::memcpy(c.stage[t][k].p, h_src + o, n);
+                if (const int rc = fill(static_cast<uint8_t*>(c.stage[t][k].p), src_off + o, n)) {
+                    rcs[t] = rc;
+                    return;
+                }
                 if (hipMemcpyAsync(static_cast<uint8_t*>(d_dst) + o, c.stage[t][k].p, n, hipMemcpyHostToDevice,
                                    c.up_st[t]) != hipSuccess ||
                     hipEventRecord(c.up_ev[t][k], c.up_st[t]) != hipSuccess) {
@@ -176,9 +190,13 @@ int upload_staged(ReplayCtx& c, void* d_dst, const uint8_t* h_src, size_t bytes,
         });
     for (auto& x : th) x.join();
     for (int rc : rcs)
-        if (rc) return fail(rc, "wal_replay: image upload");
+        if (rc) return rc == KARMA_E_IO ? rc : fail(rc, "wal_replay: image upload");
     return 0;
 }
+
+int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
+                uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
+                int device);
 
 }  // namespace
 
@@ -286,6 +304,24 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
     if ((!h_wal && !d_wal) || !h_n_records || !h_stop || !h_status || seg_bytes < 1 || wal_bytes % seg_bytes ||
         start > wal_bytes || seg_bytes >= (uint64_t(1) << 31))
         return fail(KARMA_E_INVALID, "wal_replay");
+    const uint8_t* src = static_cast<const uint8_t*>(h_wal);
+    const ImageFill copy = [src](uint8_t* dst, uint64_t off, size_t n) {
+        std::memcpy(dst, src + off, n);
+        return 0;
+    };
+    return replay_core(static_cast<const uint8_t*>(d_wal), d_wal ? nullptr : &copy, wal_bytes, seg_bytes, start,
+                       h_n_records, h_stop, h_status, h_rec_off, rec_cap, device);
+}
+
+}  // extern "C"
+
+namespace {
+
+// The replay proper (karma_wal_replay): the image is d_wal, or produced by fill and
+// streamed into HBM.  Offsets in and out are relative to the image start.
+int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
+                uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
+                int device) {
     using namespace karma::engine;
     const uint64_t nseg = wal_bytes / seg_bytes;
     const uint64_t s0 = std::min<uint64_t>(start / seg_bytes, nseg);
@@ -312,8 +348,7 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
         A.wal = static_cast<const uint8_t*>(d_wal) + base0;
     } else {
         if (const int rc = c.img.ensure(img_bytes)) return rc;
-        if (const int rc = upload_staged(c, c.img.p, static_cast<const uint8_t*>(h_wal) + base0, img_bytes, dev))
-            return rc;
+        if (const int rc = upload_staged(c, c.img.p, *fill, base0, img_bytes, dev)) return rc;
         A.wal = c.img.as<const uint8_t>();
         T.mark("image upload");
     }
@@ -416,6 +451,89 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
     *h_n_records = accepted;
     *h_stop = end;
     *h_status = status;
+    return 0;
+}
+
+}  // namespace
+
+
+extern "C" {
+
+int karma_wal_replay_dir(const char* dir, size_t seg_bytes, uint64_t start, uint64_t* h_base, uint64_t* h_n_records,
+                         uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap, int device) {
+    if (!dir || !h_base || !h_n_records || !h_stop || !h_status) return fail(KARMA_E_INVALID, "wal_replay_dir");
+    // wal::load_from_path (wal.cc:9-27): the regular files of the directory, each named by
+    // the decimal WAL offset of its first byte, in offset order
+    struct Seg {
+        uint64_t off, size;
+        std::string path;
+    };
+    std::vector<Seg> segs;
+    DIR* d = opendir(dir);
+    if (!d) return fail(KARMA_E_IO, std::string("wal_replay_dir: cannot open ") + dir);
+    while (const dirent* e = readdir(d)) {
+        const std::string name = e->d_name;
+        if (name.empty() || name.find_first_not_of("0123456789") != std::string::npos) continue;
+        const std::string path = std::string(dir) + "/" + name;
+        struct stat st;
+        if (stat(path.c_str(), &st) != 0 || !S_ISREG(st.st_mode)) continue;
+        segs.push_back(Seg{std::strtoull(name.c_str(), nullptr, 10), (uint64_t)st.st_size, path});
+    }
+    closedir(d);
+    std::sort(segs.begin(), segs.end(), [](const Seg& a, const Seg& b) { return a.off < b.off; });
+    if (segs.empty()) {
+        *h_base = 0;
+        *h_n_records = 0;
+        *h_stop = start;
+        *h_status = KARMA_WAL_END;
+        return 0;
+    }
+    if (!seg_bytes) seg_bytes = segs[0].size;
+    const uint64_t base = segs[0].off;
+    for (size_t i = 0; i < segs.size(); ++i)  // one image: equal sizes, no gaps
+        if (segs[i].size != seg_bytes || segs[i].off != base + i * seg_bytes)
+            return fail(KARMA_E_INVALID, "wal_replay_dir: segment files must have equal sizes and no gaps: " +
+                                             segs[i].path);
+    const uint64_t wal_bytes = segs.size() * seg_bytes;
+    if (start < base || start > base + wal_bytes || seg_bytes >= (uint64_t(1) << 31))
+        return fail(KARMA_E_INVALID, "wal_replay_dir: start outside the segments");
+    std::vector<int> fds(segs.size(), -1);
+    auto close_all = [&] {
+        for (int fd : fds)
+            if (fd >= 0) ::close(fd);
+    };
+    for (size_t i = 0; i < segs.size(); ++i)
+        if ((fds[i] = ::open(segs[i].path.c_str(), O_RDONLY)) < 0) {
+            close_all();
+            return fail(KARMA_E_IO, "wal_replay_dir: cannot open " + segs[i].path);
+        }
+    // the staging threads read the files straight into the pinned buffers
+    const ImageFill read_files = [&](uint8_t* dst, uint64_t off, size_t n) {
+        while (n) {
+            const uint64_t f = off / seg_bytes, in = off - f * seg_bytes;
+            const size_t take = std::min<uint64_t>(n, seg_bytes - in);
+            size_t got = 0;
+            while (got < take) {
+                const ssize_t r = ::pread(fds[f], dst + got, take - got, (off_t)(in + got));
+                if (r <= 0) return fail(KARMA_E_IO, "wal_replay_dir: short read of " + segs[f].path);
+                got += (size_t)r;
+            }
+            dst += take;
+            off += take;
+            n -= take;
+        }
+        return 0;
+    };
+    const int rc = replay_core(nullptr, &read_files, wal_bytes, seg_bytes, start - base, h_n_records, h_stop, h_status,
+                               h_rec_off, rec_cap, device);
+    close_all();
+    if (rc) return rc;
+    *h_base = base;
+    *h_stop += base;
+    if (h_rec_off) {
+        const uint64_t k = std::min<uint64_t>(*h_n_records, rec_cap);
+        for (uint64_t i = 0; i < k; ++i) h_rec_off[i] += base;
+    }
     return 0;
 }
 

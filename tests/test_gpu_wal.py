@@ -238,3 +238,30 @@ def test_replay_empty_and_start_at_end(lib):
     want = wal_model.replay(wal.tobytes(), SEG)
     assert got == (list(want[0]), want[1], want[2])
     assert _replay(lib, wal, start=wal.nbytes) == ([], wal.nbytes, wal_model.END)
+
+
+def test_replay_dir_matches_image_replay(lib, tmp_path):
+    """Segment files on disk, named by their WAL offsets (wal::load_from_path): replay of the
+    directory equals replay of the image, with WAL offsets shifted by the first segment's."""
+    seg = 64 << 10
+    src, offs, lens = _payloads(41, 3000, 1, 2000)
+    nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 2
+    wal = np.zeros(nseg * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    first = 7 * seg  # the directory's WAL starts at offset 7 segments (older segments deleted)
+    for i in range(nseg):
+        (tmp_path / str(first + i * seg)).write_bytes(wal[i * seg:(i + 1) * seg].tobytes())
+    (tmp_path / "LOCK").write_bytes(b"")  # not a segment
+    want = wal_model.replay(wal.tobytes(), seg)
+    for start in (0, int(rec[100]), int(rec[2000])):
+        w = wal_model.replay(wal.tobytes(), seg, start)
+        base, n, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        got = np.zeros(wal.nbytes // 8, np.uint64)
+        _lib.check("karma_wal_replay_dir",
+                   lib.karma_wal_replay_dir(str(tmp_path).encode(), 0, first + start, ctypes.byref(base),
+                                            ctypes.byref(n), ctypes.byref(stop), ctypes.byref(status), got.ctypes.data,
+                                            got.size, 0))
+        assert base.value == first
+        assert [int(x) - first for x in got[: n.value]] == list(w[0])
+        assert (stop.value - first, status.value) == (w[1], w[2])
+    assert want[0] == list(rec)

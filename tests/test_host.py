@@ -181,3 +181,40 @@ def test_wal_and_kfp_host_logic_without_gpu(karma_lib):
     # invalid geometry is rejected before any device work
     assert karma_lib.karma_wal_replay(wal.ctypes.data, None, wal.nbytes, 3000, 0, ctypes.byref(nr),
                                       ctypes.byref(stop), ctypes.byref(status), None, 0, -1) == _lib.KARMA_E_INVALID
+
+
+def test_wal_replay_dir_host_logic(karma_lib, tmp_path):
+    """karma_wal_replay_dir's directory handling (wal::load_from_path, wal.cc:9-27) runs before any
+    device work: files named by their decimal WAL offset, equal sizes, no gaps."""
+    u64, i32 = ctypes.c_uint64, ctypes.c_int
+    base, nr, stop, status = u64(), u64(), u64(), i32()
+
+    def call(d, seg=0, start=0):
+        return karma_lib.karma_wal_replay_dir(str(d).encode(), seg, start, ctypes.byref(base), ctypes.byref(nr),
+                                              ctypes.byref(stop), ctypes.byref(status), None, 0, -1)
+
+    assert call(tmp_path / "missing") == _lib.KARMA_E_IO
+    empty = tmp_path / "empty"
+    empty.mkdir()
+    (empty / "not-a-segment").write_bytes(b"x")  # ignored: not a decimal name
+    assert call(empty, start=7) == 0 and (nr.value, stop.value, status.value) == (0, 7, 0)
+    seg = 4096
+    ok = tmp_path / "ok"
+    ok.mkdir()
+    for off in (3 * seg, 4 * seg):
+        (ok / str(off)).write_bytes(bytes(seg))
+    (ok / "99").mkdir()  # a directory with a decimal name is not a segment
+    assert call(ok, start=0) == _lib.KARMA_E_INVALID  # start before the first segment
+    assert call(ok, start=3 * seg) == _lib.KARMA_E_NO_DEVICE  # valid: the walk needs the device
+    assert call(ok, seg=seg, start=3 * seg) == _lib.KARMA_E_NO_DEVICE
+    gap = tmp_path / "gap"
+    gap.mkdir()
+    for off in (0, 2 * seg):
+        (gap / str(off)).write_bytes(bytes(seg))
+    assert call(gap) == _lib.KARMA_E_INVALID
+    sizes = tmp_path / "sizes"
+    sizes.mkdir()
+    (sizes / "0").write_bytes(bytes(seg))
+    (sizes / str(seg)).write_bytes(bytes(seg // 2))
+    assert call(sizes) == _lib.KARMA_E_INVALID
+    assert karma_lib.karma_crc32c_strerror(_lib.KARMA_E_IO) == b"file I/O error"
