@@ -21,3 +21,4 @@ from .crc32c import (  # noqa: F401
     value_batch_fixed_host,
 )
 from ._lib import KarmaError, KarmaUnavailable, LIB_PATH  # noqa: F401
+from . import wal  # noqa: F401  (WAL append / replay and KFP frames: karma_amd.wal)

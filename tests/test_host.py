@@ -218,3 +218,17 @@ def test_wal_replay_dir_host_logic(karma_lib, tmp_path):
     (sizes / str(seg)).write_bytes(bytes(seg // 2))
     assert call(sizes) == _lib.KARMA_E_INVALID
     assert karma_lib.karma_crc32c_strerror(_lib.KARMA_E_IO) == b"file I/O error"
+
+
+def test_python_wal_api_refuses_without_gpu():
+    """karma_amd.wal raises on device work without a GPU (no CPU fallback); replay from the end
+    of an image needs none."""
+    import numpy as np
+
+    from karma_amd import wal as W
+    img = np.zeros(2 * 4096, np.uint8)
+    r = W.replay(img, 4096, start=img.nbytes)
+    assert (len(r.records), r.stop, r.status) == (0, img.nbytes, W.END)
+    with pytest.raises(K.KarmaError) as e:
+        W.replay(img, 4096)
+    assert e.value.status == _lib.KARMA_E_NO_DEVICE
