@@ -265,3 +265,36 @@ def test_replay_dir_matches_image_replay(lib, tmp_path):
         assert [int(x) - first for x in got[: n.value]] == list(w[0])
         assert (stop.value - first, status.value) == (w[1], w[2])
     assert want[0] == list(rec)
+
+
+@pytest.mark.parametrize("walk", ["split", "whole"])
+def test_replay_exact_fills_tiny_tails_and_max_records(lib, walk, monkeypatch):
+    """Records that fill a segment exactly, segment tails of 0-9 bytes (shorter than a header:
+    '0' bytes, no footer), and a payload of 2^24 - 1 bytes (the 3-byte size field's maximum) in
+    32 MiB segments.  (A size-0 record ends replay: the reference's stale-word quirk, tested in
+    test_replay_stops_where_scan_record_does.)"""
+    _walk_env(monkeypatch, walk)
+    seg = 4096
+    lens = []
+    for tail in range(10):  # first record leaves `tail` bytes after a second one
+        a = 2000
+        lens += [a, seg - 8 - a - 8 - tail]
+    lens += [seg - 8, 1, 7, seg - 8]
+    lens = np.array(lens, np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(61, 0, int(lens.sum()) + 16).copy()
+    wal = np.zeros(40 * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    want = wal_model.replay(wal.tobytes(), seg)
+    assert want[0] == list(rec)
+    assert _replay(lib, wal, seg=seg) == (list(want[0]), want[1], want[2])
+    # the largest record the format can hold
+    seg = 32 << 20
+    lens = np.array([(1 << 24) - 1, 5, 1, 100000], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(62, 0, int(lens.sum()) + 16).copy()
+    wal = np.zeros(2 * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    want = wal_model.replay(wal.tobytes(), seg)
+    assert want[0] == list(rec) and len(rec) == 4
+    assert _replay(lib, wal, seg=seg) == (list(want[0]), want[1], want[2])
