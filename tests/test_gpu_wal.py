@@ -298,3 +298,43 @@ def test_replay_exact_fills_tiny_tails_and_max_records(lib, walk, monkeypatch):
     want = wal_model.replay(wal.tobytes(), seg)
     assert want[0] == list(rec) and len(rec) == 4
     assert _replay(lib, wal, seg=seg) == (list(want[0]), want[1], want[2])
+
+
+def test_replay_randomized_against_model(lib, monkeypatch):
+    """Random images: segment sizes, record-size mixes (tiny, medium, large, WAL-looking payloads),
+    a random corruption, a random start; every walk kernel and sub-range size against the model."""
+    rng = np.random.default_rng(2024)
+    inner = np.zeros(64 << 10, np.uint8)
+    isrc, ioffs, ilens = _payloads(71, 600, 1, 100)
+    _append(lib, isrc, ioffs, ilens, inner, seg=64 << 10)
+    for case in range(12):
+        seg = int(rng.choice([4096, 16384 + 4, 65536, 262144, 1 << 20]))
+        mix = case % 4
+        n = int(rng.integers(200, 3000))
+        if mix == 0:
+            lens = rng.integers(1, 64, n)
+        elif mix == 1:
+            lens = rng.integers(1, min(4000, seg - 8), n)
+        elif mix == 2:
+            lens = np.minimum(synth.loguniform_lengths(case, n, 1, 60000), seg - 8)
+        else:
+            lens = rng.integers(100, min(6000, seg - 8), n)
+        lens = lens.astype(np.uint32)
+        if mix == 3:  # payloads cut from a WAL image: header chains inside records
+            src = np.concatenate([inner[int(rng.integers(0, 2048)):][: int(x)] if x <= inner.size - 2048 else
+                                  rng.integers(0, 256, int(x), dtype=np.uint8) for x in lens] + [np.zeros(16, np.uint8)])
+        else:
+            src = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+        offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+        nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 3
+        wal = np.zeros(nseg * seg, np.uint8)
+        cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+        if case % 3 == 1 and len(rec) > 10:  # a flipped payload or length byte somewhere
+            k = int(rng.integers(1, len(rec)))
+            wal[int(rec[k]) + int(rng.choice([5, 8]))] ^= 0x10
+        start = int(rec[int(rng.integers(0, len(rec)))]) if case % 2 and len(rec) else 0
+        want = wal_model.replay(wal.tobytes(), seg, start)
+        for walk in ("whole", "split", "split4k"):
+            _walk_env(monkeypatch, walk)
+            got = _replay(lib, wal, start=start, seg=seg)
+            assert got == (list(want[0]), want[1], want[2]), (case, walk, seg, mix)
