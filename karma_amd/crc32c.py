@@ -20,6 +20,7 @@ without the built library they raise; they never compute on the CPU.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Union
 
 from . import _lib
@@ -114,10 +115,16 @@ def _init_args(init, n_rec: int):
     return init.data_ptr(), 0, init
 
 
+_POISON = os.environ.get("KARMA_POISON_OUT") is not None  # tests: no stale CRCs in fresh outputs
+
+
 def _out_tensor(out, n: int, device):
     torch = _torch()
     if out is None:
-        return torch.empty(n, dtype=torch.uint32, device=device)
+        t = torch.empty(n, dtype=torch.uint32, device=device)
+        if _POISON:  # a kernel that skipped a record must not inherit a right answer
+            t.fill_(0xA5A5A5A5)
+        return t
     _require_cuda(out, "out")
     if out.numel() < n or out.element_size() != 4:
         raise ValueError("out must hold n 32-bit values")
