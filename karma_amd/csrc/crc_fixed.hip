@@ -68,9 +68,10 @@ __device__ __forceinline__ FixedPlan fixed_plan(const FixedArgs& A, uint64_t u, 
 // a wave hold units 8i..8i+7 of one record, end-aligned; a 3-level tree over
 // the groups (Z_U, Z_2U, Z_4U) leaves one state per 8 units, so the combine
 // kernels start one level up (a 64 MiB segment: 32768 -> 4096 states here).
-template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0>
+template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0, bool BAL = true>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[WAVE_COMB ? kLdsWordsComb : kLdsWords];
+    __shared__ uint32_t blk_next;  // BAL: the block's next wave-step (an LDS counter, lgkmcnt only)
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & (kGroupLanes - 1);
     const uint32_t grp = lane / kGroupLanes;
@@ -81,6 +82,14 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     const uint64_t step = nwaves * kGroupsPerWave;
     uint64_t wb = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     uint64_t u = wb * kGroupsPerWave + grp;
+    // BAL: the block owns wave-steps b*16 + j + r*nwaves (j < 16, r < rounds) and its 16 waves
+    // take them in that order from an LDS counter, so a wave that the CU's memory pipe serves
+    // faster does more of them (static: the waves of one CU ended up to 60 us apart;
+    // 128 GiB slice 19.81 vs 20.69 ms).
+    const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
+    const uint32_t nidx = (uint32_t)((nws + nwaves - 1) / nwaves) * kWavesPerBlock;
+    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
+    if (BAL && threadIdx.x == 0) blk_next = kWavesPerBlock;  // steps 0..15 go to waves 0..15
     // unit u's head block and init value, then its chunk loads, then the tables
     FixedPlan P = fixed_plan(A, u, U, l);
     u32x4 hv = ld16(P.hblk), tv = ld16(P.tblk);
@@ -90,7 +99,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     load_stream_tables(lds, A.blob);
     if constexpr (WAVE_COMB) copy_to_lds<3 * 1024, kBlockThreads>(lds + kCombLdsBase, A.comb_maps);
     __syncthreads();
-    for (; wb * kGroupsPerWave < U; wb += nwaves, u += step) {
+    for (; wb < nws; ) {
         uint32_t inj = 0;
         if (P.inj_at) inj = P.hfrom < 16 ? steps_in_vec(lds, kLZ4, kLT8, ~iv, hv, P.hfrom, 16u) : ~iv;
         // Every load is issued ahead of unit boundaries, with the next unit's
@@ -98,8 +107,15 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
         // its first batch: vmcnt counts in order).
         const u32x4 tcur = tv;
         FixedPlan N;
+        uint64_t wb_next = wb + nwaves;
         uint32_t R = stream_unit<PF, NT, MODE>(lds, X, l, P.L, Ld, P.inj_at, inj, [&](UnitLoads<PF>& nx) {
-            N = fixed_plan(A, u + step, U, l);
+            if constexpr (BAL) {
+                uint32_t i = 0;
+                if (lane == 0) i = atomicAdd(&blk_next, 1u);
+                i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
+                wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
+            }
+            N = fixed_plan(A, wb_next * kGroupsPerWave + grp, U, l);
             hv = ld16(N.hblk);
             tv = ld16(N.tblk);
             if constexpr (HAS_INIT) iv = *(const __attribute__((address_space(1))) uint32_t*)(A.init + N.r);
@@ -120,6 +136,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
                 A.partial[u] = R;
         }
         P = N;
+        wb = wb_next;
+        u = wb * kGroupsPerWave + grp;
     }
 }
 
@@ -275,7 +293,10 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     // Records of < 31 bytes may hold no aligned 16-byte block.  Units under 2 KiB:
     // the pipelined kernel's extra per-unit work outweighs its hidden latency
     // (1 KiB units: 0.700 vs 0.669 ms per 4 GiB; 4 KiB: 0.628 vs 0.641).
-    if (a.comb_maps) {  // k % 8 == 0, units >= 2 KiB (planner)
+    if (a.comb_maps && fixed_variant() == 7) {  // static wave-steps (A/B only)
+        if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true, 0, false>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_units_fixed<4, true, false, true, 0, false>), grid, blk, 0, s, a);
+    } else if (a.comb_maps) {  // k % 8 == 0, units >= 2 KiB (planner)
         if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true>), grid, blk, 0, s, a);
         else hipLaunchKernelGGL((k_units_fixed<4, true, false, true>), grid, blk, 0, s, a);
     } else if (a.rec_bytes < 31 || a.unit_bytes < 2048) {
@@ -288,6 +309,7 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
                 else hipLaunchKernelGGL((k_units_fixed<2, true, false, false>), grid, blk, 0, s, a);
                 break;
             case 6: hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 1>), grid, blk, 0, s, a); break;  // timing only
+            case 7: hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, false>), grid, blk, 0, s, a); break;  // static
             default:
                 if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false>), grid, blk, 0, s, a);
                 else hipLaunchKernelGGL((k_units_fixed<4, true, false, false>), grid, blk, 0, s, a);

@@ -14,7 +14,7 @@ import karma_amd as K  # noqa: E402
 
 variants = [int(v) for v in sys.argv[1:]] or [0, 1, 2, 6]
 dev = torch.device("cuda:0")
-n, rec = 1 << 20, 4096
+n, rec = int(os.environ.get("NREC", 1 << 20)), int(os.environ.get("REC", 4096))  # config 4: NREC=64 REC=67108864
 MIS = int(os.environ.get("MISALIGN", "0"))  # byte offset of the arena (alignment experiments)
 raw = torch.empty(n * rec + 256, dtype=torch.uint8, device=dev)
 K.fill_splitmix64(raw, 42)
