@@ -306,8 +306,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs 
 // (group_unit), the next descriptor is in flight meanwhile.  On config 3 it
 // measures 1% faster than k_units_ragged_pipe, unlike the
 // fixed layout, where the pipelined form wins 2.7%.
+template <bool BAL = true>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    __shared__ uint32_t blk_next;  // BAL: the block's next wave-step (an LDS counter)
+    if (BAL && threadIdx.x == 0) blk_next = kWavesPerBlock;
     load_stream_tables(lds, A.blob);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -317,17 +320,31 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     const uint64_t U_all = A.fbase[A.n_rec];
     const uint64_t U = U_all < A.unit_cap ? U_all : A.unit_cap;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t step = nwaves * kGroupsPerWave;
-    uint64_t wb = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    // BAL: as k_units_fixed, the block's wave-steps b*16 + j + r*nwaves are taken in order from
+    // an LDS counter, one step ahead (the next descriptor is loaded while a unit streams).
+    const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
+    const uint32_t nidx = (uint32_t)((nws + nwaves - 1) / nwaves) * kWavesPerBlock;
+    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
+    uint64_t wb = bw0 + (threadIdx.x >> 6);
     uint64_t u = wb * kGroupsPerWave + grp;
     UnitDesc d = u < U ? load_desc(A.desc + u) : UnitDesc{0, 0, 0};
-    for (; wb * kGroupsPerWave < U; wb += nwaves, u += step) {
+    while (wb < nws) {
         const UnitDesc cur = d;
         const bool valid = u < U;
-        d = u + step < U ? load_desc(A.desc + u + step) : UnitDesc{0, 0, 0};
+        uint64_t wb_next = wb + nwaves;
+        if constexpr (BAL) {
+            uint32_t i = 0;
+            if (lane == 0) i = atomicAdd(&blk_next, 1u);
+            i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
+            wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
+        }
+        const uint64_t un = wb_next * kGroupsPerWave + grp;
+        d = un < U ? load_desc(A.desc + un) : UnitDesc{0, 0, 0};
         const uint8_t* us = reinterpret_cast<const uint8_t*>(cur.us);
         const uint32_t R = group_unit<kRaggedPF, kRaggedNT>(lds, X, l, us, us + cur.span, us, cur.inj);
         if (valid && l == 0) A.partial[u] = R;
+        wb = wb_next;
+        u = un;
     }
 }
 
@@ -506,8 +523,10 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     units_timer_begin(s);
     if (ragged_variant() == 1)
         hipLaunchKernelGGL(k_units_ragged_pipe, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (ragged_variant() == 2)  // static wave-steps (A/B only)
+        hipLaunchKernelGGL(k_units_ragged<false>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else
-        hipLaunchKernelGGL(k_units_ragged, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+        hipLaunchKernelGGL(k_units_ragged<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
     const uint64_t cap = 2 * (uint64_t)grid_blocks;
