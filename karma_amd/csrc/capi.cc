@@ -6,6 +6,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -145,14 +146,35 @@ int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocate
 }
 
 // ---- fixed-size records ---------------------------------------------------
+// Largest in-wave split of a big batch's records (2, 4 or 8; KARMA_FOLD_MAX_K, 1 = off: A/B).
+uint64_t fold_max_k() {
+    const char* e = getenv("KARMA_FOLD_MAX_K");
+    const long v = e ? atol(e) : 2;
+    return v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
+}
+
 int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, size_t n_rec, const uint32_t* d_init,
                  uint32_t init, uint32_t* d_out, hipStream_t s) {
     const uint64_t groups = (uint64_t)ds.cu * kWavesPerBlock * kGroupsPerWave;
     const uint64_t target = kOverdecompose * groups;
     uint64_t unit, k;
+    uint32_t fold_k = 0;
     if (rec_bytes <= (size_t)kChunk || n_rec >= target) {
         unit = round_up(std::max<uint64_t>(rec_bytes, 1), kChunk);
         k = 1;
+        // Batches that fill the GPU: records of >= 2 split units are cut into 2, 4 or 8 units
+        // whose groups sit in one wave (folded there, no combine launch).  Finer wave-steps
+        // balance the CU's waves better: 1M x 4 KiB as 2M x 2 KiB units, DESIGN.md §4.
+        const uint64_t max_k = fold_max_k();
+        for (uint64_t kw = max_k; kw >= 2 && n_rec >= target; kw /= 2) {
+            const uint64_t u = round_up(ceil_div(rec_bytes, kw), kChunk);
+            if (u >= kMinSplitUnit) {
+                unit = u;
+                k = kw;
+                fold_k = (uint32_t)kw;
+                break;
+            }
+        }
     } else {
         const uint64_t k_ideal = ceil_div(target, n_rec);
         unit = std::max<uint64_t>(kMinSplitUnit, round_up(ceil_div(rec_bytes, k_ideal), kChunk));
@@ -174,6 +196,12 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
     a.partial = nullptr;
     a.blob = ds.blob;
     a.comb_maps = nullptr;
+    a.fold_k = fold_k;
+    if (fold_k) {
+        KARMA_RC(comb_blob(ds, unit, &a.comb_maps));
+        KARMA_HIP(launch_fixed(a, ds.cu, s));
+        return 0;
+    }
     if (k == 1) {
         KARMA_HIP(launch_fixed(a, ds.cu, s));
         return 0;

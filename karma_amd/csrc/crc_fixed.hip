@@ -68,9 +68,10 @@ __device__ __forceinline__ FixedPlan fixed_plan(const FixedArgs& A, uint64_t u, 
 // a wave hold units 8i..8i+7 of one record, end-aligned; a 3-level tree over
 // the groups (Z_U, Z_2U, Z_4U) leaves one state per 8 units, so the combine
 // kernels start one level up (a 64 MiB segment: 32768 -> 4096 states here).
-template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0, bool BAL = true>
+template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0, bool BAL = true, int KW = 1>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVE_COMB ? kLdsWordsComb : kLdsWords];
+    constexpr bool kMaps = WAVE_COMB || KW > 1;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kMaps ? kLdsWordsComb : kLdsWords];
     __shared__ uint32_t blk_next;  // BAL: the block's next wave-step (an LDS counter, lgkmcnt only)
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & (kGroupLanes - 1);
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     UnitLoads<PF> Ld;
     issue_unit_loads<PF, NT>(P.L, Ld);
     load_stream_tables(lds, A.blob);
-    if constexpr (WAVE_COMB) copy_to_lds<3 * 1024, kBlockThreads>(lds + kCombLdsBase, A.comb_maps);
+    if constexpr (kMaps) copy_to_lds<3 * 1024, kBlockThreads>(lds + kCombLdsBase, A.comb_maps);
     __syncthreads();
     for (; wb < nws; ) {
         uint32_t inj = 0;
@@ -129,6 +130,22 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
             t = __shfl_down(R, 32, 64);
             R = zmap(lds, kCombLdsBase + 2048, R) ^ t;
             if (P.valid && lane == 0) A.partial[wb] = R;  // state wb = units 8wb .. 8wb+7
+        } else if constexpr (KW > 1) {
+            // the record's KW units sit in groups KW*i .. KW*i+KW-1 of this wave (end-aligned: all
+            // but the first are full); fold them into the last group, whose lanes hold the tail:
+            // level d, group g takes group g - 2^d's state shifted over 2^d units (Z_{2^d U})
+            uint32_t t = __shfl_up(R, 8, 64);
+            R = zmap(lds, kCombLdsBase, t) ^ R;
+            if constexpr (KW >= 4) {
+                t = __shfl_up(R, 16, 64);
+                R = zmap(lds, kCombLdsBase + 1024, t) ^ R;
+            }
+            if constexpr (KW == 8) {
+                t = __shfl_up(R, 32, 64);
+                R = zmap(lds, kCombLdsBase + 2048, t) ^ R;
+            }
+            if (P.valid && l == 0 && (grp & (KW - 1)) == KW - 1)
+                A.out[P.r] = ~steps_in_vec(lds, kLZ4, kLT8, R, tcur, 0u, P.tto);
         } else if (P.valid && l == 0) {
             if (k == 1)
                 A.out[P.r] = ~steps_in_vec(lds, kLZ4, kLT8, R, tcur, 0u, P.tto);
@@ -293,7 +310,19 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     // Records of < 31 bytes may hold no aligned 16-byte block.  Units under 2 KiB:
     // the pipelined kernel's extra per-unit work outweighs its hidden latency
     // (1 KiB units: 0.700 vs 0.669 ms per 4 GiB; 4 KiB: 0.628 vs 0.641).
-    if (a.comb_maps && fixed_variant() == 7) {  // static wave-steps (A/B only)
+    if (a.fold_k) {  // k = fold_k units per record folded in the wave, units >= 2 KiB (planner)
+        const bool st = fixed_variant() == 7;
+#define KARMA_FOLD(KW)                                                                                          \
+    if (a.init) {                                                                                               \
+        if (st) hipLaunchKernelGGL((k_units_fixed<4, true, true, false, 0, false, KW>), grid, blk, 0, s, a);   \
+        else hipLaunchKernelGGL((k_units_fixed<4, true, true, false, 0, true, KW>), grid, blk, 0, s, a);       \
+    } else {                                                                                                    \
+        if (st) hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, false, KW>), grid, blk, 0, s, a);  \
+        else hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, true, KW>), grid, blk, 0, s, a);      \
+    }
+        if (a.fold_k == 2) { KARMA_FOLD(2) } else if (a.fold_k == 4) { KARMA_FOLD(4) } else { KARMA_FOLD(8) }
+#undef KARMA_FOLD
+    } else if (a.comb_maps && fixed_variant() == 7) {  // static wave-steps (A/B only)
         if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true, 0, false>), grid, blk, 0, s, a);
         else hipLaunchKernelGGL((k_units_fixed<4, true, false, true, 0, false>), grid, blk, 0, s, a);
     } else if (a.comb_maps) {  // k % 8 == 0, units >= 2 KiB (planner)

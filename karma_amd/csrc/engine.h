@@ -69,6 +69,8 @@ struct FixedArgs {
     const uint32_t* blob;      // kBlobWords, device
     const uint32_t* comb_maps; // k % 8 == 0: Z_U, Z_2U, Z_4U (3 x 1024 words): the 8 groups of a
                                // wave fold their 8 consecutive units into one state (else nullptr)
+    uint32_t fold_k;           // 2, 4 or 8: k == fold_k units of a record sit in one wave, which folds
+                               // them with comb_maps and writes out[] itself (0: not used)
 };
 
 // One unit of a ragged batch: the 16-aligned span [us, us + span) of a record

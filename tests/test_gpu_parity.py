@@ -72,6 +72,28 @@ def test_split_records_multilevel_combine(raw, rec, n, mis):
     _eq(got, oracle_lib.fixed_crcs(host[mis: mis + n * rec], rec))
 
 
+@pytest.mark.parametrize("rec", [4096, 4100, 4111, 8192, 12345, 20000])
+@pytest.mark.parametrize("max_k", ["2", "8"])
+def test_in_wave_split_fold(dev, rec, max_k, monkeypatch):
+    """Batches that fill the GPU cut each record into 2/4/8 units whose groups share a wave
+    (k_units_fixed KW); unaligned record starts, a partial last wave, scalar and array inits."""
+    monkeypatch.setenv("KARMA_FOLD_MAX_K", max_k)
+    n = 4 * K.device_cu_count() * 128 + 37
+    buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 11)
+    got = K.value_batch_fixed(buf, rec).cpu().numpy()
+    want = oracle_lib.splitmix_fixed_crcs(11, rec, 0, n, threads=16)
+    _eq(got, want)
+    if rec in (4100, 20000):
+        _eq(K.value_batch_fixed(buf, rec, init=0xCAFEF00D).cpu().numpy(),
+            oracle_lib.splitmix_fixed_crcs(11, rec, 0, n, init=0xCAFEF00D, threads=16))
+        init = (np.arange(n, dtype=np.uint64) * 2654435761 % (1 << 32)).astype(np.uint32)
+        d_ini = torch.from_numpy(init.view(np.int32)).to(dev)
+        got = K.value_batch_fixed(buf, rec, init=d_ini).cpu().numpy()
+        sel = np.r_[0:64, n // 2:n // 2 + 64, n - 64:n]  # Extend(c, D) = Combine(c, Value(D), |D|)
+        _eq(got[sel], [K.Combine(int(init[r]), int(want[r]), rec) for r in sel])
+
+
 def test_init_array_and_scalar(raw, dev):
     host, dbuf = raw
     rng = np.random.default_rng(9)
@@ -279,7 +301,8 @@ def test_rejects_bad_arguments(dev):
         K.value_batch_fixed(buf, 7)
 
 
-@pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", v) for v in "12"] + [("KARMA_RAGGED_VARIANT", "1")])
+@pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", v) for v in "127"] +
+                         [("KARMA_RAGGED_VARIANT", v) for v in "12"] + [("KARMA_FOLD_MAX_K", "1")])
 def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
     """The A/B kernel builds (tools/variant_bench.py) are held to the same parity as the default."""
     monkeypatch.setenv(env, val)

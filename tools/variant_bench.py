@@ -2,6 +2,9 @@
 """A/B the streaming-kernel variants (KARMA_CRC_VARIANT) in ONE process, interleaved rounds.
 
     python tools/variant_bench.py [variants...]
+
+A variant is a KARMA_CRC_VARIANT number, or ENV=VAL[,ENV=VAL...] (e.g. KARMA_FOLD_MAX_K=1);
+every spec sets all the variables any spec names (unnamed ones back to their defaults).
 """
 import os
 import sys
@@ -12,7 +15,14 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import karma_amd as K  # noqa: E402
 
-variants = [int(v) for v in sys.argv[1:]] or [0, 1, 2, 6]
+variants = sys.argv[1:] or ["0", "1", "2", "6"]
+
+
+def spec_env(v):
+    return dict(kv.split("=", 1) for kv in v.split(",")) if "=" in v else {"KARMA_CRC_VARIANT": v}
+
+
+ENV_KEYS = sorted({k for v in variants for k in spec_env(v)})
 dev = torch.device("cuda:0")
 n, rec = int(os.environ.get("NREC", 1 << 20)), int(os.environ.get("REC", 4096))  # config 4: NREC=64 REC=67108864
 MIS = int(os.environ.get("MISALIGN", "0"))  # byte offset of the arena (alignment experiments)
@@ -24,7 +34,9 @@ ref = None
 res = {v: [] for v in variants}
 for rnd in range(int(os.environ.get('ROUNDS', '8'))):
     for v in variants:
-        os.environ["KARMA_CRC_VARIANT"] = str(v)
+        for k in ENV_KEYS:
+            os.environ.pop(k, None)
+        os.environ.update(spec_env(v))
         for _ in range(2):
             K.value_batch_fixed(buf, rec, out=out)
         torch.cuda.synchronize()
@@ -40,7 +52,7 @@ for rnd in range(int(os.environ.get('ROUNDS', '8'))):
         got = out.cpu().numpy()
         if ref is None:
             ref = got.copy()
-        if v != 6:  # variant 6 is a timing experiment with wrong results by design
+        if v != "6":  # variant 6 is a timing experiment with wrong results by design
             assert np.array_equal(got, ref), f"variant {v} differs"
 for v in variants:
     ms = np.array(res[v])
