@@ -34,8 +34,8 @@ METRIC = "CRC32C GiB/s device-resident, batched WAL records, 1/2/4/8 MI355X"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=50)  # the first 20-40 dispatches run slow
     p.add_argument("--workload", default="fixed",
                    choices=["fixed", "ragged", "stream", "segment", "host", "wal_append", "wal_replay", "kfp_encode",
                             "kfp_parse"])

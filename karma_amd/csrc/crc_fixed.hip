@@ -3,8 +3,9 @@
 // Batched form of segment_file::append_record's per-record crc32c::Value
 // (karma-store/segment_file.cc:22; algorithm karma-util/crc32c.cc:275-376).
 // Record r = arena + r*rec_bytes.  Each record body is cut into k units
-// (k = 1 for batches large enough to fill the GPU), one unit per
-// group of 8 lanes; when k > 1 the unit contributions are folded by
+// (k = 1, or k = KW = 2 folded inside the wave, for batches large enough to fill
+// the GPU), one unit per group of 8 lanes; otherwise the unit
+// contributions are folded by the wave (8 units) and then k_combine_block or
 // k_combine_fixed, one level per factor of 64, with maps Z_{D*2^d}.
 #include <hip/hip_runtime.h>
 

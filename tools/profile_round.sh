@@ -13,12 +13,12 @@ OUT=gpurun_out/prof
 mkdir -p "$OUT"
 REPO=$(pwd)
 export TMPDIR=/tmp
-CMD=(python3 "$REPO/bench.py" --workload "$WL" --steps 20 --warmup 3)
+CMD=(python3 "$REPO/bench.py" --workload "$WL" --steps 300 --warmup 30)
 timeout -k 10 300 "${CMD[@]}" > "$OUT/bench_${ROUND}_${WL}.json"
 cat "$OUT/bench_${ROUND}_${WL}.json"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/$OUT/trace_${ROUND}_${WL}" -o run \
-    -- python3 "$REPO/bench.py" --workload "$WL" --steps 20 --warmup 3 --no-cpu-baseline > "$REPO/$OUT/trace_${ROUND}_${WL}.log" 2>&1
+    -- python3 "$REPO/bench.py" --workload "$WL" --steps 300 --warmup 30 --no-cpu-baseline > "$REPO/$OUT/trace_${ROUND}_${WL}.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$REPO/$OUT/pmc_fetch_${ROUND}_${WL}" -o run \
     -- python3 "$REPO/bench.py" --workload "$WL" --steps 5 --warmup 1 --no-cpu-baseline > "$REPO/$OUT/pmc_fetch_${ROUND}_${WL}.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$REPO/$OUT/pmc_write_${ROUND}_${WL}" -o run \
