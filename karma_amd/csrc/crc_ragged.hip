@@ -259,8 +259,11 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
 // and the first loads of unit u + step are in flight while unit u finishes.
 // Out-of-range groups point at descriptor 0's span (a safe address) and
 // store nothing.
+template <bool BAL = true>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    __shared__ uint32_t blk_next;  // BAL: as k_units_ragged, taken two steps ahead
+    if (BAL && threadIdx.x == 0) blk_next = kWavesPerBlock;
     load_stream_tables(lds, A.blob);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -271,34 +274,51 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs 
     const uint64_t U = U_all < A.unit_cap ? U_all : A.unit_cap;  // memory-safe if the caller's bound was low
     if (U == 0) return;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t step = nwaves * kGroupsPerWave;
-    uint64_t wb = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    uint64_t u = wb * kGroupsPerWave + grp;
-    auto desc_at = [&](uint64_t v) { return load_desc(A.desc + (v < U ? v : 0)); };
-    auto unit_of = [&](const UnitDesc& d, bool valid) {
-        const uint8_t* us = reinterpret_cast<const uint8_t*>(d.us);
-        return lane_unit(us, valid ? us + d.span : us, l);
+    const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
+    const uint32_t nidx = (uint32_t)((nws + nwaves - 1) / nwaves) * kWavesPerBlock;
+    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
+    auto next_of = [&](uint64_t w) -> uint64_t {
+        if constexpr (BAL) {
+            uint32_t i = 0;
+            if (lane == 0) i = atomicAdd(&blk_next, 1u);
+            i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
+            return i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
+        } else {
+            return w < nws ? w + nwaves : nws;
+        }
     };
-    UnitDesc d = desc_at(u);
-    LaneUnit L = unit_of(d, u < U);
+    auto desc_at = [&](uint64_t w) { const uint64_t v = w * kGroupsPerWave + grp; return load_desc(A.desc + (v < U ? v : 0)); };
+    auto unit_of = [&](const UnitDesc& d, uint64_t w) {
+        const uint8_t* us = reinterpret_cast<const uint8_t*>(d.us);
+        return lane_unit(us, w * kGroupsPerWave + grp < U ? us + d.span : us, l);
+    };
+    uint64_t wb = bw0 + (threadIdx.x >> 6);
+    uint64_t wb1 = next_of(wb);
+    UnitDesc d = desc_at(wb);
+    LaneUnit L = unit_of(d, wb);
     UnitLoads<kRaggedPF> Ld;
     issue_unit_loads<kRaggedPF, kRaggedNT>(L, Ld);
-    UnitDesc dn = desc_at(u + step);
-    for (; wb * kGroupsPerWave < U; wb += nwaves, u += step) {
-        // The descriptor two units ahead is issued with the next unit's loads,
+    UnitDesc dn = desc_at(wb1);
+    while (wb < nws) {
+        // The descriptor two steps ahead is issued with the next unit's loads,
         // never just before a wait: a load issued ahead of the main loop would
         // be waited on by the loop's first batch (vmcnt counts in order).
         UnitDesc dnn;
         LaneUnit N;
+        uint64_t wb2 = 0;
         const uint32_t R = stream_unit<kRaggedPF, kRaggedNT>(lds, X, l, L, Ld, L.us, d.inj, [&](UnitLoads<kRaggedPF>& nx) {
-            N = unit_of(dn, u + step < U);
-            dnn = desc_at(u + 2 * step);
+            N = unit_of(dn, wb1);
+            wb2 = next_of(wb1);
+            dnn = desc_at(wb2);
             issue_unit_loads<kRaggedPF, kRaggedNT>(N, nx);
         });
+        const uint64_t u = wb * kGroupsPerWave + grp;
         if (u < U && l == 0) A.partial[u] = R;
         d = dn;
         dn = dnn;
         L = N;
+        wb = wb1;
+        wb1 = wb2;
     }
 }
 
@@ -522,7 +542,9 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     units_timer_begin(s);
     if (ragged_variant() == 1)
-        hipLaunchKernelGGL(k_units_ragged_pipe, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+        hipLaunchKernelGGL(k_units_ragged_pipe<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (ragged_variant() == 3)  // pipelined, static wave-steps (A/B only)
+        hipLaunchKernelGGL(k_units_ragged_pipe<false>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (ragged_variant() == 2)  // static wave-steps (A/B only)
         hipLaunchKernelGGL(k_units_ragged<false>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else

@@ -16,7 +16,10 @@ constexpr int kChunk = 16 * kGroupLanes;       // bytes a group consumes per ste
 constexpr int kBlockThreads = 1024;            // one workgroup per CU
 constexpr int kWavesPerBlock = kBlockThreads / 64;
 constexpr int kGroupsPerWave = 64 / kGroupLanes;
-constexpr uint64_t kDefaultUnit = 8192;        // unit size for ragged batches (4 KiB: 1.9 % slower calls, 16 KiB: 3.5 %)
+#ifndef KARMA_RAGGED_UNIT
+#define KARMA_RAGGED_UNIT 8192  // a build-time A/B knob (tools/ragged_unit_ab.sh)
+#endif
+constexpr uint64_t kDefaultUnit = KARMA_RAGGED_UNIT;  // unit size for ragged batches
 
 // ---- table blob of the streaming kernel (uint32 words) ---------------------
 constexpr int kBlobStride = 0;     // Z_S slicing tables, 4 x 256

@@ -302,7 +302,7 @@ def test_rejects_bad_arguments(dev):
 
 
 @pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", v) for v in "127"] +
-                         [("KARMA_RAGGED_VARIANT", v) for v in "12"] + [("KARMA_FOLD_MAX_K", "1")])
+                         [("KARMA_RAGGED_VARIANT", v) for v in "123"] + [("KARMA_FOLD_MAX_K", "1")])
 def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
     """The A/B kernel builds (tools/variant_bench.py) are held to the same parity as the default."""
     monkeypatch.setenv(env, val)
