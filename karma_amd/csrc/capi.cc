@@ -48,6 +48,8 @@ int hip_fail(hipError_t e, const char* what) {
 
 constexpr uint64_t kMinSplitUnit = 2048;  // smallest unit when records are split
 constexpr uint64_t kOverdecompose = 4;    // units per group before splitting records
+constexpr uint64_t kSplitOverdecompose = 64;  // units per group once split (2 KiB units up to 4 GiB
+                                              // batches; 4: config 4 0.653 ms, 64: 0.609)
 
 uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 uint64_t round_up(uint64_t a, uint64_t m) { return ceil_div(a, m) * m; }
@@ -146,6 +148,13 @@ int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocate
 }
 
 // ---- fixed-size records ---------------------------------------------------
+// Units per group when records are split (KARMA_SPLIT_OVERDECOMPOSE: A/B).
+uint64_t split_overdecompose() {
+    const char* e = getenv("KARMA_SPLIT_OVERDECOMPOSE");
+    const long v = e ? atol(e) : (long)kSplitOverdecompose;
+    return v < 1 ? 1 : v > 256 ? 256 : (uint64_t)v;
+}
+
 // Largest in-wave split of a big batch's records (2, 4 or 8; KARMA_FOLD_MAX_K, 1 = off: A/B).
 uint64_t fold_max_k() {
     const char* e = getenv("KARMA_FOLD_MAX_K");
@@ -176,13 +185,23 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
             }
         }
     } else {
-        const uint64_t k_ideal = ceil_div(target, n_rec);
+        const uint64_t k_ideal = ceil_div(split_overdecompose() * groups, n_rec);
         unit = std::max<uint64_t>(kMinSplitUnit, round_up(ceil_div(rec_bytes, k_ideal), kChunk));
         k = ceil_div(rec_bytes, unit);
-        if (k == 1) unit = round_up(rec_bytes, kChunk);
-        // a whole number of waves per record (the leading units are then empty: the
-        // units are end-aligned), so each wave folds its 8 units (k_units_fixed WAVE_COMB)
-        if (k > 1) k = round_up(k, kGroupsPerWave);
+        if (k == 1) {
+            unit = round_up(rec_bytes, kChunk);
+        } else if (k <= kGroupsPerWave && fold_max_k() > 1) {
+            // 2-8 units: a power of two, folded inside the wave like the big batches' split
+            uint64_t kw = 2;
+            while (kw < k) kw *= 2;
+            unit = std::max<uint64_t>(kMinSplitUnit, round_up(ceil_div(rec_bytes, kw), kChunk));
+            k = kw;
+            fold_k = (uint32_t)kw;
+        } else {
+            // a whole number of waves per record (the leading units are then empty: the
+            // units are end-aligned), so each wave folds its 8 units (k_units_fixed WAVE_COMB)
+            k = round_up(k, kGroupsPerWave);
+        }
     }
     FixedArgs a;
     a.arena = static_cast<const uint8_t*>(d_data);

@@ -52,7 +52,8 @@ def test_native_library_is_what_runs(dev):
 
 
 @pytest.mark.parametrize("rec", [1, 2, 3, 4, 7, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 127, 128, 129, 255, 256,
-                                 257, 1000, 2047, 2048, 2049, 4095, 4096, 4097, 8192, 65535, 65536, 100000])
+                                 257, 1000, 2047, 2048, 2049, 4095, 4096, 4097, 5000, 8192, 12000, 16384, 65535, 65536,
+                                 100000])
 @pytest.mark.parametrize("mis", [0, 1, 4, 8, 13])
 def test_fixed_sizes_and_alignments(raw, rec, mis):
     host, dbuf = raw
