@@ -33,7 +33,11 @@ using namespace dev;
 constexpr int kRaggedPF = 4;
 constexpr bool kRaggedNT = true;
 
-constexpr int kScanBlock = 1024;
+#ifndef KARMA_SCAN_BLOCK
+#define KARMA_SCAN_BLOCK 1024  // records per scan/desc block: a build-time A/B knob (tools/scan_block_ab.sh)
+#endif
+constexpr int kScanBlock = KARMA_SCAN_BLOCK;
+static_assert(kScanBlock % 64 == 0 && kScanBlock <= 1024 && kScanBlock >= kBuckets, "scan block shape");
 constexpr uint64_t kU = kDefaultUnit;  // ragged units: absolute kU-byte boundaries
 constexpr int kUShift = __builtin_ctzll(kDefaultUnit);
 static_assert((kU & (kU - 1)) == 0, "unit size is a power of two");
