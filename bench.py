@@ -133,9 +133,7 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
 
 def units_kernel_name(wl: str) -> str:
     """The dominant kernel a batch runs (capi.cc planning, crc_fixed.hip / crc_ragged.hip launchers)."""
-    if wl == "ragged":
-        return "k_units_ragged_pipe" if os.environ.get("KARMA_RAGGED_VARIANT") == "1" else "k_units_ragged"
-    return "k_units_fixed_v1" if os.environ.get("KARMA_CRC_VARIANT") == "1" else "k_units_fixed"
+    return "k_units_ragged" if wl == "ragged" else "k_units_fixed"
 
 
 def pmc_traffic(path: str, workload: str, n_bytes_per_launch: int):

@@ -132,6 +132,23 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                      int device);
 
+/* Plan overrides of karma_wal_replay_tuned.  Every setting gives the same result (the
+ * replay is exact whatever the plan); they exist for tests and tuning.  Zero = the
+ * planner's choice. */
+#define KARMA_WAL_CRC_PLAN 0    /* one-record-per-group batch when every payload <= 1 KiB, else the unit plan */
+#define KARMA_WAL_CRC_DIRECT 1  /* always the one-record-per-group batch */
+#define KARMA_WAL_CRC_UNITS 2   /* always the unit plan (karma_crc32c_batch_ragged) */
+typedef struct karma_wal_tuning {
+    uint64_t walk_sub_bytes; /* header-walk sub-range size, rounded down to a 4 KiB multiple (>= 4 KiB);
+                                >= seg_bytes: one walker per segment; 0 = planned */
+    int32_t crc_batch;       /* KARMA_WAL_CRC_* */
+    int32_t reserved;        /* 0 */
+} karma_wal_tuning;
+/* karma_wal_replay with plan overrides (tuning may be NULL = karma_wal_replay). */
+int karma_wal_replay_tuned(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
+                           uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
+                           int device, const karma_wal_tuning* tuning);
+
 /* Replay of a segment directory (wal::load_from_path + sivir::open, wal.cc:9-27): the
  * regular files of `dir` named by the decimal WAL offset of their first byte, equal
  * sizes (seg_bytes, or 0 = the first file's size), no gaps.  The files are read by the

@@ -6,11 +6,16 @@ missing, importing the device entry points raises ``KarmaUnavailable``.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libkarma_crc32c.so")
+# The tools build (karma_amd/csrc/ab.h): the same C ABI plus the A/B kernel variants of
+# DESIGN.md §4, chosen by KARMA_* environment variables.  Only tools/ and the variant
+# tests load it (through `using`); the package always runs LIB_PATH.
+AB_LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "lib", "libkarma_crc32c_ab.so")
 
 KARMA_OK = 0
 KARMA_E_INVALID = -1
@@ -45,6 +50,8 @@ SIGNATURES = {
     "karma_wal_append_batch": (_i, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, _c.POINTER(_u64), _vp, _c.POINTER(_sz), _i]),
     "karma_wal_replay": (_i, [_vp, _vp, _sz, _sz, _u64, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_i), _vp, _sz,
                               _i]),
+    "karma_wal_replay_tuned": (_i, [_vp, _vp, _sz, _sz, _u64, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_i), _vp,
+                                    _sz, _i, _vp]),
     "karma_wal_replay_dir": (_i, [_c.c_char_p, _sz, _u64, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_u64),
                                   _c.POINTER(_i), _vp, _sz, _i]),
     "karma_kfp_encode_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _c.POINTER(_sz),
@@ -55,6 +62,14 @@ SIGNATURES = {
     "karma_device_cu_count": (_i, []),
     "karma_crc32c_time_next_units": (_i, [_vp, _vp]),
 }
+
+
+KARMA_WAL_CRC_PLAN, KARMA_WAL_CRC_DIRECT, KARMA_WAL_CRC_UNITS = 0, 1, 2
+
+
+class WalTuning(ctypes.Structure):
+    """karma_wal_tuning (include/karma_crc32c.h): plan overrides of karma_wal_replay_tuned."""
+    _fields_ = [("walk_sub_bytes", _u64), ("crc_batch", _c.c_int32), ("reserved", _c.c_int32)]
 
 
 class KarmaUnavailable(ImportError):
@@ -71,29 +86,49 @@ class KarmaError(RuntimeError):
 
 
 _LIB = None
+_LOADED = {}
+
+
+def load(path: str) -> ctypes.CDLL:
+    """A build of the C ABI at `path` with its signatures bound (loaded once per path)."""
+    if path not in _LOADED:
+        if not os.path.exists(path):
+            raise KarmaUnavailable(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        try:
+            handle = ctypes.CDLL(path)
+        except OSError as e:  # pragma: no cover - depends on the host
+            raise KarmaUnavailable(f"cannot load {path}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LOADED[path] = handle
+    return _LOADED[path]
 
 
 def lib() -> ctypes.CDLL:
     """The loaded library (loaded once).  Raises KarmaUnavailable when it is missing."""
     global _LIB
     if _LIB is None:
-        if not os.path.exists(LIB_PATH):
-            raise KarmaUnavailable(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
-        try:
-            handle = ctypes.CDLL(LIB_PATH)
-        except OSError as e:  # pragma: no cover - depends on the host
-            raise KarmaUnavailable(f"cannot load {LIB_PATH}: {e}") from e
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(handle, name)
-            fn.restype = res
-            fn.argtypes = args
-        _LIB = handle
+        _LIB = load(LIB_PATH)
     return _LIB
+
+
+@contextlib.contextmanager
+def using(path: str):
+    """Run the package's wrappers on another build of the C ABI (the tools build) meanwhile."""
+    global _LIB
+    prev = lib()
+    _LIB = load(path)
+    try:
+        yield _LIB
+    finally:
+        _LIB = prev
 
 
 def check(fn: str, status: int) -> None:
     if status != KARMA_OK:
-        L = lib()
+        L = lib()  # (a failure inside `using` reads the error text of the build in use)
         detail = L.karma_crc32c_strerror(status).decode()
         extra = L.karma_crc32c_last_error().decode()
         raise KarmaError(fn, status, f"{detail}: {extra}" if extra else detail)

@@ -15,6 +15,7 @@
 #include <utility>
 #include <vector>
 
+#include "ab.h"
 #include "engine.h"
 #include "karma_crc32c.h"
 
@@ -148,17 +149,16 @@ int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocate
 }
 
 // ---- fixed-size records ---------------------------------------------------
-// Units per group when records are split (KARMA_SPLIT_OVERDECOMPOSE: A/B).
+// Units per group when records are split (the tools build's KARMA_SPLIT_OVERDECOMPOSE, ab.h).
 uint64_t split_overdecompose() {
-    const char* e = getenv("KARMA_SPLIT_OVERDECOMPOSE");
-    const long v = e ? atol(e) : (long)kSplitOverdecompose;
+    const long v = KARMA_AB_KNOB("KARMA_SPLIT_OVERDECOMPOSE", (long)kSplitOverdecompose);
     return v < 1 ? 1 : v > 256 ? 256 : (uint64_t)v;
 }
 
-// Largest in-wave split of a big batch's records (2, 4 or 8; KARMA_FOLD_MAX_K, 1 = off: A/B).
+// Largest in-wave split of a big batch's records (2; the tools build's KARMA_FOLD_MAX_K
+// also tries 4, 8 and 1 = off, ab.h).
 uint64_t fold_max_k() {
-    const char* e = getenv("KARMA_FOLD_MAX_K");
-    const long v = e ? atol(e) : 2;
+    const long v = KARMA_AB_KNOB("KARMA_FOLD_MAX_K", 2);
     return v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
 }
 

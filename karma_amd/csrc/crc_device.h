@@ -183,8 +183,9 @@ __device__ __forceinline__ uint32_t tail_register(const uint32_t* lds, int z4, i
     return r;
 }
 
-// MODE (timing experiments only, wrong results): bit 0 = main-loop steps without the
-// LDS lookups (KARMA_CRC_VARIANT=6).  The shipped kernels use MODE 0.
+// MODE (timing experiments of the tools build only, wrong results): bit 0 = main-loop
+// steps without the LDS lookups (KARMA_CRC_VARIANT=6, ab.h).  The shipped library
+// instantiates MODE 0 only.
 template <int MODE = 0>
 __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
                                       uint32_t& a3, const u32x4& v) {

@@ -9,8 +9,7 @@
 // k_combine_fixed, one level per factor of 64, with maps Z_{D*2^d}.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-
+#include "ab.h"
 #include "crc_device.h"
 #include "engine.h"
 
@@ -292,12 +291,44 @@ __global__ __launch_bounds__(1024) void k_combine_block(FixedArgs A, const uint3
     }
 }
 
-// KARMA_CRC_VARIANT selects an alternative build of the streaming kernel for
-// in-process A/B measurements (tools/variant_bench.py); 0 = shipped default.
-int fixed_variant() {
-    const char* e = getenv("KARMA_CRC_VARIANT");
-    return e ? atoi(e) : 0;
+#ifdef KARMA_AB
+// Tools build only (ab.h): the alternatives measured in DESIGN.md §4, chosen per
+// call by KARMA_CRC_VARIANT (1 = v1 kernel, 2 = 2 chunks in flight, 6 = timing
+// only with WRONG CRCs, 7 = static wave-steps).  Returns false for the shipped
+// kernel (variant 0, or a plan shape the variant does not cover).
+bool launch_fixed_ab(const FixedArgs& a, dim3 grid, dim3 blk, hipStream_t s) {
+    const long v = KARMA_AB_KNOB("KARMA_CRC_VARIANT", 0);
+    if (v == 0 || a.rec_bytes < 31 || (!a.fold_k && !a.comb_maps && a.unit_bytes < 2048)) return false;
+    if (a.fold_k) {
+        if (v != 7) return false;
+#define KARMA_FOLD_STATIC(KW)                                                                              \
+    if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false, 0, false, KW>), grid, blk, 0, s, a); \
+    else hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, false, KW>), grid, blk, 0, s, a);
+        if (a.fold_k == 2) { KARMA_FOLD_STATIC(2) } else if (a.fold_k == 4) { KARMA_FOLD_STATIC(4) } else { KARMA_FOLD_STATIC(8) }
+#undef KARMA_FOLD_STATIC
+        return true;
+    }
+    if (a.comb_maps) {
+        if (v != 7) return false;
+        if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true, 0, false>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_units_fixed<4, true, false, true, 0, false>), grid, blk, 0, s, a);
+        return true;
+    }
+    switch (v) {
+        case 1: hipLaunchKernelGGL((k_units_fixed_v1<4, true>), grid, blk, 0, s, a); return true;
+        case 2:
+            if (a.init) hipLaunchKernelGGL((k_units_fixed<2, true, true, false>), grid, blk, 0, s, a);
+            else hipLaunchKernelGGL((k_units_fixed<2, true, false, false>), grid, blk, 0, s, a);
+            return true;
+        case 6: hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 1>), grid, blk, 0, s, a); return true;
+        case 7:
+            if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false, 0, false>), grid, blk, 0, s, a);
+            else hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, false>), grid, blk, 0, s, a);
+            return true;
+        default: return false;
+    }
 }
+#endif
 
 }  // namespace
 
@@ -308,43 +339,29 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     const dim3 grid((unsigned)(need < (uint64_t)grid_blocks ? need : (uint64_t)grid_blocks));
     units_timer_begin(s);
     const dim3 blk(kBlockThreads);
+#ifdef KARMA_AB
+    if (launch_fixed_ab(a, grid, blk, s)) {
+        units_timer_end(s);
+        return hipGetLastError();
+    }
+#endif
     // Records of < 31 bytes may hold no aligned 16-byte block.  Units under 2 KiB:
     // the pipelined kernel's extra per-unit work outweighs its hidden latency
     // (1 KiB units: 0.700 vs 0.669 ms per 4 GiB; 4 KiB: 0.628 vs 0.641).
     if (a.fold_k) {  // k = fold_k units per record folded in the wave, units >= 2 KiB (planner)
-        const bool st = fixed_variant() == 7;
-#define KARMA_FOLD(KW)                                                                                          \
-    if (a.init) {                                                                                               \
-        if (st) hipLaunchKernelGGL((k_units_fixed<4, true, true, false, 0, false, KW>), grid, blk, 0, s, a);   \
-        else hipLaunchKernelGGL((k_units_fixed<4, true, true, false, 0, true, KW>), grid, blk, 0, s, a);       \
-    } else {                                                                                                    \
-        if (st) hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, false, KW>), grid, blk, 0, s, a);  \
-        else hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, true, KW>), grid, blk, 0, s, a);      \
-    }
+#define KARMA_FOLD(KW)                                                                                \
+    if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false, 0, true, KW>), grid, blk, 0, s, a); \
+    else hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, true, KW>), grid, blk, 0, s, a);
         if (a.fold_k == 2) { KARMA_FOLD(2) } else if (a.fold_k == 4) { KARMA_FOLD(4) } else { KARMA_FOLD(8) }
 #undef KARMA_FOLD
-    } else if (a.comb_maps && fixed_variant() == 7) {  // static wave-steps (A/B only)
-        if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true, 0, false>), grid, blk, 0, s, a);
-        else hipLaunchKernelGGL((k_units_fixed<4, true, false, true, 0, false>), grid, blk, 0, s, a);
     } else if (a.comb_maps) {  // k % 8 == 0, units >= 2 KiB (planner)
         if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true>), grid, blk, 0, s, a);
         else hipLaunchKernelGGL((k_units_fixed<4, true, false, true>), grid, blk, 0, s, a);
     } else if (a.rec_bytes < 31 || a.unit_bytes < 2048) {
         hipLaunchKernelGGL((k_units_fixed_v1<4, true>), grid, blk, 0, s, a);
     } else {
-        switch (fixed_variant()) {
-            case 1: hipLaunchKernelGGL((k_units_fixed_v1<4, true>), grid, blk, 0, s, a); break;
-            case 2:
-                if (a.init) hipLaunchKernelGGL((k_units_fixed<2, true, true, false>), grid, blk, 0, s, a);
-                else hipLaunchKernelGGL((k_units_fixed<2, true, false, false>), grid, blk, 0, s, a);
-                break;
-            case 6: hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 1>), grid, blk, 0, s, a); break;  // timing only
-            case 7: hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, false>), grid, blk, 0, s, a); break;  // static
-            default:
-                if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false>), grid, blk, 0, s, a);
-                else hipLaunchKernelGGL((k_units_fixed<4, true, false, false>), grid, blk, 0, s, a);
-                break;
-        }
+        if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_units_fixed<4, true, false, false>), grid, blk, 0, s, a);
     }
     units_timer_end(s);
     return hipGetLastError();

@@ -19,8 +19,7 @@
 //                      records with > 64 units are folded by the whole wave
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-
+#include "ab.h"
 #include "crc_device.h"
 #include "engine.h"
 
@@ -258,7 +257,8 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
     return UnitDesc{v.x | ((uint64_t)v.y << 32), v.z, v.w};
 }
 
-// Pipelined variant (KARMA_RAGGED_VARIANT=1).  Every lane streams its
+#ifdef KARMA_AB
+// Pipelined variant (tools build, KARMA_RAGGED_VARIANT=1, ab.h).  Every lane streams its
 // group's units back to back (stream_unit): the descriptor of unit u + 2*step
 // and the first loads of unit u + step are in flight while unit u finishes.
 // Out-of-range groups point at descriptor 0's span (a safe address) and
@@ -326,6 +326,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs 
     }
 }
 
+#endif
+
 // The shipped units kernel: each unit's loads are issued when the unit starts
 // (group_unit), the next descriptor is in flight meanwhile.  On config 3 it
 // measures 1% faster than k_units_ragged_pipe, unlike the
@@ -372,10 +374,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     }
 }
 
-int ragged_variant() {
-    const char* e = getenv("KARMA_RAGGED_VARIANT");
-    return e ? atoi(e) : 0;
-}
 
 // Slot of unit j of a record (full units from fb in order, partial ones bucketed).
 __device__ __forceinline__ uint64_t unit_slot(uint64_t j, uint64_t k, uint64_t fb, uint64_t ps0, uint64_t ps1,
@@ -545,13 +543,16 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
     hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     units_timer_begin(s);
-    if (ragged_variant() == 1)
+#ifdef KARMA_AB  // tools build (ab.h): 1 = pipelined, 2 = static wave-steps, 3 = both
+    const long v = KARMA_AB_KNOB("KARMA_RAGGED_VARIANT", 0);
+    if (v == 1)
         hipLaunchKernelGGL(k_units_ragged_pipe<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
-    else if (ragged_variant() == 3)  // pipelined, static wave-steps (A/B only)
+    else if (v == 3)
         hipLaunchKernelGGL(k_units_ragged_pipe<false>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
-    else if (ragged_variant() == 2)  // static wave-steps (A/B only)
+    else if (v == 2)
         hipLaunchKernelGGL(k_units_ragged<false>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else
+#endif
         hipLaunchKernelGGL(k_units_ragged<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block

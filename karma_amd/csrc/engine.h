@@ -184,7 +184,8 @@ struct WalWalkPlan {
     uint64_t nsub, sub_bytes, sub_cap, cand_cap;
     int kernel;  // 0: sub-range walkers (+ resolve when nsub > 1), 1: one workgroup per segment
 };
-WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu);
+// sub_bytes: 0 = the planner's split, else the forced sub-range size (karma_wal_tuning).
+WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes);
 hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s);
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s);
 hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);

@@ -196,7 +196,7 @@ int upload_staged(ReplayCtx& c, void* d_dst, const ImageFill& fill, uint64_t src
 
 int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
-                int device);
+                int device, const karma_wal_tuning* tuning);
 
 }  // namespace
 
@@ -301,8 +301,16 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
 int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                      int device) {
+    return karma_wal_replay_tuned(h_wal, d_wal, wal_bytes, seg_bytes, start, h_n_records, h_stop, h_status, h_rec_off,
+                                  rec_cap, device, nullptr);
+}
+
+int karma_wal_replay_tuned(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
+                           uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
+                           int device, const karma_wal_tuning* tuning) {
     if ((!h_wal && !d_wal) || !h_n_records || !h_stop || !h_status || seg_bytes < 1 || wal_bytes % seg_bytes ||
-        start > wal_bytes || seg_bytes >= (uint64_t(1) << 31))
+        start > wal_bytes || seg_bytes >= (uint64_t(1) << 31) ||
+        (tuning && (tuning->crc_batch < 0 || tuning->crc_batch > 2)))
         return fail(KARMA_E_INVALID, "wal_replay");
     const uint8_t* src = static_cast<const uint8_t*>(h_wal);
     const ImageFill copy = [src](uint8_t* dst, uint64_t off, size_t n) {
@@ -310,7 +318,7 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
         return 0;
     };
     return replay_core(static_cast<const uint8_t*>(d_wal), d_wal ? nullptr : &copy, wal_bytes, seg_bytes, start,
-                       h_n_records, h_stop, h_status, h_rec_off, rec_cap, device);
+                       h_n_records, h_stop, h_status, h_rec_off, rec_cap, device, tuning);
 }
 
 }  // extern "C"
@@ -321,7 +329,7 @@ namespace {
 // streamed into HBM.  Offsets in and out are relative to the image start.
 int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
-                int device) {
+                int device, const karma_wal_tuning* tuning) {
     using namespace karma::engine;
     const uint64_t nseg = wal_bytes / seg_bytes;
     const uint64_t s0 = std::min<uint64_t>(start / seg_bytes, nseg);
@@ -356,7 +364,7 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     A.seg_bytes = seg_bytes;
     A.first_pos = start - base0;
     // 1. segment-parallel header walk (sub-range walkers when there are few segments)
-    const WalWalkPlan plan = wal_walk_plan(seg_bytes, nwork, c.cu);
+    const WalWalkPlan plan = wal_walk_plan(seg_bytes, nwork, c.cu, tuning ? tuning->walk_sub_bytes : 0);
     A.nsub = plan.nsub;
     A.sub_bytes = plan.sub_bytes;
     A.sub_cap = plan.sub_cap;
@@ -419,9 +427,9 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
             return fail(KARMA_E_HIP, "wal_replay: gather");
         // payload = header + 8: the arena is the image shifted by the header.  Small records
         // only: one record per group, without the ragged plan kernels.
-        const char* sm = getenv("KARMA_WAL_SMALL_MAX");  // tests: force either batch
-        const uint64_t small_max = sm && *sm ? strtoull(sm, nullptr, 10) : kSmallRecordMax;
-        if (const int rc = max_len <= small_max
+        const int batch = tuning ? tuning->crc_batch : KARMA_WAL_CRC_PLAN;
+        const bool direct = batch == KARMA_WAL_CRC_DIRECT || (batch == KARMA_WAL_CRC_PLAN && max_len <= kSmallRecordMax);
+        if (const int rc = direct
                                ? ragged_small_batch(A.wal + 8, A.off, A.len, n_all, c.crc.as<uint32_t>(), c.st)
                                : karma_crc32c_batch_ragged(A.wal + 8, A.off, A.len, n_all, w1 * seg_bytes, nullptr,
                                                            0, c.crc.as<uint32_t>(), c.st))
@@ -525,7 +533,7 @@ int karma_wal_replay_dir(const char* dir, size_t seg_bytes, uint64_t start, uint
         return 0;
     };
     const int rc = replay_core(nullptr, &read_files, wal_bytes, seg_bytes, start - base, h_n_records, h_stop, h_status,
-                               h_rec_off, rec_cap, device);
+                               h_rec_off, rec_cap, device, nullptr);
     close_all();
     if (rc) return rc;
     *h_base = base;

@@ -11,7 +11,7 @@
 //                   kind / offset.  The header chain is serial; segments and
 //                   sub-ranges walk in parallel, replacing the host's pread loop.
 //   k_wal_resolve   (sub-ranges) stitches the walkers' lists along the real chain
-//   k_wal_walk      the same walk with one workgroup per segment (A/B, tests)
+//   k_wal_walk      the same walk with one workgroup per segment (tools build only)
 //   k_wal_gather    candidates of the segments replay enters, in WAL order, into
 //                   contiguous (header offset, length, stored CRC) lists
 //   (ragged batch)  payload CRCs: the arena is the image shifted by the 8-byte
@@ -24,19 +24,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 
+#include "ab.h"
 #include "engine.h"
 #include "karma_crc32c.h"
 
 namespace karma {
 namespace engine {
 namespace {
-
-constexpr int kWalkThreads = 256;
-constexpr uint32_t kTile = 16384;          // LDS tile of the walk (two buffers)
-constexpr uint32_t kTileLoad = kTile + 16;  // + one header's slack (16-byte multiple)
-static_assert(kTileLoad % 16 == 0, "tile of whole vectors");
 
 // crc32c::Value of the stale len/type word of a size-0 record.  A type-0 record
 // of size 0 has the word 0, so the value is a constant: Value("\0\0\0\0").
@@ -47,6 +42,12 @@ constexpr uint32_t crc_word_host(uint32_t w) {
 }
 constexpr uint32_t kStaleZero = crc_word_host(0);
 static_assert(kStaleZero == 0x48674BC7u, "crc32c::Value of four zero bytes");
+
+#ifdef KARMA_AB  // k_wal_walk: the workgroup walker, tools build only (ab.h)
+constexpr int kWalkThreads = 256;
+constexpr uint32_t kTile = 16384;          // LDS tile of the walk (two buffers)
+constexpr uint32_t kTileLoad = kTile + 16;  // + one header's slack (16-byte multiple)
+static_assert(kTileLoad % 16 == 0, "tile of whole vectors");
 
 // The walker (thread 0) keeps its position in 32 bits (seg_bytes < 2^31) and
 // reads each header as three aligned LDS words funnel-shifted into place; the
@@ -175,6 +176,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
         A.span[2 * blockIdx.x + 1] = 0;
     }
 }
+
+#endif
 
 // ---- one-wave walkers -------------------------------------------------------
 // A wave walks through one 4 KiB LDS tile (4 KiB of LDS: many walkers per CU).  Every lane holds 64 bytes of the NEXT tile in registers,
@@ -594,18 +597,16 @@ __global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n) {
 // segment, so few segments leave most of the GPU idle: each segment is then cut
 // into sub-ranges (at least 16 KiB) so that about 16 walkers per CU run, and
 // k_wal_resolve stitches their lists.  Many segments: one walker per segment.
-// KARMA_WALK_VARIANT=1 forces one workgroup per segment (k_wal_walk);
-// KARMA_WALK_SUB=<bytes> forces the sub-range size (tests).
-WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu) {
+// sub_bytes != 0 forces the sub-range size (karma_wal_tuning: tests, tuning);
+// the tools build's KARMA_WALK_VARIANT=1 (ab.h) selects k_wal_walk instead.
+WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes) {
     WalWalkPlan p{1, 0, 0, 0, 0};
-    const char* v = getenv("KARMA_WALK_VARIANT");
-    const char* fs = getenv("KARMA_WALK_SUB");
     const uint64_t tiles = (seg_bytes + kWTile - 1) / kWTile;
     uint64_t sub_tiles = tiles;
-    if (v && atoi(v) == 1) {
+    if (KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 1) {
         p.kernel = 1;
-    } else if (fs && *fs) {
-        sub_tiles = std::max<uint64_t>(1, (uint64_t)atoll(fs) / kWTile);
+    } else if (sub_bytes) {
+        sub_tiles = std::max<uint64_t>(1, sub_bytes / kWTile);
     } else {
         const uint64_t want = 16 * (uint64_t)(cu > 0 ? cu : 1);  // walkers
         if (nseg > 0 && nseg < want) {
@@ -625,9 +626,13 @@ WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu) {
 
 hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s) {
     if (!nseg) return hipSuccess;
+#ifdef KARMA_AB
     if (plan.kernel == 1) {
         hipLaunchKernelGGL(k_wal_walk, dim3((unsigned)nseg), dim3(kWalkThreads), 0, s, a);
-    } else {
+        return hipGetLastError();
+    }
+#endif
+    {
         hipLaunchKernelGGL(k_wal_walk_sub, dim3((unsigned)(nseg * plan.nsub)), dim3(64), 0, s, a);
         if (plan.nsub > 1) hipLaunchKernelGGL(k_wal_resolve, dim3((unsigned)nseg), dim3(64), 0, s, a);
     }

@@ -70,19 +70,22 @@ def append(payloads, wal: np.ndarray, seg_bytes: int, cursor: int = 0, device: i
 
 
 def replay(wal=None, seg_bytes: int = 1 << 20, start: int = 0, d_wal=None, wal_bytes: Optional[int] = None,
-           device: int = -1) -> Replay:
+           device: int = -1, walk_sub_bytes: int = 0, crc_batch: int = _lib.KARMA_WAL_CRC_PLAN) -> Replay:
     """sivir::open over an image: ``wal`` in host memory (numpy), or ``d_wal`` (a CUDA tensor)
-    already in HBM."""
+    already in HBM.  ``walk_sub_bytes`` / ``crc_batch`` override the plan (karma_wal_tuning;
+    the result is the same whatever the plan)."""
     h = _u8(wal) if wal is not None else None
     if wal_bytes is None:
         wal_bytes = h.nbytes if h is not None else d_wal.numel() * d_wal.element_size()
     n, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
     rec = np.zeros(wal_bytes // 8 + 1, np.uint64)
+    tuning = _lib.WalTuning(walk_sub_bytes, crc_batch, 0)
     _lib.check("karma_wal_replay",
-               _lib.lib().karma_wal_replay(h.ctypes.data if h is not None else None,
-                                           d_wal.data_ptr() if d_wal is not None else None, wal_bytes, seg_bytes,
-                                           start, ctypes.byref(n), ctypes.byref(stop), ctypes.byref(status),
-                                           rec.ctypes.data, rec.size, device))
+               _lib.lib().karma_wal_replay_tuned(h.ctypes.data if h is not None else None,
+                                                 d_wal.data_ptr() if d_wal is not None else None, wal_bytes,
+                                                 seg_bytes, start, ctypes.byref(n), ctypes.byref(stop),
+                                                 ctypes.byref(status), rec.ctypes.data, rec.size, device,
+                                                 ctypes.byref(tuning)))
     return Replay(rec[: n.value].copy(), stop.value, status.value)
 
 

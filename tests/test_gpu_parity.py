@@ -4,6 +4,7 @@ Bit-exact comparisons through the C ABI (karma_amd wraps it with ctypes) against
 oracle/crc32c_port.c (itself pinned to the reference build by tests/test_oracle.py) and the
 committed golden fixtures; full BASELINE sizes (configs 2-4) are checked record by record.
 """
+import contextlib
 import ctypes
 import os
 
@@ -78,7 +79,16 @@ def test_split_records_multilevel_combine(raw, rec, n, mis):
 def test_in_wave_split_fold(dev, rec, max_k, monkeypatch):
     """Batches that fill the GPU cut each record into 2/4/8 units whose groups share a wave
     (k_units_fixed KW); unaligned record starts, a partial last wave, scalar and array inits."""
-    monkeypatch.setenv("KARMA_FOLD_MAX_K", max_k)
+    if max_k != "2":  # the shipped planner splits in 2; 4 and 8 are the tools build's KARMA_FOLD_MAX_K
+        monkeypatch.setenv("KARMA_FOLD_MAX_K", max_k)
+        ctx = _lib.using(_lib.AB_LIB_PATH)
+    else:
+        ctx = contextlib.nullcontext()
+    with ctx:
+        _in_wave_split_fold(dev, rec)
+
+
+def _in_wave_split_fold(dev, rec):
     n = 4 * K.device_cu_count() * 128 + 37
     buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
     K.fill_splitmix64(buf, 11)
@@ -305,8 +315,14 @@ def test_rejects_bad_arguments(dev):
 @pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", v) for v in "127"] +
                          [("KARMA_RAGGED_VARIANT", v) for v in "123"] + [("KARMA_FOLD_MAX_K", "1")])
 def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
-    """The A/B kernel builds (tools/variant_bench.py) are held to the same parity as the default."""
+    """The A/B kernels of the tools build (karma_amd/csrc/ab.h, tools/variant_bench.py) are held to
+    the same parity as the shipped ones."""
     monkeypatch.setenv(env, val)
+    with _lib.using(_lib.AB_LIB_PATH):
+        _variants_match_oracle(raw, dev)
+
+
+def _variants_match_oracle(raw, dev):
     host, dbuf = raw
     for rec, n in [(4096, 2000), (512, 5000), (1 << 16, 100), (3 << 20, 2)]:
         got = K.value_batch_fixed(dbuf[: n * rec], rec).cpu().numpy()

@@ -40,14 +40,37 @@ def _append(lib, src, offs, lens, wal, cursor=0, seg=SEG):
     return cur.value, rec[: nf.value]
 
 
+# Replay plans (every one must give scan_record's result): (tools build?, karma_wal_tuning fields)
+WALKS = {
+    "workgroup": (True, 0, _lib.KARMA_WAL_CRC_PLAN),      # k_wal_walk, one workgroup per segment (tools build)
+    "whole": (False, 1 << 30, _lib.KARMA_WAL_CRC_PLAN),   # k_wal_walk_sub, one walker per segment
+    "split": (False, 0, _lib.KARMA_WAL_CRC_PLAN),         # the plan: few segments -> sub-range walkers
+    "split4k": (False, 4096, _lib.KARMA_WAL_CRC_DIRECT),  # one-tile sub-ranges + k_wal_resolve, and every
+}                                                         # CRC batch one record per group (any length)
+_WALK = {"name": "split"}
+
+
+def _walk_env(monkeypatch, walk):
+    monkeypatch.setitem(_WALK, "name", walk)
+    if WALKS[walk][0]:
+        monkeypatch.setenv("KARMA_WALK_VARIANT", "1")  # read by the tools build only (ab.h)
+    else:
+        monkeypatch.delenv("KARMA_WALK_VARIANT", raising=False)
+
+
 def _replay(lib, wal, start=0, d_wal=None, seg=SEG, host=True):
-    """karma_wal_replay over the host image, or (host=False) over the device copy d_wal only."""
+    """karma_wal_replay over the host image, or (host=False) over the device copy d_wal only, with
+    the plan of the current walk (_walk_env)."""
+    ab, sub, batch = WALKS[_WALK["name"]]
+    L = _lib.load(_lib.AB_LIB_PATH) if ab else lib
+    tuning = _lib.WalTuning(sub, batch, 0)
     n, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
     rec = np.zeros(wal.nbytes // 8, np.uint64)
-    st = lib.karma_wal_replay(wal.ctypes.data if host else None, d_wal.data_ptr() if d_wal is not None else None,
-                              wal.nbytes, seg, start, ctypes.byref(n), ctypes.byref(stop), ctypes.byref(status),
-                              rec.ctypes.data, rec.size, 0)
-    _lib.check("karma_wal_replay", st)
+    st = L.karma_wal_replay_tuned(wal.ctypes.data if host else None, d_wal.data_ptr() if d_wal is not None else None,
+                                  wal.nbytes, seg, start, ctypes.byref(n), ctypes.byref(stop), ctypes.byref(status),
+                                  rec.ctypes.data, rec.size, 0, ctypes.byref(tuning))
+    if st:
+        raise _lib.KarmaError("karma_wal_replay_tuned", st, L.karma_crc32c_last_error().decode())
     return list(rec[: n.value]), stop.value, status.value
 
 
@@ -113,22 +136,6 @@ def test_replay_from_checkpoint_and_short_segment_tails(lib):
         got = _replay(lib, wal, start=start)
         want = wal_model.replay(wal.tobytes(), SEG, start)
         assert got == (list(want[0]), want[1], want[2])
-
-
-WALKS = {
-    "workgroup": {"KARMA_WALK_VARIANT": "1"},         # k_wal_walk, one workgroup per segment
-    "whole": {"KARMA_WALK_SUB": str(1 << 30)},        # k_wal_walk_sub, one walker per segment
-    "split": {},                                      # the plan: few segments -> sub-range walkers
-    "split4k": {"KARMA_WALK_SUB": "4096",             # one-tile sub-ranges + k_wal_resolve,
-                "KARMA_WAL_SMALL_MAX": str(1 << 24)},  # and every batch one record per group
-}
-
-
-def _walk_env(monkeypatch, walk):
-    for k in ("KARMA_WALK_VARIANT", "KARMA_WALK_SUB", "KARMA_WAL_SMALL_MAX"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in WALKS[walk].items():
-        monkeypatch.setenv(k, v)
 
 
 @pytest.mark.parametrize("walk", list(WALKS))

@@ -232,3 +232,13 @@ def test_python_wal_api_refuses_without_gpu():
     with pytest.raises(K.KarmaError) as e:
         W.replay(img, 4096)
     assert e.value.status == _lib.KARMA_E_NO_DEVICE
+
+
+def test_shipped_library_has_no_variant_knobs():
+    """The shipped library reads no KARMA_* variant from the environment: a stray variable can
+    never select a timing-only kernel (wrong CRCs) or change a plan."""
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    for knob in (b"KARMA_CRC_VARIANT", b"KARMA_RAGGED_VARIANT", b"KARMA_FOLD_MAX_K", b"KARMA_SPLIT_OVERDECOMPOSE",
+                 b"KARMA_WALK_VARIANT", b"KARMA_WALK_SUB", b"KARMA_WAL_SMALL_MAX"):
+        assert knob not in blob, knob

@@ -14,6 +14,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import karma_amd as K  # noqa: E402
 from karma_amd import _lib  # noqa: E402
+
+_lib._LIB = _lib.load(_lib.AB_LIB_PATH)  # the tools build: the KARMA_* A/B variants (karma_amd/csrc/ab.h)
 import synth  # noqa: E402
 
 L = _lib.lib()

@@ -14,6 +14,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import karma_amd as K  # noqa: E402
+from karma_amd import _lib  # noqa: E402
+
+_lib._LIB = _lib.load(_lib.AB_LIB_PATH)  # the tools build: the KARMA_* A/B variants (karma_amd/csrc/ab.h)
 
 variants = sys.argv[1:] or ["0", "1", "2", "6"]
 
