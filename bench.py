@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, GB/s (MI355X_MICROARCH.md chip table)
 GIB = float(1 << 30)
 METRIC = "CRC32C GiB/s device-resident, batched WAL records, 1/2/4/8 MI355X"
+CONFIG5_RECORDS = 256 << 20  # BASELINE configs[4]: 256M x 4 KiB records over 8 GPUs
 
 
 def parse():
@@ -42,27 +43,52 @@ def parse():
     p.add_argument("--wal-record", type=int, default=180, help="wal_* payload bytes (configs[0]: ~180 B)")
     p.add_argument("--wal-mix", default="fixed", choices=["fixed", "config3"],
                    help="wal_*: every payload --wal-record bytes, or configs[2]'s log-uniform 64 B-64 KiB mix (~4 GiB)")
-    p.add_argument("--records-per-gpu", type=int, default=1 << 20)
+    p.add_argument("--records-per-gpu", type=int, default=0,
+                   help="0 = the BASELINE config of the run: configs[1]'s 1M x 4 KiB per GPU, or with --gpus 8 "
+                        "configs[4]'s shard, 256M / 8 = 33,554,432 records of 4 KiB per GPU")
+    p.add_argument("--prewarm-ms", type=float, default=400.0,
+                   help="time-based burn of the same step before --warmup (the GPU's clocks settle: "
+                        "tools/ramp_probe.py, DESIGN.md §4); outside the timed region, reported as prewarm_ms")
     p.add_argument("--rec-bytes", type=int, default=4096)
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--call-events", choices=["auto", "on", "off"], default="auto",
                    help="bracket every call with its own events too (auto: when a call is more than one kernel)")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on (affinity)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_fixed_4k.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/profile.sh)")
     return p.parse_args()
 
 
 # ---------------------------------------------------------------------------------------------
-def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
+def host_cpus() -> int:
+    """CPUs this process may run on (its affinity mask)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - non-Linux
+        return os.cpu_count() or 1
+
+
+def cgroup_cpu_quota():
+    """The cgroup v2 CPU quota in CPUs (cpu.max), or None when unlimited / unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(workload: str, rec_bytes: int, threads: int, sample=None) -> dict:
     """Reference crc32c (oracle/_ref, built from /root/reference/karma-util/crc32c.cc) on host cores.
 
-    Bounded sample of the same workload, ~2 s on `threads` std::threads (records round-robin)
-    and ~2 s on one thread:
-      fixed/host -- 65536 records of rec_bytes of the same splitmix64 stream;
-      ragged     -- the first ~256 MiB of records of the configs[2] layout (same lengths, seed 7);
-      stream     -- 4 distinct 64 MiB segments (one thread per segment at most).
+    A bounded sample of the same workload, at least 1 GiB (larger than the host's last-level
+    cache, so it streams from DRAM like the device batch streams from HBM), checksummed for ~2 s
+    on `threads` std::threads (records round-robin; default: every CPU of the affinity mask), on
+    one thread, and on 16 threads (round 1's setting, kept for comparison):
+      fixed/host -- the first 1 GiB of records of the timed batch (`sample`, copied off the device);
+      ragged     -- the first ~1 GiB of records of the configs[2] layout (same lengths, seed 7);
+      stream     -- 16 distinct 64 MiB segments (one thread per segment at most).
     """
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib  # the CPU checker; only the cpu_baseline leg touches it
@@ -71,10 +97,11 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
     kind = "reference" if ref is not None else "port"
     if workload == "ragged":
         lens_all = synth.loguniform_lengths(7, 1 << 20, 64, 65536)
-        k = int(np.searchsorted(np.cumsum(lens_all, dtype=np.uint64), np.uint64(256 << 20)))
+        k = int(np.searchsorted(np.cumsum(lens_all, dtype=np.uint64), np.uint64(1 << 30)))
         lens = lens_all[:max(k, 1)].astype(np.uint32)
         offs, arena_bytes = synth.ragged_layout(lens, header=8)
-        buf = synth.splitmix_np(42, 0, arena_bytes + 16).copy()
+        buf = sample[: arena_bytes + 16] if sample is not None and sample.size >= arena_bytes + 16 else \
+            synth.splitmix_np(42, 0, arena_bytes + 16).copy()
         offs = np.ascontiguousarray(offs.astype(np.uint64))
         n, nbytes = lens.size, int(lens.sum())
         out = np.empty(n, dtype=np.uint32)
@@ -89,16 +116,19 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
                                                      out.ctypes.data, nthr)
     else:
         if workload in ("stream", "segment"):
-            rec_bytes, n = 64 << 20, 4
-            threads = min(threads, n)
+            rec_bytes, n = 64 << 20, 16
         else:
-            n = 65536 if rec_bytes <= 4096 else max(1, (256 << 20) // rec_bytes)
-        buf = synth.splitmix_np(42, 0, n * rec_bytes).copy()
-        out = np.empty(n, dtype=np.uint32)
+            n = max(1, (1 << 30) // rec_bytes)
         nbytes = n * rec_bytes
-        desc = f"{n} x {rec_bytes} B splitmix64 records ({nbytes >> 20} MiB)"
+        if sample is not None and sample.size >= nbytes:
+            buf = np.ascontiguousarray(sample[:nbytes])
+        else:
+            buf = synth.splitmix_np(42, 0, nbytes).copy()
+        out = np.empty(n, dtype=np.uint32)
+        desc = f"{n} x {rec_bytes} B splitmix64 records of the timed batch ({nbytes >> 20} MiB)"
 
         def run(nthr):
+            nthr = min(nthr, n)
             if ref is not None:
                 ref.ref_crc32c_fixed_mt(buf.ctypes.data, rec_bytes, n, out.ctypes.data, nthr)
             else:
@@ -116,6 +146,7 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
 
     multi, reps_m = rate(threads, 2.0)
     single, reps_s = rate(1, 2.0)
+    sixteen, _ = rate(16, 2.0) if threads != 16 else (multi, reps_m)
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as f:
@@ -126,9 +157,11 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int) -> dict:
     except OSError:
         pass
     return {"value": round(multi, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{desc}, crc32c::Value per record, round-robin over {threads} std::threads, "
-                      f"repeated {reps_m}x (~2 s)",
-            "single_thread_value": round(single, 3), "cpu_model": cpu, "host_cores_visible": os.cpu_count()}
+            "sample": f"{desc}, crc32c::Value per record, round-robin over {threads} std::threads "
+                      f"(every CPU of the affinity mask), repeated {reps_m}x (~2 s)",
+            "single_thread_value": round(single, 3), "threads16_value": round(sixteen, 3), "cpu_model": cpu,
+            "host_cpus_affinity": host_cpus(), "host_cpus_visible": os.cpu_count(),
+            "cgroup_cpu_quota": cgroup_cpu_quota()}
 
 
 def units_kernel_name(wl: str) -> str:
@@ -175,7 +208,7 @@ def wal_bench(args, L, rank):
         # every segment loses at most one record's header + payload to its footer
         wal_bytes = ((total + 8 * n) // (seg - 65544) + 2) * seg
     else:
-        n, size = args.records_per_gpu, args.wal_record
+        n, size = args.records_per_gpu or (1 << 20), args.wal_record
         lens = np.full(n, size, dtype=np.uint32)
         offs = (np.arange(n, dtype=np.uint64) * np.uint64(size)).astype(np.uint64)
         src = synth.splitmix_np(args.seed + rank, 0, n * size + 16).copy()
@@ -265,7 +298,7 @@ def wal_bench(args, L, rank):
         import oracle_lib
         ref = oracle_lib.ref()
         if ref is not None:
-            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+            thr = args.cpu_threads or min(16, host_cpus())  # 16 independent WALs (one per sivir io thread)
             k = min(n, 1 << 20)
             img = ((k // thr + per_seg - 1) // per_seg + 2) * seg
             imgs = np.zeros(img * thr, dtype=np.uint8)
@@ -307,7 +340,7 @@ def kfp_bench(args, L, rank):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import synth
     from karma_amd import _lib
-    n = args.records_per_gpu if args.records_per_gpu != (1 << 20) else (1 << 18)
+    n = args.records_per_gpu or (1 << 18)
     hl = np.full(n, 64, np.uint32)
     pl = np.full(n, args.rec_bytes, np.uint32)
     hsrc = synth.splitmix_np(args.seed + 2 * rank, 0, 64 * n + 8).copy()
@@ -356,6 +389,72 @@ def kfp_bench(args, L, rank):
             "roofline": None}
 
 
+def records_per_gpu(requested: int, world: int, workload: str):
+    """(records per GPU, is it BASELINE configs[4]'s shard): --records-per-gpu when given, else
+    configs[4] on 8 GPUs (256M x 4 KiB sharded: 33,554,432 per GPU, 128 GiB of HBM each) and
+    configs[1] otherwise (1M x 4 KiB per GPU)."""
+    if requested:
+        return requested, False
+    if world == 8 and workload == "fixed":
+        return CONFIG5_RECORDS // 8, True
+    return 1 << 20, False
+
+
+class TorchSync:
+    """Streams and events of the GPU run: the compute stream (the caller's), a second stream for
+    the gather, torch.cuda events between them."""
+
+    def __init__(self, torch, compute_stream):
+        self.torch = torch
+        self.compute_stream = compute_stream
+        self.gather_stream = torch.cuda.Stream()
+
+    def event(self):
+        return self.torch.cuda.Event()
+
+    def record(self, ev, stream):
+        ev.record(stream)
+
+    def wait(self, stream, ev):
+        stream.wait_event(ev)
+
+
+class GatherPipeline:
+    """The N > 1 step of the bench: step i checksums this rank's shard into outs[i % S] on the
+    compute stream; the gather of that buffer to rank 0 (karma_crc32c_gather_u32 over RCCL) runs
+    on the gather stream, ordered after the compute by an event, while step i + 1 computes into
+    the other buffer; step i + S first waits for the gather that last read its buffer.  With one
+    buffer and no gather (N = 1) a step is just the compute.
+
+    `compute(out)` enqueues the batch into `out`; `gather(out, stream)` enqueues the gather of
+    `out`; `sync` supplies streams and events (TorchSync here, a logging host stand-in in
+    tests/test_bench_pipeline.py, which drives this class over gloo on CPU)."""
+
+    def __init__(self, outs, compute, gather, sync):
+        self.outs, self.compute, self.gather, self.sync = outs, compute, gather, sync
+        self.computed = [sync.event() for _ in outs] if gather else []
+        self.gathered = [sync.event() for _ in outs] if gather else []
+        self.i = 0
+        self.current = outs[0]
+
+    def crc_step(self):
+        slot = self.i % len(self.outs)
+        if self.gather is not None and self.i >= len(self.outs):
+            self.sync.wait(self.sync.compute_stream, self.gathered[slot])  # its last gather is done
+        self.current = self.outs[slot]
+        self.compute(self.current)
+        self.i += 1
+
+    def gather_step(self):
+        if self.gather is None:
+            return
+        slot = (self.i - 1) % len(self.outs)  # the buffer the last crc_step wrote
+        self.sync.record(self.computed[slot], self.sync.compute_stream)
+        self.sync.wait(self.sync.gather_stream, self.computed[slot])
+        self.gather(self.outs[slot], self.sync.gather_stream)
+        self.sync.record(self.gathered[slot], self.sync.gather_stream)
+
+
 def main():
     args = parse()
     import torch
@@ -382,6 +481,7 @@ def main():
     sh = stream.cuda_stream
 
     comm = None
+    rccl_nranks = None
     if world > 1:
         import ctypes
         uid = (ctypes.c_char * _lib.UNIQUE_ID_BYTES)()
@@ -392,6 +492,11 @@ def main():
         uid = (ctypes.c_char * _lib.UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
         comm = ctypes.c_void_p()
         _lib.check("comm_init", L.karma_crc32c_comm_init(ctypes.byref(comm), world, uid, rank))
+        cnt = ctypes.c_int()
+        _lib.check("comm_count", L.karma_crc32c_comm_count(comm, ctypes.byref(cnt)))
+        rccl_nranks = cnt.value
+        if rccl_nranks != world:
+            raise SystemExit(f"RCCL reports {rccl_nranks} ranks, torch.distributed {world}")
 
     wl = args.workload
     if wl in ("wal_append", "wal_replay", "kfp_encode", "kfp_parse"):
@@ -404,7 +509,7 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
-    n_rec = args.records_per_gpu
+    n_rec, config5 = records_per_gpu(args.records_per_gpu, world, args.workload)
     rec = args.rec_bytes
     cur = {}  # the output buffer the next crc_step writes (double-buffered for N > 1)
     if wl == "fixed":
@@ -419,7 +524,11 @@ def main():
                 _lib.check("batch_fixed", st)
 
         algo_bytes = n_rec * (rec + 4)
-        workload_desc = f"{n_rec} x {rec} B records per GPU, batched CRC32C (BASELINE configs[1] shape)"
+        if config5:
+            workload_desc = f"{n_rec * world} x {rec} B records over {world} GPUs ({n_rec} per GPU), batched " \
+                            f"CRC32C + RCCL gather of the CRCs to rank 0 (BASELINE configs[4])"
+        else:
+            workload_desc = f"{n_rec} x {rec} B records per GPU, batched CRC32C (BASELINE configs[1] shape)"
     elif wl == "ragged":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import synth
@@ -492,6 +601,7 @@ def main():
         host = synth.splitmix_np(args.seed, rank * payload, payload).copy()
         hout = np.empty(n_rec, dtype=np.uint32)
         out = None
+        arena = None
 
         def crc_step():
             st = L.karma_crc32c_batch_fixed_host(host.ctypes.data, rec, n_rec, 0, hout.ctypes.data, local)
@@ -502,35 +612,34 @@ def main():
         workload_desc = f"{n_rec} x {rec} B records in pageable host memory -> H2D -> kernel -> D2H (synchronous)"
 
     gather_buf = torch.empty(n_rec * world, dtype=torch.uint32, device=dev) if (comm is not None and rank == 0) else None
-    # N > 1: the CRC gather of step i runs on its own stream while step i+1 computes into the
-    # other output buffer (double-buffered), so the collective overlaps the next kernel.
+    # N > 1: double-buffered outputs, the gather of step i overlapping step i + 1 (GatherPipeline)
     outs = [out, torch.empty_like(out)] if (comm is not None and out is not None) else [out]
-    gstream = torch.cuda.Stream() if comm is not None else None
-    computed = [torch.cuda.Event() for _ in outs]
-    gathered = [torch.cuda.Event() for _ in outs]
-    state = {"i": 0}
     kernel_step = crc_step
 
-    def crc_step():
-        slot = state["i"] % len(outs)
-        if gstream is not None and state["i"] >= len(outs):
-            stream.wait_event(gathered[slot])  # the gather that last read this buffer is done
-        cur["out"] = outs[slot]
+    def compute(o):
+        cur["out"] = o
         kernel_step()
-        state["i"] += 1
 
-    def gather_step():
-        if gstream is None or out is None:
-            return
-        slot = (state["i"] - 1) % len(outs)  # the buffer the last crc_step wrote
-        computed[slot].record(stream)
-        gstream.wait_event(computed[slot])
-        st = L.karma_crc32c_gather_u32(comm, outs[slot].data_ptr(), n_rec,
-                                       gather_buf.data_ptr() if gather_buf is not None else None, 0,
-                                       gstream.cuda_stream)
+    def gather(o, gs):
+        st = L.karma_crc32c_gather_u32(comm, o.data_ptr(), n_rec,
+                                       gather_buf.data_ptr() if gather_buf is not None else None, 0, gs.cuda_stream)
         if st:
             _lib.check("gather_u32", st)
-        gathered[slot].record(gstream)
+
+    pipe = GatherPipeline(outs, compute, gather if (comm is not None and out is not None) else None,
+                          TorchSync(torch, stream))
+    crc_step, gather_step = pipe.crc_step, pipe.gather_step
+
+    # ---- pre-warm: the batch alone (no collective: ranks stop at different counts) for a fixed
+    # time, so the clocks settle before --warmup (tools/ramp_probe.py) -----------
+    prewarm_ms = 0.0
+    if args.prewarm_ms > 0:
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < args.prewarm_ms:
+            for _ in range(4):
+                compute(outs[0])
+            torch.cuda.synchronize()
+        prewarm_ms = (time.perf_counter() - t0) * 1e3
 
     # ---- warmup -------------------------------------------------------------------------
     for _ in range(args.warmup):
@@ -639,13 +748,18 @@ def main():
                          "call_ms_avg": round(call_avg, 4),
                          "call_frac": round(algo_bytes / (call_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "compute_only_gibs": round(payload * world / (call_max * 1e-3) / GIB, 2),
+            "prewarm_ms": round(prewarm_ms, 1),
+            "rccl_nranks": rccl_nranks,
         }
         res.update(extra)
         if check:
             res["self_check"] = check
         if world == 1 and not args.no_cpu_baseline:
-            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            res["cpu_baseline"] = cpu_baseline(wl, rec, thr)
+            thr = args.cpu_threads or host_cpus()
+            sample = None
+            if wl in ("fixed", "stream", "ragged") and arena is not None:  # the first 1 GiB of the timed input
+                sample = arena[: min(arena.numel(), (1 << 30) + 16)].cpu().numpy()
+            res["cpu_baseline"] = cpu_baseline(wl, rec, thr, sample)
         print(json.dumps(res), flush=True)
 
     if comm is not None:

@@ -71,10 +71,19 @@ int karma_crc32c_batch_fixed(const void* d_data, size_t rec_bytes, size_t n_rec,
 /* d_out[r] = Extend(init_r, d_arena + d_off[r], d_len[r]).  Records may be
  * unaligned, empty, in any order and may overlap.  total_len sizes the unit
  * table: pass sum(d_len) (or any upper bound) to stay fully asynchronous;
- * pass 0 when unknown and the call reads the unit count back (one host sync). */
+ * pass 0 when unknown and the call reads the unit count back (one host sync).
+ * A total_len below sum(d_len) is not an error and never changes a result: the
+ * records whose units do not fit the table are checksummed one lane each. */
 int karma_crc32c_batch_ragged(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
                               size_t total_len, const uint32_t* d_init, uint32_t init, uint32_t* d_out,
                               karma_stream_t stream);
+
+/* The same with an upper bound of every d_len[r] (0 = unknown).  With max_len <= 1 KiB
+ * (WAL records, KFP frames) each record is checksummed by one group of 8 lanes with no
+ * planning kernels.  The result is exact whatever the bound: a wrong one costs balance. */
+int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
+                                      size_t total_len, uint32_t max_len, const uint32_t* d_init, uint32_t init,
+                                      uint32_t* d_out, karma_stream_t stream);
 
 /* *d_out = Extend(init, d_data, n): one long buffer split over the whole GPU
  * and folded back with a polynomial combine. */
@@ -90,6 +99,8 @@ int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, cons
 int karma_crc32c_get_unique_id(void* uid, size_t uid_bytes);
 int karma_crc32c_comm_init(karma_comm_t* comm, int nranks, const void* uid, int rank);
 int karma_crc32c_comm_destroy(karma_comm_t comm);
+/* *nranks = the ranks RCCL itself reports for the communicator (ncclCommCount). */
+int karma_crc32c_comm_count(karma_comm_t comm, int* nranks);
 /* d_recv (root only, count*nranks words) <- every rank's d_send (count words), rank order. */
 int karma_crc32c_gather_u32(karma_comm_t comm, const uint32_t* d_send, size_t count, uint32_t* d_recv, int root,
                             karma_stream_t stream);
@@ -109,11 +120,14 @@ int karma_crc32c_batch_fixed_sharded(karma_comm_t comm, const void* d_local, siz
 
 /* Batched append (sivir::build_sqe + segment_file::append_record / append_footer):
  * frame payloads i = 0..n-1 (h_src + h_src_off[i], h_len[i]) at WAL offset *h_cursor,
- * closing a segment with a footer when a record does not fit (can_hold).  The CRCs of
- * the whole batch come from one GPU batch.  Updates *h_cursor, writes the header offset
- * of record i to h_rec_off[i] (optional) and the number framed to *h_n_framed (records
- * that do not fit in the image are left out).  On an error *h_cursor is unchanged;
- * bytes past it may have been written (without valid CRC fields). */
+ * closing a segment with a footer when a record does not fit (can_hold).  The payload
+ * CRCs are computed on the GPU, block by block while the host frames (the payloads are
+ * streamed through the library's pinned staging; the caller's memory is never
+ * page-locked).  Updates *h_cursor, writes the header offset of record i to
+ * h_rec_off[i] (optional) and the number framed to *h_n_framed (records that do not fit
+ * in the image are left out).  Batches of more than 1 GiB of payload are framed in
+ * passes; on an error *h_cursor / *h_n_framed cover the passes completed, and bytes
+ * past *h_cursor may have been written (without valid CRC fields). */
 int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const uint32_t* h_len, size_t n,
                            void* h_wal, size_t wal_bytes, size_t seg_bytes, uint64_t* h_cursor, uint64_t* h_rec_off,
                            size_t* h_n_framed, int device);

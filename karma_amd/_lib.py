@@ -39,12 +39,14 @@ SIGNATURES = {
     "karma_crc32c_combine": (_u32, [_u32, _u32, _u64]),
     "karma_crc32c_batch_fixed": (_i, [_vp, _sz, _sz, _vp, _u32, _vp, _vp]),
     "karma_crc32c_batch_ragged": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp]),
+    "karma_crc32c_batch_ragged_bounded": (_i, [_vp, _vp, _vp, _sz, _sz, _u32, _vp, _u32, _vp, _vp]),
     "karma_crc32c_stream": (_i, [_u32, _vp, _sz, _vp, _vp]),
     "karma_crc32c_batch_fixed_host": (_i, [_vp, _sz, _sz, _u32, _vp, _i]),
     "karma_crc32c_batch_ragged_host": (_i, [_vp, _sz, _vp, _vp, _sz, _u32, _vp, _i]),
     "karma_crc32c_get_unique_id": (_i, [_vp, _sz]),
     "karma_crc32c_comm_init": (_i, [_c.POINTER(_vp), _i, _vp, _i]),
     "karma_crc32c_comm_destroy": (_i, [_vp]),
+    "karma_crc32c_comm_count": (_i, [_vp, _c.POINTER(_i)]),
     "karma_crc32c_gather_u32": (_i, [_vp, _vp, _sz, _vp, _i, _vp]),
     "karma_crc32c_batch_fixed_sharded": (_i, [_vp, _vp, _sz, _sz, _u32, _vp, _vp, _i, _vp]),
     "karma_wal_append_batch": (_i, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, _c.POINTER(_u64), _vp, _c.POINTER(_sz), _i]),

@@ -48,6 +48,7 @@ int hip_fail(hipError_t e, const char* what) {
     } while (0)
 
 constexpr uint64_t kMinSplitUnit = 2048;  // smallest unit when records are split
+constexpr uint32_t kDirectMaxLen = 1024;  // ragged records up to this: one record per group
 constexpr uint64_t kOverdecompose = 4;    // units per group before splitting records
 constexpr uint64_t kSplitOverdecompose = 64;  // units per group once split (2 KiB units up to 4 GiB
                                               // batches; 4: config 4 0.653 ms, 64: 0.609)
@@ -352,20 +353,7 @@ struct Locked {
 namespace karma::engine {
 int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
                        uint32_t* d_out, hipStream_t s) {
-    if (n_rec == 0) return KARMA_OK;
-    Locked L;
-    if (L.rc) return L.rc;
-    RaggedArgs a{};
-    a.arena = static_cast<const uint8_t*>(d_arena);
-    a.off = d_off;
-    a.len = d_len;
-    a.n_rec = n_rec;
-    a.init = nullptr;
-    a.init_scalar = 0;
-    a.out = d_out;
-    a.blob = L.ds->blob;
-    KARMA_HIP(launch_ragged_direct(a, L.ds->cu, s));
-    return KARMA_OK;
+    return karma_crc32c_batch_ragged_bounded(d_arena, d_off, d_len, n_rec, 0, 1, nullptr, 0, d_out, s);
 }
 namespace {
 thread_local hipEvent_t t_units_start = nullptr, t_units_stop = nullptr;
@@ -426,10 +414,31 @@ int karma_crc32c_batch_fixed(const void* d_data, size_t rec_bytes, size_t n_rec,
 int karma_crc32c_batch_ragged(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
                               size_t total_len, const uint32_t* d_init, uint32_t init, uint32_t* d_out,
                               karma_stream_t stream) {
+    return karma_crc32c_batch_ragged_bounded(d_arena, d_off, d_len, n_rec, total_len, 0, d_init, init, d_out, stream);
+}
+
+int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
+                                      size_t total_len, uint32_t max_len, const uint32_t* d_init, uint32_t init,
+                                      uint32_t* d_out, karma_stream_t stream) {
     if (n_rec == 0) return KARMA_OK;
     if (!d_out || !d_off || !d_len) return fail(KARMA_E_INVALID, "batch_ragged: null pointer");
     Locked L;
     if (L.rc) return L.rc;
+    if (max_len && max_len <= kDirectMaxLen) {
+        // every record small: one record per group, no plan kernels (k_ragged_direct); exact for
+        // any length, so a wrong bound costs balance, never correctness
+        RaggedArgs a{};
+        a.arena = static_cast<const uint8_t*>(d_arena);
+        a.off = d_off;
+        a.len = d_len;
+        a.n_rec = n_rec;
+        a.init = d_init;
+        a.init_scalar = init;
+        a.out = d_out;
+        a.blob = L.ds->blob;
+        KARMA_HIP(launch_ragged_direct(a, L.ds->cu, (hipStream_t)stream));
+        return KARMA_OK;
+    }
     return ragged_locked(L.dev, *L.ds, d_arena, d_off, d_len, n_rec, total_len, d_init, init, d_out,
                          (hipStream_t)stream);
 }

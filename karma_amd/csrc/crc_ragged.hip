@@ -32,10 +32,6 @@ using namespace dev;
 constexpr int kRaggedPF = 4;
 constexpr bool kRaggedNT = true;
 
-#ifndef KARMA_SCAN_BLOCK
-#define KARMA_SCAN_BLOCK 1024  // records per scan/desc block: a build-time A/B knob (tools/scan_block_ab.sh)
-#endif
-constexpr int kScanBlock = KARMA_SCAN_BLOCK;
 static_assert(kScanBlock % 64 == 0 && kScanBlock <= 1024 && kScanBlock >= kBuckets, "scan block shape");
 constexpr uint64_t kU = kDefaultUnit;  // ragged units: absolute kU-byte boundaries
 constexpr int kUShift = __builtin_ctzll(kDefaultUnit);
@@ -456,13 +452,12 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
         if (ok && u.k >= 2)  // the last unit: shift by its own length
             acc = shift_last(lds, acc, u.last, U) ^ A.partial[unit_slot(u.k - 1, u.k, fb, ps0, ps1, u.part0, u.part1)];
         if (valid) {
-            uint32_t res = 0;
-            if (ok) {
-                if (u.k == 0)
-                    res = short_record(lds, kCombZ4, kCombT8, p, A.len[r], init);
-                else
-                    res = ~tail_register(lds, kCombZ4, kCombT8, acc, u.g);
-            }
+            uint32_t res;
+            if (ok && u.k > 0)
+                res = ~tail_register(lds, kCombZ4, kCombT8, acc, u.g);
+            else  // a short record, or (the caller's total_len was low) one whose units did not
+                  // fit the table: this lane steps it alone -- slow, but never a wrong CRC
+                res = short_record(lds, kCombZ4, kCombT8, p, A.len[r], init);
             A.out[r] = res;
         }
     }
@@ -527,8 +522,6 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
     units_timer_end(s);
     return hipGetLastError();
 }
-
-uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock - 1) / kScanBlock; }
 
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;

@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 
 namespace karma {
 namespace engine {
@@ -129,7 +130,11 @@ hipError_t launch_combine_fixed(const FixedArgs& a, const uint32_t* in_states, u
 // launch: one 1024-thread block per record, m = ceil(k_in / 1024) states per thread.
 hipError_t launch_combine_block(const FixedArgs& a, const uint32_t* in_states, uint64_t k_in, uint64_t m,
                                 const uint32_t* block_blob, hipStream_t s);
-uint64_t ragged_scan_blocks(uint64_t n_rec);
+#ifndef KARMA_SCAN_BLOCK
+#define KARMA_SCAN_BLOCK 1024  // records per scan/desc block: a build-time A/B knob (tools/scan_block_ab.sh)
+#endif
+constexpr int kScanBlock = KARMA_SCAN_BLOCK;
+inline uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock - 1) / kScanBlock; }
 // Ragged: scan (full-unit offsets + partial-unit buckets; total units at
 // fbase[n_rec]), then descriptors, the unit kernel and the per-record finalize.
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
@@ -180,15 +185,27 @@ struct WalArgs {
     WalSubMeta* sub;           // per (segment, sub-range) walker
     uint32_t* span;            // per (segment, sub-range): first list slot of the accepted run, candidates before it
 };
+constexpr uint32_t kWalkTile = 4096;  // the one-wave walker's LDS tile (wal_device.hip)
+constexpr uint32_t kMaxSub = 4096;    // sub-ranges per segment (k_wal_gather stages their runs in LDS)
 struct WalWalkPlan {
     uint64_t nsub, sub_bytes, sub_cap, cand_cap;
     int kernel;  // 0: sub-range walkers (+ resolve when nsub > 1), 1: one workgroup per segment
 };
-// sub_bytes: 0 = the planner's split, else the forced sub-range size (karma_wal_tuning).
+// Host planner (wal.cc).  sub_bytes: 0 = the planner's split, else the forced sub-range
+// size (karma_wal_tuning).
 WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes);
 hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s);
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s);
 hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);
+
+// ---- KFP frames (kfp.cc) ----------------------------------------------------
+struct KfpWalk {
+    std::vector<uint64_t> frame, span_off;  // frame offsets; the CRC span of each (header + payload)
+    std::vector<uint32_t> span_len, stored;  // span lengths; the CRC stored in each frame
+    uint64_t consumed = 0;                   // bytes of the accepted frames
+};
+// The structural part of connection::read_frame's parse loop over buf; returns KARMA_KFP_*.
+int kfp_walk(const uint8_t* buf, size_t buf_bytes, size_t max_frames, KfpWalk* out);
 
 // Synthetic data: bytes of the counter-based splitmix64 stream.
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n_bytes, uint64_t seed, uint64_t first_byte, hipStream_t s);

@@ -1,0 +1,129 @@
+// karma_amd/csrc/host_stage.cc -- pinned staging uploads (host_stage.h).
+#include "host_stage.h"
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "karma_crc32c.h"
+
+namespace karma::engine {
+int set_last_error(int code, const std::string& what);  // capi.cc
+
+namespace {
+
+constexpr int kWorkers = 8;                  // copy threads, one DMA stream each
+constexpr size_t kChunk = size_t(8) << 20;   // bytes per pinned buffer (two per worker)
+
+struct Stage {
+    std::mutex mu;
+    bool ready = false;
+    hipStream_t st[kWorkers] = {};
+    hipEvent_t ev[kWorkers][2] = {};
+    void* buf[kWorkers][2] = {};
+    int init() {
+        if (ready) return 0;
+        for (int t = 0; t < kWorkers; ++t) {
+            if (hipStreamCreateWithFlags(&st[t], hipStreamNonBlocking) != hipSuccess)
+                return set_last_error(KARMA_E_HIP, "staging: stream");
+            for (int k = 0; k < 2; ++k) {
+                if (hipEventCreateWithFlags(&ev[t][k], hipEventDisableTiming) != hipSuccess)
+                    return set_last_error(KARMA_E_HIP, "staging: event");
+                if (hipHostMalloc(&buf[t][k], kChunk, hipHostMallocDefault) != hipSuccess) {
+                    buf[t][k] = nullptr;
+                    return set_last_error(KARMA_E_NOMEM, "staging: pinned buffer");
+                }
+            }
+        }
+        ready = true;
+        return 0;
+    }
+};
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<Stage>> g_stage;
+
+Stage& stage_for(int dev) {
+    std::lock_guard<std::mutex> g(g_mu);
+    if ((int)g_stage.size() <= dev) g_stage.resize(dev + 1);
+    if (!g_stage[dev]) g_stage[dev] = std::make_unique<Stage>();
+    return *g_stage[dev];
+}
+
+}  // namespace
+
+void run_threads(int n, const std::function<void(int)>& body) {
+    if (n <= 1) {
+        if (n == 1) body(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (int t = 0; t < n; ++t) th.emplace_back(body, t);
+    for (auto& x : th) x.join();
+}
+
+bool host_is_pinned(const void* h) {
+    if (!h) return false;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, h) == hipSuccess) return attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // pageable memory is unknown to the runtime
+    return false;
+}
+
+int staged_upload(int dev, void* d_dst, const HostFill& fill, uint64_t src_off, size_t bytes) {
+    if (!bytes) return 0;
+    Stage& S = stage_for(dev);
+    std::lock_guard<std::mutex> lk(S.mu);
+    if (const int rc = S.init()) return rc;
+    const size_t nchunk = (bytes + kChunk - 1) / kChunk;
+    const int nthr = (int)std::min<size_t>(kWorkers, nchunk);
+    std::vector<int> rcs(nthr, 0);
+    // worker t copies chunks t, t + T, ... into its two buffers (alternating) and DMAs each
+    // one on its own stream; a buffer is refilled once its previous DMA has completed
+    run_threads(nthr, [&](int t) {
+        if (hipSetDevice(dev) != hipSuccess) {
+            rcs[t] = KARMA_E_HIP;
+            return;
+        }
+        int k = 0;
+        for (size_t i = t; i < nchunk; i += nthr, k ^= 1) {
+            const size_t o = i * kChunk, n = std::min(kChunk, bytes - o);
+            if (hipEventSynchronize(S.ev[t][k]) != hipSuccess) {
+                rcs[t] = KARMA_E_HIP;
+                return;
+            }
+            if (const int rc = fill(static_cast<uint8_t*>(S.buf[t][k]), src_off + o, n)) {
+                rcs[t] = rc;
+                return;
+            }
+            if (hipMemcpyAsync(static_cast<uint8_t*>(d_dst) + o, S.buf[t][k], n, hipMemcpyHostToDevice, S.st[t]) !=
+                    hipSuccess ||
+                hipEventRecord(S.ev[t][k], S.st[t]) != hipSuccess) {
+                rcs[t] = KARMA_E_HIP;
+                return;
+            }
+        }
+        if (hipStreamSynchronize(S.st[t]) != hipSuccess) rcs[t] = KARMA_E_HIP;
+    });
+    for (int rc : rcs)
+        if (rc) return rc == KARMA_E_IO ? rc : set_last_error(rc, "staged upload");
+    return 0;
+}
+
+int staged_copy(int dev, void* d_dst, const void* h_src, size_t bytes) {
+    const uint8_t* src = static_cast<const uint8_t*>(h_src);
+    return staged_upload(
+        dev, d_dst,
+        [src](uint8_t* dst, uint64_t off, size_t n) {
+            std::memcpy(dst, src + off, n);
+            return 0;
+        },
+        0, bytes);
+}
+
+}  // namespace karma::engine

@@ -24,6 +24,7 @@
 #include <thread>
 #include <vector>
 
+#include "engine.h"
 #include "karma_crc32c.h"
 
 namespace karma::engine {
@@ -39,7 +40,11 @@ int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std:
                                                       out.data(), device);
     // device copy supplied: stage the offsets/lengths and run the device batch
     uint64_t total = 0;
-    for (uint32_t l : len) total += l;
+    uint32_t max_len = 0;
+    for (uint32_t l : len) {
+        total += l;
+        max_len = std::max(max_len, l);
+    }
     if (device >= 0 && hipSetDevice(device) != hipSuccess) return set_last_error(KARMA_E_HIP, "hipSetDevice");
     void *doff = nullptr, *dlen = nullptr, *dout = nullptr;
     int rc = 0;
@@ -49,8 +54,9 @@ int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std:
     else if (hipMemcpy(doff, off.data(), off.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
              hipMemcpy(dlen, len.data(), len.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         rc = set_last_error(KARMA_E_HIP, "crc_spans: hipMemcpy H2D");
-    else if ((rc = karma_crc32c_batch_ragged(d_buf, static_cast<uint64_t*>(doff), static_cast<uint32_t*>(dlen),
-                                             off.size(), total, nullptr, 0, static_cast<uint32_t*>(dout), nullptr)))
+    else if ((rc = karma_crc32c_batch_ragged_bounded(d_buf, static_cast<uint64_t*>(doff), static_cast<uint32_t*>(dlen),
+                                                     off.size(), total, max_len, nullptr, 0,
+                                                     static_cast<uint32_t*>(dout), nullptr)))
         ;
     else if (hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
         rc = set_last_error(KARMA_E_HIP, "crc_spans: hipMemcpy D2H");
@@ -58,6 +64,50 @@ int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std:
     (void)hipFree(dlen);
     (void)hipFree(dout);
     return rc;
+}
+
+// frame::parse at the cursor, advance by frame_length, repeat (connection::read_frame,
+// connection.cc:20-27): the structural checks in parse's order (frame.cc:64-116), without
+// the CRC, which the caller verifies for all frames at once.
+int kfp_walk(const uint8_t* b, size_t buf_bytes, size_t max_frames, KfpWalk* W) {
+    constexpr uint32_t kFixed = KARMA_KFP_FIXED_HEADER, kCrcLen = 4;  // frame.h:21-22
+    auto le32 = [](const uint8_t* p) {
+        uint32_t v;
+        std::memcpy(&v, p, 4);
+        return v;
+    };
+    uint64_t cur = 0;
+    int status = KARMA_KFP_OK;
+    while (W->frame.size() < max_frames) {
+        const uint64_t avail = buf_bytes - cur;
+        if (avail < kFixed + kCrcLen) break;  // nullopt: wait for more bytes (:64-66)
+        const uint32_t fl = le32(b + cur);
+        if (fl > KARMA_KFP_MAX_FRAME) {  // throws "decoded frame size is larger than the limit" (:70-73)
+            status = KARMA_KFP_BAD_SIZE;
+            break;
+        }
+        if (avail < fl) break;                  // nullopt: incomplete frame (:75-77)
+        if (b[cur + 4] != KARMA_KFP_MAGIC) {    // throws "Wrong magic code" (:86-89)
+            status = KARMA_KFP_BAD_MAGIC;
+            break;
+        }
+        if (fl < kFixed + kCrcLen) {  // unsigned wrap in :101 and :111-113: undefined in the reference
+            status = KARMA_KFP_BAD_LENGTH;
+            break;
+        }
+        const uint32_t hl = le32(b + cur + 12);
+        if (hl > fl - kFixed - kCrcLen) {  // throws "Wrong header length" (:101-104)
+            status = KARMA_KFP_BAD_HEADER_LEN;
+            break;
+        }
+        W->frame.push_back(cur);
+        W->span_off.push_back(cur + kFixed);
+        W->span_len.push_back(fl - kFixed - kCrcLen);
+        W->stored.push_back(le32(b + cur + fl - kCrcLen));
+        cur += fl;  // read_frame erases frame->size() == frame_length bytes (connection.cc:25)
+    }
+    W->consumed = cur;
+    return status;
 }
 }  // namespace karma::engine
 
@@ -104,12 +154,10 @@ int karma_kfp_encode_batch(const void* h_hdr, const uint64_t* h_hdr_off, const u
         cur += fl;
     }
     // 2. frames written by 16 threads, piece by piece; 3. each written piece's
-    //    CRCs, Extend(Value(header), payload) = Value(frame[16, 16 + hl + pl)), in one
+    //    CRCs (streamed to the device through the pinned staging, host_stage.h), Extend(Value(header), payload) = Value(frame[16, 16 + hl + pl)), in one
     //    GPU batch on a worker thread while the next piece is written
     constexpr size_t kPieces = 4;
     const size_t npc = ne >= 4 * 4096 ? kPieces : 1;
-    const bool pinned = cur && hipHostRegister(out, cur, hipHostRegisterDefault) == hipSuccess;
-    if (!pinned) (void)hipGetLastError();  // pageable copies still work
     std::atomic<size_t> written{0};
     int crc_rc = 0;
     std::thread gpu([&] {
@@ -152,7 +200,6 @@ int karma_kfp_encode_batch(const void* h_hdr, const uint64_t* h_hdr_off, const u
         written.store(p + 1, std::memory_order_release);
     }
     gpu.join();
-    if (pinned) (void)hipHostUnregister(out);
     if (crc_rc) return crc_rc;
     *h_n_encoded = ne;
     *h_bytes = cur;
@@ -164,46 +211,18 @@ int karma_kfp_parse_batch(const void* h_buf, const void* d_buf, size_t buf_bytes
                           int device) {
     if (!h_n_frames || !h_consumed || !h_status || (buf_bytes && !h_buf))
         return fail(KARMA_E_INVALID, "kfp_parse_batch: null argument");
-    const uint8_t* b = static_cast<const uint8_t*>(h_buf);
     // 1. structural walk: parse's checks in its order (frame.cc:64-116)
-    std::vector<uint64_t> frame, span_off;
-    std::vector<uint32_t> span_len, stored;
-    uint64_t cur = 0;
-    int status = KARMA_KFP_OK;
-    while (frame.size() < max_frames) {
-        const uint64_t avail = buf_bytes - cur;
-        if (avail < kFixed + kCrcLen) break;  // nullopt: wait for more bytes (:64-66)
-        const uint32_t fl = le32(b + cur);
-        if (fl > KARMA_KFP_MAX_FRAME) {  // throws "decoded frame size is larger than the limit" (:70-73)
-            status = KARMA_KFP_BAD_SIZE;
-            break;
-        }
-        if (avail < fl) break;                  // nullopt: incomplete frame (:75-77)
-        if (b[cur + 4] != KARMA_KFP_MAGIC) {    // throws "Wrong magic code" (:86-89)
-            status = KARMA_KFP_BAD_MAGIC;
-            break;
-        }
-        if (fl < kFixed + kCrcLen) {  // unsigned wrap in :101 and :111-113: undefined in the reference
-            status = KARMA_KFP_BAD_LENGTH;
-            break;
-        }
-        const uint32_t hl = le32(b + cur + 12);
-        if (hl > fl - kFixed - kCrcLen) {  // throws "Wrong header length" (:101-104)
-            status = KARMA_KFP_BAD_HEADER_LEN;
-            break;
-        }
-        frame.push_back(cur);
-        span_off.push_back(cur + kFixed);
-        span_len.push_back(fl - kFixed - kCrcLen);
-        stored.push_back(le32(b + cur + fl - kCrcLen));
-        cur += fl;  // read_frame erases frame->size() == frame_length bytes (connection.cc:25)
-    }
+    karma::engine::KfpWalk W;
+    int status = karma::engine::kfp_walk(static_cast<const uint8_t*>(h_buf), buf_bytes, max_frames, &W);
+    uint64_t cur = W.consumed;
+    const std::vector<uint64_t>& frame = W.frame;
     // 2. every frame's crc in one GPU batch; the first mismatch throws "Wrong crc32" (:125-128)
     std::vector<uint32_t> got;
-    if (const int rc = karma::engine::crc_spans(h_buf, d_buf, buf_bytes, span_off, span_len, got, device)) return rc;
+    if (const int rc = karma::engine::crc_spans(h_buf, d_buf, buf_bytes, W.span_off, W.span_len, got, device))
+        return rc;
     size_t ok = frame.size();
     for (size_t k = 0; k < got.size(); ++k)
-        if (got[k] != stored[k]) {
+        if (got[k] != W.stored[k]) {
             ok = k;
             status = KARMA_KFP_BAD_CRC;
             cur = frame[k];

@@ -31,6 +31,7 @@ struct Rccl {
     ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
     ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*commCount)(const ncclComm_t, int*) = nullptr;
     const char* (*getErrorString)(ncclResult_t) = nullptr;
     ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
@@ -62,6 +63,7 @@ Rccl& rccl() {
         bind(r.h, r.getUniqueId, "ncclGetUniqueId");
         bind(r.h, r.commInitRank, "ncclCommInitRank");
         bind(r.h, r.commDestroy, "ncclCommDestroy");
+        bind(r.h, r.commCount, "ncclCommCount");
         bind(r.h, r.getErrorString, "ncclGetErrorString");
         bind(r.h, r.gather, "ncclGather");
         bind(r.h, r.send, "ncclSend");
@@ -124,6 +126,19 @@ int karma_crc32c_comm_destroy(karma_comm_t comm) {
     const ncclResult_t e = r.h ? r.commDestroy(comm->nc) : ncclSuccess;
     delete comm;
     if (e != ncclSuccess) return rfail(std::string("ncclCommDestroy: ") + r.getErrorString(e));
+    return 0;
+}
+
+int karma_crc32c_comm_count(karma_comm_t comm, int* nranks) {
+    if (!comm || !nranks) return KARMA_E_INVALID;
+    Rccl& r = rccl();
+    if (!r.h) return rfail(r.error);
+    if (!r.commCount) {  // an RCCL without ncclCommCount: the size the communicator was built with
+        *nranks = comm->nranks;
+        return 0;
+    }
+    const ncclResult_t e = r.commCount(comm->nc, nranks);
+    if (e != ncclSuccess) return rfail(std::string("ncclCommCount: ") + r.getErrorString(e));
     return 0;
 }
 

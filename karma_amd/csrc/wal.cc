@@ -7,10 +7,7 @@
 // (segment_file.cc:33-49); a segment tail shorter than a header is padded
 // with '0' bytes only (:34-39).
 //
-// karma_wal_append_batch  = sivir::build_sqe's loop (sivir.cc:276-317): for
-//   each payload, segment.can_hold (segment_file.cc:74-77) or close the
-//   segment with append_footer and move on; then append_record.  The
-//   payload CRCs of the whole batch are computed in one GPU ragged batch.
+// (karma_wal_append_batch, sivir::build_sqe's loop, is in wal_append.cc.)
 // karma_wal_replay        = sivir::open's loop over wal::scan_record
 //   (sivir.cc:31-41, wal.cc:34-87), entirely on the device over an image in
 //   HBM (wal_device.hip): segment-parallel header walk, one ragged CRC batch
@@ -38,12 +35,45 @@
 #include <thread>
 #include <vector>
 
+#include "ab.h"
 #include "engine.h"
+#include "host_stage.h"
 #include "host_trace.h"
 #include "karma_crc32c.h"
 
 namespace karma::engine {
 int set_last_error(int code, const std::string& what);  // capi.cc
+
+// How the walk splits the segments.  The header chain is serial inside a
+// segment, so few segments leave most of the GPU idle: each segment is then cut
+// into sub-ranges (at least 16 KiB) so that about 16 walkers per CU run, and
+// k_wal_resolve stitches their lists.  Many segments: one walker per segment.
+// sub_bytes != 0 forces the sub-range size (karma_wal_tuning: tests, tuning);
+// the tools build's KARMA_WALK_VARIANT=1 (ab.h) selects k_wal_walk instead.
+WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes) {
+    WalWalkPlan p{1, 0, 0, 0, 0};
+    const uint64_t tiles = (seg_bytes + kWalkTile - 1) / kWalkTile;
+    uint64_t sub_tiles = tiles;
+    if (KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 1) {
+        p.kernel = 1;
+    } else if (sub_bytes) {
+        sub_tiles = std::max<uint64_t>(1, sub_bytes / kWalkTile);
+    } else {
+        const uint64_t want = 16 * (uint64_t)(cu > 0 ? cu : 1);  // walkers
+        if (nseg > 0 && nseg < want) {
+            const uint64_t per = (want + nseg - 1) / nseg;  // sub-ranges per segment
+            sub_tiles = std::max<uint64_t>(4, (tiles + per - 1) / per);
+        }
+    }
+    sub_tiles = std::min(sub_tiles, tiles);
+    sub_tiles = std::max(sub_tiles, (tiles + kMaxSub - 1) / kMaxSub);
+    p.sub_bytes = sub_tiles * kWalkTile;
+    p.nsub = p.kernel == 1 ? 1 : (seg_bytes + p.sub_bytes - 1) / p.sub_bytes;
+    if (p.nsub == 1) p.sub_bytes = seg_bytes;
+    p.sub_cap = p.sub_bytes / 8 + 1;
+    p.cand_cap = p.nsub * p.sub_cap;
+    return p;
+}
 
 }  // namespace karma::engine
 
@@ -107,9 +137,7 @@ struct DevBuf {
     }
 };
 
-constexpr int kUpThreads = 8;                   // upload workers
 constexpr uint32_t kSmallRecordMax = 1024;      // payloads up to this take the one-record-per-group batch
-constexpr size_t kUpChunk = size_t(8) << 20;    // bytes per staging buffer
 struct ReplayCtx {
     std::mutex mu;
     bool ready = false;
@@ -117,20 +145,12 @@ struct ReplayCtx {
     hipStream_t st = nullptr;
     DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, bad;
     DevBuf h_meta, h_small;                     // pinned readbacks
-    hipStream_t up_st[kUpThreads] = {};
-    hipEvent_t up_ev[kUpThreads][2] = {};
-    DevBuf stage[kUpThreads][2];
     int init(int dev) {
         if (ready) return 0;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(KARMA_E_HIP, "hipGetDeviceProperties");
         cu = std::max(1, prop.multiProcessorCount);
         if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return fail(KARMA_E_HIP, "stream");
-        for (int t = 0; t < kUpThreads; ++t) {
-            if (hipStreamCreateWithFlags(&up_st[t], hipStreamNonBlocking) != hipSuccess) return fail(KARMA_E_HIP, "stream");
-            for (auto& e : up_ev[t])
-                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(KARMA_E_HIP, "event");
-        }
         ready = true;
         return 0;
     }
@@ -145,54 +165,9 @@ ReplayCtx& replay_ctx(int dev) {
     return *g_rctx[dev];
 }
 
-// Host image -> device buffer without page-locking the caller's memory: worker t
-// copies chunks t, t + T, ... into its two pinned staging buffers (alternating)
-// and DMAs each one on its own stream, so the memcpy of one chunk overlaps the
-// DMA of the previous and T copies run at once.
-// Fills dst with image bytes [off, off + n) (offsets relative to the image start).
-using ImageFill = std::function<int(uint8_t* dst, uint64_t off, size_t n)>;
-
-// Streams image bytes [src_off, src_off + bytes) into d_dst through the pinned staging
-// buffers: kUpThreads threads each fill one buffer (fill) while the other's DMA runs.
-int upload_staged(ReplayCtx& c, void* d_dst, const ImageFill& fill, uint64_t src_off, size_t bytes, int dev) {
-    const size_t nchunk = (bytes + kUpChunk - 1) / kUpChunk;
-    const int nthr = (int)std::min<size_t>(kUpThreads, std::max<size_t>(1, nchunk));
-    for (int t = 0; t < nthr; ++t)
-        for (auto& b : c.stage[t])
-            if (const int rc = b.ensure(kUpChunk, true)) return rc;
-    std::vector<int> rcs(nthr, 0);
-    std::vector<std::thread> th;
-    for (int t = 0; t < nthr; ++t)
-        th.emplace_back([&, t] {
-            if (hipSetDevice(dev) != hipSuccess) {
-                rcs[t] = KARMA_E_HIP;
-                return;
-            }
-            int k = 0;
-            for (size_t i = t; i < nchunk; i += nthr, k ^= 1) {
-                const size_t o = i * kUpChunk, n = std::min(kUpChunk, bytes - o);
-                if (hipEventSynchronize(c.up_ev[t][k]) != hipSuccess) {  // the buffer's previous DMA
-                    rcs[t] = KARMA_E_HIP;
-                    return;
-                }
-                if (const int rc = fill(static_cast<uint8_t*>(c.stage[t][k].p), src_off + o, n)) {
-                    rcs[t] = rc;
-                    return;
-                }
-                if (hipMemcpyAsync(static_cast<uint8_t*>(d_dst) + o, c.stage[t][k].p, n, hipMemcpyHostToDevice,
-                                   c.up_st[t]) != hipSuccess ||
-                    hipEventRecord(c.up_ev[t][k], c.up_st[t]) != hipSuccess) {
-                    rcs[t] = KARMA_E_HIP;
-                    return;
-                }
-            }
-            if (hipStreamSynchronize(c.up_st[t]) != hipSuccess) rcs[t] = KARMA_E_HIP;
-        });
-    for (auto& x : th) x.join();
-    for (int rc : rcs)
-        if (rc) return rc == KARMA_E_IO ? rc : fail(rc, "wal_replay: image upload");
-    return 0;
-}
+// Fills dst with image bytes [off, off + n) (offsets relative to the image start); the
+// image is streamed into HBM through the library's pinned staging (host_stage.h).
+using ImageFill = karma::engine::HostFill;
 
 int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
@@ -201,102 +176,6 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
 }  // namespace
 
 extern "C" {
-
-int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const uint32_t* h_len, size_t n,
-                           void* h_wal, size_t wal_bytes, size_t seg_bytes, uint64_t* h_cursor, uint64_t* h_rec_off,
-                           size_t* h_n_framed, int device) {
-    if (!h_cursor || !h_n_framed || (n && (!h_src || !h_src_off || !h_len)) || !h_wal || seg_bytes < kHeader ||
-        wal_bytes % seg_bytes)
-        return fail(KARMA_E_INVALID, "wal_append_batch");
-    uint8_t* wal = static_cast<uint8_t*>(h_wal);
-    const uint8_t* src = static_cast<const uint8_t*>(h_src);
-    karma::engine::PhaseTimer T("wal_append");
-    // 1. CRCs of every payload: one GPU batch over the source buffer, on its own
-    //    thread while the host places and frames the records (2, 3) around it.
-    //    Records that end up not framed (image full) cost only their checksum.
-    const uint64_t nt = n >= (1u << 16) ? 16 : 1;  // source bytes the batch reads, by nt threads
-    std::vector<uint64_t> ext(nt, 0);
-    parallel_for(0, nt, 1, [&](uint64_t t) {
-        for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i)
-            ext[t] = std::max<uint64_t>(ext[t], h_src_off[i] + h_len[i]);
-    });
-    const uint64_t extent = *std::max_element(ext.begin(), ext.end());
-    std::vector<uint32_t> crc(n);
-    int crc_rc = 0;
-    std::thread gpu;
-    if (n)
-        gpu = std::thread([&, extent] {
-            crc_rc = karma_crc32c_batch_ragged_host(src, extent, h_src_off, h_len, n, 0, crc.data(), device);
-        });
-    // 2. placement (sequential: can_hold, else footer + next segment), published in
-    //    blocks; 3. framing workers write each block's length fields and payloads
-    //    (segment_file::append_record) as soon as it is placed
-    constexpr size_t kBlock = 16384;
-    std::vector<uint64_t> at(n);
-    std::atomic<size_t> placed{0}, next_block{0};
-    std::atomic<bool> placing{true};
-    const size_t nwork = std::min<size_t>(15, std::max<size_t>(1, n / kBlock));
-    std::vector<std::thread> framers;
-    for (size_t t = 0; t < nwork; ++t)
-        framers.emplace_back([&] {
-            while (true) {
-                const size_t lo = next_block.fetch_add(1) * kBlock;
-                size_t avail;
-                while ((avail = placed.load(std::memory_order_acquire)) < lo + kBlock &&
-                       placing.load(std::memory_order_acquire))
-                    std::this_thread::yield();
-                avail = placed.load(std::memory_order_acquire);
-                if (lo >= avail) return;  // placement ended before this block
-                const size_t hi = std::min(lo + kBlock, avail);
-                for (size_t i = lo; i < hi; ++i) {
-                    uint8_t* p = wal + at[i];
-                    put32(p + 4, h_len[i] << 8 | 0u);
-                    std::memcpy(p + kHeader, src + h_src_off[i], h_len[i]);
-                    if (h_rec_off) h_rec_off[i] = at[i];
-                }
-            }
-        });
-    uint64_t cur = *h_cursor;
-    size_t framed = 0;
-    std::vector<std::pair<uint64_t, uint64_t>> footers;  // (wal offset, segment end)
-    uint64_t seg_end = (cur / seg_bytes + 1) * seg_bytes;  // end of the segment holding cur
-    for (; framed < n; ++framed) {
-        const uint64_t len = h_len[framed];
-        if (len + kHeader > seg_bytes || (len >> 24)) break;  // never fits / 3-byte size field
-        if (cur == seg_end) seg_end += seg_bytes;             // the last record filled its segment
-        if (cur + kHeader + len > seg_end) {  // !can_hold -> append_footer, next segment
-            footers.emplace_back(cur, seg_end);
-            cur = seg_end;
-            seg_end += seg_bytes;
-        }
-        if (cur + kHeader + len > wal_bytes) break;
-        at[framed] = cur;
-        cur += kHeader + len;
-        if ((framed + 1) % kBlock == 0) placed.store(framed + 1, std::memory_order_release);
-    }
-    placed.store(framed, std::memory_order_release);
-    placing.store(false, std::memory_order_release);
-    T.mark("placement");
-    for (const auto& f : footers) {  // segment_file::append_footer
-        const uint64_t room = f.second - f.first;
-        if (room < kHeader) {
-            std::memset(wal + f.first, '0', room);
-        } else {
-            put32(wal + f.first, 0);
-            put32(wal + f.first + 4, uint32_t((room - kHeader) << 8 | 1u));
-            std::memset(wal + f.first + kHeader, '0', room - kHeader);
-        }
-    }
-    for (auto& x : framers) x.join();
-    T.mark("framing (payloads, lengths, footers)");
-    if (gpu.joinable()) gpu.join();
-    T.mark("wait for the CRC batch");
-    if (crc_rc) return crc_rc;  // payloads and length fields are written; no CRC field is
-    parallel_for(0, framed, 1 << 16, [&](uint64_t i) { put32(wal + at[i], crc[i]); });
-    *h_cursor = cur;
-    *h_n_framed = framed;
-    return 0;
-}
 
 int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
@@ -356,7 +235,7 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         A.wal = static_cast<const uint8_t*>(d_wal) + base0;
     } else {
         if (const int rc = c.img.ensure(img_bytes)) return rc;
-        if (const int rc = upload_staged(c, c.img.p, *fill, base0, img_bytes, dev)) return rc;
+        if (const int rc = staged_upload(dev, c.img.p, *fill, base0, img_bytes)) return rc;
         A.wal = c.img.as<const uint8_t>();
         T.mark("image upload");
     }

@@ -186,10 +186,9 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
 // (instead of streaming the whole segment).  The walk runs on every lane with
 // identical values (uniform control flow keeps the header chain in scalar
 // registers).
-constexpr uint32_t kWTile = 4096;
+constexpr uint32_t kWTile = kWalkTile;
 constexpr int kWQV = kWTile / 1024;  // 16-byte vectors per lane per tile
 constexpr uint32_t kChainCheck = 4;  // headers a sub-range walker's start must chain through
-constexpr uint32_t kMaxSub = 4096;   // sub-ranges per segment (k_wal_gather stages their runs in LDS)
 
 struct WaveLds {
     uint32_t tile[kWTile / 4 + 4];  // + a header's slack
@@ -592,37 +591,6 @@ __global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n) {
 }
 
 }  // namespace
-
-// How the walk splits the segments.  The header chain is serial inside a
-// segment, so few segments leave most of the GPU idle: each segment is then cut
-// into sub-ranges (at least 16 KiB) so that about 16 walkers per CU run, and
-// k_wal_resolve stitches their lists.  Many segments: one walker per segment.
-// sub_bytes != 0 forces the sub-range size (karma_wal_tuning: tests, tuning);
-// the tools build's KARMA_WALK_VARIANT=1 (ab.h) selects k_wal_walk instead.
-WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes) {
-    WalWalkPlan p{1, 0, 0, 0, 0};
-    const uint64_t tiles = (seg_bytes + kWTile - 1) / kWTile;
-    uint64_t sub_tiles = tiles;
-    if (KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 1) {
-        p.kernel = 1;
-    } else if (sub_bytes) {
-        sub_tiles = std::max<uint64_t>(1, sub_bytes / kWTile);
-    } else {
-        const uint64_t want = 16 * (uint64_t)(cu > 0 ? cu : 1);  // walkers
-        if (nseg > 0 && nseg < want) {
-            const uint64_t per = (want + nseg - 1) / nseg;  // sub-ranges per segment
-            sub_tiles = std::max<uint64_t>(4, (tiles + per - 1) / per);
-        }
-    }
-    sub_tiles = std::min(sub_tiles, tiles);
-    sub_tiles = std::max(sub_tiles, (tiles + kMaxSub - 1) / kMaxSub);
-    p.sub_bytes = sub_tiles * kWTile;
-    p.nsub = p.kernel == 1 ? 1 : (seg_bytes + p.sub_bytes - 1) / p.sub_bytes;
-    if (p.nsub == 1) p.sub_bytes = seg_bytes;
-    p.sub_cap = p.sub_bytes / 8 + 1;
-    p.cand_cap = p.nsub * p.sub_cap;
-    return p;
-}
 
 hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s) {
     if (!nseg) return hipSuccess;

@@ -1,0 +1,283 @@
+// tests/cpp/host_logic_test.cc -- the library's host-side logic under AddressSanitizer and
+// UBSan (test infrastructure; built by `make -C karma_amd/csrc san`, run by
+// tests/test_sanitizers.py).  Linked against the sanitized host objects of the library.
+//
+//   1. crc32c::Extend / karma_crc32c_extend_host / _portable / _combine against a bitwise
+//      CRC-32C (karma-util/crc32c.cc:275-376 semantics) at every alignment;
+//   2. WalPlacer (the writer's placement, sivir.cc:276-317, segment_file.cc:21-49, 74-77)
+//      against its invariants and a direct restatement of the writer's loop;
+//   3. kfp_walk (connection::read_frame's parse loop, frame.cc:62-130) on valid, truncated,
+//      corrupted and random buffers;
+//   4. wal_walk_plan's sub-range split for many segment sizes, counts and CU counts;
+//   5. without a device: every C ABI entry point with real arguments runs its host part
+//      (validation, placement, directory scan, structural walks) and refuses cleanly.
+#include <hip/hip_runtime_api.h>
+#include <unistd.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "karma-util/crc32c.h"
+#include "karma_crc32c.h"
+#include "wal_place.h"
+
+using namespace karma::engine;
+
+namespace {
+
+int g_fail = 0;
+#define CHECK(c)                                                                     \
+    do {                                                                             \
+        if (!(c)) {                                                                  \
+            std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #c); \
+            if (++g_fail > 20) std::exit(1);                                         \
+        }                                                                            \
+    } while (0)
+
+uint32_t crc_bitwise(uint32_t init, const uint8_t* p, size_t n) {
+    uint32_t l = init ^ 0xFFFFFFFFu;
+    for (size_t i = 0; i < n; ++i) {
+        l ^= p[i];
+        for (int k = 0; k < 8; ++k) l = (l >> 1) ^ (0x82F63B78u & (0u - (l & 1u)));
+    }
+    return l ^ 0xFFFFFFFFu;
+}
+
+void test_host_crc(std::mt19937_64& rng) {
+    std::vector<uint8_t> buf(70000 + 64);
+    for (auto& b : buf) b = uint8_t(rng());
+    for (size_t n = 0; n <= 600; ++n)
+        for (size_t a = 0; a < 16; ++a) {
+            const uint32_t init = uint32_t(rng());
+            const uint8_t* p = buf.data() + a;
+            const uint32_t want = crc_bitwise(init, p, n);
+            CHECK(karma_crc32c_extend_host(init, p, n) == want);
+            CHECK(karma_crc32c_extend_host_portable(init, p, n) == want);
+            CHECK(crc32c::Extend(init, reinterpret_cast<const char*>(p), n) == want);
+        }
+    for (size_t n : {4095, 4096, 4097, 65535, 65536, 65543, 70000}) {
+        const uint32_t want = crc_bitwise(0, buf.data() + 3, n);
+        CHECK(karma_crc32c_extend_host(0, buf.data() + 3, n) == want);
+        CHECK(karma_crc32c_extend_host_portable(0, buf.data() + 3, n) == want);
+        for (size_t cut : {size_t(0), size_t(1), n / 3, n - 1, n}) {  // Value(A||B) = Combine(Value(A), Value(B), |B|)
+            const uint32_t a = crc_bitwise(0, buf.data() + 3, cut), b = crc_bitwise(0, buf.data() + 3 + cut, n - cut);
+            CHECK(karma_crc32c_combine(a, b, n - cut) == want);
+        }
+    }
+    CHECK(crc32c::Value("123456789", 9) == 0xE3069283u);
+    CHECK(crc32c::Mask(0xE3069283u) == 0xC78AB0E5u && crc32c::Unmask(crc32c::Mask(0x12345678u)) == 0x12345678u);
+}
+
+// The writer's loop restated (wal_model.append): returns the cursor; fills at / footers.
+uint64_t place_model(const std::vector<uint64_t>& len, uint64_t seg, uint64_t wal, uint64_t cursor,
+                     std::vector<uint64_t>* at, std::vector<std::pair<uint64_t, uint64_t>>* footers) {
+    for (uint64_t n : len) {
+        if (n + 8 > seg || (n >> 24)) break;
+        const uint64_t seg_end = (cursor / seg + 1) * seg;
+        if (cursor + 8 + n > seg_end) {
+            footers->emplace_back(cursor, seg_end);
+            cursor = seg_end;
+        }
+        if (cursor + 8 + n > wal) break;
+        at->push_back(cursor);
+        cursor += 8 + n;
+    }
+    return cursor;
+}
+
+void test_placement(std::mt19937_64& rng) {
+    for (int it = 0; it < 3000; ++it) {
+        const uint64_t seg = std::vector<uint64_t>{8, 9, 16, 100, 4096, 4100, 65536, 1 << 20}[rng() % 8];
+        const uint64_t nseg = 1 + rng() % 6, wal = nseg * seg;
+        const uint64_t cursor = (rng() % 4 == 0) ? rng() % wal : 0;
+        std::vector<uint64_t> len(rng() % 200);
+        for (auto& l : len) {
+            const int k = int(rng() % 10);
+            l = k == 0 ? 0 : k == 1 ? seg - 8 : k == 2 ? seg - 7 : k == 3 ? (1u << 24) : rng() % (seg / 2 + 1);
+        }
+        std::vector<uint64_t> at_m;
+        std::vector<std::pair<uint64_t, uint64_t>> ft_m;
+        const uint64_t cur_m = place_model(len, seg, wal, cursor, &at_m, &ft_m);
+        WalPlacer P(seg, wal, cursor);
+        std::vector<uint64_t> at;
+        std::vector<std::pair<uint64_t, uint64_t>> ft;
+        for (uint64_t L : len) {
+            uint64_t a = 0, f0, f1;
+            const bool ok = P.place(L, &a, &f0, &f1);
+            if (f1 > f0) ft.emplace_back(f0, f1);
+            if (!ok) break;
+            CHECK(a / seg == (a + 8 + L - 1) / seg);  // a record never straddles a segment end
+            CHECK(a + 8 + L <= wal);
+            at.push_back(a);
+        }
+        CHECK(at == at_m);
+        CHECK(ft == ft_m);
+        CHECK(P.cur == cur_m);
+        for (const auto& f : ft) CHECK(f.second % seg == 0 && f.second > f.first && f.second - f.first < seg);
+    }
+}
+
+void put32(std::vector<uint8_t>& b, size_t at, uint32_t v) { std::memcpy(b.data() + at, &v, 4); }
+
+void test_kfp_walk(std::mt19937_64& rng) {
+    for (int it = 0; it < 2000; ++it) {
+        std::vector<uint8_t> b;
+        std::vector<uint64_t> frames;
+        const int nf = int(rng() % 20);
+        for (int f = 0; f < nf; ++f) {
+            const uint32_t hl = uint32_t(rng() % 70), pl = uint32_t(rng() % 300), fl = 16 + hl + pl + 4;
+            frames.push_back(b.size());
+            const size_t o = b.size();
+            b.resize(o + fl);
+            for (size_t i = o; i < o + fl; ++i) b[i] = uint8_t(rng());
+            put32(b, o, fl);
+            b[o + 4] = KARMA_KFP_MAGIC;
+            put32(b, o + 12, hl);
+        }
+        KfpWalk W;
+        CHECK(kfp_walk(b.data(), b.size(), 1 << 20, &W) == KARMA_KFP_OK);
+        CHECK(W.frame == frames && W.consumed == b.size());
+        if (!b.empty()) {  // truncated: the last frame is incomplete
+            KfpWalk T;
+            CHECK(kfp_walk(b.data(), b.size() - 1, 1 << 20, &T) == KARMA_KFP_OK);
+            CHECK(T.frame.size() + 1 == frames.size());
+            std::vector<uint8_t> c = b;  // one corrupted field
+            const size_t f = frames[rng() % frames.size()];
+            const int what = int(rng() % 4);
+            int want;
+            if (what == 0) {
+                put32(c, f, KARMA_KFP_MAX_FRAME + 1), want = KARMA_KFP_BAD_SIZE;
+            } else if (what == 1) {
+                c[f + 4] ^= 1, want = KARMA_KFP_BAD_MAGIC;
+            } else if (what == 2) {
+                uint32_t fl;
+                std::memcpy(&fl, c.data() + f, 4);
+                put32(c, f + 12, fl - 19), want = KARMA_KFP_BAD_HEADER_LEN;
+            } else {
+                put32(c, f, 19), want = KARMA_KFP_BAD_LENGTH;
+            }
+            KfpWalk X;
+            CHECK(kfp_walk(c.data(), c.size(), 1 << 20, &X) == want);
+            CHECK(X.consumed == f);
+        }
+    }
+    std::vector<uint8_t> junk(1 << 16);  // random bytes: whatever the verdict, every read in bounds
+    for (int it = 0; it < 4000; ++it) {
+        const size_t n = rng() % junk.size();
+        for (size_t i = 0; i < n; ++i) junk[i] = uint8_t(rng() % 5 == 0 ? KARMA_KFP_MAGIC : rng());
+        if (n >= 4 && rng() % 2) put32(junk, 0, uint32_t(20 + rng() % 64));
+        KfpWalk W;
+        (void)kfp_walk(junk.data(), n, 1 + rng() % 64, &W);
+        CHECK(W.consumed <= n);
+    }
+}
+
+void test_walk_plan() {
+    for (uint64_t seg : {8ull, 100ull, 4096ull, 4100ull, 16388ull, 65536ull, 262148ull, 1ull << 20, 32ull << 20,
+                         (1ull << 31) - 8})
+        for (uint64_t nseg : {1ull, 2ull, 7ull, 188ull, 4096ull, 100000ull})
+            for (int cu : {1, 80, 256})
+                for (uint64_t sub : {0ull, 4096ull, 16384ull, 1ull << 30}) {
+                    const WalWalkPlan p = wal_walk_plan(seg, nseg, cu, sub);
+                    CHECK(p.nsub >= 1 && p.nsub <= kMaxSub);
+                    CHECK(p.nsub * p.sub_bytes >= seg && (p.nsub - 1) * p.sub_bytes < seg);
+                    CHECK(p.nsub == 1 ? p.sub_bytes == seg : p.sub_bytes % kWalkTile == 0);
+                    CHECK(p.sub_cap == p.sub_bytes / 8 + 1 && p.cand_cap == p.nsub * p.sub_cap);
+                }
+}
+
+void test_abi_without_device() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) == hipSuccess && n > 0) {
+        std::printf("(a device is visible: the no-device checks are skipped)\n");
+        return;
+    }
+    std::vector<uint8_t> src(1 << 16, 0x5A), wal(8 * 4096);
+    std::vector<uint64_t> off(100);
+    std::vector<uint32_t> len(100, 300), out(100);
+    for (size_t i = 0; i < off.size(); ++i) off[i] = i * 300;
+    uint64_t cursor = 0, recoff[100];
+    size_t nf = 0;
+    CHECK(karma_wal_append_batch(src.data(), off.data(), len.data(), 100, wal.data(), wal.size(), 4096, &cursor, recoff,
+                                 &nf, 0) == KARMA_E_NO_DEVICE);
+    CHECK(karma_wal_append_batch(src.data(), off.data(), len.data(), 100, wal.data(), wal.size() - 1, 4096, &cursor,
+                                 recoff, &nf, 0) == KARMA_E_INVALID);
+    uint64_t nrec, stop, base;
+    int status;
+    CHECK(karma_wal_replay(wal.data(), nullptr, wal.size(), 4096, 0, &nrec, &stop, &status, recoff, 100, 0) ==
+          KARMA_E_NO_DEVICE);
+    karma_wal_tuning t{4096, KARMA_WAL_CRC_DIRECT, 0};
+    CHECK(karma_wal_replay_tuned(wal.data(), nullptr, wal.size(), 4096, 0, &nrec, &stop, &status, recoff, 100, 0,
+                                 &t) == KARMA_E_NO_DEVICE);
+    t.crc_batch = 7;
+    CHECK(karma_wal_replay_tuned(wal.data(), nullptr, wal.size(), 4096, 0, &nrec, &stop, &status, recoff, 100, 0,
+                                 &t) == KARMA_E_INVALID);
+    CHECK(karma_wal_replay(wal.data(), nullptr, wal.size(), 4096, wal.size(), &nrec, &stop, &status, recoff, 100,
+                           0) == 0 &&
+          nrec == 0 && stop == wal.size() && status == KARMA_WAL_END);
+    // a segment directory: scanned, opened, then the device is needed
+    char dir[] = "/tmp/karma_san_XXXXXX";
+    CHECK(mkdtemp(dir) != nullptr);
+    for (int i = 0; i < 3; ++i) {
+        const std::string p = std::string(dir) + "/" + std::to_string(8192 + i * 4096);
+        FILE* f = std::fopen(p.c_str(), "wb");
+        std::fwrite(wal.data(), 1, 4096, f);
+        std::fclose(f);
+    }
+    FILE* f = std::fopen((std::string(dir) + "/LOCK").c_str(), "wb");
+    std::fclose(f);
+    CHECK(karma_wal_replay_dir(dir, 0, 8192, &base, &nrec, &stop, &status, recoff, 100, 0) == KARMA_E_NO_DEVICE);
+    CHECK(karma_wal_replay_dir(dir, 0, 0, &base, &nrec, &stop, &status, recoff, 100, 0) == KARMA_E_INVALID);
+    for (int i = 0; i < 3; ++i) unlink((std::string(dir) + "/" + std::to_string(8192 + i * 4096)).c_str());
+    unlink((std::string(dir) + "/LOCK").c_str());
+    rmdir(dir);
+    CHECK(karma_wal_replay_dir("/nonexistent/karma", 0, 0, &base, &nrec, &stop, &status, recoff, 100, 0) ==
+          KARMA_E_IO);
+    // batches
+    CHECK(karma_crc32c_batch_ragged_host(src.data(), src.size(), off.data(), len.data(), 100, 0, out.data(), 0) ==
+          KARMA_E_NO_DEVICE);
+    off[99] = src.size();
+    CHECK(karma_crc32c_batch_ragged_host(src.data(), src.size(), off.data(), len.data(), 100, 0, out.data(), 0) ==
+          KARMA_E_INVALID);
+    CHECK(karma_crc32c_batch_fixed_host(src.data(), 512, 64, 0, out.data(), 0) == KARMA_E_NO_DEVICE);
+    CHECK(karma_crc32c_batch_fixed(src.data(), 512, 64, nullptr, 0, out.data(), nullptr) == KARMA_E_NO_DEVICE);
+    CHECK(karma_crc32c_batch_ragged_bounded(src.data(), off.data(), len.data(), 100, 0, 300, nullptr, 0, out.data(),
+                                            nullptr) == KARMA_E_NO_DEVICE);
+    // KFP: encode refuses at the CRC batch; parse walks the frames, then refuses
+    std::vector<uint8_t> frames(4096);
+    size_t ne = 0;
+    uint64_t bytes = 0;
+    std::vector<int16_t> op(4, 1);
+    std::vector<uint8_t> flag(4, 0);
+    std::vector<uint32_t> seq(4, 7), hl(4, 10), pl(4, 20);
+    std::vector<uint64_t> ho(4, 0), po(4, 100);
+    CHECK(karma_kfp_encode_batch(src.data(), ho.data(), hl.data(), src.data(), po.data(), pl.data(), op.data(),
+                                 flag.data(), seq.data(), 4, frames.data(), frames.size(), nullptr, &ne, &bytes,
+                                 0) == KARMA_E_NO_DEVICE);
+    size_t nfr = 0;
+    uint64_t used = 0;
+    CHECK(karma_kfp_parse_batch(frames.data(), nullptr, 0, 16, nullptr, &nfr, &used, &status, 0) == 0 && nfr == 0);
+}
+
+}  // namespace
+
+int main() {
+    std::mt19937_64 rng(20260131);
+    test_host_crc(rng);
+    test_placement(rng);
+    test_kfp_walk(rng);
+    test_walk_plan();
+    test_abi_without_device();
+    if (g_fail) {
+        std::printf("host_logic_test: %d failures\n", g_fail);
+        return 1;
+    }
+    std::printf("host_logic_test: ok\n");
+    return 0;
+}

@@ -355,3 +355,41 @@ def test_ragged_unknown_total_workspace_growth(raw, dev):
                                         torch.from_numpy(lens.astype(np.int32)).to(dev), stream=s)
         s.synchronize()
         _eq(got.cpu().numpy(), oracle_lib.ragged_crcs(host, offs, lens))
+
+
+def test_ragged_low_total_len_is_still_exact(raw, dev):
+    """total_len only sizes the unit table: a bound below sum(len) must never change a CRC (the
+    records whose units do not fit are stepped by one lane each in k_ragged_finalize)."""
+    host, dbuf = raw
+    lens = synth.loguniform_lengths(8, 3000, 1, 60000)
+    offs, arena = synth.ragged_layout(lens, header=3)
+    assert arena <= host.size
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    want = oracle_lib.ragged_crcs(host, offs, lens)
+    for total in (int(lens.sum()), int(lens.sum()) // 3, 1, 8192):
+        got = K.extend_batch_ragged(dbuf[:arena], d_off, d_len, total_len=total).cpu().numpy()
+        _eq(got, want)
+
+
+@pytest.mark.parametrize("bound", [0, 64, 1024, 1 << 20])
+def test_ragged_bounded_direct_path(raw, dev, bound):
+    """karma_crc32c_batch_ragged_bounded: with max_len <= 1 KiB one record per group (no plan
+    kernels); any bound -- too low included -- gives the exact CRCs, with per-record inits."""
+    host, dbuf = raw
+    L = _lib.lib()
+    rng = np.random.default_rng(bound + 1)
+    lens = np.concatenate([rng.integers(0, 1025, 20000), rng.integers(0, 40, 3000),
+                           [0, 1, 15, 16, 17, 31, 1023, 1024, 5000]]).astype(np.uint32)
+    offs = rng.integers(0, host.size - 6000, lens.size).astype(np.uint64)
+    init = rng.integers(0, 1 << 32, lens.size, dtype=np.uint64).astype(np.uint32)
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    d_ini = torch.from_numpy(init.view(np.int32)).to(dev)
+    out = torch.full((lens.size,), -1, dtype=torch.int32, device=dev)
+    st = L.karma_crc32c_batch_ragged_bounded(dbuf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), lens.size,
+                                             int(lens.sum()), bound, d_ini.data_ptr(), 0, out.data_ptr(),
+                                             torch.cuda.current_stream().cuda_stream)
+    _lib.check("batch_ragged_bounded", st)
+    _eq(out.cpu().numpy().view(np.uint32), oracle_lib.ragged_crcs(host, offs, lens, init))
+

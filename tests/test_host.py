@@ -242,3 +242,12 @@ def test_shipped_library_has_no_variant_knobs():
     for knob in (b"KARMA_CRC_VARIANT", b"KARMA_RAGGED_VARIANT", b"KARMA_FOLD_MAX_K", b"KARMA_SPLIT_OVERDECOMPOSE",
                  b"KARMA_WALK_VARIANT", b"KARMA_WALK_SUB", b"KARMA_WAL_SMALL_MAX"):
         assert knob not in blob, knob
+
+
+def test_library_never_page_locks_caller_memory():
+    """Host buffers reach the device through the library's own pinned staging: the library does
+    not import hipHostRegister at all (round 1's per-call register / unregister of caller pages is
+    gone)."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    imported = {ln.split()[-1].split("@")[0] for ln in out.stdout.splitlines() if ln.strip()}
+    assert "hipHostRegister" not in imported and "hipHostUnregister" not in imported

@@ -1,0 +1,107 @@
+"""WAL images of the GPU WAL tests, framed on the CPU by tests/wal_model.py (test infrastructure).
+
+The device replay tests (tests/test_gpu_wal.py) frame these payloads with karma_wal_append_batch;
+tests/test_gpu_wal.py::test_append_matches_reference_framing pins that framing to wal_model.append
+byte for byte, so the images here are the ones the GPU replays.  tests/test_sanitizers.py feeds
+them to the CPU emulation of the device walk (tests/cpp/wal_walk_emu.cc).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import synth
+import wal_model
+
+
+def frame(src, offs, lens, seg, nseg):
+    wal = bytearray(nseg * seg)
+    payloads = [src[int(o): int(o) + int(n)] for o, n in zip(offs, lens)]
+    cur, rec = wal_model.append(payloads, wal, seg, 0)
+    return np.frombuffer(bytes(wal), np.uint8).copy(), rec
+
+
+def payloads(seed, n, lo, hi):
+    lens = synth.uniform_lengths(seed, n, lo, hi)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(seed + 1, 0, int(lens.sum()) + 16).copy()
+    return src, offs, lens
+
+
+def wal_looking_payloads():
+    """test_replay_payloads_that_look_like_wal_records: payloads that are slices of a WAL image
+    (valid header chains inside records), 256 KiB segments -- the inputs of round 1's faulting run."""
+    seg = 256 << 10
+    isrc, ioffs, ilens = payloads(31, 400, 1, 200)
+    inner, _ = frame(isrc, ioffs, ilens, 64 << 10, 1)
+    rng = np.random.default_rng(3)
+    chunks, lens = [], []
+    for i in range(300):
+        if i % 2 == 0:
+            a = int(rng.integers(0, 4096))
+            n = int(rng.integers(2000, 12000))
+            chunks.append(inner[a: a + n])
+        else:
+            n = int(rng.integers(1, 3000))
+            chunks.append(rng.integers(0, 256, n, dtype=np.uint8))
+        lens.append(n)
+    lens = np.array(lens, np.uint32)
+    src = np.concatenate(chunks + [np.zeros(16, np.uint8)])
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 2
+    wal, rec = frame(src, offs, lens, seg, nseg)
+    return wal, seg, rec
+
+
+def large_records(seg):
+    """test_replay_large_records_jumps: log-uniform 1 B-60 KiB payloads."""
+    lens = synth.loguniform_lengths(17, 900, 1, 60000)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(18, 0, int(lens.sum()) + 16).copy()
+    nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 3
+    wal, rec = frame(src, offs, lens, seg, nseg)
+    return wal, seg, rec
+
+
+def segment_sizes(seg):
+    """test_replay_segment_sizes_tiles_and_misaligned_segments."""
+    n = 6000 if seg >= (64 << 10) else 600
+    src, offs, lens = payloads(13, n, 1, min(3000, seg - 8))
+    nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 3
+    wal, rec = frame(src, offs, lens, seg, nseg)
+    return wal, seg, rec
+
+
+def randomized(case, inner):
+    """test_replay_randomized_against_model's case `case` (its own generator state)."""
+    rng = np.random.default_rng(2024 + 1000 * case)
+    seg = int(rng.choice([4096, 16384 + 4, 65536, 262144, 1 << 20]))
+    mix = case % 4
+    n = int(rng.integers(200, 3000))
+    if mix == 0:
+        lens = rng.integers(1, 64, n)
+    elif mix == 1:
+        lens = rng.integers(1, min(4000, seg - 8), n)
+    elif mix == 2:
+        lens = np.minimum(synth.loguniform_lengths(case, n, 1, 60000), seg - 8)
+    else:
+        lens = rng.integers(100, min(6000, seg - 8), n)
+    lens = lens.astype(np.uint32)
+    if mix == 3:
+        src = np.concatenate([inner[int(rng.integers(0, 2048)):][: int(x)] if x <= inner.size - 2048 else
+                              rng.integers(0, 256, int(x), dtype=np.uint8) for x in lens] + [np.zeros(16, np.uint8)])
+    else:
+        src = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    nseg = int((lens.astype(np.int64) + 8).sum() // seg) + 3
+    wal, rec = frame(src, offs, lens, seg, nseg)
+    if case % 3 == 1 and len(rec) > 10:
+        k = int(rng.integers(1, len(rec)))
+        wal[int(rec[k]) + int(rng.choice([5, 8]))] ^= 0x10
+    start = int(rec[int(rng.integers(0, len(rec)))]) if case % 2 and len(rec) else 0
+    return wal, seg, start
+
+
+def inner_image():
+    isrc, ioffs, ilens = payloads(71, 600, 1, 100)
+    inner, _ = frame(isrc, ioffs, ilens, 64 << 10, 1)
+    return inner
