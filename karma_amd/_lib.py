@@ -16,6 +16,14 @@ LIB_PATH = os.path.join(_HERE, "lib", "libkarma_crc32c.so")
 # DESIGN.md §4, chosen by KARMA_* environment variables.  Only tools/ and the variant
 # tests load it (through `using`); the package always runs LIB_PATH.
 AB_LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "lib", "libkarma_crc32c_ab.so")
+# The bounds-checked debug build (karma_amd/csrc/bounds.h): the same C ABI plus
+# karma_debug_bounds_report; the GPU suite runs on it under `pytest --karma-lib bounds`.
+BOUNDS_LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "lib", "libkarma_crc32c_bounds.so")
+KB_SITES = {1: "WAL image byte outside the image", 2: "WAL image byte outside the walker's segment",
+            3: "candidate slot outside the segment's lists", 4: "candidate write dropped by the cap guard",
+            5: "sub-range report index", 6: "span index", 7: "segment meta index", 8: "gathered list index",
+            9: "gathered slot outside its sub-range", 10: "record byte outside the arena allocation",
+            11: "ragged unit slot >= unit_cap"}
 
 KARMA_OK = 0
 KARMA_E_INVALID = -1
@@ -104,6 +112,9 @@ def load(path: str) -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        if hasattr(handle, "karma_debug_bounds_report"):  # the bounds build only
+            handle.karma_debug_bounds_report.restype = _i
+            handle.karma_debug_bounds_report.argtypes = [_vp, _i]
         _LOADED[path] = handle
     return _LOADED[path]
 
@@ -114,6 +125,13 @@ def lib() -> ctypes.CDLL:
     if _LIB is None:
         _LIB = load(LIB_PATH)
     return _LIB
+
+
+def select(path: str) -> None:
+    """Make the build at `path` the package's library for the rest of the process (the test
+    suite's --karma-lib option)."""
+    global _LIB
+    _LIB = load(path)
 
 
 @contextlib.contextmanager

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "ab.h"
+#include "bounds.h"
 #include "engine.h"
 #include "karma_crc32c.h"
 
@@ -288,10 +289,28 @@ void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
     a.unit_cap = cap;
 }
 
+// The bounds build (bounds.h) checks record-byte loads against the arena's allocation.
+void bind_arena_bounds(RaggedArgs& a) {
+#ifdef KARMA_BOUNDS
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (a.arena && hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)a.arena) == hipSuccess) {
+        a.kb_lo = reinterpret_cast<uintptr_t>(base);
+        a.kb_hi = a.kb_lo + size;
+    } else {
+        (void)hipGetLastError();
+        a.kb_lo = 0;
+        a.kb_hi = ~uintptr_t(0);
+    }
+#else
+    (void)a;
+#endif
+}
+
 int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_off, const uint32_t* d_len,
                   size_t n_rec, size_t total_len, const uint32_t* d_init, uint32_t init, uint32_t* d_out,
                   hipStream_t s) {
-    RaggedArgs a;
+    RaggedArgs a{};
     a.arena = static_cast<const uint8_t*>(d_arena);
     a.off = d_off;
     a.len = d_len;
@@ -301,6 +320,7 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
     a.unit_bytes = kDefaultUnit;
     a.out = d_out;
     a.blob = ds.blob;
+    bind_arena_bounds(a);
     KARMA_RC(comb_blob(ds, kDefaultUnit, &a.comb_blob));
     uint64_t cap;
     void* ws = nullptr;
@@ -374,6 +394,27 @@ extern "C" {
 
 int karma_crc32c_abi_version(void) { return KARMA_CRC32C_ABI_VERSION; }
 
+#ifdef KARMA_BOUNDS
+// Bounds build only (bounds.h): out[0] = violations since the last reset, out[1..3] = the
+// first one's site, index and capacity.  reset != 0 clears the reports afterwards.
+int karma_debug_bounds_report(uint64_t* out, int reset) {
+    if (!out) return fail(KARMA_E_INVALID, "debug_bounds_report: null");
+    KARMA_HIP(hipDeviceSynchronize());
+    KbReport all{0, 0, 0, 0};
+    for (auto collect : {kb_collect_fixed, kb_collect_ragged, kb_collect_util, kb_collect_wal}) {
+        KbReport r{};
+        KARMA_HIP(collect(&r, reset != 0));
+        if (r.count && !all.count) all = r;
+        else all.count += r.count;
+    }
+    out[0] = all.count;
+    out[1] = all.site;
+    out[2] = all.index;
+    out[3] = all.cap;
+    return 0;
+}
+#endif
+
 const char* karma_crc32c_strerror(int status) {
     switch (status) {
         case KARMA_OK: return "ok";
@@ -436,7 +477,11 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
         a.init_scalar = init;
         a.out = d_out;
         a.blob = L.ds->blob;
-        KARMA_HIP(launch_ragged_direct(a, L.ds->cu, (hipStream_t)stream));
+        bind_arena_bounds(a);
+        // a wave takes 64 records: no more workgroups than the batch fills (each one loads
+        // the 145 KiB table image into its LDS first)
+        const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_rec, 64 * kWavesPerBlock));
+        KARMA_HIP(launch_ragged_direct(a, (int)blocks, (hipStream_t)stream));
         return KARMA_OK;
     }
     return ragged_locked(L.dev, *L.ds, d_arena, d_off, d_len, n_rec, total_len, d_init, init, d_out,

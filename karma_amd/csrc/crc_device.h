@@ -11,6 +11,7 @@
 
 #include <cstdint>
 
+#include "bounds.h"
 #include "engine.h"
 
 namespace karma {
@@ -87,12 +88,16 @@ __device__ __forceinline__ uint32_t byte_step(const uint32_t* lds, int t8, uint3
 // so hipcc emits global_load_dwordx4 (vmcnt only) instead of flat loads, whose
 // lgkmcnt share would serialise them against the LDS lookups.  NT = the
 // non-temporal policy (bytes are read exactly once).
+// (The bounds build checks every record-byte load against the kernel's arena: bounds.h.)
 template <bool NT>
 __device__ __forceinline__ u32x4 ldg(const uint8_t* p) {
+    p = KB_BYTES(p, 16);
     if constexpr (NT) return __builtin_nontemporal_load((gu32x4*)(p));
     return *(gu32x4*)(p);
 }
-__device__ __forceinline__ u32x4 ld16(const uint8_t* p) { return *(gu32x4*)(p); }
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) { return *(gu32x4*)(KB_BYTES(p, 16)); }
+// 16 bytes of library metadata (unit descriptors): not record bytes, never checked.
+__device__ __forceinline__ u32x4 ldmeta16(const void* p) { return *(gu32x4*)(p); }
 
 __device__ __forceinline__ const uint8_t* pmin(const uint8_t* a, const uint8_t* b) { return a < b ? a : b; }
 __device__ __forceinline__ const uint8_t* pmax(const uint8_t* a, const uint8_t* b) { return a > b ? a : b; }

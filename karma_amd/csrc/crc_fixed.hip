@@ -70,6 +70,8 @@ __device__ __forceinline__ FixedPlan fixed_plan(const FixedArgs& A, uint64_t u, 
 // kernels start one level up (a 64 MiB segment: 32768 -> 4096 states here).
 template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0, bool BAL = true, int KW = 1>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
+    KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
+                 (reinterpret_cast<uintptr_t>(A.arena + A.n_rec * A.rec_bytes) + 15) & ~uintptr_t(15));
     constexpr bool kMaps = WAVE_COMB || KW > 1;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kMaps ? kLdsWordsComb : kLdsWords];
     __shared__ uint32_t blk_next;  // BAL: the block's next wave-step (an LDS counter, lgkmcnt only)
@@ -163,6 +165,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
 // unit's loads issued when the unit starts.  Also the A/B baseline (variant 1).
 template <int PF, bool NT>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed_v1(FixedArgs A) {
+    KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
+                 (reinterpret_cast<uintptr_t>(A.arena + A.n_rec * A.rec_bytes) + 15) & ~uintptr_t(15));
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
     __syncthreads();
@@ -222,6 +226,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed_v1(FixedArgs A) {
 // adds the record tail and writes the CRC.  One wave per output state.
 __global__ __launch_bounds__(256) void k_combine_fixed(FixedArgs A, const uint32_t* in, uint64_t k_in, uint32_t* outs,
                                                       uint64_t k_out, const uint32_t* comb) {
+    KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
+                 (reinterpret_cast<uintptr_t>(A.arena + A.n_rec * A.rec_bytes) + 15) & ~uintptr_t(15));
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords];
     load_comb_tables<kCombCoreWords, 256>(lds, comb);
     __syncthreads();
@@ -252,6 +258,8 @@ __global__ __launch_bounds__(256) void k_combine_fixed(FixedArgs A, const uint32
 // results with Z_{64mD}, adds the record tail and writes the CRC.
 __global__ __launch_bounds__(1024) void k_combine_block(FixedArgs A, const uint32_t* in, uint64_t k_in, uint64_t m,
                                                         const uint32_t* bc) {
+    KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
+                 (reinterpret_cast<uintptr_t>(A.arena + A.n_rec * A.rec_bytes) + 15) & ~uintptr_t(15));
     __shared__ __attribute__((aligned(16))) uint32_t lds[kBlockCombWords];
     __shared__ uint32_t wv[16];
     const uint64_t r = blockIdx.x;
@@ -384,6 +392,8 @@ hipError_t launch_combine_block(const FixedArgs& a, const uint32_t* in_states, u
     hipLaunchKernelGGL(k_combine_block, dim3((unsigned)a.n_rec), dim3(1024), 0, s, a, in_states, k_in, m, block_blob);
     return hipGetLastError();
 }
+
+KB_DEFINE_COLLECT(fixed)
 
 }  // namespace engine
 }  // namespace karma

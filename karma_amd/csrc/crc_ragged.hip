@@ -176,6 +176,7 @@ __device__ BlockBase block_base(const RaggedArgs& A, uint64_t* sm) {
 // inclusive unit counts, so the descriptor stores are coalesced and balanced
 // however skewed the record sizes are.
 __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4 then the byte table
     __shared__ unsigned long long cnt[kBuckets];
     __shared__ uint32_t hist[kBuckets];
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
 // Descriptor load through address space 1 (global_load_dwordx4, vmcnt only): a
 // flat load would also count on lgkmcnt and stall the LDS lookups behind it.
 __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
-    const u32x4 v = ld16(reinterpret_cast<const uint8_t*>(d));
+    const u32x4 v = ldmeta16(d);
     return UnitDesc{v.x | ((uint64_t)v.y << 32), v.z, v.w};
 }
 
@@ -261,6 +262,7 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
 // store nothing.
 template <bool BAL = true>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs A) {
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     __shared__ uint32_t blk_next;  // BAL: as k_units_ragged, taken two steps ahead
     if (BAL && threadIdx.x == 0) blk_next = kWavesPerBlock;
@@ -330,6 +332,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs 
 // fixed layout, where the pipelined form wins 2.7%.
 template <bool BAL = true>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     __shared__ uint32_t blk_next;  // BAL: the block's next wave-step (an LDS counter)
     if (BAL && threadIdx.x == 0) blk_next = kWavesPerBlock;
@@ -361,10 +364,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
             wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
         }
         const uint64_t un = wb_next * kGroupsPerWave + grp;
-        d = un < U ? load_desc(A.desc + un) : UnitDesc{0, 0, 0};
+        d = un < U ? load_desc(&KB_READ(A.desc, un, A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
         const uint8_t* us = reinterpret_cast<const uint8_t*>(cur.us);
         const uint32_t R = group_unit<kRaggedPF, kRaggedNT>(lds, X, l, us, us + cur.span, us, cur.inj);
-        if (valid && l == 0) A.partial[u] = R;
+        if (valid && l == 0) KB_WRITE(A.partial, u, A.unit_cap, kKbUnit, R);
         wb = wb_next;
         u = un;
     }
@@ -388,6 +391,7 @@ __device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, 
 // ends, Z_last before the last unit), the unaligned tail, ~R.  Records of more
 // than 64 units: the whole wave folds all but the last unit with the 64-lane tree.
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombWords];
     load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
     __syncthreads();
@@ -472,6 +476,7 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
 // register out by shuffles.  Correct for any length; balanced when every record
 // is small.
 __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct(RaggedArgs A) {
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
     __syncthreads();
@@ -554,6 +559,8 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     hipLaunchKernelGGL(k_ragged_finalize, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
+
+KB_DEFINE_COLLECT(ragged)
 
 }  // namespace engine
 }  // namespace karma

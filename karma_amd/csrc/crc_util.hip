@@ -39,6 +39,7 @@ __global__ __launch_bounds__(256) void k_fill_splitmix(uint8_t* dst, uint64_t n_
 // non-temporal 16-byte loads per lane in flight (the fastest read shape of
 // tools/hbm_probe.hip on MI355X); xor-reduced so nothing is dead code.
 __global__ __launch_bounds__(256) void k_stream_probe(const uint8_t* src, uint64_t n_bytes, uint32_t* out) {
+    KB_SET_ARENA(src, src + n_bytes);
     const uint64_t n16 = n_bytes / 16;
     const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
     const uint64_t lo = per * blockIdx.x, hi = lo + per < n16 ? lo + per : n16;
@@ -76,6 +77,8 @@ hipError_t launch_stream_probe(const uint8_t* src, uint64_t n_bytes, uint32_t* o
     hipLaunchKernelGGL(k_stream_probe, dim3(grid_blocks), dim3(256), 0, s, src, n_bytes, out);
     return hipGetLastError();
 }
+
+KB_DEFINE_COLLECT(util)
 
 }  // namespace engine
 }  // namespace karma

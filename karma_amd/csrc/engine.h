@@ -114,6 +114,7 @@ struct RaggedArgs {
     uint32_t* partial;         // register contribution per unit slot
     const uint32_t* blob;      // stream blob (kBlobWords)
     const uint32_t* comb_blob; // kCombWords for unit_bytes
+    uintptr_t kb_lo, kb_hi;    // bounds build only: the arena's allocation (bounds.h); else 0
 };
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
@@ -184,6 +185,9 @@ struct WalArgs {
     uint64_t sub_cap;          // list slots per sub-range: sub_bytes / 8 + 1 (cand_cap = nsub * sub_cap)
     WalSubMeta* sub;           // per (segment, sub-range) walker
     uint32_t* span;            // per (segment, sub-range): first list slot of the accepted run, candidates before it
+    uint64_t img_bytes;        // bytes at wal (nwork segments)
+    uint64_t nwork;            // segments walked
+    uint64_t n_all;            // gathered candidates (the contiguous lists' length)
 };
 constexpr uint32_t kWalkTile = 4096;  // the one-wave walker's LDS tile (wal_device.hip)
 constexpr uint32_t kMaxSub = 4096;    // sub-ranges per segment (k_wal_gather stages their runs in LDS)

@@ -2,6 +2,7 @@
 #include "host_stage.h"
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -65,6 +66,67 @@ void run_threads(int n, const std::function<void(int)>& body) {
     th.reserve(n);
     for (int t = 0; t < n; ++t) th.emplace_back(body, t);
     for (auto& x : th) x.join();
+}
+
+namespace {
+
+// Parked threads woken by a generation counter.  Never destroyed (the threads stay
+// parked in a wait at process exit): no static-destruction order against the HIP runtime.
+struct Pool {
+    std::mutex run_mu;  // one run at a time
+    std::mutex mu;
+    std::condition_variable go, done;
+    uint64_t gen = 0;
+    int want = 0, finished = 0;
+    const std::function<void(int)>* body = nullptr;
+    std::vector<std::thread> th;
+    void loop(int t) {  // pool thread t runs body(t + 1)
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        while (true) {
+            go.wait(lk, [&] { return gen != seen; });
+            seen = gen;
+            if (t + 1 >= want) continue;
+            const std::function<void(int)>* b = body;
+            lk.unlock();
+            (*b)(t + 1);
+            lk.lock();
+            if (++finished == want - 1) done.notify_one();
+        }
+    }
+};
+
+Pool& pool() {
+    static Pool* p = [] {
+        Pool* q = new Pool;
+        for (int t = 0; t < kPoolThreads; ++t) q->th.emplace_back([q, t] { q->loop(t); });
+        for (auto& x : q->th) x.detach();
+        return q;
+    }();
+    return *p;
+}
+
+}  // namespace
+
+void run_pool(int n, const std::function<void(int)>& body) {
+    n = std::min(n, kPoolThreads + 1);
+    if (n <= 1) {
+        if (n == 1) body(0);
+        return;
+    }
+    Pool& P = pool();
+    std::lock_guard<std::mutex> one(P.run_mu);
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        P.body = &body;
+        P.want = n;
+        P.finished = 0;
+        ++P.gen;
+    }
+    P.go.notify_all();
+    body(0);
+    std::unique_lock<std::mutex> lk(P.mu);
+    P.done.wait(lk, [&] { return P.finished == P.want - 1; });
 }
 
 bool host_is_pinned(const void* h) {

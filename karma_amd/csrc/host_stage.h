@@ -36,4 +36,11 @@ bool host_is_pinned(const void* h);
 // body(t) for t in [0, n) on n std::threads (n small: the host stages of a call).
 void run_threads(int n, const std::function<void(int)>& body);
 
+// body(t) for t in [0, n): t = 0 on the calling thread, the others on the library's
+// persistent host threads (created on first use and parked between calls, so a call
+// pays a wake-up, not n thread creations).  Returns when every body has returned.
+// n is capped at kPoolThreads + 1.  Calls from several threads are serialised.
+constexpr int kPoolThreads = 15;
+void run_pool(int n, const std::function<void(int)>& body);
+
 }  // namespace karma::engine

@@ -240,6 +240,8 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         T.mark("image upload");
     }
     A.base0 = base0;
+    A.img_bytes = img_bytes;
+    A.nwork = nwork;
     A.seg_bytes = seg_bytes;
     A.first_pos = start - base0;
     // 1. segment-parallel header walk (sub-range walkers when there are few segments)
@@ -301,6 +303,7 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         A.stored = c.stored.as<uint32_t>();
         A.crc = c.crc.as<uint32_t>();
         A.first_bad = c.bad.as<uint64_t>();
+        A.n_all = n_all;
         if (hipMemcpyAsync(c.cbase.p, cb, w1 * 8, hipMemcpyHostToDevice, c.st) != hipSuccess ||
             launch_wal_gather(A, w1, c.st) != hipSuccess)
             return fail(KARMA_E_HIP, "wal_replay: gather");

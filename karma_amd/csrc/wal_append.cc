@@ -9,26 +9,28 @@
 // segment tail shorter than a header is '0' bytes only (:34-39).
 //
 // The path is PCIe-bound (the payloads start in host memory), so every stage is
-// overlapped with the upload:
-//   1. placement (sequential: can_hold, else footer + next segment), published
-//      in blocks of records;
-//   2. framing workers take the blocks as they are published: each writes its
-//      records' length fields and payloads into the WAL image AND copies the
-//      payloads, packed, into the library's pinned staging (the source bytes are
-//      read once, the second copy comes from cache), then DMAs the block on its
-//      stream and runs the block's CRC batch (one record per group of 8 lanes
-//      when every payload <= 1 KiB) and the D2H of its CRCs there;
-//   3. the CRC fields are written when every block's stream has drained.
+// overlapped with the upload, on the library's persistent host threads (run_pool):
+//   1. placement (thread 0, sequential: can_hold, else footer + next segment),
+//      published in blocks of records (small blocks first, so the pipeline fills fast);
+//   2. framing workers take the blocks as they are published (a condition variable,
+//      no spinning: the box's CPU quota is shared by every thread): each writes its
+//      records' length fields and payloads into the WAL image AND packs the payloads
+//      into the library's pinned staging (one copy when the block's payloads are
+//      contiguous in the source), then enqueues the block's DMA, its CRC batch (one
+//      record per group of 8 lanes when every payload <= 1 KiB) and the D2H of its
+//      CRCs on one of 8 streams, and records the block's event;
+//   3. when no block is left to frame, the threads write the CRC fields block by
+//      block as each block's event completes, while later blocks are still in flight.
 // Nothing is page-locked per call: the staging is pinned once and grows.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "engine.h"
@@ -46,18 +48,13 @@ namespace {
 using karma::engine::set_last_error;
 
 constexpr uint64_t kHeader = karma::engine::kWalHeader;  // store::RECORD_HEADER_LENGTH (common.h:11)
-constexpr size_t kBlockRecords = 16384;          // a published block: at most this many records
-constexpr uint64_t kBlockBytes = uint64_t(4) << 20;  // ... or about this many payload bytes
+constexpr size_t kBlockRecords = 16384;              // a published block: at most this many records
+constexpr uint64_t kBlockBytesFirst = uint64_t(256) << 10;  // payload bytes of the first block,
+constexpr uint64_t kBlockBytesMax = uint64_t(4) << 20;      // doubling up to this
 constexpr uint64_t kCallBytes = uint64_t(1) << 30;   // payload bytes staged per pass (larger batches loop)
-constexpr int kStreams = 8;                      // DMA / CRC streams the blocks rotate over
-constexpr int kMaxWorkers = 15;                  // framing workers (+ the placing thread)
+constexpr int kStreams = 8;                          // DMA / CRC streams the blocks rotate over
 
-inline void put32(uint8_t* p, uint32_t v) {
-    p[0] = uint8_t(v);
-    p[1] = uint8_t(v >> 8);
-    p[2] = uint8_t(v >> 16);
-    p[3] = uint8_t(v >> 24);
-}
+inline void put32(uint8_t* p, uint32_t v) { std::memcpy(p, &v, 4); }  // little-endian host
 
 struct Buf {
     void* p = nullptr;
@@ -84,20 +81,33 @@ struct Buf {
     }
 };
 
-// Per-device append context: the streams and the grow-only staging (pinned) and
-// device copies of the packed payloads, their offsets, lengths and CRCs.
+// Per-device append context: the streams, one event per block, the grow-only staging
+// (pinned) and device copies of the packed payloads, their offsets, lengths and CRCs,
+// and the host placement arrays (kept: a fresh 8 MiB vector costs its page faults).
 struct AppendCtx {
     std::mutex mu;
     bool ready = false;
     hipStream_t st[kStreams] = {};
+    std::vector<hipEvent_t> ev;
     Buf h_pay, h_off, h_len, h_crc;  // pinned
     Buf d_pay, d_off, d_len, d_crc;  // device
+    std::vector<uint64_t> at;
+    std::vector<size_t> bstart;
     int init() {
         if (ready) return 0;
         for (auto& s : st)
             if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
                 return set_last_error(KARMA_E_HIP, "wal_append: stream");
         ready = true;
+        return 0;
+    }
+    int events(size_t n) {
+        while (ev.size() < n) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+                return set_last_error(KARMA_E_HIP, "wal_append: event");
+            ev.push_back(e);
+        }
         return 0;
     }
 };
@@ -112,18 +122,14 @@ AppendCtx& ctx_for(int dev) {
     return *g_ctx[dev];
 }
 
-// One pass over records [0, n) of the caller's arrays (payload total <= kCallBytes, or a
-// single record): frames what fits from *cursor, returns the number framed.
+// One pass over records [0, n) of the caller's arrays (payload total pay_total <= kCallBytes,
+// or a single record): frames what fits from *cursor, returns the number framed.
 int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_off, const uint32_t* len, size_t n,
-                uint8_t* wal, size_t wal_bytes, size_t seg_bytes, uint64_t* cursor, uint64_t* rec_off,
-                size_t* n_framed) {
+                uint64_t pay_total, uint32_t max_len, uint8_t* wal, size_t wal_bytes, size_t seg_bytes,
+                uint64_t* cursor, uint64_t* rec_off, size_t* n_framed) {
     karma::engine::PhaseTimer T("wal_append");
-    uint64_t pay_total = 0;
-    uint32_t max_len = 0;
-    for (size_t i = 0; i < n; ++i) {
-        pay_total += len[i];
-        max_len = std::max(max_len, len[i]);
-    }
+    // blocks: at most n / kBlockRecords + (payload / smallest block) + the doubling steps
+    const size_t max_blocks = n / kBlockRecords + pay_total / kBlockBytesFirst + 32;
     if (const int rc = C.h_pay.ensure(pay_total + 16, true)) return rc;
     if (const int rc = C.d_pay.ensure(pay_total + 16, false)) return rc;
     if (const int rc = C.h_off.ensure(n * 8, true)) return rc;
@@ -132,121 +138,157 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
     if (const int rc = C.d_len.ensure(n * 4, false)) return rc;
     if (const int rc = C.h_crc.ensure(n * 4, true)) return rc;
     if (const int rc = C.d_crc.ensure(n * 4, false)) return rc;
-    T.mark("sizes + buffers");
+    if (const int rc = C.events(max_blocks)) return rc;
+    if (C.at.size() < n) C.at.resize(n);
+    if (C.bstart.size() < max_blocks + 2) C.bstart.resize(max_blocks + 2);
+    T.mark("buffers");
     uint8_t* hp = C.h_pay.as<uint8_t>();
     uint64_t* ho = C.h_off.as<uint64_t>();
     uint32_t* hl = C.h_len.as<uint32_t>();
     uint32_t* hc = C.h_crc.as<uint32_t>();
+    uint64_t* at = C.at.data();
+    size_t* bstart = C.bstart.data();
+    bstart[0] = 0;
 
-    // 1. placement, published block by block: bstart[k] = first record of block k
-    std::vector<uint64_t> at(n);
-    std::vector<size_t> bstart(n + 2, 0);
-    std::atomic<size_t> published{0};  // blocks whose end is known (bstart[k + 1] valid)
-    std::atomic<bool> placing{true};
-    std::atomic<size_t> next_block{0};
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t published = 0;  // blocks whose end is known (bstart[k + 1] valid); under mu
+    bool placing = true;   // under mu
+    int framing = 0;       // threads still in stage 2; under mu
+    std::atomic<size_t> next_block{0}, next_fill{0};
     std::atomic<int> crc_rc{0};
-    const int nwork = (int)std::min<size_t>(kMaxWorkers, std::max<size_t>(1, n / 2048));
-    std::vector<std::thread> workers;
-    for (int t = 0; t < nwork; ++t)
-        workers.emplace_back([&] {
-            if (hipSetDevice(dev) != hipSuccess) {
-                crc_rc = KARMA_E_HIP;
-                return;
-            }
-            while (true) {
-                const size_t k = next_block.fetch_add(1);
-                size_t pub;
-                while ((pub = published.load(std::memory_order_acquire)) <= k && placing.load(std::memory_order_acquire))
-                    std::this_thread::yield();
-                pub = published.load(std::memory_order_acquire);
-                if (k >= pub) return;  // placement ended before this block
-                const size_t lo = bstart[k], hi = bstart[k + 1];
-                // 2. frame (segment_file::append_record) and pack the payloads for the device
-                for (size_t i = lo; i < hi; ++i) {
-                    uint8_t* p = wal + at[i];
-                    const uint32_t L = len[i];
-                    put32(p + 4, L << 8 | 0u);
-                    std::memcpy(p + kHeader, src + src_off[i], L);
-                    std::memcpy(hp + ho[i], p + kHeader, L);  // from cache
-                    hl[i] = L;
-                }
-                const uint64_t plo = ho[lo], phi = ho[hi - 1] + hl[hi - 1];
-                hipStream_t s = C.st[k % kStreams];
-                const size_t nr = hi - lo;
-                uint8_t* dp = C.d_pay.as<uint8_t>();
-                uint64_t* doff = C.d_off.as<uint64_t>() + lo;
-                for (size_t i = lo; i < hi; ++i) ho[i] -= plo;  // the block's kernel sees its own slice
-                if (hipMemcpyAsync(dp + plo, hp + plo, phi - plo, hipMemcpyHostToDevice, s) != hipSuccess ||
-                    hipMemcpyAsync(doff, ho + lo, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-                    hipMemcpyAsync(C.d_len.as<uint32_t>() + lo, hl + lo, nr * 4, hipMemcpyHostToDevice, s) !=
-                        hipSuccess) {
-                    crc_rc = KARMA_E_HIP;
-                    return;
-                }
-                if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, doff, C.d_len.as<uint32_t>() + lo, nr,
-                                                                     phi - plo, max_len, nullptr, 0,
-                                                                     C.d_crc.as<uint32_t>() + lo, s)) {
-                    crc_rc = rc;
-                    return;
-                }
-                if (hipMemcpyAsync(hc + lo, C.d_crc.as<uint32_t>() + lo, nr * 4, hipMemcpyDeviceToHost, s) !=
-                    hipSuccess) {
-                    crc_rc = KARMA_E_HIP;
-                    return;
-                }
-            }
-        });
-    karma::engine::WalPlacer place(seg_bytes, wal_bytes, *cursor);
-    size_t framed = 0, nb = 0;
-    uint64_t packed = 0, bbytes = 0;
-    std::vector<std::pair<uint64_t, uint64_t>> footers;  // (wal offset, segment end)
-    for (; framed < n; ++framed) {
-        const uint64_t L = len[framed];
-        uint64_t f0, f1;
-        const bool ok = place.place(L, &at[framed], &f0, &f1);
-        if (f1 > f0) footers.emplace_back(f0, f1);
-        if (!ok) break;
-        ho[framed] = packed;
-        packed += L;
-        bbytes += L;
-        if (framed + 1 - bstart[nb] == kBlockRecords || bbytes >= kBlockBytes) {
-            bstart[++nb] = framed + 1;
-            bbytes = 0;
-            published.store(nb, std::memory_order_release);
+    size_t framed = 0;
+    uint64_t end_cursor = *cursor;
+    // Thread 0 places and then helps; every thread frames blocks while any are left, then
+    // writes CRC fields of completed blocks.  Returns only when its own work is done.
+    auto frame_block = [&](size_t k) {
+        const size_t lo = bstart[k], hi = bstart[k + 1];
+        bool contiguous = true;
+        for (size_t i = lo; i < hi; ++i) {  // segment_file::append_record: length field + payload
+            uint8_t* p = wal + at[i];
+            const uint32_t L = len[i];
+            put32(p + 4, L << 8 | 0u);
+            std::memcpy(p + kHeader, src + src_off[i], L);
+            hl[i] = L;
+            if (i > lo && src_off[i] != src_off[i - 1] + len[i - 1]) contiguous = false;
         }
-    }
-    if (bstart[nb] < framed) {
-        bstart[++nb] = framed;
-        published.store(nb, std::memory_order_release);
-    }
-    placing.store(false, std::memory_order_release);
-    T.mark("placement");
-    for (const auto& f : footers) {  // segment_file::append_footer
-        const uint64_t room = f.second - f.first;
-        if (room < kHeader) {
-            std::memset(wal + f.first, '0', room);
+        const uint64_t plo = ho[lo], phi = ho[hi - 1] + hl[hi - 1];
+        if (contiguous) {
+            std::memcpy(hp + plo, src + src_off[lo], phi - plo);
         } else {
-            put32(wal + f.first, 0);
-            put32(wal + f.first + 4, uint32_t((room - kHeader) << 8 | 1u));
-            std::memset(wal + f.first + kHeader, '0', room - kHeader);
+            for (size_t i = lo; i < hi; ++i) std::memcpy(hp + ho[i], wal + at[i] + kHeader, hl[i]);  // from cache
         }
-    }
-    for (auto& x : workers) x.join();
-    T.mark("framing + uploads enqueued");
-    for (auto& s : C.st)
+        for (size_t i = lo; i < hi; ++i) ho[i] -= plo;  // the block's kernel sees its own slice
+        hipStream_t s = C.st[k % kStreams];
+        const size_t nr = hi - lo;
+        uint8_t* dp = C.d_pay.as<uint8_t>();
+        uint64_t* doff = C.d_off.as<uint64_t>() + lo;
+        uint32_t* dlen = C.d_len.as<uint32_t>() + lo;
+        if (hipMemcpyAsync(dp + plo, hp + plo, phi - plo, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(doff, ho + lo, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(dlen, hl + lo, nr * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+            return KARMA_E_HIP;
+        if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, doff, dlen, nr, phi - plo, max_len, nullptr, 0,
+                                                             C.d_crc.as<uint32_t>() + lo, s))
+            return rc;
+        if (hipMemcpyAsync(hc + lo, C.d_crc.as<uint32_t>() + lo, nr * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipEventRecord(C.ev[k], s) != hipSuccess)
+            return KARMA_E_HIP;
+        return 0;
+    };
+    auto worker = [&](int t) {
+        if (t > 0 && hipSetDevice(dev) != hipSuccess) {  // thread 0 is the caller's (device set)
+            int zero = 0;
+            crc_rc.compare_exchange_strong(zero, (int)KARMA_E_HIP);
+        }
+        if (t == 0) {  // 1. placement (sivir::build_sqe's loop), published block by block
+            karma::engine::WalPlacer place(seg_bytes, wal_bytes, *cursor);
+            std::vector<std::pair<uint64_t, uint64_t>> footers;  // (wal offset, segment end)
+            size_t nb = 0, f = 0;
+            uint64_t packed = 0, bbytes = 0, blimit = kBlockBytesFirst;
+            for (; f < n; ++f) {
+                const uint64_t L = len[f];
+                uint64_t f0, f1;
+                const bool ok = place.place(L, &at[f], &f0, &f1);
+                if (f1 > f0) footers.emplace_back(f0, f1);
+                if (!ok) break;
+                ho[f] = packed;
+                packed += L;
+                bbytes += L;
+                if (f + 1 - bstart[nb] == kBlockRecords || bbytes >= blimit) {
+                    std::lock_guard<std::mutex> lk(mu);
+                    bstart[++nb] = f + 1;
+                    published = nb;
+                    bbytes = 0;
+                    blimit = std::min(2 * blimit, kBlockBytesMax);
+                    cv.notify_all();
+                }
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (bstart[nb] < f) bstart[++nb] = f;
+                published = nb;
+                placing = false;
+                framed = f;
+                end_cursor = place.cur;
+            }
+            cv.notify_all();
+            for (const auto& fp : footers) {  // segment_file::append_footer
+                const uint64_t room = fp.second - fp.first;
+                if (room < kHeader) {
+                    std::memset(wal + fp.first, '0', room);
+                } else {
+                    put32(wal + fp.first, 0);
+                    put32(wal + fp.first + 4, uint32_t((room - kHeader) << 8 | 1u));
+                    std::memset(wal + fp.first + kHeader, '0', room - kHeader);
+                }
+            }
+        }
+        // 2. framing, DMA and CRC batches, block by block
+        while (!crc_rc.load(std::memory_order_relaxed)) {
+            const size_t k = next_block.fetch_add(1);
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return published > k || !placing; });
+                if (k >= published) break;  // placement ended before this block
+            }
+            if (const int rc = frame_block(k)) {
+                int zero = 0;
+                crc_rc.compare_exchange_strong(zero, rc);
+                break;
+            }
+        }
+        // 3. CRC fields of the blocks in order, each once its event has completed.  Every
+        // block must have been enqueued first (an event never recorded in this call would
+        // not wait), so the threads meet here; the DMAs and kernels are still in flight.
+        size_t nb;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            if (--framing == 0) cv.notify_all();
+            cv.wait(lk, [&] { return framing == 0; });
+            nb = published;
+        }
+        while (!crc_rc.load(std::memory_order_relaxed)) {
+            const size_t k = next_fill.fetch_add(1);
+            if (k >= nb) break;
+            if (hipEventSynchronize(C.ev[k]) != hipSuccess) {
+                int zero = 0;
+                crc_rc.compare_exchange_strong(zero, (int)KARMA_E_HIP);
+                break;
+            }
+            for (size_t i = bstart[k]; i < bstart[k + 1]; ++i) put32(wal + at[i], hc[i]);
+        }
+    };
+    const int nthr = (int)std::min<size_t>(karma::engine::kPoolThreads + 1, std::max<size_t>(1, n / 1024));
+    framing = nthr;
+    karma::engine::run_pool(nthr, worker);
+    T.mark("placement + framing + CRCs");
+    for (auto& s : C.st)  // nothing of this call may be in flight when it returns
         if (hipStreamSynchronize(s) != hipSuccess && !crc_rc) crc_rc = KARMA_E_HIP;
-    T.mark("CRC batches");
-    if (const int rc = crc_rc.load()) {  // payloads and length fields are written; no CRC field is
+    if (const int rc = crc_rc.load())  // payloads and length fields are written; CRC fields may not be
         return rc == KARMA_E_HIP ? set_last_error(rc, "wal_append: device pipeline") : rc;
-    }
-    // 3. the CRC fields
-    const int nthr = (int)std::min<size_t>(16, std::max<size_t>(1, framed / 65536));
-    karma::engine::run_threads(nthr, [&](int t) {
-        for (size_t i = framed * t / nthr; i < framed * (t + 1) / nthr; ++i) put32(wal + at[i], hc[i]);
-    });
-    T.mark("CRC fields");
-    if (rec_off) std::memcpy(rec_off, at.data(), framed * sizeof(uint64_t));
-    *cursor = place.cur;
+    if (rec_off) std::memcpy(rec_off, at, framed * sizeof(uint64_t));
+    *cursor = end_cursor;
     *n_framed = framed;
     return 0;
 }
@@ -275,11 +317,15 @@ extern "C" int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_o
     size_t done = 0;
     while (done < n) {  // passes of at most kCallBytes of payload (at least one record)
         size_t m = 1;
-        for (uint64_t bytes = h_len[done]; done + m < n && bytes + h_len[done + m] <= kCallBytes; ++m)
+        uint64_t bytes = h_len[done];
+        uint32_t max_len = h_len[done];
+        for (; done + m < n && bytes + h_len[done + m] <= kCallBytes; ++m) {
             bytes += h_len[done + m];
+            max_len = std::max(max_len, h_len[done + m]);
+        }
         size_t framed = 0;
-        if (const int rc = append_pass(C, dev, src, h_src_off + done, h_len + done, m, wal, wal_bytes, seg_bytes, &cur,
-                                       h_rec_off ? h_rec_off + done : nullptr, &framed))
+        if (const int rc = append_pass(C, dev, src, h_src_off + done, h_len + done, m, bytes, max_len, wal, wal_bytes,
+                                       seg_bytes, &cur, h_rec_off ? h_rec_off + done : nullptr, &framed))
             return rc;  // *h_cursor and *h_n_framed keep the passes already complete
         done += framed;
         *h_cursor = cur;

@@ -26,6 +26,7 @@
 #include <algorithm>
 
 #include "ab.h"
+#include "bounds.h"
 #include "engine.h"
 #include "karma_crc32c.h"
 
@@ -198,7 +199,33 @@ struct Seg {  // one segment as a walker sees it
     const uint8_t* img;
     uint32_t seg;
     bool vec;  // img 16-byte aligned
+#ifdef KARMA_BOUNDS
+    const uint8_t* wlo;  // the image (bounds build: every byte read must lie in it)
+    const uint8_t* whi;
+#endif
 };
+
+__device__ __forceinline__ Seg make_seg(const WalArgs& A, uint64_t s) {
+    const uint8_t* img = A.wal + s * A.seg_bytes;
+#ifdef KARMA_BOUNDS
+    return Seg{img, (uint32_t)A.seg_bytes, (reinterpret_cast<uintptr_t>(img) & 15u) == 0, A.wal, A.wal + A.img_bytes};
+#else
+    return Seg{img, (uint32_t)A.seg_bytes, (reinterpret_cast<uintptr_t>(img) & 15u) == 0};
+#endif
+}
+
+// S.img + off for an n-byte read (the bounds build checks it against the segment and the image).
+__device__ __forceinline__ const uint8_t* seg_at(const Seg& S, uint64_t off, uint32_t n) {
+#ifdef KARMA_BOUNDS
+    if (!kb_ok(off + n <= S.seg, kKbSegment, off, S.seg)) return S.img;
+    const uint8_t* p = S.img + off;
+    if (!kb_ok(p >= S.wlo && p + n <= S.whi, kKbImage, (uint64_t)(p - S.wlo), (uint64_t)(S.whi - S.wlo))) return S.wlo;
+    return p;
+#else
+    (void)n;
+    return S.img + off;
+#endif
+}
 
 // This lane's share of the tile at t: vectors lane + 64 q (q < kWQV) and the slack
 // vector.  The fast case is branch-free: a per-lane branch around a load makes the
@@ -207,8 +234,8 @@ struct Seg {  // one segment as a walker sees it
 __device__ __forceinline__ void wtile_fetch(const Seg& S, uint32_t lane, uint32_t t, uint4 (&r)[kWQV + 1]) {
     if (S.vec && (uint64_t)t + kWTile + 16 <= S.seg) {  // uniform: whole vectors
 #pragma unroll
-        for (int q = 0; q < kWQV; ++q) r[q] = *reinterpret_cast<const uint4*>(S.img + t + (lane + 64u * q) * 16u);
-        r[kWQV] = *reinterpret_cast<const uint4*>(S.img + t + kWTile);  // the slack (every lane, one line)
+        for (int q = 0; q < kWQV; ++q) r[q] = *reinterpret_cast<const uint4*>(seg_at(S, t + (lane + 64u * q) * 16u, 16));
+        r[kWQV] = *reinterpret_cast<const uint4*>(seg_at(S, t + kWTile, 16));  // the slack (every lane, one line)
         return;
     }
     // the segment's last tile, or a misaligned segment: bytes inside the segment, zeros past it
@@ -217,7 +244,7 @@ __device__ __forceinline__ void wtile_fetch(const Seg& S, uint32_t lane, uint32_
         const uint32_t o = q < kWQV ? (lane + 64u * q) * 16u : kWTile;
         uint32_t w[4] = {0u, 0u, 0u, 0u};
         for (uint32_t b = 0; b < 16; ++b)
-            if ((uint64_t)t + o + b < S.seg) w[b >> 2] |= uint32_t(S.img[t + o + b]) << (8 * (b & 3));
+            if ((uint64_t)t + o + b < S.seg) w[b >> 2] |= uint32_t(*seg_at(S, t + o + b, 1)) << (8 * (b & 3));
         r[q] = uint4{w[0], w[1], w[2], w[3]};
     }
 }
@@ -235,14 +262,14 @@ __device__ __forceinline__ void wtile_store(WaveLds& W, uint32_t lane, const uin
 constexpr uint32_t kWSmall = 1024;
 __device__ __forceinline__ void wsmall_fetch(const Seg& S, uint32_t lane, uint32_t t, uint4& v, uint4& slack) {
     if (S.vec && (uint64_t)t + kWSmall + 16 <= S.seg) {
-        v = *reinterpret_cast<const uint4*>(S.img + t + lane * 16u);
-        slack = *reinterpret_cast<const uint4*>(S.img + t + kWSmall);
+        v = *reinterpret_cast<const uint4*>(seg_at(S, t + lane * 16u, 16));
+        slack = *reinterpret_cast<const uint4*>(seg_at(S, t + kWSmall, 16));
         return;
     }
     uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     for (uint32_t b = 0; b < 16; ++b) {
-        if ((uint64_t)t + lane * 16u + b < S.seg) w[b >> 2] |= uint32_t(S.img[t + lane * 16u + b]) << (8 * (b & 3));
-        if ((uint64_t)t + kWSmall + b < S.seg) w[4 + (b >> 2)] |= uint32_t(S.img[t + kWSmall + b]) << (8 * (b & 3));
+        if ((uint64_t)t + lane * 16u + b < S.seg) w[b >> 2] |= uint32_t(*seg_at(S, t + lane * 16u + b, 1)) << (8 * (b & 3));
+        if ((uint64_t)t + kWSmall + b < S.seg) w[4 + (b >> 2)] |= uint32_t(*seg_at(S, t + kWSmall + b, 1)) << (8 * (b & 3));
     }
     v = uint4{w[0], w[1], w[2], w[3]};
     slack = uint4{w[4], w[5], w[6], w[7]};
@@ -275,8 +302,20 @@ struct WalkEnd {
 // is a candidate, a size-0 record compares the stored CRC with Value of the stale
 // len/type word (wal.cc:50-60), type 1 skips to the segment end, anything else
 // stops the walk.  Candidates go to crec / clen (cap slots).
-__device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t pos, uint32_t hi, uint32_t* crec,
-                              uint32_t* clen, uint32_t* ccrc, uint64_t cap) {
+__device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t pos, uint32_t hi, const WalArgs& A,
+                              uint64_t slot0, uint64_t cap) {
+    const uint64_t total = A.nwork * A.cand_cap;  // every list slot (bounds build)
+    (void)total;
+    auto put = [&](uint64_t i, uint32_t rec, uint32_t n, uint32_t c) {  // list entry i (< cap: else dropped)
+#ifdef KARMA_BOUNDS
+        kb_ok(i < cap, kKbCandDropped, i, cap);
+#endif
+        if (i < cap) {
+            KB_WRITE(A.cand_rec, slot0 + i, total, kKbCand, rec);
+            KB_WRITE(A.cand_len, slot0 + i, total, kKbCand, n);
+            KB_WRITE(A.cand_crc, slot0 + i, total, kKbCand, c);
+        }
+    };
     const uint32_t seg = S.seg;
     WalkEnd E{0u, 0u, 0u, seg, pos};
     if ((uint64_t)pos + 8 > seg || pos >= hi) return E;  // wal.cc:40-45: a shorter rest is skipped
@@ -291,11 +330,7 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
             mycrc = c;
         }
         if (++k == 64) {
-            if (E.count + lane < cap) {
-                crec[E.count + lane] = myrec;
-                clen[E.count + lane] = mylen;
-                ccrc[E.count + lane] = mycrc;
-            }
+            put(E.count + lane, myrec, mylen, mycrc);
             E.count += 64;
             k = 0;
         }
@@ -366,11 +401,7 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
             tsz = kWSmall;
         }
     }
-    if (lane < k && E.count + lane < cap) {  // the last, partial run
-        crec[E.count + lane] = myrec;
-        clen[E.count + lane] = mylen;
-        ccrc[E.count + lane] = mycrc;
-    }
+    if (lane < k) put(E.count + lane, myrec, mylen, mycrc);  // the last, partial run
     E.count += k;
     E.pos = pos;
     return E;
@@ -421,7 +452,7 @@ __device__ uint32_t find_start(WaveLds& W, const Seg& S, uint32_t lane, uint32_t
                     if (next < t0 + kWTile) {  // still in the tile (+ its slack): from LDS
                         tile_header(W, next, t0, crc, st);
                     } else {
-                        const uint8_t* h = S.img + next;
+                        const uint8_t* h = seg_at(S, next, 8);
                         crc = uint32_t(h[0]) | uint32_t(h[1]) << 8 | uint32_t(h[2]) << 16 | uint32_t(h[3]) << 24;
                         st = uint32_t(h[4]) | uint32_t(h[5]) << 8 | uint32_t(h[6]) << 16 | uint32_t(h[7]) << 24;
                     }
@@ -448,7 +479,7 @@ __global__ __launch_bounds__(64) void k_wal_walk_sub(WalArgs A) {
     const uint32_t lane = threadIdx.x;
     const uint64_t P = A.nsub, s = blockIdx.x / P, j = blockIdx.x % P;
     const uint64_t rel = s * A.seg_bytes;
-    const Seg S{A.wal + rel, (uint32_t)A.seg_bytes, ((reinterpret_cast<uintptr_t>(A.wal + rel)) & 15u) == 0};
+    const Seg S = make_seg(A, s);
     const uint32_t lo = (uint32_t)(j * A.sub_bytes);
     const uint32_t hi = (uint64_t)lo + A.sub_bytes < S.seg ? lo + (uint32_t)A.sub_bytes : S.seg;
     const uint32_t start = s == 0 ? (uint32_t)A.first_pos : 0u;
@@ -460,14 +491,14 @@ __global__ __launch_bounds__(64) void k_wal_walk_sub(WalArgs A) {
     else
         first = find_start(W, S, lane, lo, hi);
     const uint64_t slot = s * A.cand_cap + j * A.sub_cap;
-    const WalkEnd E = walk_range(W, S, lane, first, hi, A.cand_rec + slot, A.cand_len + slot, A.cand_crc + slot, A.sub_cap);
+    const WalkEnd E = walk_range(W, S, lane, first, hi, A, slot, A.sub_cap);
     if (lane != 0) return;
     if (P == 1) {
-        A.meta[s] = WalSegMeta{E.count, E.kind, A.base0 + rel + (E.kind ? E.stop : S.seg), E.max_len, 0u};
-        A.span[2 * s] = 0;
-        A.span[2 * s + 1] = 0;
+        KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{E.count, E.kind, A.base0 + rel + (E.kind ? E.stop : S.seg), E.max_len, 0u}));
+        KB_WRITE(A.span, 2 * s, 2 * A.nwork, kKbSpan, 0u);
+        KB_WRITE(A.span, 2 * s + 1, 2 * A.nwork, kKbSpan, 0u);
     } else {
-        A.sub[blockIdx.x] = WalSubMeta{first, E.count, E.kind, E.stop, E.pos, E.max_len, {0u, 0u}};
+        KB_WRITE(A.sub, blockIdx.x, A.nwork * P, kKbSubMeta, (WalSubMeta{first, E.count, E.kind, E.stop, E.pos, E.max_len, {0u, 0u}}));
     }
 }
 
@@ -482,17 +513,15 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
     const uint32_t lane = threadIdx.x;
     const uint64_t P = A.nsub, s = blockIdx.x;
     const uint64_t rel = s * A.seg_bytes;
-    const Seg S{A.wal + rel, (uint32_t)A.seg_bytes, ((reinterpret_cast<uintptr_t>(A.wal + rel)) & 15u) == 0};
+    const Seg S = make_seg(A, s);
     const uint32_t seg = S.seg;
-    const WalSubMeta* M = A.sub + s * P;
-    uint32_t* crec = A.cand_rec + s * A.cand_cap;
-    uint32_t* clen = A.cand_len + s * A.cand_cap;
-    uint32_t* ccrc = A.cand_crc + s * A.cand_cap;
+    const uint64_t c0 = s * A.cand_cap, total = A.nwork * A.cand_cap;  // the segment's first list slot
+    (void)total;
     uint32_t pos = s == 0 ? (uint32_t)A.first_pos : 0u;
     uint32_t count = 0, kind = 0, stop = seg, mx = 0;
     WalSubMeta mine{};  // lane l holds walker j0 + l's report: 64 loads at once, not one per step
     for (uint64_t j = 0; j < P; ++j) {
-        if (j % 64 == 0 && j + lane < P) mine = M[j + lane];
+        if (j % 64 == 0 && j + lane < P) mine = KB_READ(A.sub, s * P + j + lane, A.nwork * P, kKbSubMeta);
         const uint32_t lo = (uint32_t)(j * A.sub_bytes);
         const uint32_t hi = (uint64_t)lo + A.sub_bytes < seg ? lo + (uint32_t)A.sub_bytes : seg;
         uint32_t st = (uint32_t)(j * A.sub_cap), n = 0;
@@ -510,12 +539,18 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
                 idx = 0;
             } else if (m.first < pos && m.count > 1) {  // pos among the list's later entries?
                 uint32_t a = 1, b = m.count;             // search [a, b)
+                auto rec_at = [&](uint32_t i) {  // entry i of walker j's list (bounds build: in its slots)
+#ifdef KARMA_BOUNDS
+                    kb_ok(i < A.sub_cap, kKbRunSlot, i, A.sub_cap);
+#endif
+                    return KB_READ(A.cand_rec, c0 + st + i, total, kKbCand);
+                };
                 while (a < b) {
                     const uint32_t mid = (a + b) / 2;
-                    if (crec[st + mid] < pos) a = mid + 1;
+                    if (rec_at(mid) < pos) a = mid + 1;
                     else b = mid;
                 }
-                if (a < m.count && crec[st + a] == pos) idx = a;
+                if (a < m.count && rec_at(a) == pos) idx = a;
             }
             if (idx >= 0) {
                 st += (uint32_t)idx;
@@ -527,7 +562,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
                     stop = m.stop;
                 }
             } else {
-                const WalkEnd E = walk_range(W, S, lane, pos, hi, crec + st, clen + st, ccrc + st, A.sub_cap);
+                const WalkEnd E = walk_range(W, S, lane, pos, hi, A, c0 + st, A.sub_cap);
                 n = E.count;
                 pos = E.pos;
                 mx = E.max_len > mx ? E.max_len : mx;
@@ -538,12 +573,12 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
             }
         }
         if (lane == 0) {
-            A.span[2 * (s * P + j)] = st;
-            A.span[2 * (s * P + j) + 1] = count;  // candidates before the run
+            KB_WRITE(A.span, 2 * (s * P + j), 2 * A.nwork * P, kKbSpan, st);
+            KB_WRITE(A.span, 2 * (s * P + j) + 1, 2 * A.nwork * P, kKbSpan, count);  // candidates before the run
         }
         count += n;
     }
-    if (lane == 0) A.meta[s] = WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg), mx, 0u};
+    if (lane == 0) KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg), mx, 0u}));
 }
 
 // Candidates of segment s0 + blockIdx.x (one block per segment) into the
@@ -559,7 +594,8 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
     const uint32_t* ccrc = A.cand_crc + blockIdx.x * A.cand_cap;
     const uint32_t P = (uint32_t)A.nsub;
     const uint2* sp = reinterpret_cast<const uint2*>(A.span) + blockIdx.x * A.nsub;
-    for (uint32_t j = threadIdx.x; j < P; j += blockDim.x) spans[j] = sp[j];
+    for (uint32_t j = threadIdx.x; j < P; j += blockDim.x)
+        spans[j] = KB_READ(sp, j, (A.nwork - blockIdx.x) * A.nsub, kKbSpan);
     __syncthreads();
     const uint32_t count = A.meta[blockIdx.x].count;
     const uint64_t g0 = A.cand_base[blockIdx.x];
@@ -571,9 +607,12 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
             else b = mid;
         }
         const uint32_t slot = spans[a].x + (i - spans[a].y);
-        A.off[g0 + i] = rel + crec[slot];
-        A.len[g0 + i] = clen[slot];
-        A.stored[g0 + i] = ccrc[slot];
+#ifdef KARMA_BOUNDS
+        kb_ok(slot >= a * A.sub_cap && slot < (a + 1) * A.sub_cap, kKbRunSlot, slot, A.sub_cap);
+#endif
+        KB_WRITE(A.off, g0 + i, A.n_all, kKbList, rel + KB_READ(crec, slot, A.cand_cap, kKbCand));
+        KB_WRITE(A.len, g0 + i, A.n_all, kKbList, KB_READ(clen, slot, A.cand_cap, kKbCand));
+        KB_WRITE(A.stored, g0 + i, A.n_all, kKbList, KB_READ(ccrc, slot, A.cand_cap, kKbCand));
     }
 }
 
@@ -620,6 +659,8 @@ hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t 
     hipLaunchKernelGGL(k_wal_compare, dim3((unsigned)blocks), dim3(256), 0, s, a, n);
     return hipGetLastError();
 }
+
+KB_DEFINE_COLLECT(wal)
 
 }  // namespace engine
 }  // namespace karma

@@ -119,6 +119,25 @@ void test_placement(std::mt19937_64& rng) {
         CHECK(at == at_m);
         CHECK(ft == ft_m);
         CHECK(P.cur == cur_m);
+        // the run form of the parallel writer (wal_append.cc): same records, footers and cursor
+        size_t n_valid = 0;
+        while (n_valid < len.size() && len[n_valid] + 8 <= seg && !(len[n_valid] >> 24)) ++n_valid;
+        std::vector<uint64_t> V(n_valid + 1, 0);
+        for (size_t i = 0; i < n_valid; ++i) V[i + 1] = V[i] + len[i] + 8;
+        std::vector<WalRun> runs;
+        std::vector<WalFooter> rft;
+        uint64_t rcur = cursor;
+        const size_t placed = place_runs(seg, wal, &rcur, n_valid, [&](size_t i) { return V[i]; },
+                                         [&](size_t i) { return len[i]; }, &runs, &rft);
+        std::vector<uint64_t> rat;
+        for (const auto& r : runs)
+            for (size_t i = r.i0; i < r.i1; ++i) rat.push_back(r.base + V[i]);
+        std::vector<std::pair<uint64_t, uint64_t>> rftp;
+        for (const auto& f : rft) rftp.emplace_back(f.f0, f.f1);
+        CHECK(placed == at.size());
+        CHECK(rat == at);
+        CHECK(rftp == ft);
+        CHECK(rcur == P.cur);
         for (const auto& f : ft) CHECK(f.second % seg == 0 && f.second > f.first && f.second - f.first < seg);
     }
 }
