@@ -10,17 +10,17 @@
 //
 // The path is PCIe-bound (the payloads start in host memory), so every stage is
 // overlapped with the upload, on the library's persistent host threads (run_pool):
-//   1. placement (thread 0, sequential: can_hold, else footer + next segment),
-//      published in blocks of records (small blocks first, so the pipeline fills fast);
-//   2. framing workers take the blocks as they are published (a condition variable,
-//      no spinning: the box's CPU quota is shared by every thread): each writes its
-//      records' length fields and payloads into the WAL image AND packs the payloads
-//      into the library's pinned staging (one copy when the block's payloads are
-//      contiguous in the source), then enqueues the block's DMA, its CRC batch (one
-//      record per group of 8 lanes when every payload <= 1 KiB) and the D2H of its
-//      CRCs on one of 8 streams, and records the block's event;
-//   3. when no block is left to frame, the threads write the CRC fields block by
-//      block as each block's event completes, while later blocks are still in flight.
+//   1. a parallel prefix sum of the record sizes, cut into blocks of records (small
+//      blocks first, so the pipeline fills fast), then sivir's loop in run form (one
+//      binary search per segment, wal_place.h) on one thread while the others start 2.;
+//   2. the threads take the blocks in turn: each packs its payloads into the library's
+//      pinned staging (one copy when they are contiguous in the source) and enqueues the
+//      block's DMA, its CRC batch (one record per group of 8 lanes when every payload
+//      <= 1 KiB) and the D2H of its CRCs on one of 8 streams;
+//   3. block by block, in order, as each block's CRCs come back: the records are written
+//      into the image, CRC field, length field and payload in one pass (between blocks
+//      of 2., and the rest once every block is enqueued).
+// No thread spins (the box's CPU quota is shared by every thread of the process).
 // Nothing is page-locked per call: the staging is pinned once and grows.
 #include <hip/hip_runtime_api.h>
 
@@ -122,8 +122,40 @@ AppendCtx& ctx_for(int dev) {
     return *g_ctx[dev];
 }
 
+// A reusable barrier for the threads of one run_pool call.
+struct Barrier {
+    std::mutex mu;
+    std::condition_variable cv;
+    int n, left;
+    uint64_t gen = 0;
+    explicit Barrier(int n_) : n(n_), left(n_) {}
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (--left == 0) {
+            left = n;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+
 // One pass over records [0, n) of the caller's arrays (payload total pay_total <= kCallBytes,
 // or a single record): frames what fits from *cursor, returns the number framed.
+//
+// Every stage runs on all the pool's threads:
+//   a. V(i) = sum_{j<i} (len_j + 8), a parallel prefix sum (kept in at[], turned into WAL
+//      offsets in place when the record is framed) and the packed payload offsets V(i) - 8 i;
+//   b. thread 0: placement in run form (wal_place.h place_runs, one binary search per
+//      segment: WalPlacer's result), the footers and the blocks (small first, doubling);
+//   c. per block: its records framed into the image (length field + payload) and their
+//      payloads packed into pinned staging in the same pass, then its DMA, CRC batch and
+//      CRC readback enqueued on one of 8 streams;
+//   d. per block, in order, once its CRCs are back: the CRC fields -- between blocks of c.
+//      (the block's image lines are then still in the caches), and the rest once every
+//      block is enqueued.
 int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_off, const uint32_t* len, size_t n,
                 uint64_t pay_total, uint32_t max_len, uint8_t* wal, size_t wal_bytes, size_t seg_bytes,
                 uint64_t* cursor, uint64_t* rec_off, size_t* n_framed) {
@@ -148,143 +180,170 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
     uint32_t* hc = C.h_crc.as<uint32_t>();
     uint64_t* at = C.at.data();
     size_t* bstart = C.bstart.data();
-    bstart[0] = 0;
 
-    std::mutex mu;
-    std::condition_variable cv;
-    size_t published = 0;  // blocks whose end is known (bstart[k + 1] valid); under mu
-    bool placing = true;   // under mu
-    int framing = 0;       // threads still in stage 2; under mu
+    const int nthr = (int)std::min<size_t>(karma::engine::kPoolThreads + 1, std::max<size_t>(1, n / 4096));
+    Barrier bar(nthr);
+    std::vector<uint64_t> csum(nthr + 1, 0);
+    std::vector<size_t> cbad(nthr, n);
+    std::vector<karma::engine::WalRun> runs;
+    std::vector<karma::engine::WalFooter> footers;
+    size_t n_valid = 0, framed = 0, nb = 0;
+    uint64_t vtotal = 0, end_cursor = *cursor;
     std::atomic<size_t> next_block{0}, next_fill{0};
     std::atomic<int> crc_rc{0};
-    size_t framed = 0;
-    uint64_t end_cursor = *cursor;
-    // Thread 0 places and then helps; every thread frames blocks while any are left, then
-    // writes CRC fields of completed blocks.  Returns only when its own work is done.
+    std::unique_ptr<std::atomic<uint8_t>[]> enq(new std::atomic<uint8_t>[max_blocks]);
+    for (size_t k = 0; k < max_blocks; ++k) enq[k].store(0, std::memory_order_relaxed);
+    auto set_rc = [&](int rc) {
+        int zero = 0;
+        crc_rc.compare_exchange_strong(zero, rc);
+    };
+    auto chunk = [&](int t, size_t m) { return std::make_pair(m * t / nthr, m * (t + 1) / nthr); };
+    // V(i) for i <= n_valid (V(n_valid) = vtotal; at[i] holds V(i) until the block is framed)
+    auto V = [&](size_t i) { return i < n_valid ? at[i] : vtotal; };
+
+    // c. one block: its records framed into the image (WAL offset, length field, payload) and
+    // their payloads packed into pinned staging in the same pass (the source is read once;
+    // the packing copy comes from the caches), then its DMA, CRC batch and CRC readback
     auto frame_block = [&](size_t k) {
         const size_t lo = bstart[k], hi = bstart[k + 1];
+        size_t r = std::upper_bound(runs.begin(), runs.end(), lo,
+                                    [](size_t i, const karma::engine::WalRun& w) { return i < w.i0; }) -
+                   runs.begin() - 1;  // the run holding record lo
         bool contiguous = true;
         for (size_t i = lo; i < hi; ++i) {  // segment_file::append_record: length field + payload
+            while (i >= runs[r].i1) ++r;
+            at[i] += runs[r].base;  // V(i) -> WAL offset
             uint8_t* p = wal + at[i];
             const uint32_t L = len[i];
             put32(p + 4, L << 8 | 0u);
             std::memcpy(p + kHeader, src + src_off[i], L);
-            hl[i] = L;
             if (i > lo && src_off[i] != src_off[i - 1] + len[i - 1]) contiguous = false;
         }
         const uint64_t plo = ho[lo], phi = ho[hi - 1] + hl[hi - 1];
         if (contiguous) {
             std::memcpy(hp + plo, src + src_off[lo], phi - plo);
         } else {
-            for (size_t i = lo; i < hi; ++i) std::memcpy(hp + ho[i], wal + at[i] + kHeader, hl[i]);  // from cache
+            for (size_t i = lo; i < hi; ++i) std::memcpy(hp + ho[i], wal + at[i] + kHeader, hl[i]);
         }
-        for (size_t i = lo; i < hi; ++i) ho[i] -= plo;  // the block's kernel sees its own slice
         hipStream_t s = C.st[k % kStreams];
         const size_t nr = hi - lo;
         uint8_t* dp = C.d_pay.as<uint8_t>();
+        uint64_t* hoff = ho + lo;  // the block's kernel sees its own slice: offsets rebased onto dp + plo
         uint64_t* doff = C.d_off.as<uint64_t>() + lo;
+        for (size_t i = 0; i < nr; ++i) hoff[i] -= plo;
         uint32_t* dlen = C.d_len.as<uint32_t>() + lo;
         if (hipMemcpyAsync(dp + plo, hp + plo, phi - plo, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(doff, ho + lo, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(doff, hoff, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
             hipMemcpyAsync(dlen, hl + lo, nr * 4, hipMemcpyHostToDevice, s) != hipSuccess)
-            return KARMA_E_HIP;
+            return (int)KARMA_E_HIP;
         if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, doff, dlen, nr, phi - plo, max_len, nullptr, 0,
                                                              C.d_crc.as<uint32_t>() + lo, s))
             return rc;
         if (hipMemcpyAsync(hc + lo, C.d_crc.as<uint32_t>() + lo, nr * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipEventRecord(C.ev[k], s) != hipSuccess)
-            return KARMA_E_HIP;
+            return (int)KARMA_E_HIP;
         return 0;
     };
-    auto worker = [&](int t) {
-        if (t > 0 && hipSetDevice(dev) != hipSuccess) {  // thread 0 is the caller's (device set)
-            int zero = 0;
-            crc_rc.compare_exchange_strong(zero, (int)KARMA_E_HIP);
-        }
-        if (t == 0) {  // 1. placement (sivir::build_sqe's loop), published block by block
-            karma::engine::WalPlacer place(seg_bytes, wal_bytes, *cursor);
-            std::vector<std::pair<uint64_t, uint64_t>> footers;  // (wal offset, segment end)
-            size_t nb = 0, f = 0;
-            uint64_t packed = 0, bbytes = 0, blimit = kBlockBytesFirst;
-            for (; f < n; ++f) {
-                const uint64_t L = len[f];
-                uint64_t f0, f1;
-                const bool ok = place.place(L, &at[f], &f0, &f1);
-                if (f1 > f0) footers.emplace_back(f0, f1);
-                if (!ok) break;
-                ho[f] = packed;
-                packed += L;
-                bbytes += L;
-                if (f + 1 - bstart[nb] == kBlockRecords || bbytes >= blimit) {
-                    std::lock_guard<std::mutex> lk(mu);
-                    bstart[++nb] = f + 1;
-                    published = nb;
-                    bbytes = 0;
-                    blimit = std::min(2 * blimit, kBlockBytesMax);
-                    cv.notify_all();
-                }
-            }
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                if (bstart[nb] < f) bstart[++nb] = f;
-                published = nb;
-                placing = false;
-                framed = f;
-                end_cursor = place.cur;
-            }
-            cv.notify_all();
-            for (const auto& fp : footers) {  // segment_file::append_footer
-                const uint64_t room = fp.second - fp.first;
-                if (room < kHeader) {
-                    std::memset(wal + fp.first, '0', room);
-                } else {
-                    put32(wal + fp.first, 0);
-                    put32(wal + fp.first + 4, uint32_t((room - kHeader) << 8 | 1u));
-                    std::memset(wal + fp.first + kHeader, '0', room - kHeader);
-                }
-            }
-        }
-        // 2. framing, DMA and CRC batches, block by block
+    // d. the CRC fields of the oldest blocks whose CRCs are back (every such event is this
+    // call's: enq); wait = block on the next one instead of returning
+    auto fill_ready = [&](bool wait) {
         while (!crc_rc.load(std::memory_order_relaxed)) {
-            const size_t k = next_block.fetch_add(1);
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return published > k || !placing; });
-                if (k >= published) break;  // placement ended before this block
+            size_t f = next_fill.load();
+            if (f >= nb) return;
+            if (!wait && (!enq[f].load(std::memory_order_acquire) || hipEventQuery(C.ev[f]) != hipSuccess)) return;
+            if (!next_fill.compare_exchange_strong(f, f + 1)) continue;
+            if (wait && hipEventSynchronize(C.ev[f]) != hipSuccess) {
+                set_rc(KARMA_E_HIP);
+                return;
             }
-            if (const int rc = frame_block(k)) {
-                int zero = 0;
-                crc_rc.compare_exchange_strong(zero, rc);
-                break;
-            }
-        }
-        // 3. CRC fields of the blocks in order, each once its event has completed.  Every
-        // block must have been enqueued first (an event never recorded in this call would
-        // not wait), so the threads meet here; the DMAs and kernels are still in flight.
-        size_t nb;
-        {
-            std::unique_lock<std::mutex> lk(mu);
-            if (--framing == 0) cv.notify_all();
-            cv.wait(lk, [&] { return framing == 0; });
-            nb = published;
-        }
-        while (!crc_rc.load(std::memory_order_relaxed)) {
-            const size_t k = next_fill.fetch_add(1);
-            if (k >= nb) break;
-            if (hipEventSynchronize(C.ev[k]) != hipSuccess) {
-                int zero = 0;
-                crc_rc.compare_exchange_strong(zero, (int)KARMA_E_HIP);
-                break;
-            }
-            for (size_t i = bstart[k]; i < bstart[k + 1]; ++i) put32(wal + at[i], hc[i]);
+            for (size_t i = bstart[f]; i < bstart[f + 1]; ++i) put32(wal + at[i], hc[i]);
         }
     };
-    const int nthr = (int)std::min<size_t>(karma::engine::kPoolThreads + 1, std::max<size_t>(1, n / 1024));
-    framing = nthr;
+
+    auto worker = [&](int t) {
+        if (t > 0 && hipSetDevice(dev) != hipSuccess) set_rc(KARMA_E_HIP);  // thread 0 is the caller's
+        // a. chunk sums of len + 8 and the first record that can never be placed
+        {
+            const auto [c0, c1] = chunk(t, n);
+            uint64_t sum = 0;
+            for (size_t i = c0; i < c1; ++i) {
+                const uint64_t L = len[i];
+                if (L + kHeader > seg_bytes || (L >> 24)) {  // WalPlacer::place refuses it
+                    cbad[t] = i;
+                    break;
+                }
+                sum += L + kHeader;
+            }
+            csum[t + 1] = sum;
+        }
+        bar.wait();
+        if (t == 0) {
+            n_valid = n;
+            for (int c = 0; c < nthr; ++c) n_valid = std::min(n_valid, cbad[c]);
+            for (int c = 0; c < nthr; ++c) csum[c + 1] += csum[c];
+        }
+        bar.wait();
+        {
+            const auto [c0, c1] = chunk(t, n);
+            uint64_t v = csum[t];
+            for (size_t i = c0; i < std::min(c1, n_valid); ++i) {
+                at[i] = v;
+                ho[i] = v - kHeader * i;  // packed payload offset
+                hl[i] = len[i];
+                v += len[i] + kHeader;
+            }
+            if ((c0 <= n_valid && n_valid < c1) || (n_valid == n && t == nthr - 1)) vtotal = v;  // V(n_valid)
+        }
+        bar.wait();
+        if (t == 0) T.mark("a. prefix");
+        // b. placement (sivir::build_sqe's loop in run form), the footers and the blocks
+        if (t == 0) {
+            framed = karma::engine::place_runs(seg_bytes, wal_bytes, &end_cursor, n_valid, V,
+                                               [&](size_t i) { return (uint64_t)len[i]; }, &runs, &footers);
+            for (const auto& f : footers) {  // segment_file::append_footer
+                const uint64_t room = f.f1 - f.f0;
+                if (room < kHeader) {
+                    std::memset(wal + f.f0, '0', room);
+                } else {
+                    put32(wal + f.f0, 0);
+                    put32(wal + f.f0 + 4, uint32_t((room - kHeader) << 8 | 1u));
+                    std::memset(wal + f.f0 + kHeader, '0', room - kHeader);
+                }
+            }
+            bstart[0] = 0;  // [b, e): payload bytes <= blimit, or kBlockRecords records
+            uint64_t blimit = kBlockBytesFirst;
+            for (size_t b = 0; b < framed;) {
+                size_t lo = b + 1, hi = std::min(framed, b + kBlockRecords);
+                while (lo < hi) {
+                    const size_t mid = lo + (hi - lo + 1) / 2;
+                    if (ho[mid - 1] + hl[mid - 1] - ho[b] <= blimit) lo = mid;
+                    else hi = mid - 1;
+                }
+                bstart[++nb] = lo;
+                b = lo;
+                blimit = std::min(2 * blimit, kBlockBytesMax);
+            }
+            T.mark("b. placement + blocks");
+        }
+        bar.wait();
+        // c. + d.: frame, pack and enqueue blocks; between blocks, the CRC fields of the blocks
+        // whose CRCs are back (their image lines are then still in the caches)
+        for (size_t k; !crc_rc.load(std::memory_order_relaxed) && (k = next_block.fetch_add(1)) < nb;) {
+            if (const int rc = frame_block(k)) {
+                set_rc(rc);
+                break;
+            }
+            enq[k].store(1, std::memory_order_release);
+            fill_ready(false);
+        }
+        bar.wait();  // every block enqueued (an event not recorded in this call would not wait)
+        if (t == 0) T.mark("c. frame + enqueue");
+        fill_ready(true);
+    };
     karma::engine::run_pool(nthr, worker);
-    T.mark("placement + framing + CRCs");
+    T.mark("d. CRC fields");
     for (auto& s : C.st)  // nothing of this call may be in flight when it returns
-        if (hipStreamSynchronize(s) != hipSuccess && !crc_rc) crc_rc = KARMA_E_HIP;
+        if (hipStreamSynchronize(s) != hipSuccess) set_rc(KARMA_E_HIP);
     if (const int rc = crc_rc.load())  // payloads and length fields are written; CRC fields may not be
         return rc == KARMA_E_HIP ? set_last_error(rc, "wal_append: device pipeline") : rc;
     if (rec_off) std::memcpy(rec_off, at, framed * sizeof(uint64_t));
