@@ -71,21 +71,24 @@ __device__ __forceinline__ bool kb_ok(bool ok, unsigned site, unsigned long long
 
 // The arena range the current kernel's record-byte loads must stay in (set at kernel entry
 // with kb_set_arena; one per workgroup).
+// [slo, shi) is a second range a kernel may read on purpose: the "safe address" its empty
+// units load from (the table blob), else empty.
 struct KbRange {
-    uintptr_t lo, hi;
+    uintptr_t lo, hi, slo, shi;
 };
 __device__ __forceinline__ KbRange& kb_arena() {
     __shared__ KbRange r;
     return r;
 }
-__device__ __forceinline__ void kb_set_arena(uintptr_t lo, uintptr_t hi) {
-    if (threadIdx.x == 0) kb_arena() = KbRange{lo, hi};
+__device__ __forceinline__ void kb_set_arena(uintptr_t lo, uintptr_t hi, uintptr_t slo = 0, uintptr_t shi = 0) {
+    if (threadIdx.x == 0) kb_arena() = KbRange{lo, hi, slo, shi};
     __syncthreads();
 }
 // p checked for n bytes; a violating load reads the arena's first block instead.
 __device__ __forceinline__ const uint8_t* kb_bytes(const uint8_t* p, unsigned n) {
     const KbRange r = kb_arena();
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    if (a >= r.slo && a + n <= r.shi) return p;
     if (kb_ok(a >= r.lo && a + n <= r.hi, kKbArena, a - r.lo, r.hi - r.lo)) return p;
     return reinterpret_cast<const uint8_t*>(r.lo);
 }
@@ -112,6 +115,8 @@ __device__ __forceinline__ const uint8_t* kb_bytes(const uint8_t* p, unsigned n)
     } while (0)
 #define KB_BYTES(p, n) ::karma::engine::kb_bytes((p), (n))
 #define KB_SET_ARENA(lo, hi) ::karma::engine::kb_set_arena((uintptr_t)(lo), (uintptr_t)(hi))
+#define KB_SET_ARENA_SAFE(lo, hi, slo, shi) \
+    ::karma::engine::kb_set_arena((uintptr_t)(lo), (uintptr_t)(hi), (uintptr_t)(slo), (uintptr_t)(shi))
 #endif  // __HIP__
 
 #else  // the shipped build: plain accesses
@@ -124,6 +129,9 @@ __device__ __forceinline__ const uint8_t* kb_bytes(const uint8_t* p, unsigned n)
 #define KB_BYTES(p, n) (p)
 #define KB_SET_ARENA(lo, hi) \
     do {                     \
+    } while (0)
+#define KB_SET_ARENA_SAFE(lo, hi, slo, shi) \
+    do {                                  \
     } while (0)
 #define KB_DEFINE_COLLECT(name)
 

@@ -61,7 +61,10 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 struct DevState {
     bool ready = false;
     int cu = 0;
-    uint32_t* blob = nullptr;
+    uint32_t* blob = nullptr;       // the streaming kernels' tables (stride 128)
+    uint32_t* lane_blob = nullptr;  // the tools build's k_ragged_lanes tables (stride 16)
+    uint32_t* quad_blob = nullptr;  // k_ragged_direct4's tables (stride 64)
+    uint32_t* pair_blob = nullptr;  // the tools build's 2-lane groups (stride 32)
     std::map<uint64_t, uint32_t*> comb;  // unit bytes -> combine blob
     std::map<std::pair<uint64_t, uint64_t>, uint32_t*> bcomb;  // (unit bytes, states per thread) -> block blob
 };
@@ -96,6 +99,17 @@ int dev_state(int dev, DevState** out) {
         build_stream_blob(host.data());
         KARMA_HIP(hipMalloc(&d.blob, kBlobWords * sizeof(uint32_t)));
         KARMA_HIP(hipMemcpy(d.blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+        build_quad_blob(host.data());
+        KARMA_HIP(hipMalloc(&d.quad_blob, kBlobWords * sizeof(uint32_t)));
+        KARMA_HIP(hipMemcpy(d.quad_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+#ifdef KARMA_AB
+        build_pair_blob(host.data());
+        KARMA_HIP(hipMalloc(&d.pair_blob, kBlobWords * sizeof(uint32_t)));
+        KARMA_HIP(hipMemcpy(d.pair_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+        build_lane_blob(host.data());
+        KARMA_HIP(hipMalloc(&d.lane_blob, kBlobWords * sizeof(uint32_t)));
+        KARMA_HIP(hipMemcpy(d.lane_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+#endif
         d.ready = true;
     }
     *out = &d;
@@ -466,7 +480,7 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
     Locked L;
     if (L.rc) return L.rc;
     if (max_len && max_len <= kDirectMaxLen) {
-        // every record small: one record per group, no plan kernels (k_ragged_direct); exact for
+        // every record small: one record per 4-lane group, no plan kernels (k_ragged_direct4); exact for
         // any length, so a wrong bound costs balance, never correctness
         RaggedArgs a{};
         a.arena = static_cast<const uint8_t*>(d_arena);
@@ -476,11 +490,13 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
         a.init = d_init;
         a.init_scalar = init;
         a.out = d_out;
-        a.blob = L.ds->blob;
+        const long dv = KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0);  // tools build: the other kernels
+        a.blob = dv == 1 || dv == 2 ? L.ds->blob : dv == 3 ? L.ds->lane_blob : dv == 5 ? L.ds->pair_blob : L.ds->quad_blob;
         bind_arena_bounds(a);
-        // a wave takes 64 records: no more workgroups than the batch fills (each one loads
-        // the 145 KiB table image into its LDS first)
-        const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_rec, 64 * kWavesPerBlock));
+        // a wave takes 64 records (lanes variant: a workgroup 1024): no more workgroups than
+        // the batch fills (each one loads the 145 KiB table image into its LDS first)
+        const uint64_t per_block = dv == 3 ? kBlockThreads : 64 * kWavesPerBlock;
+        const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_rec, per_block));
         KARMA_HIP(launch_ragged_direct(a, (int)blocks, (hipStream_t)stream));
         return KARMA_OK;
     }

@@ -210,6 +210,11 @@ __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t&
 __device__ __forceinline__ const uint8_t* floor128(const uint8_t* p) {
     return reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(kChunk - 1));
 }
+// The chunk of a group of G lanes: 16 G bytes on the absolute 16 G-byte grid.
+template <int G>
+__device__ __forceinline__ const uint8_t* floor_chunk(const uint8_t* p) {
+    return reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(16 * G - 1));
+}
 
 // Register contribution of the 16-aligned span [us, ue).  The span is read in
 // 128-byte chunks on the ABSOLUTE 128-byte grid (every group load is one whole
@@ -291,21 +296,25 @@ struct LaneUnit {
     bool lok;               // this lane's window in the last chunk lies inside the unit
 };
 
+// G lanes per group (8 for the streaming kernels; 4 for the small-record kernel), a chunk
+// of 16 G bytes.
+template <int G = kGroupLanes>
 __device__ __forceinline__ LaneUnit lane_unit(const uint8_t* us, const uint8_t* ue, uint32_t l) {
+    constexpr int64_t C = 16 * G;
     LaneUnit L;
     L.us = us;
     L.ue = ue;
     L.nch = 0;
-    L.m = kGroupLanes - 1;
+    L.m = G - 1;
     L.lok = false;
     L.w = us;
     L.lclamp = us;
     if (ue > us) {
-        const uint8_t* base = floor128(us);
-        L.nch = (ue - base + kChunk - 1) / kChunk;
-        L.m = (uint32_t)((reinterpret_cast<uintptr_t>(ue) - 16) >> 4) & (kGroupLanes - 1);
+        const uint8_t* base = floor_chunk<G>(us);
+        L.nch = (ue - base + C - 1) / C;
+        L.m = (uint32_t)((reinterpret_cast<uintptr_t>(ue) - 16) >> 4) & (G - 1);
         L.w = base + 16 * l;
-        const uint8_t* wl = base + (L.nch - 1) * kChunk + 16 * l;
+        const uint8_t* wl = base + (L.nch - 1) * C + 16 * l;
         L.lok = wl < ue;
         L.lclamp = L.lok ? wl : ue - 16;
     }
@@ -326,12 +335,12 @@ struct UnitLoads {
     u32x4 nb[PF];
 };
 
-template <int PF, bool NT>
+template <int PF, bool NT, int G = kGroupLanes>
 __device__ __forceinline__ void issue_unit_loads(const LaneUnit& L, UnitLoads<PF>& Ld) {
     const bool ok0 = L.nch > 0 && L.w >= L.us && L.w < L.ue;
     Ld.v0 = ldg<NT>(ok0 ? L.w : L.lclamp);
 #pragma unroll
-    for (int q = 0; q < PF; ++q) Ld.nb[q] = ldg<NT>(pmin(L.w + (q + 1) * kChunk, L.lclamp));
+    for (int q = 0; q < PF; ++q) Ld.nb[q] = ldg<NT>(pmin(L.w + (q + 1) * 16 * G, L.lclamp));
 }
 
 // Streams unit L whose first loads are in Ld; `issue_next(Ld)` is called once,
@@ -341,23 +350,26 @@ __device__ __forceinline__ void issue_unit_loads(const LaneUnit& L, UnitLoads<PF
 // two-bank ring that never runs dry measured no faster: DESIGN.md §4).
 // Every lane of the wave must call this (cross-lane shuffles); the result is
 // valid in group lane 0.
-template <int PF, bool NT, int MODE = 0, typename IssueNext>
+// (G < 8: the LDS image's stride tables must be Z_{16 G}, and the tree takes log2 G levels.)
+template <int PF, bool NT, int MODE = 0, int G = kGroupLanes, typename IssueNext>
 __device__ __forceinline__ uint32_t stream_unit(const uint32_t* lds, uint32_t X, uint32_t l, const LaneUnit& L,
                                                 UnitLoads<PF>& Ld, const uint8_t* inj_at, uint32_t inj,
                                                 IssueNext&& issue_next) {
+    static_assert(G == 8 || G == 4 || G == 2, "groups of 8, 4 or 2 lanes");
+    constexpr int C = 16 * G;
     const bool ok0 = L.nch > 0 && L.w >= L.us && L.w < L.ue;
     u32x4 v = ok0 ? Ld.v0 : u32x4{0u, 0u, 0u, 0u};
     if (ok0 && L.w == inj_at) v.x ^= inj;
     uint32_t a0 = v.x, a1 = v.y, a2 = v.z, a3 = v.w;
     int64_t rem = L.nch - 1;  // chunks after chunk 0; the final one is masked per lane
-    const uint8_t* w = L.w + kChunk;
+    const uint8_t* w = L.w + C;
     while (rem > PF) {
         u32x4 cur[PF];
 #pragma unroll
         for (int q = 0; q < PF; ++q) cur[q] = Ld.nb[q];
-        w += PF * kChunk;
+        w += PF * C;
 #pragma unroll
-        for (int q = 0; q < PF; ++q) Ld.nb[q] = ldg<NT>(pmin(w + q * kChunk, L.lclamp));
+        for (int q = 0; q < PF; ++q) Ld.nb[q] = ldg<NT>(pmin(w + q * C, L.lclamp));
 #pragma unroll
         for (int q = 0; q < PF; ++q) step4<MODE>(lds, X, a0, a1, a2, a3, cur[q]);
         rem -= PF;
@@ -374,13 +386,17 @@ __device__ __forceinline__ uint32_t stream_unit(const uint32_t* lds, uint32_t X,
     // holding the unit's last window rotated to the end
     uint32_t c = lane_fold(lds, a0, a1, a2, a3);
     const uint32_t lane = threadIdx.x & 63u;
-    c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + L.m + 1) & (kGroupLanes - 1))), 64);
-    uint32_t t = __shfl_down(c, 1, kGroupLanes);
+    c = __shfl(c, (int)((lane & ~(G - 1u)) | ((l + L.m + 1) & (G - 1))), 64);
+    uint32_t t = __shfl_down(c, 1, G);
     c = zmap(lds, kLZ16, c) ^ t;
-    t = __shfl_down(c, 2, kGroupLanes);
-    c = zmap(lds, kLZ32, c) ^ t;
-    t = __shfl_down(c, 4, kGroupLanes);
-    c = zmap(lds, kLZ64, c) ^ t;
+    if constexpr (G >= 4) {
+        t = __shfl_down(c, 2, G);
+        c = zmap(lds, kLZ32, c) ^ t;
+    }
+    if constexpr (G == 8) {
+        t = __shfl_down(c, 4, G);
+        c = zmap(lds, kLZ64, c) ^ t;
+    }
     return c;
 }
 

@@ -467,7 +467,214 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     }
 }
 
-// Batches of small records (WAL replay of short records): one record per group,
+// Batches of small records (WAL replay of short records, the bounded ragged ABI, the
+// writer's CRC blocks): one record per group of G = 4 lanes, its whole body one unit, no
+// plan kernels (scan, descriptors and finalize cost more than the CRCs of 180-byte
+// records).  Chunks are 64 bytes on the absolute 64-byte grid, read with the quad blob's
+// Z_64 stride tables; the group tree has two levels.  The head and tail byte steps are
+// serial LDS lookups with a per-record trip count, so a wave does them for 64 records at
+// once (lane i: record base + i), then streams the 64 bodies in 4 rounds of 16 groups,
+// passing each record's entering register in and its body register out by shuffles.
+// The rounds are software-pipelined (stream_unit): round r + 1's loads are issued before
+// round r's last chunks are stepped, and each record's tail block is loaded with its
+// extent.  A group with no body in a round (a short record, or past the batch) streams an
+// empty unit at a valid address (the table blob): every load is issued unconditionally.
+// Correct for any length; balanced when every record is small.
+// Why 4 lanes: the kernel is instruction-bound on small records, and the per-round set-up,
+// lane fold and tree are shared by 16 records instead of 8 (8-lane groups: 0.237 ms per
+// replay call of 1M x 180 B, 4: 0.202, 2: 0.222 -- their loads then spread over 32 cache
+// lines per instruction; one record per lane: 0.327).  G = 2 is the tools
+// build's KARMA_DIRECT_VARIANT=5 (the pair blob, Z_32).
+template <int G>
+__global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) {
+    constexpr int NG = 64 / G, NR = 64 / NG;  // groups per wave, rounds
+    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.blob, A.blob + kBlobWords);  // the blob: empty units' address
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const uint32_t X = lane_const();
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(A.blob);  // 16-aligned, always mapped
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; base < A.n_rec;
+         base += nwaves * 64) {
+        const uint64_t ri = base + lane;
+        const bool vi = ri < A.n_rec;
+        const uint8_t* pi = vi ? A.arena + A.off[ri] : A.arena;
+        const uint32_t ni = vi ? A.len[ri] : 0u;
+        const uint32_t initi = vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
+        const Geom gi = geom(pi, ni);
+        const bool body = vi && !gi.is_short;
+        const uint64_t ai = reinterpret_cast<uintptr_t>(body ? gi.a : safe);
+        const uint64_t bi = reinterpret_cast<uintptr_t>(body ? gi.b : safe);
+        auto unit_of = [&](uint32_t r) {  // round r's record of this group: base + NG r + grp
+            const int src = (int)(r * NG + grp);
+            const uint8_t* us = reinterpret_cast<const uint8_t*>((uintptr_t)__shfl((long long)ai, src));
+            const uint8_t* ue = reinterpret_cast<const uint8_t*>((uintptr_t)__shfl((long long)bi, src));
+            return lane_unit<G>(us, ue, l);
+        };
+        LaneUnit L = unit_of(0);
+        UnitLoads<kRaggedPF> Ld;
+        issue_unit_loads<kRaggedPF, kRaggedNT, G>(L, Ld);
+        const bool tail = body && gi.e > gi.b;
+        const u32x4 tv = ld16(tail ? gi.b : safe);
+        const uint32_t hi = body ? head_register(lds, kLZ4, kLT8, pi, gi, initi) : 0u;
+        uint32_t Ri = 0;
+#pragma unroll 1
+        for (uint32_t round = 0; round < NR; ++round) {
+            const uint32_t sh = __shfl(hi, (int)(round * NG + grp));
+            LaneUnit N = L;
+            const uint32_t R = stream_unit<kRaggedPF, kRaggedNT, 0, G>(lds, X, l, L, Ld, L.us, sh,
+                                                                       [&](UnitLoads<kRaggedPF>& nx) {
+                if (round + 1 < NR) {
+                    N = unit_of(round + 1);
+                    issue_unit_loads<kRaggedPF, kRaggedNT, G>(N, nx);
+                }
+            });
+            const uint32_t Rr = __shfl(R, (int)((lane % NG) * G));  // group (lane % NG)'s register
+            if (lane / NG == round) Ri = Rr;
+            L = N;
+        }
+        if (vi)
+            A.out[ri] = gi.is_short ? short_record(lds, kLZ4, kLT8, pi, ni, initi)
+                                    : ~steps_in_vec(lds, kLZ4, kLT8, Ri, tv, 0u, tail ? (uint32_t)(gi.e - gi.b) : 0u);
+    }
+}
+
+#ifdef KARMA_AB
+// Tools build (KARMA_DIRECT_VARIANT=1, ab.h): small records one per group of 8 lanes, the
+// shipped kernel before k_ragged_direct4 (0.237 vs 0.202 ms per 1M x 180 B replay call,
+// DESIGN.md §8a).  Batches of small records: one record per group, its whole body one unit, no plan kernels (scan, descriptors and
+// finalize cost more than the CRCs of 180-byte records).  The head and tail byte steps are
+// serial LDS lookups with a per-record trip count, so a wave does them for 64 records at
+// once (lane i: record base + i), and streams the 64 bodies in 8 rounds of 8 groups,
+// passing each record's entering register in and its body register out by shuffles.
+// The rounds are software-pipelined (stream_unit): round r + 1's loads are issued before
+// round r's last chunks are stepped, and each record's tail block is loaded with its
+// extent, so a wave waits on memory about once per 64 records instead of once per round.
+// A group with no body in a round (a short record, or past the batch) streams an empty
+// unit at a valid address (the table blob): every load is issued unconditionally.
+// Correct for any length; balanced when every record is small.
+__global__ __launch_bounds__(kBlockThreads) void k_ragged_direct(RaggedArgs A) {
+    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.blob, A.blob + kBlobWords);  // the blob: empty units' address
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(A.blob);  // 16-aligned, always mapped
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; base < A.n_rec;
+         base += nwaves * 64) {
+        // lane i: record base + i -- its extent, entering register and tail block
+        const uint64_t ri = base + lane;
+        const bool vi = ri < A.n_rec;
+        const uint8_t* pi = vi ? A.arena + A.off[ri] : A.arena;
+        const uint32_t ni = vi ? A.len[ri] : 0u;
+        const uint32_t initi = vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
+        const Geom gi = geom(pi, ni);
+        const bool body = vi && !gi.is_short;
+        const uint64_t ai = reinterpret_cast<uintptr_t>(body ? gi.a : safe);
+        const uint64_t bi = reinterpret_cast<uintptr_t>(body ? gi.b : safe);
+        // round r's unit of this group: record base + 8 r + grp (shuffles with every lane active)
+        auto unit_of = [&](uint32_t r) {
+            const int src = (int)(r * kGroupsPerWave + grp);
+            const uint8_t* us = reinterpret_cast<const uint8_t*>((uintptr_t)__shfl((long long)ai, src));
+            const uint8_t* ue = reinterpret_cast<const uint8_t*>((uintptr_t)__shfl((long long)bi, src));
+            return lane_unit(us, ue, l);
+        };
+        LaneUnit L = unit_of(0);
+        UnitLoads<kRaggedPF> Ld;
+        issue_unit_loads<kRaggedPF, kRaggedNT>(L, Ld);
+        const bool tail = body && gi.e > gi.b;
+        const u32x4 tv = ld16(tail ? gi.b : safe);
+        const uint32_t hi = body ? head_register(lds, kLZ4, kLT8, pi, gi, initi) : 0u;
+        uint32_t Ri = 0;
+#pragma unroll 1
+        for (uint32_t round = 0; round < 8; ++round) {
+            const uint32_t sh = __shfl(hi, (int)(round * kGroupsPerWave + grp));
+            LaneUnit N = L;
+            const uint32_t R = stream_unit<kRaggedPF, kRaggedNT>(lds, X, l, L, Ld, L.us, sh, [&](UnitLoads<kRaggedPF>& nx) {
+                if (round + 1 < 8) {
+                    N = unit_of(round + 1);
+                    issue_unit_loads<kRaggedPF, kRaggedNT>(N, nx);
+                }
+            });
+            const uint32_t Rr = __shfl(R, (int)((lane & 7u) * kGroupLanes));  // group (lane & 7)'s register
+            if (lane / kGroupsPerWave == round) Ri = Rr;
+            L = N;
+        }
+        if (vi)
+            A.out[ri] = gi.is_short ? short_record(lds, kLZ4, kLT8, pi, ni, initi)
+                                    : ~steps_in_vec(lds, kLZ4, kLT8, Ri, tv, 0u, tail ? (uint32_t)(gi.e - gi.b) : 0u);
+    }
+}
+
+// Tools build (KARMA_DIRECT_VARIANT=3, ab.h): small records one per LANE, measured slower
+// than k_ragged_direct on the WAL replay's 180-byte records (0.327 vs 0.240 ms per replay
+// call): a lane's 16-byte loads of its own record make every load
+// instruction touch 64 cache lines.  Each lane runs the
+// reference's own structure over its record (crc32c.cc:323-370): the unaligned head byte
+// steps, four word slots striding 16 bytes through the aligned body (Z_16 from the
+// bank-replicated LDS tables of the lane blob, one v_perm_b32 per lookup address), the
+// STEP4W lane fold and the unaligned tail.  There is no cross-lane work at all (no group
+// tree, no rounds, no shuffles), which is what bounds the one-record-per-group kernel on
+// 180-byte records (k_ragged_direct: ~110 VALU instructions per record, mostly fold, tree
+// and unit set-up for two chunks of data).  A lane loads up to kLaneWindows 16-byte
+// windows of its body at once: the 8 windows of one cache line are in flight together, so
+// each line is requested from L2 once.
+constexpr int kLaneWindows = 16;
+
+__global__ __launch_bounds__(kBlockThreads) void k_ragged_lanes(RaggedArgs A) {
+    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.blob, A.blob + kBlobWords);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);  // the lane blob: Z_16 replicated, Z4, the byte table
+    __syncthreads();
+    const uint32_t X = lane_const();
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(A.blob);
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < A.n_rec; r += nthr) {
+        const uint8_t* p = A.arena + A.off[r];
+        const uint32_t n = A.len[r];
+        const uint32_t init = A.init ? A.init[r] : A.init_scalar;
+        const Geom g = geom(p, n);
+        if (g.is_short) {
+            A.out[r] = short_record(lds, kLZ4, kLT8, p, n, init);
+            continue;
+        }
+        const uint64_t nw = (uint64_t)(g.b - g.a) / 16;  // aligned body windows (>= 1)
+        const bool tail = g.e > g.b;
+        // first batch of windows, the head and the tail blocks: all in flight at once
+        u32x4 v[kLaneWindows];
+        uint64_t m = nw < kLaneWindows ? nw : kLaneWindows;
+#pragma unroll
+        for (int q = 0; q < kLaneWindows; ++q) v[q] = ldg<true>(g.a + 16 * ((uint64_t)q < m ? q : m - 1));
+        const u32x4 tv = ld16(tail ? g.b : safe);
+        const uint32_t h = head_register(lds, kLZ4, kLT8, p, g, init);
+        uint32_t a0 = v[0].x ^ h, a1 = v[0].y, a2 = v[0].z, a3 = v[0].w;
+#pragma unroll
+        for (int q = 1; q < kLaneWindows; ++q)
+            if ((uint64_t)q < m) step4(lds, X, a0, a1, a2, a3, v[q]);
+        for (uint64_t c = kLaneWindows; c < nw; c += kLaneWindows) {  // longer bodies: further batches
+            m = nw - c < kLaneWindows ? nw - c : kLaneWindows;
+            const uint8_t* w = g.a + 16 * c;
+#pragma unroll
+            for (int q = 0; q < kLaneWindows; ++q) v[q] = ldg<true>(w + 16 * ((uint64_t)q < m ? q : m - 1));
+#pragma unroll
+            for (int q = 0; q < kLaneWindows; ++q)
+                if ((uint64_t)q < m) step4(lds, X, a0, a1, a2, a3, v[q]);
+        }
+        const uint32_t R = lane_fold(lds, a0, a1, a2, a3);  // the register at the body end
+        A.out[r] = ~steps_in_vec(lds, kLZ4, kLT8, R, tv, 0u, tail ? (uint32_t)(g.e - g.b) : 0u);
+    }
+}
+
+// The first form of k_ragged_direct (tools build, KARMA_DIRECT_VARIANT=2, ab.h): each round's
+// loads issued when the round starts.  Batches of small records: one record per group,
 // its whole body one unit, no plan kernels (scan, descriptors and finalize cost
 // more than the CRCs of 180-byte records).  The head and tail byte steps are
 // serial LDS lookups with a per-record trip count, so a wave does them for 64
@@ -475,7 +682,7 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
 // rounds of 8 groups, passing each record's entering register in and its body
 // register out by shuffles.  Correct for any length; balanced when every record
 // is small.
-__global__ __launch_bounds__(kBlockThreads) void k_ragged_direct(RaggedArgs A) {
+__global__ __launch_bounds__(kBlockThreads) void k_ragged_direct_v1(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
@@ -518,12 +725,26 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct(RaggedArgs A) {
     }
 }
 
+#endif
+
 }  // namespace
 
 hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     units_timer_begin(s);
-    hipLaunchKernelGGL(k_ragged_direct, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+#ifdef KARMA_AB
+    const long v = KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0);
+    if (v == 1)
+        hipLaunchKernelGGL(k_ragged_direct, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 2)
+        hipLaunchKernelGGL(k_ragged_direct_v1, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 3)
+        hipLaunchKernelGGL(k_ragged_lanes, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 5)
+        hipLaunchKernelGGL(k_ragged_direct4<2>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else
+#endif
+        hipLaunchKernelGGL(k_ragged_direct4<4>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     return hipGetLastError();
 }

@@ -57,6 +57,11 @@ constexpr uint64_t kBlockCombMaxPerThread = 64;  // one launch folds up to 64 Ki
 
 // Host builders (gf2.h): fill a blob for stride kChunk / for unit size D.
 void build_stream_blob(uint32_t* out /*kBlobWords*/);
+// The same layout with Z_16 as the stride tables: k_ragged_lanes, one record per lane.
+void build_lane_blob(uint32_t* out /*kBlobWords*/);
+// ... and with Z_64: k_ragged_direct4, one record per group of 4 lanes.
+void build_quad_blob(uint32_t* out /*kBlobWords*/);
+void build_pair_blob(uint32_t* out /*kBlobWords*/);  // Z_32: the tools build's 2-lane groups
 void build_combine_blob(uint64_t unit_bytes, uint32_t* out /*kCombWords*/);
 void build_block_combine_blob(uint64_t unit_bytes, uint64_t per_thread, uint32_t* out /*kBlockCombWords*/);
 
@@ -140,7 +145,8 @@ inline uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock 
 // fbase[n_rec]), then descriptors, the unit kernel and the per-record finalize.
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s);
-// One record per group, no plan kernels (uses arena, off, len, n_rec, init, out, blob).
+// One record per group of 4 lanes, no plan kernels (uses arena, off, len, n_rec, init, out, and
+// blob = build_quad_blob's; the tools build's KARMA_DIRECT_VARIANT picks the alternatives).
 hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // Library-internal entry (capi.cc) for callers that know every record is small
 // (WAL replay): CRCs of arena[off[r], off[r] + len[r]) with Value's init.

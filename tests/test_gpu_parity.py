@@ -374,12 +374,19 @@ def test_ragged_low_total_len_is_still_exact(raw, dev):
         _eq(got, want)
 
 
+@pytest.mark.parametrize("variant", ["shipped", "1", "2", "3", "4", "5"])
 @pytest.mark.parametrize("bound", [0, 64, 1024, 1 << 20])
-def test_ragged_bounded_direct_path(raw, dev, bound):
+def test_ragged_bounded_direct_path(raw, dev, bound, variant, monkeypatch):
     """karma_crc32c_batch_ragged_bounded: with max_len <= 1 KiB one record per group (no plan
-    kernels); any bound -- too low included -- gives the exact CRCs, with per-record inits."""
+    kernels); any bound -- too low included -- gives the exact CRCs, with per-record inits.
+    Variants 1-5 are the tools build's small-record kernels (KARMA_DIRECT_VARIANT: 8-lane groups
+    pipelined / un-pipelined, one record per lane, the shipped 4-lane groups, 2-lane groups)."""
     host, dbuf = raw
-    L = _lib.lib()
+    if variant == "shipped":
+        L = _lib.lib()
+    else:
+        monkeypatch.setenv("KARMA_DIRECT_VARIANT", variant)
+        L = _lib.load(_lib.AB_LIB_PATH)
     rng = np.random.default_rng(bound + 1)
     lens = np.concatenate([rng.integers(0, 1025, 20000), rng.integers(0, 40, 3000),
                            [0, 1, 15, 16, 17, 31, 1023, 1024, 5000]]).astype(np.uint32)
@@ -392,6 +399,6 @@ def test_ragged_bounded_direct_path(raw, dev, bound):
     st = L.karma_crc32c_batch_ragged_bounded(dbuf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), lens.size,
                                              int(lens.sum()), bound, d_ini.data_ptr(), 0, out.data_ptr(),
                                              torch.cuda.current_stream().cuda_stream)
-    _lib.check("batch_ragged_bounded", st)
+    assert st == 0, L.karma_crc32c_last_error()
     _eq(out.cpu().numpy().view(np.uint32), oracle_lib.ragged_crcs(host, offs, lens, init))
 

@@ -46,16 +46,23 @@ WALKS = {
     "whole": (False, 1 << 30, _lib.KARMA_WAL_CRC_PLAN),   # k_wal_walk_sub, one walker per segment
     "split": (False, 0, _lib.KARMA_WAL_CRC_PLAN),         # the plan: few segments -> sub-range walkers
     "split4k": (False, 4096, _lib.KARMA_WAL_CRC_DIRECT),  # one-tile sub-ranges + k_wal_resolve, and every
-}                                                         # CRC batch one record per group (any length)
+                                                          # CRC batch one record per group (any length)
+    "octet": (True, 4096, _lib.KARMA_WAL_CRC_DIRECT),     # the same with the tools build's 8-lane groups
+}
+_DIRECT_VARIANT = {"octet": "1"}  # KARMA_DIRECT_VARIANT of the tools-build plans
 _WALK = {"name": "split"}
 
 
 def _walk_env(monkeypatch, walk):
     monkeypatch.setitem(_WALK, "name", walk)
-    if WALKS[walk][0]:
+    if WALKS[walk][0] and walk not in _DIRECT_VARIANT:
         monkeypatch.setenv("KARMA_WALK_VARIANT", "1")  # read by the tools build only (ab.h)
     else:
         monkeypatch.delenv("KARMA_WALK_VARIANT", raising=False)
+    if walk in _DIRECT_VARIANT:
+        monkeypatch.setenv("KARMA_DIRECT_VARIANT", _DIRECT_VARIANT[walk])
+    else:
+        monkeypatch.delenv("KARMA_DIRECT_VARIANT", raising=False)
 
 
 def _replay(lib, wal, start=0, d_wal=None, seg=SEG, host=True):
@@ -200,7 +207,7 @@ def test_replay_large_records_jumps(lib, seg, walk, monkeypatch):
         assert got == (list(w[0]), w[1], w[2])
 
 
-@pytest.mark.parametrize("walk", ["split", "split4k"])
+@pytest.mark.parametrize("walk", ["split", "split4k", "octet"])
 def test_replay_payloads_that_look_like_wal_records(lib, walk, monkeypatch):
     """Payloads that are themselves WAL images (valid header chains inside records): a sub-range
     walker can start on a header inside a payload, and the resolver must then walk the sub-range

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Device-resident WAL replay A/B (run on the GPU box from the repo root):
+
+    python tools/replay_study.py [--mix fixed|config3] [--rounds 5] [--calls 20]
+
+Builds the bench's WAL image (1M x 180 B records, or configs[2]'s mix, in 1 MiB segments) with
+karma_wal_append_batch, copies it into HBM, and times karma_wal_replay_tuned over the device
+copy for each variant in interleaved rounds (same process, same image):
+
+    shipped              the shipped library, default plan
+    sub=<bytes>          the shipped library, sub-range walkers of <bytes> (walk_sub_bytes)
+    direct               tools build, KARMA_DIRECT_VARIANT=1 (k_ragged_direct: one record per 8 lanes)
+    direct_v1            tools build, KARMA_DIRECT_VARIANT=2 (the same, un-pipelined rounds)
+    lanes                tools build, KARMA_DIRECT_VARIANT=3 (k_ragged_lanes: one record per lane)
+    direct4              tools build, KARMA_DIRECT_VARIANT=4 (= the shipped k_ragged_direct4<4>)
+    direct2              tools build, KARMA_DIRECT_VARIANT=5 (k_ragged_direct4<2>: pairs of lanes)
+    units                the shipped library, ragged plan instead of the direct kernel (crc_batch)
+
+Every call's result is checked (record count).  Prints ms per call and GB/s of image bytes per
+variant (median over rounds).
+"""
+import argparse
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--mix", default="fixed", choices=["fixed", "config3"])
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--calls", type=int, default=20)
+    p.add_argument("--variants", default="shipped,direct4,direct_v1,sub=24576,sub=32768,sub=40960")
+    a = p.parse_args()
+    import torch
+    import synth
+    from karma_amd import _lib
+    seg = 1 << 20
+    if a.mix == "config3":
+        count = int((4 << 30) / (((65536 - 64) / np.log(1024)) + 8))
+        lens = synth.loguniform_lengths(7, count, 64, 65536).astype(np.uint32)
+        wal_bytes = ((int(lens.sum()) + 8 * count) // (seg - 65544) + 2) * seg
+    else:
+        count, size = 1 << 20, 180
+        lens = np.full(count, size, dtype=np.uint32)
+        wal_bytes = ((count + seg // (size + 8) - 1) // (seg // (size + 8)) + 1) * seg
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(42, 0, int(lens.sum()) + 16).copy()
+    wal = np.zeros(wal_bytes, dtype=np.uint8)
+    L = _lib.lib()
+    cur, nf = ctypes.c_uint64(0), ctypes.c_size_t()
+    _lib.check("append", L.karma_wal_append_batch(src.ctypes.data, offs.ctypes.data, lens.ctypes.data, count,
+                                                  wal.ctypes.data, wal_bytes, seg, ctypes.byref(cur), None,
+                                                  ctypes.byref(nf), 0))
+    assert nf.value == count
+    d_wal = torch.from_numpy(wal).cuda()
+    torch.cuda.synchronize()
+    AB = _lib.load(_lib.AB_LIB_PATH)
+    n, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+
+    def call(lib, sub, batch):
+        t = _lib.WalTuning(sub, batch, 0)
+        st = lib.karma_wal_replay_tuned(None, d_wal.data_ptr(), wal_bytes, seg, 0, ctypes.byref(n), ctypes.byref(stop),
+                                        ctypes.byref(status), None, 0, 0, ctypes.byref(t))
+        assert st == 0 and n.value == count, (st, n.value)
+
+    variants = {}
+    for v in a.variants.split(","):
+        if v == "shipped":
+            variants[v] = (L, 0, 0, None)
+        elif v == "direct":
+            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "1"))
+        elif v == "direct_v1":
+            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "2"))
+        elif v == "lanes":
+            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "3"))
+        elif v == "direct4":
+            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "4"))
+        elif v == "direct2":
+            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "5"))
+        elif v == "units":
+            variants[v] = (L, 0, 2, None)
+        elif v.startswith("sub="):
+            variants[v] = (L, int(v[4:]), 0, None)
+    res = {v: [] for v in variants}
+    for r in range(a.rounds):
+        for v, (lib, sub, batch, env) in variants.items():
+            if env:
+                os.environ[env[0]] = env[1]
+            for _ in range(3):
+                call(lib, sub, batch)
+            t0 = time.perf_counter()
+            for _ in range(a.calls):
+                call(lib, sub, batch)
+            res[v].append((time.perf_counter() - t0) / a.calls * 1e3)
+            if env:
+                del os.environ[env[0]]
+        print(f"round {r}: " + "  ".join(f"{v} {res[v][-1]:.4f}" for v in variants), flush=True)
+    for v in variants:
+        ms = float(np.median(res[v]))
+        print(f"{v:>14}: {ms:.4f} ms/call  {wal_bytes / ms / 1e6:.1f} GB/s image  "
+              f"{int(lens.sum()) / ms / 1e6:.1f} GB/s payload", flush=True)
+
+
+if __name__ == "__main__":
+    main()
