@@ -389,6 +389,27 @@ int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_
                        uint32_t* d_out, hipStream_t s) {
     return karma_crc32c_batch_ragged_bounded(d_arena, d_off, d_len, n_rec, 0, 1, nullptr, 0, d_out, s);
 }
+int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
+                           uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
+                           hipStream_t s) {
+    if (!n_cap) return 0;
+    Locked L;
+    if (L.rc) return L.rc;
+    RaggedArgs a{};
+    a.arena = static_cast<const uint8_t*>(d_arena);
+    a.off = d_off;
+    a.len = d_len;
+    a.n_rec = n_cap;
+    a.out = d_out;
+    a.blob = L.ds->quad_blob;
+    a.n_dev = d_n;
+    a.gate_len = d_gate_len;
+    a.gate_max = gate_max;
+    bind_arena_bounds(a);
+    const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_cap, 64 * kWavesPerBlock));
+    KARMA_HIP(launch_ragged_direct_dev(a, (int)blocks, s));
+    return 0;
+}
 namespace {
 thread_local hipEvent_t t_units_start = nullptr, t_units_stop = nullptr;
 }

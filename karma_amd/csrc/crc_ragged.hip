@@ -29,7 +29,8 @@ namespace {
 
 using namespace dev;
 
-constexpr int kRaggedPF = 4;
+constexpr int kRaggedPF = 4;       // chunk loads in flight per lane: small-record and pipelined kernels
+constexpr int kRaggedUnitsPF = 6;  // ... and the shipped units kernel (k_units_ragged)
 constexpr bool kRaggedNT = true;
 
 static_assert(kScanBlock % 64 == 0 && kScanBlock <= 1024 && kScanBlock >= kBuckets, "scan block shape");
@@ -330,7 +331,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs 
 // (group_unit), the next descriptor is in flight meanwhile.  On config 3 it
 // measures 1% faster than k_units_ragged_pipe, unlike the
 // fixed layout, where the pipelined form wins 2.7%.
-template <bool BAL = true>
+// PF = 6 chunk loads in flight per lane (4: config 3 units 0.6736 vs 0.6680 ms, aligned 4 KiB
+// records 0.6656 vs 0.6525; 8: no better than 4 -- profiles/r02_ragged_pf_ab.txt).  With one
+// 1024-thread workgroup per CU (the 145 KiB LDS image) the chunks in flight per CU are what
+// keeps HBM busy across the unit boundaries this kernel does not pipeline.
+template <bool BAL = true, int PF = kRaggedUnitsPF>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
@@ -366,7 +371,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
         const uint64_t un = wb_next * kGroupsPerWave + grp;
         d = un < U ? load_desc(&KB_READ(A.desc, un, A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
         const uint8_t* us = reinterpret_cast<const uint8_t*>(cur.us);
-        const uint32_t R = group_unit<kRaggedPF, kRaggedNT>(lds, X, l, us, us + cur.span, us, cur.inj);
+        const uint32_t R = group_unit<PF, kRaggedNT>(lds, X, l, us, us + cur.span, us, cur.inj);
         if (valid && l == 0) KB_WRITE(A.partial, u, A.unit_cap, kKbUnit, R);
         wb = wb_next;
         u = un;
@@ -488,6 +493,11 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
 template <int G>
 __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) {
     constexpr int NG = 64 / G, NR = 64 / NG;  // groups per wave, rounds
+    uint64_t n_rec = A.n_rec;
+    if (A.n_dev) {  // a device-sized batch: the count is known on the device only
+        if (*A.gate_len > A.gate_max) return;
+        n_rec = *A.n_dev;
+    }
     KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.blob, A.blob + kBlobWords);  // the blob: empty units' address
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     load_stream_tables(lds, A.blob);
@@ -498,10 +508,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
     const uint32_t X = lane_const();
     const uint8_t* safe = reinterpret_cast<const uint8_t*>(A.blob);  // 16-aligned, always mapped
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; base < A.n_rec;
+    for (uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; base < n_rec;
          base += nwaves * 64) {
         const uint64_t ri = base + lane;
-        const bool vi = ri < A.n_rec;
+        const bool vi = ri < n_rec;
         const uint8_t* pi = vi ? A.arena + A.off[ri] : A.arena;
         const uint32_t ni = vi ? A.len[ri] : 0u;
         const uint32_t initi = vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
@@ -749,6 +759,12 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
     return hipGetLastError();
 }
 
+hipError_t launch_ragged_direct_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
+    if (a.n_rec == 0 || !a.n_dev || !a.gate_len) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ragged_direct4<4>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     if (a.unit_bytes != kU) return hipErrorInvalidValue;
@@ -762,9 +778,13 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
     hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     units_timer_begin(s);
-#ifdef KARMA_AB  // tools build (ab.h): 1 = pipelined, 2 = static wave-steps, 3 = both
+#ifdef KARMA_AB  // tools build (ab.h): 1 = pipelined, 2 = static wave-steps, 3 = both, 4 / 8 = chunks in flight
     const long v = KARMA_AB_KNOB("KARMA_RAGGED_VARIANT", 0);
-    if (v == 1)
+    if (v == 4)
+        hipLaunchKernelGGL((k_units_ragged<true, 4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 8)
+        hipLaunchKernelGGL((k_units_ragged<true, 8>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 1)
         hipLaunchKernelGGL(k_units_ragged_pipe<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 3)
         hipLaunchKernelGGL(k_units_ragged_pipe<false>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);

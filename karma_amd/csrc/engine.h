@@ -120,6 +120,11 @@ struct RaggedArgs {
     const uint32_t* blob;      // stream blob (kBlobWords)
     const uint32_t* comb_blob; // kCombWords for unit_bytes
     uintptr_t kb_lo, kb_hi;    // bounds build only: the arena's allocation (bounds.h); else 0
+    // Device-sized batches (WAL replay's small-record path): when n_dev is set the kernel reads
+    // n_rec there, and does nothing unless *gate_len <= gate_max.  (k_ragged_direct4 only.)
+    const uint64_t* n_dev;
+    const uint32_t* gate_len;
+    uint32_t gate_max;
 };
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
@@ -148,10 +153,18 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
 // One record per group of 4 lanes, no plan kernels (uses arena, off, len, n_rec, init, out, and
 // blob = build_quad_blob's; the tools build's KARMA_DIRECT_VARIANT picks the alternatives).
 hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s);
+// k_ragged_direct4 with a device-sized batch (a.n_dev / a.gate_len set): WAL replay's
+// device-planned path, whatever the tools build's variant.
+hipError_t launch_ragged_direct_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // Library-internal entry (capi.cc) for callers that know every record is small
 // (WAL replay): CRCs of arena[off[r], off[r] + len[r]) with Value's init.
 int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
                        uint32_t* d_out, hipStream_t s);
+// The same with the record count in device memory (*d_n, at most n_cap records), run only when
+// *d_gate_len <= gate_max (else the kernel does nothing).
+int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
+                           uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
+                           hipStream_t s);
 
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {
@@ -162,6 +175,18 @@ struct WalSegMeta {
     uint32_t pad;
 };
 static_assert(sizeof(WalSegMeta) == 24, "one 24-byte record per segment");
+
+// What replay reads, from the segments' metas (k_wal_plan, on the device): segments [0, w1),
+// n_all candidates in them, their largest payload, and the structural stop.
+struct WalSummary {
+    uint64_t n_all;
+    uint64_t end;      // WAL offset where the walk stopped (the image end when every segment ended cleanly)
+    uint32_t w1;
+    uint32_t status;   // KARMA_WAL_END / _CORRUPT / _BAD_TYPE (structural)
+    uint32_t max_len;  // an upper bound of the payload lengths
+    uint32_t pad;
+};
+static_assert(sizeof(WalSummary) == 32, "one 32-byte summary");
 
 // One sub-range walker's result: where it started (a header it found, or the
 // sub-range end: none), its list length, its stop kind / offset and where it left
@@ -179,7 +204,7 @@ struct WalArgs {
     uint32_t* cand_crc;        //              and the CRC fields of their headers
     uint64_t cand_cap;         // seg_bytes / 8 + 1
     WalSegMeta* meta;          // per segment
-    const uint64_t* cand_base; // per segment: first slot in the contiguous lists
+    uint64_t* cand_base;       // per segment: first slot in the contiguous lists (k_wal_plan)
     uint64_t* off;             // header offset relative to wal, per candidate
     uint32_t* len;
     uint32_t* stored;          // CRC field of the header
@@ -193,7 +218,10 @@ struct WalArgs {
     uint32_t* span;            // per (segment, sub-range): first list slot of the accepted run, candidates before it
     uint64_t img_bytes;        // bytes at wal (nwork segments)
     uint64_t nwork;            // segments walked
-    uint64_t n_all;            // gathered candidates (the contiguous lists' length)
+    uint64_t n_all;            // capacity of the contiguous lists (bounds build checks)
+    WalSummary* sum;           // k_wal_plan's result
+    uint64_t wal_end;          // WAL offset of the image end
+    uint32_t direct_max;       // gated kernels (k_wal_compare) run only when sum->max_len <= this
 };
 constexpr uint32_t kWalkTile = 4096;  // the one-wave walker's LDS tile (wal_device.hip)
 constexpr uint32_t kMaxSub = 4096;    // sub-ranges per segment (k_wal_gather stages their runs in LDS)
@@ -205,8 +233,13 @@ struct WalWalkPlan {
 // size (karma_wal_tuning).
 WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes);
 hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s);
+// The replay plan on the device: a.sum, a.cand_base (first list slot per segment) and
+// *a.first_bad = ~0, from the walk's metas of nseg segments.
+hipError_t launch_wal_plan(const WalArgs& a, uint64_t nseg, hipStream_t s);
+// Gather: one block per segment of the nseg walked; segments from sum->w1 on do nothing.
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s);
-hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);
+// Compare over n candidates, or (gated) over sum->n_all, only when sum->max_len <= direct_max.
+hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, bool gated, hipStream_t s);
 
 // ---- KFP frames (kfp.cc) ----------------------------------------------------
 struct KfpWalk {

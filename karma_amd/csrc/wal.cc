@@ -140,13 +140,14 @@ struct DevBuf {
 };
 
 constexpr uint32_t kSmallRecordMax = 1024;      // payloads up to this take the one-record-per-group batch
+constexpr uint64_t kDevicePlanMax = uint64_t(256) << 20;  // images up to this: the device-planned path
 struct ReplayCtx {
     std::mutex mu;
     bool ready = false;
     int cu = 1;
     hipStream_t st = nullptr;
-    DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, bad;
-    DevBuf h_meta, h_small;                     // pinned readbacks
+    DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, bad, sum;
+    DevBuf h_small;                             // pinned readback (summary, first mismatch)
     int init(int dev) {
         if (ready) return 0;
         hipDeviceProp_t prop;
@@ -256,75 +257,91 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     if (const int rc = c.clen.ensure(nwork * A.cand_cap * 4)) return rc;
     if (const int rc = c.ccrc.ensure(nwork * A.cand_cap * 4)) return rc;
     if (const int rc = c.meta.ensure(nwork * sizeof(WalSegMeta))) return rc;
-    if (const int rc = c.h_meta.ensure(nwork * sizeof(WalSegMeta), true)) return rc;
     if (const int rc = c.sub.ensure(nwork * plan.nsub * sizeof(WalSubMeta))) return rc;
     if (const int rc = c.span.ensure(nwork * plan.nsub * 2 * sizeof(uint32_t))) return rc;
+    if (const int rc = c.cbase.ensure(nwork * 8)) return rc;
+    if (const int rc = c.bad.ensure(8)) return rc;
+    if (const int rc = c.sum.ensure(sizeof(WalSummary))) return rc;
+    if (const int rc = c.h_small.ensure(64, true)) return rc;  // the summary + first_bad readback
     A.cand_rec = c.crec.as<uint32_t>();
     A.cand_len = c.clen.as<uint32_t>();
     A.cand_crc = c.ccrc.as<uint32_t>();
     A.meta = c.meta.as<WalSegMeta>();
     A.sub = c.sub.as<WalSubMeta>();
     A.span = c.span.as<uint32_t>();
-    if (launch_wal_walk(A, nwork, plan, c.st) != hipSuccess ||
-        hipMemcpyAsync(c.h_meta.p, A.meta, nwork * sizeof(WalSegMeta), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
-        hipStreamSynchronize(c.st) != hipSuccess)
-        return fail(KARMA_E_HIP, "wal_replay: header walk");
-    T.mark("header walk (device)");
-    // replay enters segment s+1 only if segment s ended cleanly
-    const WalSegMeta* M = c.h_meta.as<WalSegMeta>();
-    int status = KARMA_WAL_END;
-    uint64_t end = wal_bytes, w1 = nwork;  // segments [0, w1) relative to s0 are read
-    for (uint64_t w = 0; w < nwork; ++w)
-        if (M[w].kind != KARMA_WAL_END) {
-            status = (int)M[w].kind;
-            end = M[w].stop;
-            w1 = w + 1;
-            break;
-        }
-    if (const int rc = c.cbase.ensure(w1 * 8)) return rc;
-    if (const int rc = c.h_small.ensure(std::max<size_t>(w1 * 8, 64), true)) return rc;
-    uint64_t* cb = c.h_small.as<uint64_t>();
-    uint64_t n_all = 0;
-    uint32_t max_len = 0;
-    for (uint64_t w = 0; w < w1; ++w) {
-        cb[w] = n_all;
-        n_all += M[w].count;
-        max_len = std::max(max_len, M[w].max_len);
-    }
-    uint64_t accepted = n_all;
-    if (n_all) {
-        // 2. contiguous candidate lists, one ragged CRC batch, first mismatch
-        if (const int rc = c.off.ensure(n_all * 8)) return rc;
-        if (const int rc = c.len.ensure(n_all * 4)) return rc;
-        if (const int rc = c.stored.ensure(n_all * 4)) return rc;
-        if (const int rc = c.crc.ensure(n_all * 4)) return rc;
-        if (const int rc = c.bad.ensure(8)) return rc;
-        A.cand_base = c.cbase.as<uint64_t>();
+    A.cand_base = c.cbase.as<uint64_t>();
+    A.first_bad = c.bad.as<uint64_t>();
+    A.sum = c.sum.as<WalSummary>();
+    A.wal_end = wal_bytes;
+    const int batch = tuning ? tuning->crc_batch : KARMA_WAL_CRC_PLAN;
+    A.direct_max = batch == KARMA_WAL_CRC_DIRECT ? ~0u : kSmallRecordMax;
+    auto bind_lists = [&](uint64_t cap) {  // the contiguous lists for up to cap candidates
+        if (const int rc = c.off.ensure(cap * 8)) return rc;
+        if (const int rc = c.len.ensure(cap * 4)) return rc;
+        if (const int rc = c.stored.ensure(cap * 4)) return rc;
+        if (const int rc = c.crc.ensure(cap * 4)) return rc;
         A.off = c.off.as<uint64_t>();
         A.len = c.len.as<uint32_t>();
         A.stored = c.stored.as<uint32_t>();
         A.crc = c.crc.as<uint32_t>();
-        A.first_bad = c.bad.as<uint64_t>();
-        A.n_all = n_all;
-        if (hipMemcpyAsync(c.cbase.p, cb, w1 * 8, hipMemcpyHostToDevice, c.st) != hipSuccess ||
-            launch_wal_gather(A, w1, c.st) != hipSuccess)
-            return fail(KARMA_E_HIP, "wal_replay: gather");
-        // payload = header + 8: the arena is the image shifted by the header.  Small records
-        // only: one record per group, without the ragged plan kernels.
-        const int batch = tuning ? tuning->crc_batch : KARMA_WAL_CRC_PLAN;
-        const bool direct = batch == KARMA_WAL_CRC_DIRECT || (batch == KARMA_WAL_CRC_PLAN && max_len <= kSmallRecordMax);
-        if (const int rc = direct
-                               ? ragged_small_batch(A.wal + 8, A.off, A.len, n_all, c.crc.as<uint32_t>(), c.st)
-                               : karma_crc32c_batch_ragged(A.wal + 8, A.off, A.len, n_all, w1 * seg_bytes, nullptr,
-                                                           0, c.crc.as<uint32_t>(), c.st))
+        A.n_all = cap;
+        return 0;
+    };
+    // 2. the replay plan on the device (k_wal_plan: the segments replay enters, their list
+    //    offsets, the summary).  Images up to kDevicePlanMax take the device-planned path: the
+    //    lists are sized for the most candidates the image can hold (a header every 8 bytes),
+    //    and the gather, the small-record CRC batch and the compare are enqueued right behind
+    //    the walk; the two CRC kernels check the summary themselves and do nothing when a payload
+    //    is over 1 KiB.  One host round trip then reads the summary and the first mismatch, and
+    //    only WALs with larger records need a second one (the ragged plan is sized on the host).
+    const uint64_t cap_all = img_bytes / 8 + nwork;
+    // (the tools build's other small-record kernels, KARMA_DIRECT_VARIANT, take the host-sized path)
+    const bool dev_plan = img_bytes <= kDevicePlanMax && batch != KARMA_WAL_CRC_UNITS &&
+                          KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 0;
+    if (launch_wal_walk(A, nwork, plan, c.st) != hipSuccess || launch_wal_plan(A, nwork, c.st) != hipSuccess)
+        return fail(KARMA_E_HIP, "wal_replay: header walk");
+    if (dev_plan) {
+        if (const int rc = bind_lists(cap_all)) return rc;
+        if (launch_wal_gather(A, nwork, c.st) != hipSuccess) return fail(KARMA_E_HIP, "wal_replay: gather");
+        if (const int rc = ragged_small_batch_dev(A.wal + 8, A.off, A.len, &A.sum->n_all, cap_all, &A.sum->max_len,
+                                                  A.direct_max, c.crc.as<uint32_t>(), c.st))
             return rc;
-        uint64_t* hb = c.h_small.as<uint64_t>();  // cb was consumed by the H2D above (stream-ordered)
-        if (hipMemsetAsync(A.first_bad, 0xff, 8, c.st) != hipSuccess ||
-            launch_wal_compare(A, n_all, c.cu, c.st) != hipSuccess ||
+        if (launch_wal_compare(A, cap_all, c.cu, true, c.st) != hipSuccess)
+            return fail(KARMA_E_HIP, "wal_replay: CRC check");
+    }
+    const WalSummary* S = c.h_small.as<WalSummary>();
+    uint64_t* hb = reinterpret_cast<uint64_t*>(c.h_small.as<uint8_t>() + sizeof(WalSummary));
+    if (hipMemcpyAsync(c.h_small.p, A.sum, sizeof(WalSummary), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+        hipMemcpyAsync(hb, A.first_bad, 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+        hipStreamSynchronize(c.st) != hipSuccess)
+        return fail(KARMA_E_HIP, "wal_replay: walk + plan");
+    T.mark(dev_plan ? "walk + plan + gather + CRCs (device)" : "walk + plan (device)");
+    // replay enters segment s+1 only if segment s ended cleanly (k_wal_plan)
+    int status = (int)S->status;
+    uint64_t end = S->end;
+    const uint64_t w1 = S->w1, n_all = S->n_all;
+    const uint32_t max_len = S->max_len;
+    const bool small = batch == KARMA_WAL_CRC_DIRECT || (batch == KARMA_WAL_CRC_PLAN && max_len <= kSmallRecordMax);
+    uint64_t accepted = n_all;
+    if (n_all && !(dev_plan && small)) {
+        // 3. the host-sized CRC batch: large payloads (the ragged plan), or an image too large
+        //    for the device-planned lists
+        if (!dev_plan) {
+            if (const int rc = bind_lists(n_all)) return rc;
+            if (launch_wal_gather(A, nwork, c.st) != hipSuccess) return fail(KARMA_E_HIP, "wal_replay: gather");
+        }
+        // payload = header + 8: the arena is the image shifted by the header
+        if (const int rc = small ? ragged_small_batch(A.wal + 8, A.off, A.len, n_all, c.crc.as<uint32_t>(), c.st)
+                                 : karma_crc32c_batch_ragged(A.wal + 8, A.off, A.len, n_all, w1 * seg_bytes, nullptr,
+                                                             0, c.crc.as<uint32_t>(), c.st))
+            return rc;
+        if (launch_wal_compare(A, n_all, c.cu, false, c.st) != hipSuccess ||
             hipMemcpyAsync(hb, A.first_bad, 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
             hipStreamSynchronize(c.st) != hipSuccess)
             return fail(KARMA_E_HIP, "wal_replay: CRC check");
         T.mark("CRC batch + compare");
+    }
+    if (n_all) {
         if (hb[0] < n_all) {  // the first mismatch in WAL order is where scan_record logs "Corrupt record"
             accepted = hb[0];
             status = KARMA_WAL_CORRUPT;

@@ -321,9 +321,9 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
     if ((uint64_t)pos + 8 > seg || pos >= hi) return E;  // wal.cc:40-45: a shorter rest is skipped
     // The list is built in registers, entry i of each run of 64 in lane i, and written
     // out 64 entries at a time (coalesced): no LDS traffic besides the header reads.
-    uint32_t myrec = 0, mylen = 0, mycrc = 0, k = 0;
+    uint32_t myrec = 0, mylen = 0, mycrc = 0, k = 0, vmax = 0;  // vmax: uniform, in a vector register
     auto push = [&](uint32_t p, uint32_t n, uint32_t c) {
-        E.max_len = n > E.max_len ? n : E.max_len;
+        vmax = n > vmax ? n : vmax;
         if (lane == k) {
             myrec = p;
             mylen = n;
@@ -349,20 +349,27 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
         uint32_t done = 0;
         {
             const uint32_t tend = t0 + tsz < hi ? t0 + tsz : hi, lim = seg - 8;
-            while (pos <= lim && pos < tend) {
-                uint32_t crc, st, size, npos;
-                while (true) {  // fast path: type-0 records with a payload that fits
+            const uint32_t fend = lim + 1 < tend ? lim + 1 : tend;  // a header at pos needs pos < fend
+            while (pos < fend) {
+                uint32_t crc, st, npos;
+                // Fast path: type-0 records with a payload that fits.  The chain runs on the
+                // vector unit with every lane holding the same values (the scalar unit is
+                // shared by the CU's 4 SIMDs and bounded the walk at ~30 scalar instructions
+                // per header); only the next position and the exit test cross
+                // to scalar registers.
+                while (true) {
                     tile_header(W, pos, t0, crc, st);
-                    crc = __builtin_amdgcn_readfirstlane(crc);
-                    st = __builtin_amdgcn_readfirstlane(st);
-                    size = st >> 8;
-                    npos = pos + 8 + size;  // < 2^32: seg < 2^31, size < 2^24
-                    if ((st & 0xffu) != 0 || size == 0 || npos > seg) break;
-                    push(pos, size, crc);
-                    pos = npos;
-                    if (pos > lim || pos >= tend) break;
+                    const uint32_t vnpos = pos + 8 + (st >> 8);  // < 2^32: seg < 2^31, size < 2^24
+                    const uint32_t bad = (st & 0xffu) | (uint32_t)(st < 256u) | (uint32_t)(vnpos > seg);
+                    if (__builtin_amdgcn_readfirstlane(bad)) break;
+                    push(pos, st >> 8, crc);
+                    pos = __builtin_amdgcn_readfirstlane(vnpos);
+                    if (pos >= fend) break;
                 }
-                if (pos > lim || pos >= tend) break;
+                if (pos >= fend) break;
+                crc = __builtin_amdgcn_readfirstlane(crc);  // the special header: scalar from here on
+                st = __builtin_amdgcn_readfirstlane(st);
+                npos = pos + 8 + (st >> 8);
                 const uint32_t type = st & 0xffu;
                 if (type == 0 && npos <= seg && crc == kStaleZero) {  // size 0: the stale word
                     push(pos, 0u, crc);
@@ -404,6 +411,7 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
     if (lane < k) put(E.count + lane, myrec, mylen, mycrc);  // the last, partial run
     E.count += k;
     E.pos = pos;
+    E.max_len = __builtin_amdgcn_readfirstlane(vmax);
     return E;
 }
 
@@ -581,6 +589,60 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
     if (lane == 0) KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg), mx, 0u}));
 }
 
+// The replay plan on the device (one block): replay enters segment s + 1 only when segment s
+// ended cleanly, so it reads segments [0, w1) with w1 = the first segment whose walk did not end
+// (+ 1); their candidates are gathered at cand_base[w] = the exclusive prefix of the counts.
+// Writes A.sum (and resets *A.first_bad) so no host round trip is needed before the gather.
+__global__ __launch_bounds__(1024) void k_wal_plan(WalArgs A) {
+    __shared__ uint32_t s_w1, s_max;
+    __shared__ unsigned long long s_wsum[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint64_t nw = A.nwork;
+    if (tid == 0) {
+        s_w1 = (uint32_t)nw;
+        s_max = 0;
+    }
+    __syncthreads();
+    for (uint64_t w = tid; w < nw; w += blockDim.x)
+        if (A.meta[w].kind != KARMA_WAL_END) atomicMin(&s_w1, (uint32_t)(w + 1));
+    __syncthreads();
+    const uint32_t w1 = s_w1;
+    uint64_t carry = 0;
+    uint32_t mx = 0;
+    for (uint64_t b = 0; b < w1; b += blockDim.x) {  // exclusive prefix of the counts, 1024 at a time
+        const uint64_t w = b + tid;
+        const uint64_t c = w < w1 ? A.meta[w].count : 0;
+        if (w < w1) mx = A.meta[w].max_len > mx ? A.meta[w].max_len : mx;
+        uint64_t x = c;  // inclusive wave scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t t = __shfl_up(x, d);
+            if ((int)lane >= d) x += t;
+        }
+        if (lane == 63) s_wsum[wave] = x;
+        __syncthreads();
+        uint64_t pre = 0, tot = 0;
+        for (uint32_t v = 0; v < blockDim.x / 64; ++v) {
+            if (v < wave) pre += s_wsum[v];
+            tot += s_wsum[v];
+        }
+        if (w < w1) A.cand_base[w] = carry + pre + x - c;
+        carry += tot;
+        __syncthreads();  // s_wsum is rewritten by the next chunk
+    }
+    atomicMax(&s_max, mx);
+    __syncthreads();
+    if (tid == 0) {
+        WalSummary S{carry, A.wal_end, w1, KARMA_WAL_END, s_max, 0u};
+        if (w1 > 0 && A.meta[w1 - 1].kind != KARMA_WAL_END) {
+            S.status = A.meta[w1 - 1].kind;
+            S.end = A.meta[w1 - 1].stop;
+        }
+        *A.sum = S;
+        *A.first_bad = ~0ull;
+    }
+}
+
 // Candidates of segment s0 + blockIdx.x (one block per segment) into the
 // contiguous lists at slot A.cand_base[blockIdx.x]: header offset (relative to
 // A.wal), length and the CRC field stored in the header (the walk kept it).  The segment's list is
@@ -588,6 +650,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
 // candidate i finds its run by a binary search over the runs staged in LDS.
 __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
     __shared__ uint2 spans[kMaxSub];
+    if (blockIdx.x >= A.sum->w1) return;  // replay does not enter this segment
     const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;
     const uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
     const uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
@@ -618,7 +681,11 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
 
 // The first candidate (in WAL order) whose payload CRC differs from the stored
 // one; size-0 records were checked by the walk.
-__global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n) {
+__global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n, bool gated) {
+    if (gated) {  // the device-planned small-record path: the count is known on the device only
+        if (A.sum->max_len > A.direct_max) return;
+        n = A.sum->n_all;
+    }
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t first = ~0ull;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += stride)
@@ -646,17 +713,23 @@ hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& p
     return hipGetLastError();
 }
 
+hipError_t launch_wal_plan(const WalArgs& a, uint64_t nseg, hipStream_t s) {
+    (void)nseg;
+    hipLaunchKernelGGL(k_wal_plan, dim3(1), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s) {
     if (!nseg) return hipSuccess;
     hipLaunchKernelGGL(k_wal_gather, dim3((unsigned)nseg), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s) {
-    if (!n) return hipSuccess;
+hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, bool gated, hipStream_t s) {
+    if (!n) return hipSuccess;  // (gated: n = the lists' capacity)
     uint64_t blocks = (n + 255) / 256;
     if (blocks > (uint64_t)cu * 8) blocks = (uint64_t)cu * 8;
-    hipLaunchKernelGGL(k_wal_compare, dim3((unsigned)blocks), dim3(256), 0, s, a, n);
+    hipLaunchKernelGGL(k_wal_compare, dim3((unsigned)blocks), dim3(256), 0, s, a, n, gated);
     return hipGetLastError();
 }
 
