@@ -391,7 +391,7 @@ int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_
 }
 int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
                            uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
-                           hipStream_t s) {
+                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s) {
     if (!n_cap) return 0;
     Locked L;
     if (L.rc) return L.rc;
@@ -405,6 +405,8 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
     a.n_dev = d_n;
     a.gate_len = d_gate_len;
     a.gate_max = gate_max;
+    a.cmp_stored = d_stored;
+    a.cmp_bad = reinterpret_cast<unsigned long long*>(d_first_bad);
     bind_arena_bounds(a);
     const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_cap, 64 * kWavesPerBlock));
     KARMA_HIP(launch_ragged_direct_dev(a, (int)blocks, s));

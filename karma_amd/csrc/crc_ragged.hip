@@ -547,9 +547,12 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
             if (lane / NG == round) Ri = Rr;
             L = N;
         }
-        if (vi)
-            A.out[ri] = gi.is_short ? short_record(lds, kLZ4, kLT8, pi, ni, initi)
-                                    : ~steps_in_vec(lds, kLZ4, kLT8, Ri, tv, 0u, tail ? (uint32_t)(gi.e - gi.b) : 0u);
+        if (vi) {
+            const uint32_t res = gi.is_short ? short_record(lds, kLZ4, kLT8, pi, ni, initi)
+                                             : ~steps_in_vec(lds, kLZ4, kLT8, Ri, tv, 0u, tail ? (uint32_t)(gi.e - gi.b) : 0u);
+            A.out[ri] = res;
+            if (A.cmp_stored && ni && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
+        }
     }
 }
 

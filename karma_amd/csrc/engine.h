@@ -125,6 +125,10 @@ struct RaggedArgs {
     const uint64_t* n_dev;
     const uint32_t* gate_len;
     uint32_t gate_max;
+    // ... and, when cmp_stored is set, the kernel also compares each record's CRC with
+    // cmp_stored[r] (records of length 0 excepted) and keeps the first mismatch in *cmp_bad.
+    const uint32_t* cmp_stored;
+    unsigned long long* cmp_bad;
 };
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
@@ -162,9 +166,11 @@ int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_
                        uint32_t* d_out, hipStream_t s);
 // The same with the record count in device memory (*d_n, at most n_cap records), run only when
 // *d_gate_len <= gate_max (else the kernel does nothing).
+// With d_stored set it is also the CRC check: the first record whose CRC differs from
+// d_stored[r] (length 0 excepted) goes to *d_first_bad (atomicMin).
 int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
                            uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
-                           hipStream_t s);
+                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s);
 
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {
@@ -180,13 +186,14 @@ static_assert(sizeof(WalSegMeta) == 24, "one 24-byte record per segment");
 // n_all candidates in them, their largest payload, and the structural stop.
 struct WalSummary {
     uint64_t n_all;
-    uint64_t end;      // WAL offset where the walk stopped (the image end when every segment ended cleanly)
+    uint64_t end;        // WAL offset where the walk stopped (the image end when every segment ended cleanly)
     uint32_t w1;
-    uint32_t status;   // KARMA_WAL_END / _CORRUPT / _BAD_TYPE (structural)
-    uint32_t max_len;  // an upper bound of the payload lengths
+    uint32_t status;     // KARMA_WAL_END / _CORRUPT / _BAD_TYPE (structural)
+    uint32_t max_len;    // an upper bound of the payload lengths
     uint32_t pad;
+    uint64_t first_bad;  // the first candidate whose payload CRC differs (~0: none), set by the CRC check
 };
-static_assert(sizeof(WalSummary) == 32, "one 32-byte summary");
+static_assert(sizeof(WalSummary) == 40, "one 40-byte summary, read back in one copy");
 
 // One sub-range walker's result: where it started (a header it found, or the
 // sub-range end: none), its list length, its stop kind / offset and where it left
@@ -209,7 +216,7 @@ struct WalArgs {
     uint32_t* len;
     uint32_t* stored;          // CRC field of the header
     const uint32_t* crc;       // payload CRC from the ragged batch
-    uint64_t* first_bad;       // min candidate index with crc != stored
+    uint64_t* first_bad;       // min candidate index with crc != stored (&sum->first_bad)
     // The walk splits each segment into nsub sub-ranges of sub_bytes (wal_walk_plan).
     uint64_t nsub;
     uint64_t sub_bytes;        // a multiple of the walker's 4 KiB tile
@@ -221,7 +228,6 @@ struct WalArgs {
     uint64_t n_all;            // capacity of the contiguous lists (bounds build checks)
     WalSummary* sum;           // k_wal_plan's result
     uint64_t wal_end;          // WAL offset of the image end
-    uint32_t direct_max;       // gated kernels (k_wal_compare) run only when sum->max_len <= this
 };
 constexpr uint32_t kWalkTile = 4096;  // the one-wave walker's LDS tile (wal_device.hip)
 constexpr uint32_t kMaxSub = 4096;    // sub-ranges per segment (k_wal_gather stages their runs in LDS)
@@ -238,8 +244,8 @@ hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& p
 hipError_t launch_wal_plan(const WalArgs& a, uint64_t nseg, hipStream_t s);
 // Gather: one block per segment of the nseg walked; segments from sum->w1 on do nothing.
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s);
-// Compare over n candidates, or (gated) over sum->n_all, only when sum->max_len <= direct_max.
-hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, bool gated, hipStream_t s);
+// The first of n candidates whose payload CRC differs from the stored one (atomicMin into *first_bad).
+hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);
 
 // ---- KFP frames (kfp.cc) ----------------------------------------------------
 struct KfpWalk {

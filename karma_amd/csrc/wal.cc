@@ -146,8 +146,8 @@ struct ReplayCtx {
     bool ready = false;
     int cu = 1;
     hipStream_t st = nullptr;
-    DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, bad, sum;
-    DevBuf h_small;                             // pinned readback (summary, first mismatch)
+    DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, sum;
+    DevBuf h_small;                             // pinned readback of the summary
     int init(int dev) {
         if (ready) return 0;
         hipDeviceProp_t prop;
@@ -260,9 +260,8 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     if (const int rc = c.sub.ensure(nwork * plan.nsub * sizeof(WalSubMeta))) return rc;
     if (const int rc = c.span.ensure(nwork * plan.nsub * 2 * sizeof(uint32_t))) return rc;
     if (const int rc = c.cbase.ensure(nwork * 8)) return rc;
-    if (const int rc = c.bad.ensure(8)) return rc;
     if (const int rc = c.sum.ensure(sizeof(WalSummary))) return rc;
-    if (const int rc = c.h_small.ensure(64, true)) return rc;  // the summary + first_bad readback
+    if (const int rc = c.h_small.ensure(64, true)) return rc;  // the summary readback
     A.cand_rec = c.crec.as<uint32_t>();
     A.cand_len = c.clen.as<uint32_t>();
     A.cand_crc = c.ccrc.as<uint32_t>();
@@ -270,11 +269,11 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     A.sub = c.sub.as<WalSubMeta>();
     A.span = c.span.as<uint32_t>();
     A.cand_base = c.cbase.as<uint64_t>();
-    A.first_bad = c.bad.as<uint64_t>();
     A.sum = c.sum.as<WalSummary>();
+    A.first_bad = &A.sum->first_bad;
     A.wal_end = wal_bytes;
     const int batch = tuning ? tuning->crc_batch : KARMA_WAL_CRC_PLAN;
-    A.direct_max = batch == KARMA_WAL_CRC_DIRECT ? ~0u : kSmallRecordMax;
+    const uint32_t direct_max = batch == KARMA_WAL_CRC_DIRECT ? ~0u : kSmallRecordMax;  // the device-side gate
     auto bind_lists = [&](uint64_t cap) {  // the contiguous lists for up to cap candidates
         if (const int rc = c.off.ensure(cap * 8)) return rc;
         if (const int rc = c.len.ensure(cap * 4)) return rc;
@@ -303,16 +302,13 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     if (dev_plan) {
         if (const int rc = bind_lists(cap_all)) return rc;
         if (launch_wal_gather(A, nwork, c.st) != hipSuccess) return fail(KARMA_E_HIP, "wal_replay: gather");
+        // the CRC batch is also the check (first mismatch into the summary): no compare launch
         if (const int rc = ragged_small_batch_dev(A.wal + 8, A.off, A.len, &A.sum->n_all, cap_all, &A.sum->max_len,
-                                                  A.direct_max, c.crc.as<uint32_t>(), c.st))
+                                                  direct_max, c.crc.as<uint32_t>(), A.stored, A.first_bad, c.st))
             return rc;
-        if (launch_wal_compare(A, cap_all, c.cu, true, c.st) != hipSuccess)
-            return fail(KARMA_E_HIP, "wal_replay: CRC check");
     }
-    const WalSummary* S = c.h_small.as<WalSummary>();
-    uint64_t* hb = reinterpret_cast<uint64_t*>(c.h_small.as<uint8_t>() + sizeof(WalSummary));
-    if (hipMemcpyAsync(c.h_small.p, A.sum, sizeof(WalSummary), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
-        hipMemcpyAsync(hb, A.first_bad, 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+    WalSummary* S = c.h_small.as<WalSummary>();
+    if (hipMemcpyAsync(S, A.sum, sizeof(WalSummary), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
         hipStreamSynchronize(c.st) != hipSuccess)
         return fail(KARMA_E_HIP, "wal_replay: walk + plan");
     T.mark(dev_plan ? "walk + plan + gather + CRCs (device)" : "walk + plan (device)");
@@ -335,19 +331,20 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
                                  : karma_crc32c_batch_ragged(A.wal + 8, A.off, A.len, n_all, w1 * seg_bytes, nullptr,
                                                              0, c.crc.as<uint32_t>(), c.st))
             return rc;
-        if (launch_wal_compare(A, n_all, c.cu, false, c.st) != hipSuccess ||
-            hipMemcpyAsync(hb, A.first_bad, 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+        if (launch_wal_compare(A, n_all, c.cu, c.st) != hipSuccess ||
+            hipMemcpyAsync(&S->first_bad, A.first_bad, 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
             hipStreamSynchronize(c.st) != hipSuccess)
             return fail(KARMA_E_HIP, "wal_replay: CRC check");
         T.mark("CRC batch + compare");
     }
     if (n_all) {
-        if (hb[0] < n_all) {  // the first mismatch in WAL order is where scan_record logs "Corrupt record"
-            accepted = hb[0];
+        if (S->first_bad < n_all) {  // the first mismatch in WAL order is where scan_record logs "Corrupt record"
+            accepted = S->first_bad;
             status = KARMA_WAL_CORRUPT;
-            if (hipMemcpy(hb, A.off + accepted, 8, hipMemcpyDeviceToHost) != hipSuccess)
+            uint64_t at = 0;
+            if (hipMemcpy(&at, A.off + accepted, 8, hipMemcpyDeviceToHost) != hipSuccess)
                 return fail(KARMA_E_HIP, "wal_replay: D2H");
-            end = base0 + hb[0];
+            end = base0 + at;
         }
         if (h_rec_off && rec_cap && accepted) {
             const uint64_t k = std::min<uint64_t>(accepted, rec_cap);

@@ -592,7 +592,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
 // The replay plan on the device (one block): replay enters segment s + 1 only when segment s
 // ended cleanly, so it reads segments [0, w1) with w1 = the first segment whose walk did not end
 // (+ 1); their candidates are gathered at cand_base[w] = the exclusive prefix of the counts.
-// Writes A.sum (and resets *A.first_bad) so no host round trip is needed before the gather.
+// Writes A.sum (first_bad reset) so no host round trip is needed before the gather.
 __global__ __launch_bounds__(1024) void k_wal_plan(WalArgs A) {
     __shared__ uint32_t s_w1, s_max;
     __shared__ unsigned long long s_wsum[16];
@@ -633,13 +633,12 @@ __global__ __launch_bounds__(1024) void k_wal_plan(WalArgs A) {
     atomicMax(&s_max, mx);
     __syncthreads();
     if (tid == 0) {
-        WalSummary S{carry, A.wal_end, w1, KARMA_WAL_END, s_max, 0u};
+        WalSummary S{carry, A.wal_end, w1, KARMA_WAL_END, s_max, 0u, ~0ull};
         if (w1 > 0 && A.meta[w1 - 1].kind != KARMA_WAL_END) {
             S.status = A.meta[w1 - 1].kind;
             S.end = A.meta[w1 - 1].stop;
         }
         *A.sum = S;
-        *A.first_bad = ~0ull;
     }
 }
 
@@ -681,11 +680,7 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
 
 // The first candidate (in WAL order) whose payload CRC differs from the stored
 // one; size-0 records were checked by the walk.
-__global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n, bool gated) {
-    if (gated) {  // the device-planned small-record path: the count is known on the device only
-        if (A.sum->max_len > A.direct_max) return;
-        n = A.sum->n_all;
-    }
+__global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t first = ~0ull;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += stride)
@@ -725,11 +720,11 @@ hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, bool gated, hipStream_t s) {
-    if (!n) return hipSuccess;  // (gated: n = the lists' capacity)
+hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s) {
+    if (!n) return hipSuccess;
     uint64_t blocks = (n + 255) / 256;
     if (blocks > (uint64_t)cu * 8) blocks = (uint64_t)cu * 8;
-    hipLaunchKernelGGL(k_wal_compare, dim3((unsigned)blocks), dim3(256), 0, s, a, n, gated);
+    hipLaunchKernelGGL(k_wal_compare, dim3((unsigned)blocks), dim3(256), 0, s, a, n);
     return hipGetLastError();
 }
 
