@@ -297,11 +297,15 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     // (the tools build's other small-record kernels, KARMA_DIRECT_VARIANT, take the host-sized path)
     const bool dev_plan = img_bytes <= kDevicePlanMax && batch != KARMA_WAL_CRC_UNITS &&
                           KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 0;
-    if (launch_wal_walk(A, nwork, plan, c.st) != hipSuccess || launch_wal_plan(A, nwork, c.st) != hipSuccess)
+    // (up to 1024 segments the device-planned gather reduces the metas itself: no plan launch)
+    const bool fused_plan = dev_plan && nwork <= 1024;
+    if (launch_wal_walk(A, nwork, plan, c.st) != hipSuccess ||
+        (!fused_plan && launch_wal_plan(A, nwork, c.st) != hipSuccess))
         return fail(KARMA_E_HIP, "wal_replay: header walk");
     if (dev_plan) {
         if (const int rc = bind_lists(cap_all)) return rc;
-        if (launch_wal_gather(A, nwork, c.st) != hipSuccess) return fail(KARMA_E_HIP, "wal_replay: gather");
+        if (launch_wal_gather(A, nwork, fused_plan, c.st) != hipSuccess)
+            return fail(KARMA_E_HIP, "wal_replay: gather");
         // the CRC batch is also the check (first mismatch into the summary): no compare launch
         if (const int rc = ragged_small_batch_dev(A.wal + 8, A.off, A.len, &A.sum->n_all, cap_all, &A.sum->max_len,
                                                   direct_max, c.crc.as<uint32_t>(), A.stored, A.first_bad, c.st))
@@ -324,7 +328,8 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         //    for the device-planned lists
         if (!dev_plan) {
             if (const int rc = bind_lists(n_all)) return rc;
-            if (launch_wal_gather(A, nwork, c.st) != hipSuccess) return fail(KARMA_E_HIP, "wal_replay: gather");
+            if (launch_wal_gather(A, nwork, false, c.st) != hipSuccess)
+                return fail(KARMA_E_HIP, "wal_replay: gather");
         }
         // payload = header + 8: the arena is the image shifted by the header
         if (const int rc = small ? ragged_small_batch(A.wal + 8, A.off, A.len, n_all, c.crc.as<uint32_t>(), c.st)

@@ -647,9 +647,60 @@ __global__ __launch_bounds__(1024) void k_wal_plan(WalArgs A) {
 // A.wal), length and the CRC field stored in the header (the walk kept it).  The segment's list is
 // its accepted runs in order (A.span: first slot, candidates before the run);
 // candidate i finds its run by a binary search over the runs staged in LDS.
+// FUSED_PLAN (at most 1024 segments, the device-planned path): there is no k_wal_plan
+// launch; every block reduces the metas itself (w1, its own list offset) and block 0 writes
+// the summary.
+template <bool FUSED_PLAN>
 __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
     __shared__ uint2 spans[kMaxSub];
-    if (blockIdx.x >= A.sum->w1) return;  // replay does not enter this segment
+    uint64_t g0;
+    if constexpr (FUSED_PLAN) {
+        __shared__ uint32_t s_w1, s_max;
+        __shared__ unsigned long long s_pre[16], s_all[16];
+        const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+        const uint32_t nw = (uint32_t)A.nwork;  // <= blockDim.x
+        if (tid == 0) {
+            s_w1 = nw;
+            s_max = 0;
+        }
+        __syncthreads();
+        WalSegMeta m{0u, KARMA_WAL_END, 0u, 0u, 0u};
+        if (tid < nw) m = A.meta[tid];
+        if (tid < nw && m.kind != KARMA_WAL_END) atomicMin(&s_w1, tid + 1);
+        __syncthreads();
+        const uint32_t w1 = s_w1;
+        if (blockIdx.x >= w1 && blockIdx.x != 0) return;  // replay does not enter this segment
+        unsigned long long pre = tid < blockIdx.x ? m.count : 0, all = tid < w1 ? m.count : 0;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) {
+            pre += __shfl_xor(pre, d);
+            all += __shfl_xor(all, d);
+        }
+        if (lane == 0) {
+            s_pre[wave] = pre;
+            s_all[wave] = all;
+        }
+        if (tid < w1) atomicMax(&s_max, m.max_len);
+        __syncthreads();
+        g0 = 0;
+        uint64_t n_all = 0;
+        for (uint32_t v = 0; v < blockDim.x / 64; ++v) {
+            g0 += s_pre[v];
+            n_all += s_all[v];
+        }
+        if (blockIdx.x == 0 && tid == 0) {
+            WalSummary S{n_all, A.wal_end, w1, KARMA_WAL_END, s_max, 0u, ~0ull};
+            if (A.meta[w1 - 1].kind != KARMA_WAL_END) {
+                S.status = A.meta[w1 - 1].kind;
+                S.end = A.meta[w1 - 1].stop;
+            }
+            *A.sum = S;
+        }
+        if (blockIdx.x >= w1) return;
+    } else {
+        if (blockIdx.x >= A.sum->w1) return;  // replay does not enter this segment
+        g0 = A.cand_base[blockIdx.x];
+    }
     const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;
     const uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
     const uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
@@ -660,7 +711,6 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
         spans[j] = KB_READ(sp, j, (A.nwork - blockIdx.x) * A.nsub, kKbSpan);
     __syncthreads();
     const uint32_t count = A.meta[blockIdx.x].count;
-    const uint64_t g0 = A.cand_base[blockIdx.x];
     for (uint32_t i = threadIdx.x; i < count; i += blockDim.x) {
         uint32_t a = 0, b = P;  // the last run whose prefix is <= i: [a, b)
         while (b - a > 1) {
@@ -714,9 +764,14 @@ hipError_t launch_wal_plan(const WalArgs& a, uint64_t nseg, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, hipStream_t s) {
+hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, hipStream_t s) {
     if (!nseg) return hipSuccess;
-    hipLaunchKernelGGL(k_wal_gather, dim3((unsigned)nseg), dim3(1024), 0, s, a);
+    if (fused_plan) {
+        if (nseg > 1024) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_wal_gather<true>, dim3((unsigned)nseg), dim3(1024), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_wal_gather<false>, dim3((unsigned)nseg), dim3(1024), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -352,3 +352,23 @@ def test_replay_randomized_against_model(lib, monkeypatch):
             _walk_env(monkeypatch, walk)
             got = _replay(lib, wal, start=start, seg=seg)
             assert got == (list(want[0]), want[1], want[2]), (case, walk, seg, mix)
+
+
+@pytest.mark.parametrize("nseg", [1000, 1024, 1025, 3000])
+def test_replay_segment_counts_around_the_fused_plan(lib, nseg):
+    """Up to 1024 segments the device-planned gather reduces the segments' metas itself; above, a
+    separate k_wal_plan launch does (wal.cc).  Both must give scan_record's result, from the start,
+    from a checkpoint, and with a corrupted record."""
+    seg = 4096
+    src, offs, lens = _payloads(nseg, nseg * 14, 1, 300)
+    wal = np.zeros(nseg * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    for start in (0, int(rec[len(rec) // 3])):
+        got = _replay(lib, wal, start=start, seg=seg)
+        w = wal_model.replay(wal.tobytes(), seg, start)
+        assert got == (list(w[0]), w[1], w[2])
+    k = len(rec) * 2 // 3
+    wal[int(rec[k]) + 8] ^= 1  # a payload bit: replay stops at record k ("Corrupt record")
+    got = _replay(lib, wal, seg=seg)
+    w = wal_model.replay(wal.tobytes(), seg)
+    assert got == (list(w[0]), w[1], w[2]) and len(got[0]) == k
