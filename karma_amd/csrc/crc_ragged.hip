@@ -261,7 +261,7 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
 // and the first loads of unit u + step are in flight while unit u finishes.
 // Out-of-range groups point at descriptor 0's span (a safe address) and
 // store nothing.
-template <bool BAL = true>
+template <bool BAL = true, int PF = kRaggedPF>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
@@ -299,8 +299,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs 
     uint64_t wb1 = next_of(wb);
     UnitDesc d = desc_at(wb);
     LaneUnit L = unit_of(d, wb);
-    UnitLoads<kRaggedPF> Ld;
-    issue_unit_loads<kRaggedPF, kRaggedNT>(L, Ld);
+    UnitLoads<PF> Ld;
+    issue_unit_loads<PF, kRaggedNT>(L, Ld);
     UnitDesc dn = desc_at(wb1);
     while (wb < nws) {
         // The descriptor two steps ahead is issued with the next unit's loads,
@@ -309,11 +309,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs 
         UnitDesc dnn;
         LaneUnit N;
         uint64_t wb2 = 0;
-        const uint32_t R = stream_unit<kRaggedPF, kRaggedNT>(lds, X, l, L, Ld, L.us, d.inj, [&](UnitLoads<kRaggedPF>& nx) {
+        const uint32_t R = stream_unit<PF, kRaggedNT>(lds, X, l, L, Ld, L.us, d.inj, [&](UnitLoads<PF>& nx) {
             N = unit_of(dn, wb1);
             wb2 = next_of(wb1);
             dnn = desc_at(wb2);
-            issue_unit_loads<kRaggedPF, kRaggedNT>(N, nx);
+            issue_unit_loads<PF, kRaggedNT>(N, nx);
         });
         const uint64_t u = wb * kGroupsPerWave + grp;
         if (u < U && l == 0) A.partial[u] = R;
@@ -781,12 +781,15 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
     hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     units_timer_begin(s);
-#ifdef KARMA_AB  // tools build (ab.h): 1 = pipelined, 2 = static wave-steps, 3 = both, 4 / 8 = chunks in flight
+#ifdef KARMA_AB  // tools build (ab.h): 1 = pipelined, 2 = static wave-steps, 3 = both, 4 / 8 = chunks in
+                 // flight, 16 = pipelined with 6 in flight
     const long v = KARMA_AB_KNOB("KARMA_RAGGED_VARIANT", 0);
     if (v == 4)
         hipLaunchKernelGGL((k_units_ragged<true, 4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 8)
         hipLaunchKernelGGL((k_units_ragged<true, 8>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 16)
+        hipLaunchKernelGGL((k_units_ragged_pipe<true, 6>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 1)
         hipLaunchKernelGGL(k_units_ragged_pipe<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 3)

@@ -19,12 +19,15 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "engine.h"
+#include "host_stage.h"
 #include "karma_crc32c.h"
 
 namespace karma::engine {
@@ -38,31 +41,54 @@ int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std:
     if (off.empty()) return 0;
     if (!d_buf) return karma_crc32c_batch_ragged_host(h_buf, buf_bytes, off.data(), len.data(), off.size(), 0,
                                                       out.data(), device);
-    // device copy supplied: stage the offsets/lengths and run the device batch
+    // device copy supplied: stage the offsets/lengths and run the device batch (grow-only
+    // device buffers kept per device: no allocation per call)
     uint64_t total = 0;
     uint32_t max_len = 0;
     for (uint32_t l : len) {
         total += l;
         max_len = std::max(max_len, l);
     }
+    int dev = 0;
     if (device >= 0 && hipSetDevice(device) != hipSuccess) return set_last_error(KARMA_E_HIP, "hipSetDevice");
-    void *doff = nullptr, *dlen = nullptr, *dout = nullptr;
+    if (hipGetDevice(&dev) != hipSuccess) return set_last_error(KARMA_E_HIP, "hipGetDevice");
+    struct SpanBufs {
+        std::mutex mu;
+        void *off = nullptr, *len = nullptr, *out = nullptr;
+        size_t cap = 0;  // records
+    };
+    static std::mutex g_mu;
+    static std::vector<std::unique_ptr<SpanBufs>> g_bufs;
+    SpanBufs* B;
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        if ((int)g_bufs.size() <= dev) g_bufs.resize(dev + 1);
+        if (!g_bufs[dev]) g_bufs[dev] = std::make_unique<SpanBufs>();
+        B = g_bufs[dev].get();
+    }
+    std::lock_guard<std::mutex> lk(B->mu);
+    if (B->cap < off.size()) {
+        (void)hipFree(B->off);
+        (void)hipFree(B->len);
+        (void)hipFree(B->out);
+        B->off = B->len = B->out = nullptr;
+        B->cap = 0;
+        const size_t cap = off.size() + off.size() / 8;
+        if (hipMalloc(&B->off, cap * 8) != hipSuccess || hipMalloc(&B->len, cap * 4) != hipSuccess ||
+            hipMalloc(&B->out, cap * 4) != hipSuccess)
+            return set_last_error(KARMA_E_NOMEM, "crc_spans: hipMalloc");
+        B->cap = cap;
+    }
     int rc = 0;
-    if (hipMalloc(&doff, off.size() * 8) != hipSuccess || hipMalloc(&dlen, len.size() * 4) != hipSuccess ||
-        hipMalloc(&dout, out.size() * 4) != hipSuccess)
-        rc = set_last_error(KARMA_E_NOMEM, "crc_spans: hipMalloc");
-    else if (hipMemcpy(doff, off.data(), off.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
-             hipMemcpy(dlen, len.data(), len.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    if (hipMemcpy(B->off, off.data(), off.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(B->len, len.data(), len.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         rc = set_last_error(KARMA_E_HIP, "crc_spans: hipMemcpy H2D");
-    else if ((rc = karma_crc32c_batch_ragged_bounded(d_buf, static_cast<uint64_t*>(doff), static_cast<uint32_t*>(dlen),
-                                                     off.size(), total, max_len, nullptr, 0,
-                                                     static_cast<uint32_t*>(dout), nullptr)))
+    else if ((rc = karma_crc32c_batch_ragged_bounded(d_buf, static_cast<uint64_t*>(B->off),
+                                                     static_cast<uint32_t*>(B->len), off.size(), total, max_len,
+                                                     nullptr, 0, static_cast<uint32_t*>(B->out), nullptr)))
         ;
-    else if (hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    else if (hipMemcpy(out.data(), B->out, out.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
         rc = set_last_error(KARMA_E_HIP, "crc_spans: hipMemcpy D2H");
-    (void)hipFree(doff);
-    (void)hipFree(dlen);
-    (void)hipFree(dout);
     return rc;
 }
 
@@ -124,6 +150,224 @@ inline uint32_t le32(const uint8_t* p) {
 
 int fail(int code, const char* what) { return karma::engine::set_last_error(code, what); }
 
+// ---- the encoder's pipeline (the structure of wal_append.cc) ------------------------------
+constexpr int kEncStreams = 8;                          // DMA / CRC streams the blocks rotate over
+constexpr size_t kEncBlockFrames = 16384;               // a block: at most this many frames,
+constexpr uint64_t kEncBlockBytesFirst = uint64_t(256) << 10;  // or about this many span bytes
+constexpr uint64_t kEncBlockBytesMax = uint64_t(4) << 20;      // (doubling from the first block)
+constexpr uint64_t kEncCallBytes = uint64_t(1) << 30;   // span bytes staged per pass
+
+struct EncBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    bool host = false;
+    int ensure(size_t want, bool pinned_host) {
+        if (p && bytes >= want) return 0;
+        if (p) (void)(host ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        bytes = 0;
+        want = std::max<size_t>(want + want / 8, 4096);
+        if ((pinned_host ? hipHostMalloc(&p, want, hipHostMallocDefault) : hipMalloc(&p, want)) != hipSuccess) {
+            p = nullptr;
+            return fail(KARMA_E_NOMEM, "kfp_encode_batch: allocation");
+        }
+        bytes = want;
+        host = pinned_host;
+        return 0;
+    }
+    template <typename T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+// Per-device encoder context: streams, one event per block, grow-only pinned staging and device
+// copies of the packed CRC spans, their offsets, lengths and CRCs.
+struct EncCtx {
+    std::mutex mu;
+    bool ready = false;
+    hipStream_t st[kEncStreams] = {};
+    std::vector<hipEvent_t> ev;
+    EncBuf h_span, h_off, h_len, h_crc, d_span, d_off, d_len, d_crc;
+    std::vector<size_t> bstart;
+    int init() {
+        if (ready) return 0;
+        for (auto& x : st)
+            if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess)
+                return fail(KARMA_E_HIP, "kfp_encode_batch: stream");
+        ready = true;
+        return 0;
+    }
+    int events(size_t k) {
+        while (ev.size() < k) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+                return fail(KARMA_E_HIP, "kfp_encode_batch: event");
+            ev.push_back(e);
+        }
+        return 0;
+    }
+};
+
+std::mutex g_enc_mu;
+std::vector<std::unique_ptr<EncCtx>> g_enc;
+
+EncCtx& enc_ctx(int dev) {
+    std::lock_guard<std::mutex> g(g_enc_mu);
+    if ((int)g_enc.size() <= dev) g_enc.resize(dev + 1);
+    if (!g_enc[dev]) g_enc[dev] = std::make_unique<EncCtx>();
+    return *g_enc[dev];
+}
+
+struct EncFrames {
+    const uint8_t* hdr;
+    const uint64_t* hdr_off;
+    const uint32_t* hdr_len;
+    const uint8_t* pay;
+    const uint64_t* pay_off;
+    const uint32_t* pay_len;
+    const int16_t* op;
+    const uint8_t* flag;
+    const uint32_t* seq;
+    uint8_t* out;
+    const uint64_t* at;  // frame offsets in out
+};
+
+// Frames [f0, f0 + m) (span bytes `span`, <= kEncCallBytes unless one frame), on the library's
+// host threads: the threads take blocks of frames in turn, write each frame
+// (frame::encode's fields, header, payload) and pack its CRC span -- header + payload,
+// Value(frame[16, frame_length - 4)) = Extend(Value(header), payload), frame.cc:56-57 -- into
+// pinned staging in the same pass, then enqueue the block's DMA, CRC batch and CRC readback on
+// one of 8 streams; between blocks, and once every block is enqueued, they write the CRC fields
+// of the blocks whose CRCs are back, in order.
+int encode_pass(EncCtx& C, int dev, const EncFrames& F, size_t f0, size_t m, uint64_t span) {
+    const size_t max_blocks = m / kEncBlockFrames + span / kEncBlockBytesFirst + 32;
+    if (const int rc = C.h_span.ensure(span + 16, true)) return rc;
+    if (const int rc = C.d_span.ensure(span + 16, false)) return rc;
+    if (const int rc = C.h_off.ensure(m * 8, true)) return rc;
+    if (const int rc = C.d_off.ensure(m * 8, false)) return rc;
+    if (const int rc = C.h_len.ensure(m * 4, true)) return rc;
+    if (const int rc = C.d_len.ensure(m * 4, false)) return rc;
+    if (const int rc = C.h_crc.ensure(m * 4, true)) return rc;
+    if (const int rc = C.d_crc.ensure(m * 4, false)) return rc;
+    if (const int rc = C.events(max_blocks)) return rc;
+    if (C.bstart.size() < max_blocks + 2) C.bstart.resize(max_blocks + 2);
+    uint64_t* so = C.h_off.as<uint64_t>();  // packed span offset per frame (rebased per block when enqueued)
+    uint32_t* sl = C.h_len.as<uint32_t>();
+    uint32_t* hc = C.h_crc.as<uint32_t>();
+    uint8_t* hs = C.h_span.as<uint8_t>();
+    size_t* bstart = C.bstart.data();
+    // the blocks, and the packed span offsets
+    size_t nb = 0;
+    uint32_t max_len = 0;
+    {
+        uint64_t packed = 0, bbytes = 0, blimit = kEncBlockBytesFirst;
+        bstart[0] = 0;
+        for (size_t i = 0; i < m; ++i) {
+            const uint32_t L = F.hdr_len[f0 + i] + F.pay_len[f0 + i];
+            so[i] = packed;
+            sl[i] = L;
+            max_len = std::max(max_len, L);
+            packed += L;
+            bbytes += L;
+            if (i + 1 - bstart[nb] == kEncBlockFrames || bbytes >= blimit || i + 1 == m) {
+                bstart[++nb] = i + 1;
+                bbytes = 0;
+                blimit = std::min(2 * blimit, kEncBlockBytesMax);
+            }
+        }
+    }
+    std::atomic<size_t> next_block{0}, next_fill{0};
+    std::atomic<int> crc_rc{0};
+    std::unique_ptr<std::atomic<uint8_t>[]> enq(new std::atomic<uint8_t>[nb]);
+    for (size_t k = 0; k < nb; ++k) enq[k].store(0, std::memory_order_relaxed);
+    auto set_rc = [&](int rc) {
+        int zero = 0;
+        crc_rc.compare_exchange_strong(zero, rc);
+    };
+    auto frame_block = [&](size_t k) {
+        const size_t lo = bstart[k], hi = bstart[k + 1];
+        for (size_t i = lo; i < hi; ++i) {  // frame::encode (frame.cc:29-60)
+            const size_t g = f0 + i;
+            const uint32_t hl = F.hdr_len[g], pl = F.pay_len[g];
+            const uint32_t fl = kFixed + hl + pl + kCrcLen;
+            uint8_t* f = F.out + F.at[g];
+            std::memcpy(f, &fl, 4);
+            f[4] = KARMA_KFP_MAGIC;
+            std::memcpy(f + 5, &F.op[g], 2);
+            f[7] = F.flag[g];
+            std::memcpy(f + 8, &F.seq[g], 4);
+            std::memcpy(f + 12, &hl, 4);
+            if (hl) std::memcpy(f + kFixed, F.hdr + F.hdr_off[g], hl);
+            if (pl) std::memcpy(f + kFixed + hl, F.pay + F.pay_off[g], pl);
+            if (hl + pl) std::memcpy(hs + so[i], f + kFixed, hl + pl);  // the span, from the caches
+        }
+        const uint64_t plo = so[lo], phi = so[hi - 1] + sl[hi - 1];
+        for (size_t i = lo; i < hi; ++i) so[i] -= plo;  // the block's kernel sees its own slice
+        hipStream_t s = C.st[k % kEncStreams];
+        const size_t nr = hi - lo;
+        uint8_t* dp = C.d_span.as<uint8_t>();
+        uint64_t* doff = C.d_off.as<uint64_t>() + lo;
+        uint32_t* dlen = C.d_len.as<uint32_t>() + lo;
+        if ((phi > plo && hipMemcpyAsync(dp + plo, hs + plo, phi - plo, hipMemcpyHostToDevice, s) != hipSuccess) ||
+            hipMemcpyAsync(doff, so + lo, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(dlen, sl + lo, nr * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+            return (int)KARMA_E_HIP;
+        if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, doff, dlen, nr, phi - plo, max_len, nullptr, 0,
+                                                             C.d_crc.as<uint32_t>() + lo, s))
+            return rc;
+        if (hipMemcpyAsync(hc + lo, C.d_crc.as<uint32_t>() + lo, nr * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipEventRecord(C.ev[k], s) != hipSuccess)
+            return (int)KARMA_E_HIP;
+        return 0;
+    };
+    auto fill = [&](size_t k) {  // the CRC fields of block k (frame.cc:58-59)
+        for (size_t i = bstart[k]; i < bstart[k + 1]; ++i) {
+            const size_t g = f0 + i;
+            std::memcpy(F.out + F.at[g] + kFixed + sl[i], &hc[i], 4);
+        }
+    };
+    auto fill_ready = [&](bool wait) {
+        while (!crc_rc.load(std::memory_order_relaxed)) {
+            size_t f = next_fill.load();
+            if (f >= nb) return;
+            if (!wait && (!enq[f].load(std::memory_order_acquire) || hipEventQuery(C.ev[f]) != hipSuccess)) return;
+            if (!next_fill.compare_exchange_strong(f, f + 1)) continue;
+            if (wait && hipEventSynchronize(C.ev[f]) != hipSuccess) {
+                set_rc(KARMA_E_HIP);
+                return;
+            }
+            fill(f);
+        }
+    };
+    const int nthr = (int)std::min<size_t>(karma::engine::kPoolThreads + 1, std::max<size_t>(1, m / 1024));
+    std::mutex bmu;
+    std::condition_variable bcv;
+    int framing = nthr;
+    karma::engine::run_pool(nthr, [&](int t) {
+        if (t > 0 && hipSetDevice(dev) != hipSuccess) set_rc(KARMA_E_HIP);  // thread 0 is the caller's
+        for (size_t k; !crc_rc.load(std::memory_order_relaxed) && (k = next_block.fetch_add(1)) < nb;) {
+            if (const int rc = frame_block(k)) {
+                set_rc(rc);
+                break;
+            }
+            enq[k].store(1, std::memory_order_release);
+            fill_ready(false);
+        }
+        {  // every block enqueued (an event not recorded in this call would not wait)
+            std::unique_lock<std::mutex> lk(bmu);
+            if (--framing == 0) bcv.notify_all();
+            bcv.wait(lk, [&] { return framing == 0; });
+        }
+        fill_ready(true);
+    });
+    for (auto& x : C.st)  // nothing of this call may be in flight when it returns
+        if (hipStreamSynchronize(x) != hipSuccess) set_rc(KARMA_E_HIP);
+    if (const int rc = crc_rc.load())
+        return rc == KARMA_E_HIP ? fail(rc, "kfp_encode_batch: device pipeline") : rc;
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -153,54 +397,27 @@ int karma_kfp_encode_batch(const void* h_hdr, const uint64_t* h_hdr_off, const u
         at.push_back(cur);
         cur += fl;
     }
-    // 2. frames written by 16 threads, piece by piece; 3. each written piece's
-    //    CRCs (streamed to the device through the pinned staging, host_stage.h), Extend(Value(header), payload) = Value(frame[16, 16 + hl + pl)), in one
-    //    GPU batch on a worker thread while the next piece is written
-    constexpr size_t kPieces = 4;
-    const size_t npc = ne >= 4 * 4096 ? kPieces : 1;
-    std::atomic<size_t> written{0};
-    int crc_rc = 0;
-    std::thread gpu([&] {
-        for (size_t p = 0; p < npc && !crc_rc; ++p) {
-            const size_t lo = ne * p / npc, hi = ne * (p + 1) / npc;
-            while (written.load(std::memory_order_acquire) <= p) std::this_thread::yield();
-            if (lo == hi) continue;
-            std::vector<uint64_t> so(hi - lo);
-            std::vector<uint32_t> sl(hi - lo), crc;
-            for (size_t k = lo; k < hi; ++k) {
-                so[k - lo] = at[k] + kFixed;
-                sl[k - lo] = h_hdr_len[k] + h_pay_len[k];
-            }
-            if ((crc_rc = karma::engine::crc_spans(out, nullptr, cur, so, sl, crc, device))) break;
-            for (size_t k = 0; k < crc.size(); ++k) std::memcpy(out + so[k] + sl[k], &crc[k], 4);
+    if (ne) {
+        int dev = 0, nd = 0;
+        if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return fail(KARMA_E_NO_DEVICE, "no HIP device visible");
+        if (device >= nd) return fail(KARMA_E_INVALID, "kfp_encode_batch: device index out of range");
+        if (device >= 0 && hipSetDevice(device) != hipSuccess) return fail(KARMA_E_HIP, "hipSetDevice");
+        if (hipGetDevice(&dev) != hipSuccess) return fail(KARMA_E_HIP, "hipGetDevice");
+        EncCtx& C = enc_ctx(dev);
+        std::lock_guard<std::mutex> lk(C.mu);
+        if (const int rc = C.init()) return rc;
+        // 2. passes of at most kEncCallBytes of CRC span (header + payload) per pass
+        for (size_t done = 0; done < ne;) {
+            size_t m = 1;
+            uint64_t span = h_hdr_len[done] + (uint64_t)h_pay_len[done];
+            for (; done + m < ne && span + h_hdr_len[done + m] + h_pay_len[done + m] <= kEncCallBytes; ++m)
+                span += h_hdr_len[done + m] + (uint64_t)h_pay_len[done + m];
+            const EncFrames F{hdr, h_hdr_off, h_hdr_len, pay, h_pay_off, h_pay_len, h_op, h_flag, h_seq, out, at.data()};
+            if (const int rc = encode_pass(C, dev, F, done, m, span)) return rc;
+            done += m;
         }
-    });
-    for (size_t p = 0; p < npc; ++p) {
-        const size_t lo = ne * p / npc, hi = ne * (p + 1) / npc;
-        const size_t nthr = std::min<size_t>(16, std::max<size_t>(1, (hi - lo) / 1024));
-        std::vector<std::thread> th;
-        for (size_t t = 0; t < nthr; ++t)
-            th.emplace_back([&, t] {
-                for (size_t i = lo + (hi - lo) * t / nthr; i < lo + (hi - lo) * (t + 1) / nthr; ++i) {
-                    const uint32_t hl = h_hdr_len[i], pl = h_pay_len[i];
-                    const uint32_t fl = kFixed + hl + pl + kCrcLen;
-                    uint8_t* f = out + at[i];
-                    std::memcpy(f, &fl, 4);
-                    f[4] = KARMA_KFP_MAGIC;
-                    std::memcpy(f + 5, &h_op[i], 2);
-                    f[7] = h_flag[i];
-                    std::memcpy(f + 8, &h_seq[i], 4);
-                    std::memcpy(f + 12, &hl, 4);
-                    if (hl) std::memcpy(f + kFixed, hdr + h_hdr_off[i], hl);
-                    if (pl) std::memcpy(f + kFixed + hl, pay + h_pay_off[i], pl);
-                    if (h_frame_off) h_frame_off[i] = at[i];
-                }
-            });
-        for (auto& x : th) x.join();
-        written.store(p + 1, std::memory_order_release);
+        if (h_frame_off) std::memcpy(h_frame_off, at.data(), ne * sizeof(uint64_t));
     }
-    gpu.join();
-    if (crc_rc) return crc_rc;
     *h_n_encoded = ne;
     *h_bytes = cur;
     return 0;
