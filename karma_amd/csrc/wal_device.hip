@@ -321,20 +321,35 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
     if ((uint64_t)pos + 8 > seg || pos >= hi) return E;  // wal.cc:40-45: a shorter rest is skipped
     // The list is built in registers, entry i of each run of 64 in lane i, and written
     // out 64 entries at a time (coalesced): no LDS traffic besides the header reads.
-    uint32_t myrec = 0, mylen = 0, mycrc = 0, k = 0, vmax = 0;  // vmax: uniform, in a vector register
-    auto push = [&](uint32_t p, uint32_t n, uint32_t c) {
-        vmax = n > vmax ? n : vmax;
-        if (lane == k) {
-            myrec = p;
+    uint32_t myrec = 0, mylen = 0, mycrc = 0, k = 0, vmax = 0;  // vmax: per lane, reduced at the end
+    // Append entries 0..na-1 (entry j in lane j of rec_j / len_j / crc_j) to the run: run
+    // lane (k + j) mod 64 takes entry j, the run is written out when it fills.
+    auto push_many = [&](uint32_t rec_j, uint32_t len_j, uint32_t crc_j, uint32_t na) {
+        const uint32_t src = (lane - k) & 63u;
+        const uint32_t r = __shfl(rec_j, (int)src), n = __shfl(len_j, (int)src), c = __shfl(crc_j, (int)src);
+        const bool take = src < na;
+        if (take && lane >= k) {
+            myrec = r;
             mylen = n;
             mycrc = c;
+            vmax = n > vmax ? n : vmax;
         }
-        if (++k == 64) {
+        if (k + na >= 64) {
             put(E.count + lane, myrec, mylen, mycrc);
             E.count += 64;
-            k = 0;
+            if (take && lane < k) {  // the entries that wrapped into the next run
+                myrec = r;
+                mylen = n;
+                mycrc = c;
+                vmax = n > vmax ? n : vmax;
+            }
+            k = k + na - 64;
+        } else {
+            k += na;
         }
     };
+    auto push = [&](uint32_t p, uint32_t n, uint32_t c) { push_many(p, n, c, 1u); };  // uniform values
+    uint32_t g = 0;  // the guessed header stride: 8 + the last record's size
     const uint32_t tlim = hi < seg ? hi : seg;  // tiles from here on hold no header before hi
     // Sequential headers go through 4 KiB tiles with the next one prefetched; after a
     // jump past the prefetched tile the walk reads a 1 KiB window at the header, and
@@ -352,23 +367,45 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
             const uint32_t fend = lim + 1 < tend ? lim + 1 : tend;  // a header at pos needs pos < fend
             while (pos < fend) {
                 uint32_t crc, st, npos;
-                // Fast path: type-0 records with a payload that fits.  The chain runs on the
-                // vector unit with every lane holding the same values (the scalar unit is
-                // shared by the CU's 4 SIMDs and bounded the walk at ~30 scalar instructions
-                // per header); only the next position and the exit test cross
-                // to scalar registers.
+                // Fast path: type-0 records with a payload that fits.  Lane j reads the header
+                // at pos + j*g, g the last record's stride: when the records repeat their size
+                // (the common case: a log of one record type), one round of header reads
+                // accepts every header of the tile up to the first size change -- the chain is
+                // confirmed lane by lane (lane j's next header is at lane j+1's position).  With
+                // sizes that change every record it is one header a round, as a plain walk.
+                // Only the round's outcome crosses to scalar registers (the scalar unit is
+                // shared by the CU's 4 SIMDs and bounded an all-scalar walk).
+                bool special = false;
                 while (true) {
-                    tile_header(W, pos, t0, crc, st);
-                    const uint32_t vnpos = pos + 8 + (st >> 8);  // < 2^32: seg < 2^31, size < 2^24
-                    const uint32_t bad = (st & 0xffu) | (uint32_t)(st < 256u) | (uint32_t)(vnpos > seg);
-                    if (__builtin_amdgcn_readfirstlane(bad)) break;
-                    push(pos, st >> 8, crc);
-                    pos = __builtin_amdgcn_readfirstlane(vnpos);
+                    const uint32_t pj = pos + lane * g;  // < 2^32: pos < 2^31, 63 g < 2^30
+                    const bool inwin = pj < fend;
+                    const uint32_t hp = inwin ? pj : pos;
+                    uint32_t c_, s_;
+                    tile_header(W, hp, t0, c_, s_);
+                    const uint32_t nx = hp + 8 + (s_ >> 8);  // < 2^32: seg < 2^31, size < 2^24
+                    const bool ok = inwin && (s_ & 0xffu) == 0 && s_ >= 256u && nx <= seg;
+                    const uint64_t brk = __ballot(!(ok && nx == pj + g));
+                    const uint32_t f = brk ? (uint32_t)__builtin_ctzll(brk) : 64u;  // lanes < f chain on
+                    const uint32_t okf = f < 64 ? __builtin_amdgcn_readlane((uint32_t)ok, f) : 0u;
+                    const uint32_t na = f + okf;  // lane f's header is real too (lanes < f led to it)
+                    if (na) push_many(hp, s_ >> 8, c_, na);
+                    if (f == 64) {
+                        pos = __builtin_amdgcn_readlane(nx, 63);
+                    } else if (okf) {
+                        pos = __builtin_amdgcn_readlane(nx, f);
+                        g = __builtin_amdgcn_readlane(s_ >> 8, f) + 8;
+                    } else {  // lane f's position holds a header the fast path does not take
+                        pos += f * g;
+                        if (pos < fend) {
+                            crc = __builtin_amdgcn_readlane(c_, f);
+                            st = __builtin_amdgcn_readlane(s_, f);
+                            special = true;
+                        }
+                        break;
+                    }
                     if (pos >= fend) break;
                 }
-                if (pos >= fend) break;
-                crc = __builtin_amdgcn_readfirstlane(crc);  // the special header: scalar from here on
-                st = __builtin_amdgcn_readfirstlane(st);
+                if (!special) break;
                 npos = pos + 8 + (st >> 8);
                 const uint32_t type = st & 0xffu;
                 if (type == 0 && npos <= seg && crc == kStaleZero) {  // size 0: the stale word
@@ -411,6 +448,10 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
     if (lane < k) put(E.count + lane, myrec, mylen, mycrc);  // the last, partial run
     E.count += k;
     E.pos = pos;
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(vmax, d);
+        vmax = o > vmax ? o : vmax;
+    }
     E.max_len = __builtin_amdgcn_readfirstlane(vmax);
     return E;
 }

@@ -3,8 +3,9 @@
 // tests/test_sanitizers.py).
 //
 // Restates, wave by wave and lane by lane, the control flow and the address arithmetic of
-//   karma_amd/csrc/wal_device.hip  wal_walk_plan, k_wal_walk_sub (find_start, walk_range,
-//                                  wtile_fetch / wsmall_fetch, tile_header), k_wal_resolve,
+//   karma_amd/csrc/wal_device.hip  wal_walk_plan, k_wal_walk_sub (find_start, walk_range with
+//                                  its speculative header rounds, wtile_fetch / wsmall_fetch,
+//                                  tile_header), k_wal_resolve,
 //                                  k_wal_gather, k_wal_compare
 //   karma_amd/csrc/wal.cc          replay_core's planning around them
 //   karma_amd/csrc/crc_ragged.hip  the 16-byte blocks k_ragged_direct reads per record
@@ -124,14 +125,16 @@ struct WalkEnd {
     uint32_t count = 0, max_len = 0, kind = 0, stop = 0, pos = 0;
 };
 
-// walk_range (wal_device.hip): uniform walk; the 64-entry runs are flushed lane by lane
+// walk_range (wal_device.hip): the 64-entry runs are flushed lane by lane.  The fast path
+// reads a round of 64 headers, lane j at pos + j * g (g: the last record's stride), and takes
+// the lanes up to the first one whose next header is not the next lane's position.
 WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List& out) {
     const uint32_t seg = S.seg;
     WalkEnd E;
     E.stop = seg;
     E.pos = pos;
     if ((uint64_t)pos + 8 > seg || pos >= hi) return E;
-    uint32_t run[64][3], k = 0;
+    uint32_t run[64][3], k = 0, g = 0;
     auto push = [&](uint32_t p, uint32_t n, uint32_t c) {
         E.max_len = std::max(E.max_len, n);
         run[k][0] = p, run[k][1] = n, run[k][2] = c;
@@ -151,18 +154,49 @@ WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List&
         uint32_t done = 0;
         {
             const uint32_t tend = t0 + tsz < hi ? t0 + tsz : hi, lim = seg - 8;
-            while (pos <= lim && pos < tend) {
-                uint32_t crc, st, size, npos;
-                while (true) {
-                    tile_header(W, pos, t0, crc, st);
-                    size = st >> 8;
-                    npos = pos + 8 + size;
-                    if ((st & 0xffu) != 0 || size == 0 || npos > seg) break;
-                    push(pos, size, crc);
-                    pos = npos;
-                    if (pos > lim || pos >= tend) break;
+            const uint32_t fend = lim + 1 < tend ? lim + 1 : tend;
+            while (pos < fend) {
+                uint32_t crc = 0, st = 0, npos;
+                bool special = false;
+                while (true) {  // one round: every lane reads its header, then the ballot
+                    uint32_t hc[64], hs[64], hn[64];
+                    bool ok[64], chain[64];
+                    for (uint32_t lane = 0; lane < 64; ++lane) {
+                        const uint32_t pj = pos + lane * g;
+                        const bool inwin = pj < fend;
+                        const uint32_t hp = inwin ? pj : pos;
+                        tile_header(W, hp, t0, hc[lane], hs[lane]);
+                        hn[lane] = hp + 8 + (hs[lane] >> 8);
+                        ok[lane] = inwin && (hs[lane] & 0xffu) == 0 && hs[lane] >= 256u && hn[lane] <= seg;
+                        chain[lane] = ok[lane] && hn[lane] == pj + g;
+                    }
+                    uint32_t f = 64;
+                    for (uint32_t lane = 0; lane < 64; ++lane)
+                        if (!chain[lane]) {
+                            f = lane;
+                            break;
+                        }
+                    const bool okf = f < 64 && ok[f];
+                    const uint32_t na = f + (okf ? 1 : 0);
+                    for (uint32_t j = 0; j < na; ++j) push(pos + j * g, hs[j] >> 8, hc[j]);
+                    if (f == 64) {
+                        pos = hn[63];
+                    } else if (okf) {
+                        pos = hn[f];
+                        g = (hs[f] >> 8) + 8;
+                    } else {
+                        pos += f * g;
+                        if (pos < fend) {
+                            crc = hc[f];
+                            st = hs[f];
+                            special = true;
+                        }
+                        break;
+                    }
+                    if (pos >= fend) break;
                 }
-                if (pos > lim || pos >= tend) break;
+                if (!special) break;
+                npos = pos + 8 + (st >> 8);
                 const uint32_t type = st & 0xffu;
                 if (type == 0 && npos <= seg && crc == kStaleZero) {
                     push(pos, 0u, crc);
@@ -261,7 +295,7 @@ Plan walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes) {
     if (sub_bytes) {
         sub_tiles = std::max<uint64_t>(1, sub_bytes / kWTile);
     } else {
-        const uint64_t want = 16 * (uint64_t)(cu > 0 ? cu : 1);
+        const uint64_t want = 20 * (uint64_t)(cu > 0 ? cu : 1);
         if (nseg > 0 && nseg < want) {
             const uint64_t per = (want + nseg - 1) / nseg;
             sub_tiles = std::max<uint64_t>(4, (tiles + per - 1) / per);

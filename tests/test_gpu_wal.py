@@ -354,6 +354,46 @@ def test_replay_randomized_against_model(lib, monkeypatch):
             assert got == (list(want[0]), want[1], want[2]), (case, walk, seg, mix)
 
 
+@pytest.mark.parametrize("walk", ["whole", "split", "split4k"])
+@pytest.mark.parametrize("seg", [4096 + 4, 65536, 1 << 20])
+def test_replay_uniform_runs_speculative_walk(lib, seg, walk, monkeypatch):
+    """Runs of one record size (the walker reads a round of headers at the last stride, lane j at
+    pos + j * stride, and takes every header up to the first size change): run lengths 1..300,
+    sizes from 1 B to a tile and beyond, runs that cross tiles, windows and segments; then a bad
+    type, a length bit and an empty record in the middle of a run, where the round must stop at
+    exactly that header."""
+    _walk_env(monkeypatch, walk)
+    rng = np.random.default_rng(seg + len(walk))
+    sizes = [1, 7, 8, 24, 180, 1000, 4088, 5000]
+    lens = []
+    while len(lens) < 12000:
+        size = int(rng.choice(sizes))
+        lens += [min(size, seg - 8)] * int(rng.integers(1, 301 if size < 1000 else 20))
+    lens = np.array(lens, np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(seg, 0, int(lens.sum()) + 16).copy()
+    nseg = int((lens.astype(np.int64) + 8).sum() // (seg - 4096) + 3)
+    wal = np.zeros(nseg * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    want = wal_model.replay(wal.tobytes(), seg)
+    assert want[0] == list(rec)
+    assert _replay(lib, wal, seg=seg) == (list(want[0]), want[1], want[2])
+    runs = np.nonzero((lens[1:-1] == lens[:-2]) & (lens[1:-1] == lens[2:]))[0] + 1  # inside a run
+    for what in ("bad_type", "length_bit", "empty"):
+        bad = wal.copy()
+        k = int(runs[int(rng.integers(0, runs.size))])
+        h = int(rec[k])
+        if what == "bad_type":
+            bad[h + 4] = 3
+        elif what == "length_bit":
+            bad[h + 5] ^= 0x01
+        else:
+            bad[h: h + 8] = 0
+        w = wal_model.replay(bad.tobytes(), seg)
+        assert len(w[0]) == k
+        assert _replay(lib, bad, seg=seg) == (list(w[0]), w[1], w[2]), what
+
+
 @pytest.mark.parametrize("nseg", [1000, 1024, 1025, 3000])
 def test_replay_segment_counts_around_the_fused_plan(lib, nseg):
     """Up to 1024 segments the device-planned gather reduces the segments' metas itself; above, a

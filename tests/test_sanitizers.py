@@ -92,6 +92,17 @@ def test_emulated_walk_misaligned_segments(san_build, seg):
     _check(san_build, wal, seg, int(rec[1]))
 
 
+@pytest.mark.parametrize("seg", [4096 + 4, 1 << 20])
+def test_emulated_walk_uniform_runs(san_build, seg):
+    """Runs of one size: the speculative header rounds; then a bad type inside a run."""
+    wal, seg, rec, lens = wal_images.uniform_runs(seg)
+    _check(san_build, wal, seg, 0)
+    runs = np.nonzero((lens[1:-1] == lens[:-2]) & (lens[1:-1] == lens[2:]))[0] + 1
+    k = int(runs[len(runs) // 2])
+    wal[int(rec[k]) + 4] = 3
+    _check(san_build, wal, seg, int(rec[2]))
+
+
 def test_emulated_walk_randomized(san_build):
     inner = wal_images.inner_image()
     for case in range(8):

@@ -105,3 +105,20 @@ def inner_image():
     isrc, ioffs, ilens = payloads(71, 600, 1, 100)
     inner, _ = frame(isrc, ioffs, ilens, 64 << 10, 1)
     return inner
+
+
+def uniform_runs(seg, seed=5):
+    """test_replay_uniform_runs_speculative_walk: runs of one record size (1 B to past a tile),
+    so the walker's header rounds take many headers at once and stop at every size change."""
+    rng = np.random.default_rng(seed)
+    sizes = [1, 7, 8, 24, 180, 1000, 4088, 5000]
+    lens = []
+    while len(lens) < 6000:
+        size = int(rng.choice(sizes))
+        lens += [min(size, seg - 8)] * int(rng.integers(1, 301 if size < 1000 else 20))
+    lens = np.array(lens, np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
+    src = synth.splitmix_np(seed, 0, int(lens.sum()) + 16).copy()
+    nseg = int((lens.astype(np.int64) + 8).sum() // (seg - 4096) + 3)
+    wal, rec = frame(src, offs, lens, seg, nseg)
+    return wal, seg, rec, lens
