@@ -568,9 +568,67 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
     (void)total;
     uint32_t pos = s == 0 ? (uint32_t)A.first_pos : 0u;
     uint32_t count = 0, kind = 0, stop = seg, mx = 0;
-    WalSubMeta mine{};  // lane l holds walker j0 + l's report: 64 loads at once, not one per step
-    for (uint64_t j = 0; j < P; ++j) {
-        if (j % 64 == 0 && j + lane < P) mine = KB_READ(A.sub, s * P + j + lane, A.nwork * P, kKbSubMeta);
+    // Fast pass, 64 sub-ranges at a time (lane l: sub-range j0 + l): when every walker started
+    // exactly where the one before it left off (the usual case: find_start lands on the real
+    // chain), each run is accepted whole, and the spans are a prefix sum.  Lane l takes the
+    // previous lane's exit as its entry and checks the serial loop's conditions for it; from
+    // the first lane that fails, the serial loop below takes over.
+    uint64_t j = 0;
+    while (j < P) {
+        const uint64_t jj = j + lane;
+        const bool in = jj < P;
+        WalSubMeta m{};
+        if (in) m = KB_READ(A.sub, s * P + jj, A.nwork * P, kKbSubMeta);
+        const uint32_t lo = (uint32_t)(jj * A.sub_bytes);
+        const uint32_t hi = (uint64_t)lo + A.sub_bytes < seg ? lo + (uint32_t)A.sub_bytes : seg;
+        uint32_t pj = __shfl_up(m.exit, 1);
+        if (lane == 0) pj = pos;
+        const uint64_t km = __ballot(in && m.kind != 0);
+        const bool kbefore = kind != 0 || (km & ((1ull << lane) - 1ull)) != 0;  // replay stopped before
+        const bool acc = in && !kbefore && pj < hi && (uint64_t)pj + 8 <= seg && m.first == pj;
+        const uint64_t bad = __ballot(!(!in || kbefore || acc));
+        const uint32_t f = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;  // lanes < f follow the serial loop
+        const bool take = lane < f && acc;
+        const uint32_t n = take ? m.count : 0u;
+        uint32_t pre = n;  // inclusive prefix of n
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(pre, d);
+            if ((int)lane >= d) pre += t;
+        }
+        if (in && lane < f) {
+            KB_WRITE(A.span, 2 * (s * P + jj), 2 * A.nwork * P, kKbSpan, (uint32_t)(jj * A.sub_cap));
+            KB_WRITE(A.span, 2 * (s * P + jj) + 1, 2 * A.nwork * P, kKbSpan, count + pre - n);
+        }
+        count += __shfl(pre, 63);
+        uint32_t vmx = take ? m.max_len : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t o = __shfl_xor(vmx, d);
+            vmx = o > vmx ? o : vmx;
+        }
+        mx = vmx > mx ? vmx : mx;
+        const uint64_t kt = __ballot(take && m.kind != 0);
+        if (kt) {
+            const int l = __builtin_ctzll(kt);
+            kind = __builtin_amdgcn_readlane(m.kind, l);
+            stop = __builtin_amdgcn_readlane(m.stop, l);
+        }
+        const uint64_t tm = __ballot(take);
+        if (tm) pos = __builtin_amdgcn_readlane(m.exit, 63 - __builtin_clzll(tm));
+        pos = __builtin_amdgcn_readfirstlane(pos);
+        count = __builtin_amdgcn_readfirstlane(count);
+        mx = __builtin_amdgcn_readfirstlane(mx);
+        if (f < 64) {
+            j += f;
+            break;
+        }
+        j += 64;
+    }
+    WalSubMeta mine{};  // lane l holds walker (j & ~63) + l's report: 64 loads at once, not one per step
+    for (const uint64_t j1 = j; j < P; ++j) {
+        if ((j % 64 == 0 || j == j1) && (j & ~63ull) + lane < P)
+            mine = KB_READ(A.sub, s * P + (j & ~63ull) + lane, A.nwork * P, kKbSubMeta);
         const uint32_t lo = (uint32_t)(j * A.sub_bytes);
         const uint32_t hi = (uint64_t)lo + A.sub_bytes < seg ? lo + (uint32_t)A.sub_bytes : seg;
         uint32_t st = (uint32_t)(j * A.sub_cap), n = 0;
@@ -694,6 +752,12 @@ __global__ __launch_bounds__(1024) void k_wal_plan(WalArgs A) {
 template <bool FUSED_PLAN>
 __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
     __shared__ uint2 spans[kMaxSub];
+    __shared__ uint32_t s_count;
+    // the segment's spans first: their load is in flight with the metas' (one latency, not two)
+    const uint32_t P = (uint32_t)A.nsub;
+    const uint2* sp = reinterpret_cast<const uint2*>(A.span) + blockIdx.x * A.nsub;
+    for (uint32_t j = threadIdx.x; j < P; j += blockDim.x)
+        spans[j] = KB_READ(sp, j, (A.nwork - blockIdx.x) * A.nsub, kKbSpan);
     uint64_t g0;
     if constexpr (FUSED_PLAN) {
         __shared__ uint32_t s_w1, s_max;
@@ -708,6 +772,7 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
         WalSegMeta m{0u, KARMA_WAL_END, 0u, 0u, 0u};
         if (tid < nw) m = A.meta[tid];
         if (tid < nw && m.kind != KARMA_WAL_END) atomicMin(&s_w1, tid + 1);
+        if (tid == blockIdx.x) s_count = m.count;
         __syncthreads();
         const uint32_t w1 = s_w1;
         if (blockIdx.x >= w1 && blockIdx.x != 0) return;  // replay does not enter this segment
@@ -741,31 +806,46 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
     } else {
         if (blockIdx.x >= A.sum->w1) return;  // replay does not enter this segment
         g0 = A.cand_base[blockIdx.x];
+        if (threadIdx.x == 0) s_count = A.meta[blockIdx.x].count;
     }
     const uint64_t rel = (uint64_t)blockIdx.x * A.seg_bytes;
     const uint32_t* crec = A.cand_rec + blockIdx.x * A.cand_cap;
     const uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
     const uint32_t* ccrc = A.cand_crc + blockIdx.x * A.cand_cap;
-    const uint32_t P = (uint32_t)A.nsub;
-    const uint2* sp = reinterpret_cast<const uint2*>(A.span) + blockIdx.x * A.nsub;
-    for (uint32_t j = threadIdx.x; j < P; j += blockDim.x)
-        spans[j] = KB_READ(sp, j, (A.nwork - blockIdx.x) * A.nsub, kKbSpan);
     __syncthreads();
-    const uint32_t count = A.meta[blockIdx.x].count;
-    for (uint32_t i = threadIdx.x; i < count; i += blockDim.x) {
-        uint32_t a = 0, b = P;  // the last run whose prefix is <= i: [a, b)
-        while (b - a > 1) {
-            const uint32_t mid = (a + b) / 2;
-            if (spans[mid].y <= i) a = mid;
-            else b = mid;
-        }
-        const uint32_t slot = spans[a].x + (i - spans[a].y);
+    const uint32_t count = s_count;
+    // kGatherU candidates per thread per trip, every load issued before the first store: one
+    // memory latency per trip instead of one per candidate (a segment of 1 MiB holds ~5600
+    // candidates of 180 B: one trip of 1024 threads)
+    constexpr int kGatherU = 8;
+    for (uint32_t i0 = threadIdx.x; i0 < count; i0 += kGatherU * blockDim.x) {
+        uint32_t vr[kGatherU], vn[kGatherU], vc[kGatherU];
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            if (i >= count) break;
+            uint32_t a = 0, b = P;  // the last run whose prefix is <= i: [a, b)
+            while (b - a > 1) {
+                const uint32_t mid = (a + b) / 2;
+                if (spans[mid].y <= i) a = mid;
+                else b = mid;
+            }
+            const uint32_t slot = spans[a].x + (i - spans[a].y);
 #ifdef KARMA_BOUNDS
-        kb_ok(slot >= a * A.sub_cap && slot < (a + 1) * A.sub_cap, kKbRunSlot, slot, A.sub_cap);
+            kb_ok(slot >= a * A.sub_cap && slot < (a + 1) * A.sub_cap, kKbRunSlot, slot, A.sub_cap);
 #endif
-        KB_WRITE(A.off, g0 + i, A.n_all, kKbList, rel + KB_READ(crec, slot, A.cand_cap, kKbCand));
-        KB_WRITE(A.len, g0 + i, A.n_all, kKbList, KB_READ(clen, slot, A.cand_cap, kKbCand));
-        KB_WRITE(A.stored, g0 + i, A.n_all, kKbList, KB_READ(ccrc, slot, A.cand_cap, kKbCand));
+            vr[u] = KB_READ(crec, slot, A.cand_cap, kKbCand);
+            vn[u] = KB_READ(clen, slot, A.cand_cap, kKbCand);
+            vc[u] = KB_READ(ccrc, slot, A.cand_cap, kKbCand);
+        }
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            if (i >= count) break;
+            KB_WRITE(A.off, g0 + i, A.n_all, kKbList, rel + vr[u]);
+            KB_WRITE(A.len, g0 + i, A.n_all, kKbList, vn[u]);
+            KB_WRITE(A.stored, g0 + i, A.n_all, kKbList, vc[u]);
+        }
     }
 }
 
