@@ -43,6 +43,10 @@ def parse():
     p.add_argument("--wal-record", type=int, default=180, help="wal_* payload bytes (configs[0]: ~180 B)")
     p.add_argument("--wal-mix", default="fixed", choices=["fixed", "config3"],
                    help="wal_*: every payload --wal-record bytes, or configs[2]'s log-uniform 64 B-64 KiB mix (~4 GiB)")
+    p.add_argument("--wal-image", default="pinned", choices=["pinned", "pageable"],
+                   help="wal_*: the WAL image in page-locked host memory (a writer's own write buffer, like "
+                        "sivir's aligned O_DIRECT buffer: replay DMAs it with no staging copy) or in pageable memory "
+                        "(replay stages it); the other mode is measured too (a shorter run) and reported beside it")
     p.add_argument("--records-per-gpu", type=int, default=0,
                    help="0 = the BASELINE config of the run: configs[1]'s 1M x 4 KiB per GPU, or with --gpus 8 "
                         "configs[4]'s shard, 256M / 8 = 33,554,432 records of 4 KiB per GPU")
@@ -215,7 +219,10 @@ def wal_bench(args, L, rank):
         per_seg = seg // (size + 8)
         wal_bytes = ((n + per_seg - 1) // per_seg + 1) * seg
     payload = int(lens.sum())
-    wal = np.zeros(wal_bytes, dtype=np.uint8)
+    import torch
+    images = {"pageable": np.zeros(wal_bytes, dtype=np.uint8),
+              "pinned": torch.zeros(wal_bytes, dtype=torch.uint8).pin_memory().numpy()}
+    wal = images[args.wal_image]
     cur, nf = ctypes.c_uint64(0), ctypes.c_size_t()
 
     def append():
@@ -233,6 +240,8 @@ def wal_bench(args, L, rank):
         assert nrec.value == n
 
     append()
+    other = "pageable" if args.wal_image == "pinned" else "pinned"
+    images[other][:] = wal  # the same image in the other kind of host memory
     step = append if args.workload == "wal_append" else replay
     dev_rate = dir_rate = None
     if args.workload == "wal_replay":  # the same replay over a copy already in HBM (no upload)
@@ -282,11 +291,23 @@ def wal_bench(args, L, rank):
         step()
     dt = (time.perf_counter() - t0) / args.steps
     mix = f"{n} x {size} B" if size else f"{n} log-uniform 64 B-64 KiB ({payload / GIB:.2f} GiB)"
+    # the other kind of host memory, a shorter run of the same step
+    keep, wal = wal, images[other]
+    for _ in range(2):
+        step()
+    k_other = max(3, args.steps // 4)
+    t1 = time.perf_counter()
+    for _ in range(k_other):
+        step()
+    other_rate = payload / ((time.perf_counter() - t1) / k_other) / GIB
+    wal = keep
     res = {"metric": METRIC + f" [{args.workload}: host memory end to end]",
            "value": round(payload / dt / GIB, 3), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "u8", "data": "synthetic splitmix64 payloads in pageable host memory",
-           "records_per_s": round(n / dt, 1),
+           "vs_baseline": None, "dtype": "u8",
+           "data": f"synthetic splitmix64 payloads; the WAL image in {args.wal_image} host memory",
+           "records_per_s": round(n / dt, 1), "wal_image": args.wal_image,
+           f"{other}_image_value": round(other_rate, 3),
            "device_resident_value": round(dev_rate, 3) if dev_rate is not None else None,
            "segment_files_value": round(dir_rate, 3) if dir_rate is not None else None,
            "config": {"workload": f"{mix} WAL records, 1 MiB segments, "

@@ -137,6 +137,18 @@ bool host_is_pinned(const void* h) {
     return false;
 }
 
+bool host_range_pinned(const void* h, size_t bytes) {
+    if (!host_is_pinned(h)) return false;
+    hipDeviceptr_t base = nullptr;
+    size_t sz = 0;
+    if (hipMemGetAddressRange(&base, &sz, const_cast<void*>(h)) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const uintptr_t b = reinterpret_cast<uintptr_t>(base), q = reinterpret_cast<uintptr_t>(h);
+    return q >= b && q + bytes <= b + sz;
+}
+
 int staged_upload(int dev, void* d_dst, const HostFill& fill, uint64_t src_off, size_t bytes) {
     if (!bytes) return 0;
     Stage& S = stage_for(dev);

@@ -32,6 +32,8 @@ int staged_copy(int dev, void* d_dst, const void* h_src, size_t bytes);
 // True when h is page-locked host memory the device can DMA from directly
 // (hipHostMalloc'd or registered by its owner).
 bool host_is_pinned(const void* h);
+// True when [h, h + bytes) lies inside one page-locked host allocation.
+bool host_range_pinned(const void* h, size_t bytes);
 
 // body(t) for t in [0, n) on n std::threads (n small: the host stages of a call).
 void run_threads(int n, const std::function<void(int)>& body);

@@ -174,7 +174,7 @@ using ImageFill = karma::engine::HostFill;
 
 int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
-                int device, const karma_wal_tuning* tuning);
+                int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned = nullptr);
 
 }  // namespace
 
@@ -199,8 +199,10 @@ int karma_wal_replay_tuned(const void* h_wal, const void* d_wal, size_t wal_byte
         std::memcpy(dst, src + off, n);
         return 0;
     };
+    // a page-locked image is DMA'd as it is (no staging copies)
+    const uint8_t* pinned = !d_wal && karma::engine::host_range_pinned(src, wal_bytes) ? src : nullptr;
     return replay_core(static_cast<const uint8_t*>(d_wal), d_wal ? nullptr : &copy, wal_bytes, seg_bytes, start,
-                       h_n_records, h_stop, h_status, h_rec_off, rec_cap, device, tuning);
+                       h_n_records, h_stop, h_status, h_rec_off, rec_cap, device, tuning, pinned);
 }
 
 }  // extern "C"
@@ -208,10 +210,11 @@ int karma_wal_replay_tuned(const void* h_wal, const void* d_wal, size_t wal_byte
 namespace {
 
 // The replay proper (karma_wal_replay): the image is d_wal, or produced by fill and
-// streamed into HBM.  Offsets in and out are relative to the image start.
+// streamed into HBM (or, h_pinned: the same image in page-locked host memory, one DMA).
+// Offsets in and out are relative to the image start.
 int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
-                int device, const karma_wal_tuning* tuning) {
+                int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned) {
     using namespace karma::engine;
     const uint64_t nseg = wal_bytes / seg_bytes;
     const uint64_t s0 = std::min<uint64_t>(start / seg_bytes, nseg);
@@ -238,7 +241,13 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         A.wal = static_cast<const uint8_t*>(d_wal) + base0;
     } else {
         if (const int rc = c.img.ensure(img_bytes)) return rc;
-        if (const int rc = staged_upload(dev, c.img.p, *fill, base0, img_bytes)) return rc;
+        if (h_pinned) {
+            if (hipMemcpyAsync(c.img.p, h_pinned + base0, img_bytes, hipMemcpyHostToDevice, c.st) != hipSuccess ||
+                hipStreamSynchronize(c.st) != hipSuccess)
+                return fail(KARMA_E_HIP, "wal_replay: image upload");
+        } else if (const int rc = staged_upload(dev, c.img.p, *fill, base0, img_bytes)) {
+            return rc;
+        }
         A.wal = c.img.as<const uint8_t>();
         T.mark("image upload");
     }

@@ -92,6 +92,46 @@ def test_append_matches_reference_framing(lib):
     assert wal.tobytes() == bytes(model)
 
 
+@pytest.mark.parametrize("mix", ["small", "mixed", "large"])
+def test_append_into_pinned_image_matches_pageable(lib, mix):
+    """A page-locked image (a writer's own buffer): append gives the pageable image's bytes and the
+    model's (segment footers, padding records, records > 1 KiB, an image that fills up, a pass
+    from a checkpoint cursor); replay from the pinned image (one DMA, no staging copies) gives
+    the pageable image's result."""
+    if mix == "small":
+        src, offs, lens = _payloads(41, 30000, 1, 300)
+    elif mix == "mixed":
+        src, offs, lens = _payloads(42, 6000, 1, 6000)
+    else:
+        src, offs, lens = _payloads(43, 600, 1000, 60000)
+    seg = SEG if mix != "large" else 256 << 10
+    # every segment loses less than one record to its footer
+    nseg = int((lens.astype(np.int64) + 8).sum() // (seg - int(lens.max()) - 8)) + 2
+    for cut in (0, nseg // 2):  # cut: an image too small (not every record fits)
+        wal = np.zeros((nseg - cut) * seg, np.uint8)
+        cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+        pinned = torch.zeros(wal.nbytes, dtype=torch.uint8).pin_memory()
+        pw = pinned.numpy()
+        cur2, rec2 = _append(lib, src, offs, lens, pw, seg=seg)
+        assert cur2 == cur and list(rec2) == list(rec)
+        assert np.array_equal(pw, wal)
+        assert (len(rec) == lens.size) == (cut == 0)
+        if cut == 0:
+            want = wal_model.replay(pw.tobytes(), seg)
+            assert want[0] == list(rec)
+        # replay from the pinned image (one DMA, no staging) == from the pageable one
+        for start in (0, int(rec[len(rec) // 3])):
+            assert _replay(lib, pw, start=start, seg=seg) == _replay(lib, wal, start=start, seg=seg)
+        # appended to from a checkpoint cursor (the pass starts mid-image)
+        k = len(rec) // 2
+        pw2 = pw.copy()
+        pw2[int(rec[k]):] = 0
+        p2 = torch.from_numpy(pw2).pin_memory()
+        cur3, rec3 = _append(lib, src, offs[k:], lens[k:], p2.numpy(), cursor=int(rec[k]), seg=seg)
+        assert cur3 == cur and list(rec3) == list(rec[k:])
+        assert np.array_equal(p2.numpy(), wal)
+
+
 def test_replay_round_trip_and_zero_tail(lib):
     src, offs, lens = _payloads(5, 4000, 1, 2000)
     wal = np.zeros(64 * SEG, np.uint8)
