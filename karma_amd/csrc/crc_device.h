@@ -189,8 +189,8 @@ __device__ __forceinline__ uint32_t tail_register(const uint32_t* lds, int z4, i
 }
 
 // MODE (timing experiments of the tools build only, wrong results): bit 0 = main-loop
-// steps without the LDS lookups (KARMA_CRC_VARIANT=6, ab.h).  The shipped library
-// instantiates MODE 0 only.
+// steps without the LDS lookups (KARMA_CRC_VARIANT=6, ab.h), bit 1 = stream_unit without
+// the lane fold and group tree.  The shipped library instantiates MODE 0 only.
 template <int MODE = 0>
 __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
                                       uint32_t& a3, const u32x4& v) {
@@ -384,6 +384,7 @@ __device__ __forceinline__ uint32_t stream_unit(const uint32_t* lds, uint32_t X,
         if (q < rem - 1 || (q == rem - 1 && L.lok)) step4<MODE>(lds, X, a0, a1, a2, a3, cur[q]);
     // lane fold (crc32c.cc STEP4W order), then the 8-lane tree with the lane
     // holding the unit's last window rotated to the end
+    if constexpr ((MODE & 2) != 0) return a0 ^ a1 ^ a2 ^ a3;  // timing build only: no fold, no tree
     uint32_t c = lane_fold(lds, a0, a1, a2, a3);
     const uint32_t lane = threadIdx.x & 63u;
     c = __shfl(c, (int)((lane & ~(G - 1u)) | ((l + L.m + 1) & (G - 1))), 64);

@@ -490,7 +490,8 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
 // replay call of 1M x 180 B, 4: 0.202, 2: 0.222 -- their loads then spread over 32 cache
 // lines per instruction; one record per lane: 0.327).  G = 2 is the tools
 // build's KARMA_DIRECT_VARIANT=5 (the pair blob, Z_32).
-template <int G>
+template <int G, int MODE = 0>  // MODE != 0: timing-only variants of the tools build (bits 0-1:
+                                 // stream_unit's, crc_device.h; bit 2: no head / tail steps)
 __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) {
     constexpr int NG = 64 / G, NR = 64 / NG;  // groups per wave, rounds
     uint64_t n_rec = A.n_rec;
@@ -530,13 +531,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
         issue_unit_loads<kRaggedPF, kRaggedNT, G>(L, Ld);
         const bool tail = body && gi.e > gi.b;
         const u32x4 tv = ld16(tail ? gi.b : safe);
-        const uint32_t hi = body ? head_register(lds, kLZ4, kLT8, pi, gi, initi) : 0u;
+        const uint32_t hi = body ? ((MODE & 4) ? initi : head_register(lds, kLZ4, kLT8, pi, gi, initi)) : 0u;
         uint32_t Ri = 0;
 #pragma unroll 1
         for (uint32_t round = 0; round < NR; ++round) {
             const uint32_t sh = __shfl(hi, (int)(round * NG + grp));
             LaneUnit N = L;
-            const uint32_t R = stream_unit<kRaggedPF, kRaggedNT, 0, G>(lds, X, l, L, Ld, L.us, sh,
+            const uint32_t R = stream_unit<kRaggedPF, kRaggedNT, MODE, G>(lds, X, l, L, Ld, L.us, sh,
                                                                        [&](UnitLoads<kRaggedPF>& nx) {
                 if (round + 1 < NR) {
                     N = unit_of(round + 1);
@@ -549,7 +550,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
         }
         if (vi) {
             const uint32_t res = gi.is_short ? short_record(lds, kLZ4, kLT8, pi, ni, initi)
-                                             : ~steps_in_vec(lds, kLZ4, kLT8, Ri, tv, 0u, tail ? (uint32_t)(gi.e - gi.b) : 0u);
+                                 : (MODE & 4) ? Ri ^ tv.x
+                                              : ~steps_in_vec(lds, kLZ4, kLT8, Ri, tv, 0u, tail ? (uint32_t)(gi.e - gi.b) : 0u);
             A.out[ri] = res;
             if (A.cmp_stored && ni && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
         }
@@ -755,6 +757,16 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL(k_ragged_lanes, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 5)
         hipLaunchKernelGGL(k_ragged_direct4<2>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 6)  // timing only (wrong CRCs): no body lookups / no fold and tree / neither
+        hipLaunchKernelGGL((k_ragged_direct4<4, 1>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 7)
+        hipLaunchKernelGGL((k_ragged_direct4<4, 2>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 8)
+        hipLaunchKernelGGL((k_ragged_direct4<4, 3>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 9)  // timing only: no head / tail steps; 10: none of the three
+        hipLaunchKernelGGL((k_ragged_direct4<4, 4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 10)
+        hipLaunchKernelGGL((k_ragged_direct4<4, 7>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else
 #endif
         hipLaunchKernelGGL(k_ragged_direct4<4>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
