@@ -302,8 +302,9 @@ struct WalkEnd {
 // is a candidate, a size-0 record compares the stored CRC with Value of the stale
 // len/type word (wal.cc:50-60), type 1 skips to the segment end, anything else
 // stops the walk.  Candidates go to crec / clen (cap slots).
+// resident: the tile start W already holds (find_start's tile), or ~0u.
 __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t pos, uint32_t hi, const WalArgs& A,
-                              uint64_t slot0, uint64_t cap) {
+                              uint64_t slot0, uint64_t cap, uint32_t resident = ~0u) {
     const uint64_t total = A.nwork * A.cand_cap;  // every list slot (bounds build)
     (void)total;
     auto put = [&](uint64_t i, uint32_t rec, uint32_t n, uint32_t c) {  // list entry i (< cap: else dropped)
@@ -356,8 +357,10 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
     // goes back to tiles when it leaves a window for the next one.
     uint32_t t0 = pos / kWTile * kWTile, tsz = kWTile;
     uint4 r[kWQV + 1];
-    wtile_fetch(S, lane, t0, r);
-    wtile_store(W, lane, r);
+    if (t0 != resident) {  // else find_start left this tile in W: no second load of it
+        wtile_fetch(S, lane, t0, r);
+        wtile_store(W, lane, r);
+    }
     while (true) {
         const bool more = tsz == kWTile && (uint64_t)t0 + kWTile < tlim;
         if (more) wtile_fetch(S, lane, t0 + kWTile, r);  // in flight while the walk runs
@@ -540,7 +543,8 @@ __global__ __launch_bounds__(64) void k_wal_walk_sub(WalArgs A) {
     else
         first = find_start(W, S, lane, lo, hi);
     const uint64_t slot = s * A.cand_cap + j * A.sub_cap;
-    const WalkEnd E = walk_range(W, S, lane, first, hi, A, slot, A.sub_cap);
+    // find_start leaves the sub-range's first tile in W
+    const WalkEnd E = walk_range(W, S, lane, first, hi, A, slot, A.sub_cap, start < lo && first < hi ? lo : ~0u);
     if (lane != 0) return;
     if (P == 1) {
         KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{E.count, E.kind, A.base0 + rel + (E.kind ? E.stop : S.seg), E.max_len, 0u}));
