@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--call-events", choices=["auto", "on", "off"], default="auto",
                    help="bracket every call with its own events too (auto: when a call is more than one kernel)")
+    p.add_argument("--no-numa-bind", action="store_true",
+                   help="do not restrict the process to the CPUs of its GPU's NUMA node")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on (affinity)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_fixed_4k.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/profile.sh)")
@@ -71,6 +73,33 @@ def host_cpus() -> int:
         return len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover - non-Linux
         return os.cpu_count() or 1
+
+
+def bind_to_gpu_node(torch, local: int):
+    """Restrict this process to the CPUs of its GPU's PCIe root (sysfs local_cpulist), as a
+    deployment runs one process per GPU bound to that GPU's NUMA node (numactl --cpunodebind).
+    Done before any host buffer is allocated, so the bench's host memory is first-touched on
+    that node too.  Host-memory paths (WAL append / replay from host memory) depend on it: the
+    library's copy threads otherwise float over both sockets (1M x 180 B append: 27 GiB/s
+    unbound, 33 bound).  Returns a description, or None if unknown."""
+    try:
+        p = torch.cuda.get_device_properties(local)
+        bus = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bus}/local_cpulist") as f:
+            spec = f.read().strip()
+        with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
+            node = f.read().strip()
+        cpus = set()
+        for part in spec.split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        want = cpus & os.sched_getaffinity(0)
+        if not want:
+            return None
+        os.sched_setaffinity(0, want)
+        return f"NUMA node {node} of GPU {bus}: {len(want)} CPUs ({spec})"
+    except (AttributeError, OSError, ValueError):
+        return None
 
 
 def cgroup_cpu_quota():
@@ -491,6 +520,7 @@ def main():
     local = local % max(ndev, 1)  # one rank per GPU; several ranks per GPU only for plumbing checks
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    numa = None if args.no_numa_bind else bind_to_gpu_node(torch, local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
@@ -523,6 +553,7 @@ def main():
     if wl in ("wal_append", "wal_replay", "kfp_encode", "kfp_parse"):
         res = wal_bench(args, L, rank) if wl.startswith("wal") else kfp_bench(args, L, rank)
         if rank == 0:
+            res["host_binding"] = numa
             print(json.dumps(res), flush=True)
         if comm is not None:
             L.karma_crc32c_comm_destroy(comm)
@@ -770,6 +801,7 @@ def main():
                          "call_frac": round(algo_bytes / (call_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "compute_only_gibs": round(payload * world / (call_max * 1e-3) / GIB, 2),
             "prewarm_ms": round(prewarm_ms, 1),
+            "host_binding": numa,
             "rccl_nranks": rccl_nranks,
         }
         res.update(extra)

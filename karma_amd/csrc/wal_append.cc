@@ -53,20 +53,36 @@ constexpr uint64_t kBlockBytesFirst = uint64_t(256) << 10;  // payload bytes of 
 constexpr uint64_t kBlockBytesMax = uint64_t(4) << 20;      // doubling up to this
 constexpr uint64_t kCallBytes = uint64_t(1) << 30;   // payload bytes staged per pass (larger batches loop)
 constexpr int kStreams = 8;                          // DMA / CRC streams the blocks rotate over
+constexpr uint32_t kZeroCopyMaxLen = 1024;           // the bounded ABI's one-record-per-group limit (capi.cc)
 
 inline void put32(uint8_t* p, uint32_t v) { std::memcpy(p, &v, 4); }  // little-endian host
+
+// One record's payload: 16-byte moves (the last one overlapping) for the small records of a
+// log; a library call per 180-byte record cost about as much as the copy itself.
+inline void copy_payload(uint8_t* d, const uint8_t* s, size_t L) {
+    if (L < 16 || L > 1024) {
+        std::memcpy(d, s, L);
+        return;
+    }
+    size_t k = 0;
+    for (; k + 16 <= L; k += 16) std::memcpy(d + k, s + k, 16);
+    if (k < L) std::memcpy(d + L - 16, s + L - 16, 16);
+}
 
 struct Buf {
     void* p = nullptr;
     size_t bytes = 0;
     bool host = false;
-    int ensure(size_t want, bool pinned_host) {
+    // pinned_host: page-locked host memory; coherent: fine-grained (the GPU reads and writes it
+    // over PCIe uncached, so a kernel sees what the host wrote just before the launch)
+    int ensure(size_t want, bool pinned_host, bool coherent = false) {
         if (p && bytes >= want) return 0;
         if (p) (void)(host ? hipHostFree(p) : hipFree(p));
         p = nullptr;
         bytes = 0;
         want = std::max<size_t>(want + want / 8, 4096);
-        const hipError_t e = pinned_host ? hipHostMalloc(&p, want, hipHostMallocDefault) : hipMalloc(&p, want);
+        const hipError_t e = pinned_host ? hipHostMalloc(&p, want, coherent ? hipHostMallocCoherent : hipHostMallocDefault)
+                                         : hipMalloc(&p, want);
         if (e != hipSuccess) {
             p = nullptr;
             return set_last_error(e == hipErrorOutOfMemory ? KARMA_E_NOMEM : KARMA_E_HIP, "wal_append: allocation");
@@ -164,11 +180,11 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
     const size_t max_blocks = n / kBlockRecords + pay_total / kBlockBytesFirst + 32;
     if (const int rc = C.h_pay.ensure(pay_total + 16, true)) return rc;
     if (const int rc = C.d_pay.ensure(pay_total + 16, false)) return rc;
-    if (const int rc = C.h_off.ensure(n * 8, true)) return rc;
+    if (const int rc = C.h_off.ensure(n * 8, true, true)) return rc;
     if (const int rc = C.d_off.ensure(n * 8, false)) return rc;
-    if (const int rc = C.h_len.ensure(n * 4, true)) return rc;
+    if (const int rc = C.h_len.ensure(n * 4, true, true)) return rc;
     if (const int rc = C.d_len.ensure(n * 4, false)) return rc;
-    if (const int rc = C.h_crc.ensure(n * 4, true)) return rc;
+    if (const int rc = C.h_crc.ensure(n * 4, true, true)) return rc;
     if (const int rc = C.d_crc.ensure(n * 4, false)) return rc;
     if (const int rc = C.events(max_blocks)) return rc;
     if (C.at.size() < n) C.at.resize(n);
@@ -209,39 +225,50 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
         size_t r = std::upper_bound(runs.begin(), runs.end(), lo,
                                     [](size_t i, const karma::engine::WalRun& w) { return i < w.i0; }) -
                    runs.begin() - 1;  // the run holding record lo
+        // the block's packed payloads [plo, phi) (V(i) - 8 i: read before this loop turns at[]
+        // into WAL offsets; at[hi] belongs to the next block, which may be converting it)
+        const uint64_t plo = at[lo] - kHeader * lo, phi = at[hi - 1] - kHeader * (hi - 1) + len[hi - 1];
         bool contiguous = true;
+        for (size_t i = lo + 1; i < hi && contiguous; ++i) contiguous = src_off[i] == src_off[i - 1] + len[i - 1];
         for (size_t i = lo; i < hi; ++i) {  // segment_file::append_record: length field + payload
             while (i >= runs[r].i1) ++r;
-            at[i] += runs[r].base;  // V(i) -> WAL offset
+            const uint64_t v = at[i], pk = v - kHeader * i;  // V(i), packed payload offset
+            at[i] = v + runs[r].base;                         // V(i) -> WAL offset
             uint8_t* p = wal + at[i];
             const uint32_t L = len[i];
             put32(p + 4, L << 8 | 0u);
-            std::memcpy(p + kHeader, src + src_off[i], L);
-            if (i > lo && src_off[i] != src_off[i - 1] + len[i - 1]) contiguous = false;
+            copy_payload(p + kHeader, src + src_off[i], L);
+            if (!contiguous) copy_payload(hp + pk, src + src_off[i], L);
+            ho[i] = pk - plo;  // the block's kernel sees its own slice: offsets rebased onto dp + plo
+            hl[i] = L;
         }
-        const uint64_t plo = ho[lo], phi = ho[hi - 1] + hl[hi - 1];
-        if (contiguous) {
-            std::memcpy(hp + plo, src + src_off[lo], phi - plo);
-        } else {
-            for (size_t i = lo; i < hi; ++i) std::memcpy(hp + ho[i], wal + at[i] + kHeader, hl[i]);
-        }
+        if (contiguous) std::memcpy(hp + plo, src + src_off[lo], phi - plo);
         hipStream_t s = C.st[k % kStreams];
         const size_t nr = hi - lo;
         uint8_t* dp = C.d_pay.as<uint8_t>();
-        uint64_t* hoff = ho + lo;  // the block's kernel sees its own slice: offsets rebased onto dp + plo
+        uint64_t* hoff = ho + lo;
         uint64_t* doff = C.d_off.as<uint64_t>() + lo;
-        for (size_t i = 0; i < nr; ++i) hoff[i] -= plo;
         uint32_t* dlen = C.d_len.as<uint32_t>() + lo;
-        if (hipMemcpyAsync(dp + plo, hp + plo, phi - plo, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(doff, hoff, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(dlen, hl + lo, nr * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        if (hipMemcpyAsync(dp + plo, hp + plo, phi - plo, hipMemcpyHostToDevice, s) != hipSuccess)
             return (int)KARMA_E_HIP;
-        if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, doff, dlen, nr, phi - plo, max_len, nullptr, 0,
-                                                             C.d_crc.as<uint32_t>() + lo, s))
-            return rc;
-        if (hipMemcpyAsync(hc + lo, C.d_crc.as<uint32_t>() + lo, nr * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipEventRecord(C.ev[k], s) != hipSuccess)
-            return (int)KARMA_E_HIP;
+        if (max_len <= kZeroCopyMaxLen) {
+            // the small-record kernel reads each record's offset and length once and writes its CRC
+            // once: it does so over PCIe, from and into the fine-grained host arrays, so the block's
+            // only copy is its payload DMA (the small copies each cost the DMA engine ~10 us)
+            if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, hoff, hl + lo, nr, phi - plo, max_len, nullptr,
+                                                                 0, hc + lo, s))
+                return rc;
+        } else {
+            if (hipMemcpyAsync(doff, hoff, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+                hipMemcpyAsync(dlen, hl + lo, nr * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+                return (int)KARMA_E_HIP;
+            if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, doff, dlen, nr, phi - plo, max_len, nullptr,
+                                                                 0, C.d_crc.as<uint32_t>() + lo, s))
+                return rc;
+            if (hipMemcpyAsync(hc + lo, C.d_crc.as<uint32_t>() + lo, nr * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+                return (int)KARMA_E_HIP;
+        }
+        if (hipEventRecord(C.ev[k], s) != hipSuccess) return (int)KARMA_E_HIP;
         return 0;
     };
     // d. the CRC fields of the oldest blocks whose CRCs are back (every such event is this
@@ -288,8 +315,6 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
             uint64_t v = csum[t];
             for (size_t i = c0; i < std::min(c1, n_valid); ++i) {
                 at[i] = v;
-                ho[i] = v - kHeader * i;  // packed payload offset
-                hl[i] = len[i];
                 v += len[i] + kHeader;
             }
             if ((c0 <= n_valid && n_valid < c1) || (n_valid == n && t == nthr - 1)) vtotal = v;  // V(n_valid)
@@ -316,7 +341,7 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
                 size_t lo = b + 1, hi = std::min(framed, b + kBlockRecords);
                 while (lo < hi) {
                     const size_t mid = lo + (hi - lo + 1) / 2;
-                    if (ho[mid - 1] + hl[mid - 1] - ho[b] <= blimit) lo = mid;
+                    if (V(mid) - V(b) - kHeader * (mid - b) <= blimit) lo = mid;  // payload bytes of [b, mid)
                     else hi = mid - 1;
                 }
                 bstart[++nb] = lo;
@@ -344,6 +369,7 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
     T.mark("d. CRC fields");
     for (auto& s : C.st)  // nothing of this call may be in flight when it returns
         if (hipStreamSynchronize(s) != hipSuccess) set_rc(KARMA_E_HIP);
+    T.mark("e. stream syncs");
     if (const int rc = crc_rc.load())  // payloads and length fields are written; CRC fields may not be
         return rc == KARMA_E_HIP ? set_last_error(rc, "wal_append: device pipeline") : rc;
     if (rec_off) std::memcpy(rec_off, at, framed * sizeof(uint64_t));
@@ -367,6 +393,7 @@ extern "C" int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_o
     if (device >= nd) return set_last_error(KARMA_E_INVALID, "wal_append: device index out of range");
     if (device >= 0 && hipSetDevice(device) != hipSuccess) return set_last_error(KARMA_E_HIP, "hipSetDevice");
     if (hipGetDevice(&dev) != hipSuccess) return set_last_error(KARMA_E_HIP, "hipGetDevice");
+    karma::engine::PhaseTimer T("wal_append call");
     AppendCtx& C = ctx_for(dev);
     std::lock_guard<std::mutex> lk(C.mu);
     if (const int rc = C.init()) return rc;
@@ -378,6 +405,22 @@ extern "C" int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_o
         size_t m = 1;
         uint64_t bytes = h_len[done];
         uint32_t max_len = h_len[done];
+        // whole runs of kSumRun records while they fit (a loop the compiler vectorises: the
+        // record-by-record form cost ~1 ms per million records), then record by record
+        constexpr size_t kSumRun = 4096;
+        while (done + m + kSumRun <= n) {
+            uint64_t s = 0;
+            uint32_t mx = 0;
+            const uint32_t* l = h_len + done + m;
+            for (size_t k = 0; k < kSumRun; ++k) {
+                s += l[k];
+                mx = std::max(mx, l[k]);
+            }
+            if (bytes + s > kCallBytes) break;
+            bytes += s;
+            max_len = std::max(max_len, mx);
+            m += kSumRun;
+        }
         for (; done + m < n && bytes + h_len[done + m] <= kCallBytes; ++m) {
             bytes += h_len[done + m];
             max_len = std::max(max_len, h_len[done + m]);
@@ -391,5 +434,6 @@ extern "C" int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_o
         *h_n_framed = done;
         if (framed < m) break;  // the image is full (or a record can never fit)
     }
+    T.mark("whole call");
     return 0;
 }
