@@ -80,6 +80,20 @@ std::mutex g_mu;
 std::vector<DevState> g_dev;
 std::map<std::pair<int, void*>, Workspace> g_ws;
 
+// The ragged plan's look-back words per (device, stream) (RaggedArgs::lb, crc_ragged.hip):
+// [0] counts started plan blocks, [1 + b] block b's full-unit status and [1 + half + b] its
+// partial-unit status, tagged with the call's seq.
+// Calls on one stream run in order, so a call sees only its own tag or older ones.  The
+// words are zeroed when allocated and whenever the 22-bit tag wraps.
+struct Lookback {
+    unsigned long long* words = nullptr;
+    uint64_t cap = 0;   // words: 1 + 2 * half
+    uint64_t half = 0;  // plan blocks a call may have
+    uint64_t seq = 0;   // tag of the last call
+    uint64_t ctr = 0;   // value of words[0] after the last call's blocks
+};
+std::map<std::pair<int, void*>, Lookback> g_lb;
+
 int current_device(int* dev) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(KARMA_E_NO_DEVICE, "no HIP device visible");
@@ -161,6 +175,42 @@ int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocate
         w.bytes = want;
     }
     *out = w.ptr;
+    return 0;
+}
+
+// Caller holds g_mu.  Binds this call's look-back words, tag and block-id base for nb
+// plan blocks.
+int bind_lookback(int dev, hipStream_t s, uint64_t nb, RaggedArgs& a) {
+    Lookback& L = g_lb[{dev, (void*)s}];
+    bool clear = false;
+    if (L.half < nb) {
+        if (L.words) {
+            KARMA_HIP(hipStreamSynchronize(s));
+            KARMA_HIP(hipFree(L.words));
+            L.words = nullptr;
+            L.cap = L.half = 0;
+        }
+        const uint64_t half = std::max<uint64_t>(2 * nb, 2048);
+        KARMA_HIP(hipMalloc(&L.words, (1 + 2 * half) * sizeof(unsigned long long)));
+        L.half = half;
+        L.cap = 1 + 2 * half;
+        clear = true;
+    }
+    // (the tools build can lower the wrap point to test it: KARMA_LB_SEQ_MAX, ab.h)
+    const uint64_t seq_max = (uint64_t)KARMA_AB_KNOB("KARMA_LB_SEQ_MAX", 1l << 22);
+    if (++L.seq >= std::min<uint64_t>(seq_max, 1ull << 22)) {
+        L.seq = 1;
+        clear = true;
+    }
+    if (clear) {
+        KARMA_HIP(hipMemsetAsync(L.words, 0, L.cap * sizeof(unsigned long long), s));
+        L.ctr = 0;
+    }
+    a.lb = L.words;
+    a.lbp = L.words + 1 + L.half;
+    a.lb_base = L.ctr;
+    a.lb_seq = (uint32_t)L.seq;
+    L.ctr += nb;
     return 0;
 }
 
@@ -276,7 +326,7 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 
 // ---- ragged records -------------------------------------------------------
 struct RaggedLayout {
-    size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off, total;
+    size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off, tail_off, total;
 };
 
 RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
@@ -288,7 +338,8 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     L.psums_off = L.sums_off + align256(nb * sizeof(uint64_t));
     L.desc_off = L.psums_off + align256(nb * sizeof(uint64_t));
     L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
-    L.total = L.part_off + align256(cap * sizeof(uint32_t));
+    L.tail_off = L.part_off + align256(cap * sizeof(uint32_t));
+    L.total = L.tail_off + align256(cap * sizeof(uint32_t));
     return L;
 }
 
@@ -300,6 +351,7 @@ void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
     a.block_psums = reinterpret_cast<uint64_t*>(b + L.psums_off);
     a.desc = reinterpret_cast<UnitDesc*>(b + L.desc_off);
     a.partial = reinterpret_cast<uint32_t*>(b + L.part_off);
+    a.tailc = reinterpret_cast<uint32_t*>(b + L.tail_off);
     a.unit_cap = cap;
 }
 
@@ -336,18 +388,21 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
     a.blob = ds.blob;
     bind_arena_bounds(a);
     KARMA_RC(comb_blob(ds, kDefaultUnit, &a.comb_blob));
-    uint64_t cap;
+    // the tools build's KARMA_RAGGED_PLAN=2: round 1's two-pass plan (scan + k_ragged_desc)
+    const bool two_pass = KARMA_AB_KNOB("KARMA_RAGGED_PLAN", 1) == 2;
+    // Unit table: full units in [0, cap_full), partial units (at most 2 per record) after them.
+    uint64_t cap_full, cap;
     void* ws = nullptr;
     if (total_len > 0) {
-        cap = 2 * n_rec + ceil_div(total_len, kDefaultUnit);
+        cap_full = std::max<uint64_t>(1, ceil_div(total_len, kDefaultUnit));
+        cap = cap_full + 2 * n_rec;
         const RaggedLayout L = ragged_layout(n_rec, cap);
         KARMA_RC(workspace(dev, s, L.total, &ws));
         bind_ragged(a, ws, L, cap);
-        KARMA_HIP(launch_ragged_scan(a, s));
+        if (two_pass) KARMA_HIP(launch_ragged_scan(a, s));
     } else {
-        // Unknown total: scan, read the block totals back, size the unit table, and scan
-        // again if the workspace had to grow (a new allocation holds none of the results,
-        // even when it lands at the old address).
+        // Unknown total: count the units (k_ragged_scan), read the block totals back and size
+        // the unit table.
         cap = n_rec;
         RaggedLayout L = ragged_layout(n_rec, cap);
         KARMA_RC(workspace(dev, s, L.total, &ws));
@@ -358,16 +413,23 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         KARMA_HIP(hipMemcpyAsync(sums.data(), a.block_sums, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
         KARMA_HIP(hipMemcpyAsync(sums.data() + nb, a.block_psums, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
         KARMA_HIP(hipStreamSynchronize(s));
-        uint64_t units = 0;
-        for (uint64_t v : sums) units += v;
-        cap = std::max<uint64_t>(units, 1);
+        uint64_t full = 0, parts = 0;
+        for (uint64_t i = 0; i < nb; ++i) {
+            full += sums[i];
+            parts += sums[nb + i];
+        }
+        cap_full = std::max<uint64_t>(full, 1);
+        cap = cap_full + parts;
         L = ragged_layout(n_rec, cap);
         bool fresh = false;
         KARMA_RC(workspace(dev, s, L.total, &ws, &fresh));
         bind_ragged(a, ws, L, cap);
-        if (fresh) KARMA_HIP(launch_ragged_scan(a, s));
+        // (a new allocation holds none of the scan's results, even at the old address)
+        if (fresh && two_pass) KARMA_HIP(launch_ragged_scan(a, s));
     }
-    KARMA_HIP(launch_ragged_main(a, ds.cu, s));
+    a.part_base = two_pass ? 0 : cap_full;
+    if (!two_pass) KARMA_RC(bind_lookback(dev, s, ragged_scan_blocks(n_rec), a));
+    KARMA_HIP(launch_ragged_main(a, ds.cu, s, two_pass));
     return 0;
 }
 

@@ -6,12 +6,12 @@
 // body end) so every group of 8 lanes gets at most one unit's worth of work
 // regardless of how skewed the record sizes are:
 //
-//   k_ragged_scan      full units per record -> exclusive scan (record order);
-//                      partial first units -> buckets by chunk count, longest
-//                      first, after all full units
-//   k_ragged_desc      one thread per record: entering register over the
+//   k_ragged_plan      one thread per record, one pass: unit counts, the slots
+//                      of each block of records (a decoupled look-back over the
+//                      blocks' unit counts), the entering register over the
 //                      unaligned head (crc32c.cc:323-329 analogue) and one
 //                      16-byte descriptor {span start, span length, inj} per unit
+//                      (round 1's k_ragged_scan + k_ragged_desc in one launch)
 //   k_units_ragged     the streaming kernel over the descriptor list: every
 //                      wave streams 8 units of (nearly) equal length
 //   k_ragged_finalize  one lane per record: Horner fold of its unit
@@ -110,6 +110,63 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
     return pre + inc - v;
 }
 
+// The unit descriptors of the block's records (one thread per record, every lane of the wave
+// calls this).  fb: the slot of the record's first full unit; cnt: the block's partial-run
+// cursors by chunk count (LDS); full slots at or past full_cap and any slot at or past
+// unit_cap are dropped (a caller's total_len too low: k_ragged_finalize steps those records
+// alone).  The first unit carries the record's init and head offset, the last its tail length
+// (UnitDesc): the plan reads no record bytes.
+__device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool valid, uint64_t r, uint64_t fb,
+                                 unsigned long long* cnt, uint64_t full_cap) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
+    const uint64_t A0 = a >> kUShift;
+    uint32_t init = 0, hoff = 0, t = 0;
+    if (valid) {
+        A.fbase[r] = fb;
+        init = A.init ? A.init[r] : A.init_scalar;
+        hoff = (uint32_t)(reinterpret_cast<uintptr_t>(A.arena + A.off[r]) & 15u);
+        t = (uint32_t)(u.g.e - u.g.b);
+        if (u.part0) {
+            const uint64_t slot = atomicAdd(&cnt[u.c0], 1ull);
+            A.pslot[2 * r] = slot;
+            const uintptr_t e0 = ((A0 + 1) << kUShift) < b ? ((A0 + 1) << kUShift) : b;
+            if (slot < A.unit_cap)
+                A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a) | desc_flags(true, hoff, u.k == 1, t), init};
+        }
+        if (u.part1) {
+            const uint64_t slot = atomicAdd(&cnt[u.c1], 1ull);
+            A.pslot[2 * r + 1] = slot;
+            const uintptr_t s1 = (A0 + u.k - 1) << kUShift;
+            if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1) | desc_flags(false, 0, true, t), 0u};
+        }
+    }
+    // Full units of the wave's 64 records are consecutive slots: the wave writes them together,
+    // lane i taking slot F0 + i and finding its record by a search over the lanes' inclusive
+    // unit counts, so the stores are coalesced and balanced however skewed the record sizes are.
+    const uint64_t nfull = valid ? u.full : 0;
+    const uint64_t incl = wave_incl_scan(nfull);
+    const uint64_t T = __shfl(incl, 63);
+    const uint64_t F0 = __shfl(fb, 0);
+    for (uint64_t base = 0; base < T; base += 64) {  // uniform trip count: shuffles see every lane
+        const uint64_t i = base + lane;
+        int o = 0;  // owner: the first lane whose inclusive count exceeds i
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1)
+            if (__shfl(incl, o + s - 1) <= i) o += s;
+        o = o < 63 ? o : 63;
+        const uint64_t incl_o = __shfl(incl, o), full_o = __shfl(nfull, o), A0_o = __shfl(A0, o), k_o = __shfl(u.k, o);
+        const uint32_t part0_o = __shfl(u.part0, o), part1_o = __shfl(u.part1, o);
+        const uint32_t init_o = __shfl(init, o), hoff_o = __shfl(hoff, o), t_o = __shfl(t, o);
+        const uint64_t j = i - (incl_o - full_o) + part0_o;  // unit index within the owner's record
+        const uint64_t slot = F0 + i;
+        if (i < T && slot < full_cap)
+            A.desc[slot] = UnitDesc{(A0_o + j) << kUShift,
+                                    (uint32_t)kU | desc_flags(j == 0, hoff_o, !part1_o && j + 1 == k_o, t_o),
+                                    j == 0 ? init_o : 0u};
+    }
+}
+
 // Per scan block: exclusive scan of full units (record order), and the
 // block's totals of full and partial units (block_sums / block_psums).
 // k_ragged_desc turns the block totals into slots: full units take [0, F) in
@@ -131,6 +188,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
     }
 }
 
+#ifdef KARMA_AB  // the two-pass plan (k_ragged_scan + k_ragged_desc): tools build, KARMA_RAGGED_PLAN=2
 // Block b's full-unit prefix, its partial-unit prefix and the grand totals,
 // reduced from the scan's block totals by every desc block (nb loads per
 // block: cheaper than another launch or a grid-wide fence).
@@ -177,19 +235,15 @@ __device__ BlockBase block_base(const RaggedArgs& A, uint64_t* sm) {
 // inclusive unit counts, so the descriptor stores are coalesced and balanced
 // however skewed the record sizes are.
 __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
-    KB_SET_ARENA(A.kb_lo, A.kb_hi);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4 then the byte table
     __shared__ unsigned long long cnt[kBuckets];
     __shared__ uint32_t hist[kBuckets];
     __shared__ uint64_t sm[4 * (kScanBlock / 64)];
-    copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
     if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     const BlockBase B = block_base(A, sm);  // has a barrier
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.fbase[A.n_rec] = B.F + B.P;  // total units
         A.fbase[A.n_rec + 1] = B.F;
     }
-    const uint32_t lane = threadIdx.x & 63u;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = r < A.n_rec;
     RecUnits u{};
@@ -207,45 +261,155 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_desc(RaggedArgs A) {
         }
     }
     __syncthreads();
-    uint64_t fb = 0;
-    uint32_t h = 0;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
-    const uint64_t A0 = a >> kUShift;
-    if (valid) {
-        fb = A.fbase[r] + B.full_pre;
-        A.fbase[r] = fb;
-        if (u.k) h = head_register(lds, 0, 1024, A.arena + A.off[r], u.g, A.init ? A.init[r] : A.init_scalar);
-        if (u.part0) {
-            const uint64_t slot = atomicAdd(&cnt[u.c0], 1ull);
-            A.pslot[2 * r] = slot;
-            const uintptr_t e0 = ((A0 + 1) << kUShift) < b ? ((A0 + 1) << kUShift) : b;
-            if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a), h};
-        }
-        if (u.part1) {
-            const uint64_t slot = atomicAdd(&cnt[u.c1], 1ull);
-            A.pslot[2 * r + 1] = slot;
-            const uintptr_t s1 = (A0 + u.k - 1) << kUShift;
-            if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1), 0u};
-        }
-    }
-    // full units of the wave's records, slot F0 + t for t in [0, T)
-    const uint64_t nfull = valid ? u.full : 0;
-    const uint64_t incl = wave_incl_scan(nfull);
-    const uint64_t T = __shfl(incl, 63);
-    const uint64_t F0 = __shfl(fb, 0);
-    for (uint64_t base = 0; base < T; base += 64) {  // uniform trip count: shuffles see every lane
-        const uint64_t t = base + lane;
-        int o = 0;  // owner: the first lane whose inclusive count exceeds t
+    const uint64_t fb = valid ? A.fbase[r] + B.full_pre : 0;
+    write_unit_descs(A, u, valid, r, fb, cnt, A.unit_cap);
+}
+
+#endif  // KARMA_AB
+
+// ---- the single-pass plan ----------------------------------------------------
+// Block status words for the decoupled look-back (RaggedArgs::lb): seq << 42 | flag << 40 |
+// value.  The words are read and written with agent-scope atomics (cache-coherent across
+// the XCDs); nothing else a block writes is read by another block of the same launch, so no
+// release fence is needed (on gfx950 one would write back the XCD's L2).
+constexpr uint64_t kLbValueMask = (1ull << 40) - 1;
+constexpr uint64_t kLbAgg = 1ull << 40, kLbIncl = 2ull << 40;
+
+__device__ __forceinline__ void lb_store(unsigned long long* p, uint64_t v) {
+    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One look-back step for one status array: lane l holds the word of block j - l (blocks
+// before 0: an inclusive total of 0).  Adds the values of lanes 0..k, k the first lane holding
+// an inclusive total (all 64 if none), to excl; true when one was found.
+__device__ __forceinline__ bool lb_take(uint64_t w, uint64_t& excl) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t incl = __ballot(((w >> 40) & 3u) == 2u);
+    const uint32_t k = incl ? (uint32_t)(__ffsll((long long)incl) - 1) : 63u;
+    uint64_t v = lane <= k ? (w & kLbValueMask) : 0;
 #pragma unroll
-        for (int s = 32; s > 0; s >>= 1)
-            if (__shfl(incl, o + s - 1) <= t) o += s;
-        o = o < 63 ? o : 63;
-        const uint64_t incl_o = __shfl(incl, o), full_o = __shfl(nfull, o), A0_o = __shfl(A0, o);
-        const uint32_t part0_o = __shfl(u.part0, o), h_o = __shfl(h, o);
-        const uint64_t j = t - (incl_o - full_o) + part0_o;  // unit index within the owner's record
-        const uint64_t slot = F0 + t;
-        if (t < T && slot < A.unit_cap) A.desc[slot] = UnitDesc{(A0_o + j) << kUShift, (uint32_t)kU, j == 0 ? h_o : 0u};
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+    excl += v;
+    return incl != 0;
+}
+
+__device__ __forceinline__ uint64_t lb_wait(unsigned long long* p, uint32_t seq) {
+    uint64_t w = lb_load(p);
+    while ((w >> 42) != seq) {  // not published yet (this call's tag)
+        __builtin_amdgcn_s_sleep(1);
+        w = lb_load(p);
     }
+    return w;
+}
+
+// Wave 0 of plan block b: publish the block's full and partial unit counts, sum the counts
+// of the blocks before it (64 per step, newest first, each array until the first block that
+// has published its inclusive total there), publish the inclusive totals and return the
+// exclusive ones (uniform).  Every block it waits for has started (ids are taken in start
+// order) and publishes its own counts before waiting on anything, so the wait ends.
+__device__ void lookback(const RaggedArgs& A, uint64_t b, uint64_t full_b, uint64_t part_b, uint64_t& exF,
+                         uint64_t& exP) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t tag = (uint64_t)A.lb_seq << 42;
+    unsigned long long* lf = A.lb + 1;
+    unsigned long long* lp = A.lbp;
+    exF = exP = 0;
+    if (b > 0) {
+        if (lane == 0) {
+            lb_store(lf + b, tag | kLbAgg | full_b);
+            lb_store(lp + b, tag | kLbAgg | part_b);
+        }
+        bool doneF = false, doneP = false;
+        for (int64_t j = (int64_t)b - 1; !(doneF && doneP); j -= 64) {
+            const int64_t i = j - (int64_t)lane;
+            uint64_t wf = tag | kLbIncl, wp = tag | kLbIncl;
+            if (i >= 0) {
+                if (!doneF) wf = lb_wait(lf + i, A.lb_seq);
+                if (!doneP) wp = lb_wait(lp + i, A.lb_seq);
+            }
+            if (!doneF) doneF = lb_take(wf, exF);
+            if (!doneP) doneP = lb_take(wp, exP);
+        }
+    }
+    if (lane == 0) {
+        lb_store(lf + b, tag | kLbIncl | (exF + full_b));
+        lb_store(lp + b, tag | kLbIncl | (exP + part_b));
+    }
+}
+
+// One pass over the records (one thread per record, plan block b = kScanBlock records):
+// unit counts, the slots of the block's units from the look-back, the entering register
+// over each record's unaligned head, and one 16-byte descriptor per unit.  Full units take
+// slots [0, F) in record order; partial units [part_base, part_base + P), each block's run
+// sorted by chunk count, longest first (the two-pass plan's order, which the units kernel
+// streams 3 % faster on configs[2] than block-interleaved runs).  Replaces k_ragged_scan +
+// k_ragged_desc: one launch, and no block reads every other block's totals.
+__global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
+    __shared__ unsigned long long cnt[kBuckets];
+    __shared__ uint32_t hist[kBuckets];
+    __shared__ uint64_t sm[kScanBlock / 64];
+    __shared__ uint64_t s_id, s_fbase;
+    if (threadIdx.x == 0) s_id = atomicAdd(A.lb, 1ull) - A.lb_base;  // ids in start order
+    if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t b = s_id;
+    const uint64_t r = b * kScanBlock + threadIdx.x;
+    const bool valid = r < A.n_rec;
+    RecUnits u{};
+    if (valid) {
+        u = rec_units(A, r);
+        if (u.part0) atomicAdd(&hist[u.c0], 1u);
+        if (u.part1) atomicAdd(&hist[u.c1], 1u);
+    }
+    // full units (high bits) and partial units (low 16 bits: at most 2 per record) in one scan
+    const uint64_t packed = valid ? (u.full << 16) | (u.part0 + u.part1) : 0;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan(packed, sm, tot) >> 16;  // has barriers (hist complete after)
+    const uint64_t full_b = tot >> 16, part_b = tot & 0xffffu;
+    if (threadIdx.x < 64) {
+        uint64_t exF, exP;
+        lookback(A, b, full_b, part_b, exF, exP);
+        if (threadIdx.x == 0) {
+            s_fbase = exF;
+            unsigned long long s = A.part_base + exP;  // the block's partial run, longest bucket first
+            for (int c = kBuckets - 1; c >= 0; --c) {
+                cnt[c] = s;
+                s += hist[c];
+            }
+            if (b + 1 == gridDim.x) {
+                A.fbase[A.n_rec] = exF + full_b + exP + part_b;  // total units
+                A.fbase[A.n_rec + 1] = exF + full_b;             // full units
+            }
+        }
+    }
+    __syncthreads();
+    write_unit_descs(A, u, valid, r, s_fbase + ex, cnt, A.part_base);
+}
+
+// Units of the batch in streaming order: u in [0, U).  Full units are slots [0, F); the
+// partial units follow at part_base (the single-pass plan; 0 = the two-pass plan, whose
+// partial units follow the full ones directly).  Slots past the table (a caller's total_len
+// too low) are left out; k_ragged_finalize steps their records alone.
+struct UnitMap {
+    uint64_t U, Fc, shift;
+    __device__ __forceinline__ uint64_t slot(uint64_t u) const { return u < Fc ? u : u + shift; }
+};
+__device__ __forceinline__ UnitMap unit_map(const RaggedArgs& A) {
+    UnitMap m;
+    const uint64_t all = A.fbase[A.n_rec];
+    if (!A.part_base) {
+        m.U = m.Fc = all < A.unit_cap ? all : A.unit_cap;
+        m.shift = 0;
+    } else {
+        const uint64_t F = A.fbase[A.n_rec + 1], P = all - F, pcap = A.unit_cap - A.part_base;
+        m.Fc = F < A.part_base ? F : A.part_base;
+        m.U = m.Fc + (P < pcap ? P : pcap);
+        m.shift = A.part_base - m.Fc;
+    }
+    return m;
 }
 
 // Descriptor load through address space 1 (global_load_dwordx4, vmcnt only): a
@@ -255,82 +419,88 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
     return UnitDesc{v.x | ((uint64_t)v.y << 32), v.z, v.w};
 }
 
-#ifdef KARMA_AB
-// Pipelined variant (tools build, KARMA_RAGGED_VARIANT=1, ab.h).  Every lane streams its
-// group's units back to back (stream_unit): the descriptor of unit u + 2*step
-// and the first loads of unit u + step are in flight while unit u finishes.
-// Out-of-range groups point at descriptor 0's span (a safe address) and
-// store nothing.
-template <bool BAL = true, int PF = kRaggedPF>
-__global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs A) {
-    KB_SET_ARENA(A.kb_lo, A.kb_hi);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
-    __shared__ uint32_t blk_next;  // BAL: as k_units_ragged, taken two steps ahead
-    if (BAL && threadIdx.x == 0) blk_next = kWavesPerBlock;
-    load_stream_tables(lds, A.blob);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t l = lane & (kGroupLanes - 1);
-    const uint32_t grp = lane / kGroupLanes;
-    const uint32_t X = lane_const();
-    const uint64_t U_all = A.fbase[A.n_rec];
-    const uint64_t U = U_all < A.unit_cap ? U_all : A.unit_cap;  // memory-safe if the caller's bound was low
-    if (U == 0) return;
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
-    const uint32_t nidx = (uint32_t)((nws + nwaves - 1) / nwaves) * kWavesPerBlock;
-    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
-    auto next_of = [&](uint64_t w) -> uint64_t {
-        if constexpr (BAL) {
-            uint32_t i = 0;
-            if (lane == 0) i = atomicAdd(&blk_next, 1u);
-            i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
-            return i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
-        } else {
-            return w < nws ? w + nwaves : nws;
+// Register contribution of one ragged unit (d, UnitDesc) to its record: group_unit's
+// streaming loop, plus the record's edges taken from the lines the unit loads anyway.
+//   head (kDescFirst): the lane whose chunk-0 window is the body's first one loads the
+//     16-byte block before it (the same cache line unless the body starts on a line), steps
+//     ~init over the head bytes and xors the result into the body's first word;
+//   tail (kDescLast): group lane 0 loads the block at the body end (usually in the unit's
+//     last line) and steps a zero register over the tail bytes: *tail = that register, and
+//     the record's CRC is ~(Z_t(R_b) ^ *tail), R_b its register at the body end
+//     (k_ragged_finalize applies Z_t).
+// The edge loads are issued before the body's, at safe addresses when unused, and the edge
+// steps depend on them only, so they run while the body's loads are in flight (vmcnt counts
+// in issue order); the epilogue after the group tree has no extra work.  The results are
+// valid in group lane 0; every lane of the wave must call this.
+template <int PF, bool NT>
+__device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X, uint32_t l, const UnitDesc& d,
+                                                uint32_t& tail) {
+    const uint8_t* us = reinterpret_cast<const uint8_t*>(d.us);
+    const uint8_t* ue = us + (d.span & kDescBytes);
+    const bool first = (d.span & kDescFirst) != 0, last = (d.span & kDescLast) != 0;
+    const uint32_t hoff = (d.span >> 17) & 15u, t = (d.span >> 22) & 15u;
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    uint32_t m = kGroupLanes - 1;
+    tail = 0;
+    if (ue > us) {
+        const uint8_t* base = floor128(us);
+        const int64_t nch = (ue - base + kChunk - 1) / kChunk;
+        m = (uint32_t)((reinterpret_cast<uintptr_t>(ue) - 16) >> 4) & (kGroupLanes - 1);
+        const uint8_t* w = base + 16 * l;
+        const uint8_t* wl = base + (nch - 1) * kChunk + 16 * l;
+        const bool lok = wl < ue;
+        const uint8_t* lclamp = lok ? wl : ue - 16;
+        const bool hl = first && hoff != 0 && w == us;
+        const bool tl = last && t != 0 && l == 0;
+        const u32x4 hv = ld16(hl ? us - 16 : us);
+        const u32x4 tv = ld16(tl ? ue : us);
+        const bool ok = w >= us && w < ue;
+        u32x4 v = ok ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
+        int64_t rem = nch - 1;
+        w += kChunk;
+        u32x4 nb[PF];
+#pragma unroll
+        for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
+        uint32_t h = ~d.inj;
+        if (hl) h = steps_in_vec(lds, kLZ4, kLT8, h, hv, hoff, 16u);
+        if (tl) tail = steps_in_vec(lds, kLZ4, kLT8, 0u, tv, 0u, t);
+        if (first && w - kChunk == us) v.x ^= h;
+        a0 = v.x;
+        a1 = v.y;
+        a2 = v.z;
+        a3 = v.w;
+        while (rem > PF) {
+            u32x4 cur[PF];
+#pragma unroll
+            for (int q = 0; q < PF; ++q) cur[q] = nb[q];
+            w += PF * kChunk;
+#pragma unroll
+            for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
+#pragma unroll
+            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+            rem -= PF;
         }
-    };
-    auto desc_at = [&](uint64_t w) { const uint64_t v = w * kGroupsPerWave + grp; return load_desc(A.desc + (v < U ? v : 0)); };
-    auto unit_of = [&](const UnitDesc& d, uint64_t w) {
-        const uint8_t* us = reinterpret_cast<const uint8_t*>(d.us);
-        return lane_unit(us, w * kGroupsPerWave + grp < U ? us + d.span : us, l);
-    };
-    uint64_t wb = bw0 + (threadIdx.x >> 6);
-    uint64_t wb1 = next_of(wb);
-    UnitDesc d = desc_at(wb);
-    LaneUnit L = unit_of(d, wb);
-    UnitLoads<PF> Ld;
-    issue_unit_loads<PF, kRaggedNT>(L, Ld);
-    UnitDesc dn = desc_at(wb1);
-    while (wb < nws) {
-        // The descriptor two steps ahead is issued with the next unit's loads,
-        // never just before a wait: a load issued ahead of the main loop would
-        // be waited on by the loop's first batch (vmcnt counts in order).
-        UnitDesc dnn;
-        LaneUnit N;
-        uint64_t wb2 = 0;
-        const uint32_t R = stream_unit<PF, kRaggedNT>(lds, X, l, L, Ld, L.us, d.inj, [&](UnitLoads<PF>& nx) {
-            N = unit_of(dn, wb1);
-            wb2 = next_of(wb1);
-            dnn = desc_at(wb2);
-            issue_unit_loads<PF, kRaggedNT>(N, nx);
-        });
-        const uint64_t u = wb * kGroupsPerWave + grp;
-        if (u < U && l == 0) A.partial[u] = R;
-        d = dn;
-        dn = dnn;
-        L = N;
-        wb = wb1;
-        wb1 = wb2;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+            if (q < rem - 1 || (q == rem - 1 && lok)) step4(lds, X, a0, a1, a2, a3, nb[q]);
+        }
     }
+    uint32_t c = lane_fold(lds, a0, a1, a2, a3);
+    const uint32_t lane = threadIdx.x & 63u;
+    c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + m + 1) & (kGroupLanes - 1))), 64);
+    uint32_t t1 = __shfl_down(c, 1, kGroupLanes);
+    c = zmap(lds, kLZ16, c) ^ t1;
+    t1 = __shfl_down(c, 2, kGroupLanes);
+    c = zmap(lds, kLZ32, c) ^ t1;
+    t1 = __shfl_down(c, 4, kGroupLanes);
+    c = zmap(lds, kLZ64, c) ^ t1;
+    return c;
 }
 
-#endif
-
-// The shipped units kernel: each unit's loads are issued when the unit starts
-// (group_unit), the next descriptor is in flight meanwhile.  On config 3 it
-// measures 1% faster than k_units_ragged_pipe, unlike the
-// fixed layout, where the pipelined form wins 2.7%.
+// The units kernel: each unit's loads are issued when the unit starts (ragged_unit), the
+// next descriptor is in flight meanwhile.  (A software-pipelined form, stream_unit's, measured
+// 0.3-0.8 % slower on config 3 in round 2, unlike the fixed layout, where it wins 2.7 %:
+// DESIGN.md §4.)
 // PF = 6 chunk loads in flight per lane (4: config 3 units 0.6736 vs 0.6680 ms, aligned 4 KiB
 // records 0.6656 vs 0.6525; 8: no better than 4 -- profiles/r02_ragged_pf_ab.txt).  With one
 // 1024-thread workgroup per CU (the 145 KiB LDS image) the chunks in flight per CU are what
@@ -347,8 +517,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     const uint32_t l = lane & (kGroupLanes - 1);
     const uint32_t grp = lane / kGroupLanes;
     const uint32_t X = lane_const();
-    const uint64_t U_all = A.fbase[A.n_rec];
-    const uint64_t U = U_all < A.unit_cap ? U_all : A.unit_cap;
+    const UnitMap M = unit_map(A);
+    const uint64_t U = M.U;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     // BAL: as k_units_fixed, the block's wave-steps b*16 + j + r*nwaves are taken in order from
     // an LDS counter, one step ahead (the next descriptor is loaded while a unit streams).
@@ -357,7 +527,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
     uint64_t wb = bw0 + (threadIdx.x >> 6);
     uint64_t u = wb * kGroupsPerWave + grp;
-    UnitDesc d = u < U ? load_desc(A.desc + u) : UnitDesc{0, 0, 0};
+    UnitDesc d = u < U ? load_desc(A.desc + M.slot(u)) : UnitDesc{0, 0, 0};
     while (wb < nws) {
         const UnitDesc cur = d;
         const bool valid = u < U;
@@ -369,10 +539,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
             wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
         }
         const uint64_t un = wb_next * kGroupsPerWave + grp;
-        d = un < U ? load_desc(&KB_READ(A.desc, un, A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
-        const uint8_t* us = reinterpret_cast<const uint8_t*>(cur.us);
-        const uint32_t R = group_unit<PF, kRaggedNT>(lds, X, l, us, us + cur.span, us, cur.inj);
-        if (valid && l == 0) KB_WRITE(A.partial, u, A.unit_cap, kKbUnit, R);
+        d = un < U ? load_desc(&KB_READ(A.desc, M.slot(un), A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
+        uint32_t tail;
+        const uint32_t R = ragged_unit<PF, kRaggedNT>(lds, X, l, cur, tail);
+        if (valid && l == 0) {
+            KB_WRITE(A.partial, M.slot(u), A.unit_cap, kKbUnit, R);
+            if (cur.span & kDescLast) KB_WRITE(A.tailc, M.slot(u), A.unit_cap, kKbUnit, tail);
+        }
         wb = wb_next;
         u = un;
     }
@@ -419,7 +592,8 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
             init = A.init ? A.init[r] : A.init_scalar;
             p = A.arena + A.off[r];
         }
-        const bool ok = valid && fb + u.full <= A.unit_cap && (!u.part0 || ps0 < A.unit_cap) &&
+        const bool ok = valid && fb + u.full <= (A.part_base ? A.part_base : A.unit_cap) &&
+                        (!u.part0 || ps0 < A.unit_cap) &&
                         (!u.part1 || ps1 < A.unit_cap);
         uint32_t acc = 0;
         bool huge = false;
@@ -460,10 +634,13 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
         }
         if (ok && u.k >= 2)  // the last unit: shift by its own length
             acc = shift_last(lds, acc, u.last, U) ^ A.partial[unit_slot(u.k - 1, u.k, fb, ps0, ps1, u.part0, u.part1)];
+        if (ok && u.k > 0 && u.g.e > u.g.b)  // the tail: Z_t, and the tail bytes' register from the units kernel
+            acc = steps_in_vec(lds, kCombZ4, kCombT8, acc, u32x4{0u, 0u, 0u, 0u}, 0u, (uint32_t)(u.g.e - u.g.b)) ^
+                  A.tailc[unit_slot(u.k - 1, u.k, fb, ps0, ps1, u.part0, u.part1)];
         if (valid) {
             uint32_t res;
             if (ok && u.k > 0)
-                res = ~tail_register(lds, kCombZ4, kCombT8, acc, u.g);
+                res = ~acc;
             else  // a short record, or (the caller's total_len was low) one whose units did not
                   // fit the table: this lane steps it alone -- slow, but never a wrong CRC
                 res = short_record(lds, kCombZ4, kCombT8, p, A.len[r], init);
@@ -788,24 +965,25 @@ hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
+hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool two_pass) {
     if (a.n_rec == 0) return hipSuccess;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
-    hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+#ifdef KARMA_AB
+    if (two_pass)
+        hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);  // after launch_ragged_scan
+    else
+#endif
+    {
+        if (two_pass || !a.lb || a.lb_seq == 0 || a.lb_seq >= (1u << 22)) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_ragged_plan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+    }
     units_timer_begin(s);
-#ifdef KARMA_AB  // tools build (ab.h): 1 = pipelined, 2 = static wave-steps, 3 = both, 4 / 8 = chunks in
-                 // flight, 16 = pipelined with 6 in flight
+#ifdef KARMA_AB  // tools build (ab.h): 2 = static wave-steps, 4 / 8 = chunks in flight
     const long v = KARMA_AB_KNOB("KARMA_RAGGED_VARIANT", 0);
     if (v == 4)
         hipLaunchKernelGGL((k_units_ragged<true, 4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 8)
         hipLaunchKernelGGL((k_units_ragged<true, 8>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
-    else if (v == 16)
-        hipLaunchKernelGGL((k_units_ragged_pipe<true, 6>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
-    else if (v == 1)
-        hipLaunchKernelGGL(k_units_ragged_pipe<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
-    else if (v == 3)
-        hipLaunchKernelGGL(k_units_ragged_pipe<false>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 2)
         hipLaunchKernelGGL(k_units_ragged<false>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else

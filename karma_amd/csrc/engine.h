@@ -83,20 +83,32 @@ struct FixedArgs {
 };
 
 // One unit of a ragged batch: the 16-aligned span [us, us + span) of a record
-// body and the value xored into its first word (the record's entering
-// register for the record's first unit, 0 otherwise).
+// body and what the units kernel does at the record's edges, so that no other
+// kernel reads record bytes (the head and tail blocks share the unit's first and
+// last cache lines, or the neighbouring ones):
+//   kDescFirst (the record's first unit): the record starts hoff bytes into the
+//     16-byte block before us (hoff 0: at us); the register entering the body is
+//     ~init stepped over those head bytes, xored into the body's first word.
+//   kDescLast (the record's last unit): the record ends t bytes after us + span;
+//     the units kernel also steps a zero register over those tail bytes (tailc).
 struct UnitDesc {
     uint64_t us;
-    uint32_t span;
-    uint32_t inj;
+    uint32_t span;  // bytes (low 16 bits) | kDescFirst | hoff << 17 | kDescLast | t << 22
+    uint32_t inj;   // init (kDescFirst), else 0
 };
 static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
+constexpr uint32_t kDescBytes = 0xffffu;
+constexpr uint32_t kDescFirst = 1u << 16;
+constexpr uint32_t kDescLast = 1u << 21;
+constexpr uint32_t desc_flags(bool first, uint32_t hoff, bool last, uint32_t t) {
+    return (first ? kDescFirst | (hoff << 17) : 0u) | (last ? kDescLast | (t << 22) : 0u);
+}
 
 // Ragged batches cut record bodies at absolute unit_bytes boundaries (so full
-// units are 4 KiB-aligned and every chunk is a whole cache line) and order the
+// units are unit-aligned and every chunk is a whole cache line) and order the
 // units for balance: all full units first, in record order, then
-// the partial first/last units bucketed by chunk count, longest first, so the
-// 8 units a wave streams together have (nearly) equal length.
+// each block's partial first/last units bucketed by chunk count, longest first,
+// so the 8 units a wave streams together have (nearly) equal length.
 constexpr int kBuckets = 65;  // chunk counts 1..64 of a partial unit (index = chunks)
 static_assert(kDefaultUnit / kChunk < kBuckets, "a partial unit has at most unit/kChunk chunks");
 
@@ -113,10 +125,22 @@ struct RaggedArgs {
     uint64_t* pslot;           // 2 * n_rec: slots of the record's partial first / last unit
     uint64_t* block_sums;      // per scan block: full-unit offset
     uint64_t* block_psums;     // per scan block: partial units, then the block's first partial slot
+    // Single-pass plan (k_ragged_plan): decoupled look-back over per-block status words.
+    // lb[0] counts the blocks that started (plan-block ids in start order, from lb_base on);
+    // lb[1 + b] = seq << 42 | flag << 40 | value (flag 1: block b's own full-unit count, 2:
+    // the full units of blocks 0..b); lbp[b] the same for partial units.  lb_seq (1 .. 2^22 - 1) tags this call's words (capi.cc).
+    unsigned long long* lb;
+    unsigned long long* lbp;   // the same for the blocks' partial unit counts
+    uint64_t lb_base;
+    uint32_t lb_seq;
     UnitDesc* desc;            // unit_cap entries
     uint64_t unit_cap;         // capacity of desc / partial
+    uint64_t part_base;        // single-pass plan: first slot of the partial units (full units
+                               //   take [0, part_base)); 0: the two-pass plan (partial units
+                               //   follow the full ones)
     uint32_t* out;
     uint32_t* partial;         // register contribution per unit slot
+    uint32_t* tailc;           // per unit slot of a record's last unit: its tail bytes' register
     const uint32_t* blob;      // stream blob (kBlobWords)
     const uint32_t* comb_blob; // kCombWords for unit_bytes
     uintptr_t kb_lo, kb_hi;    // bounds build only: the arena's allocation (bounds.h); else 0
@@ -150,10 +174,13 @@ hipError_t launch_combine_block(const FixedArgs& a, const uint32_t* in_states, u
 #endif
 constexpr int kScanBlock = KARMA_SCAN_BLOCK;
 inline uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock - 1) / kScanBlock; }
-// Ragged: scan (full-unit offsets + partial-unit buckets; total units at
-// fbase[n_rec]), then descriptors, the unit kernel and the per-record finalize.
+// Ragged: the plan (one pass: unit slots, descriptors and the entering registers; total
+// units at fbase[n_rec]), then the unit kernel and the per-record finalize.
+// launch_ragged_scan only counts units (block_sums / block_psums), for callers that must size
+// the unit table first.  two_pass (tools build only): scan + k_ragged_desc instead of the
+// single-pass plan.
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
-hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s);
+hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool two_pass = false);
 // One record per group of 4 lanes, no plan kernels (uses arena, off, len, n_rec, init, out, and
 // blob = build_quad_blob's; the tools build's KARMA_DIRECT_VARIANT picks the alternatives).
 hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s);

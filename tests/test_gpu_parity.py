@@ -315,7 +315,8 @@ def test_rejects_bad_arguments(dev):
 
 
 @pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", v) for v in "127"] +
-                         [("KARMA_RAGGED_VARIANT", v) for v in "123"] + [("KARMA_FOLD_MAX_K", "1")])
+                         [("KARMA_RAGGED_VARIANT", v) for v in "248"] + [("KARMA_FOLD_MAX_K", "1")] +
+                         [("KARMA_RAGGED_PLAN", "2")])
 def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
     """The A/B kernels of the tools build (karma_amd/csrc/ab.h, tools/variant_bench.py) are held to
     the same parity as the shipped ones."""
@@ -341,6 +342,35 @@ def _variants_match_oracle(raw, dev):
     d_ini = torch.from_numpy(ini.astype(np.uint32).view(np.int32)).to(dev)
     got = K.extend_batch_ragged(dbuf[:arena], d_off, d_len, init=d_ini, total_len=int(lens.sum())).cpu().numpy()
     _eq(got, oracle_lib.ragged_crcs(host, offs, lens, ini.astype(np.uint32)))
+
+
+@pytest.mark.parametrize("build", ["shipped", "tag_wrap"])
+def test_ragged_plan_many_blocks_lookback(raw, dev, build, monkeypatch):
+    """The single-pass plan (k_ragged_plan) chains its blocks' unit counts by a decoupled
+    look-back: 2M records = 2048 plan blocks, alternating with small batches on one stream, so
+    every call's status words overwrite older ones.  tag_wrap: the tools build with the 22-bit
+    call tag wrapping every 2 calls (KARMA_LB_SEQ_MAX), so the words are cleared between calls."""
+    host, dbuf = raw
+    rng = np.random.default_rng(21)
+    big = rng.integers(32, 300, 2 << 20).astype(np.uint32)
+    big_off = rng.integers(0, host.size - 300, big.size).astype(np.uint64)
+    small = rng.integers(0, 40000, 3000).astype(np.uint32)
+    small_off = rng.integers(0, host.size - 40000, small.size).astype(np.uint64)
+    want_big = oracle_lib.ragged_crcs(host, big_off, big)
+    want_small = oracle_lib.ragged_crcs(host, small_off, small)
+    cases = [(big, big_off, want_big), (small, small_off, want_small)]
+    dl = [(torch.from_numpy(o.astype(np.int64)).to(dev), torch.from_numpy(n.astype(np.int32)).to(dev)) for n, o, _ in cases]
+    if build == "tag_wrap":
+        monkeypatch.setenv("KARMA_LB_SEQ_MAX", "3")
+        ctx = _lib.using(_lib.AB_LIB_PATH)
+    else:
+        ctx = contextlib.nullcontext()
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with ctx, torch.cuda.stream(s):
+        for i in range(7):
+            (n, o, want), (d_off, d_len) = cases[i % 2], dl[i % 2]
+            _eq(K.extend_batch_ragged(dbuf, d_off, d_len, total_len=int(n.sum())).cpu().numpy(), want)
 
 
 def test_ragged_unknown_total_workspace_growth(raw, dev):
