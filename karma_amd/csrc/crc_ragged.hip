@@ -116,8 +116,12 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
 // unit_cap are dropped (a caller's total_len too low: k_ragged_finalize steps those records
 // alone).  The first unit carries the record's init and head offset, the last its tail length
 // (UnitDesc): the plan reads no record bytes.
+// (EP, the tools build's KARMA_RAGGED_EDGES=1: round 2's first form, the entering register h
+// stepped here from the record's head bytes and stored as inj, no edge flags; the tail is then
+// finalize's.)
+template <bool EP = false>
 __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool valid, uint64_t r, uint64_t fb,
-                                 unsigned long long* cnt, uint64_t full_cap) {
+                                 unsigned long long* cnt, uint64_t full_cap, uint32_t h = 0) {
     const uint32_t lane = threadIdx.x & 63u;
     const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
     const uint64_t A0 = a >> kUShift;
@@ -127,18 +131,23 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
         init = A.init ? A.init[r] : A.init_scalar;
         hoff = (uint32_t)(reinterpret_cast<uintptr_t>(A.arena + A.off[r]) & 15u);
         t = (uint32_t)(u.g.e - u.g.b);
+        if (EP) {
+            init = h;
+            hoff = t = 0;
+        }
         if (u.part0) {
             const uint64_t slot = atomicAdd(&cnt[u.c0], 1ull);
             A.pslot[2 * r] = slot;
             const uintptr_t e0 = ((A0 + 1) << kUShift) < b ? ((A0 + 1) << kUShift) : b;
             if (slot < A.unit_cap)
-                A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a) | desc_flags(true, hoff, u.k == 1, t), init};
+                A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a) | (EP ? 0u : desc_flags(true, hoff, u.k == 1, t)), init};
         }
         if (u.part1) {
             const uint64_t slot = atomicAdd(&cnt[u.c1], 1ull);
             A.pslot[2 * r + 1] = slot;
             const uintptr_t s1 = (A0 + u.k - 1) << kUShift;
-            if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1) | desc_flags(false, 0, true, t), 0u};
+            if (slot < A.unit_cap)
+                A.desc[slot] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1) | (EP ? 0u : desc_flags(false, 0, true, t)), 0u};
         }
     }
     // Full units of the wave's 64 records are consecutive slots: the wave writes them together,
@@ -162,7 +171,7 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
         const uint64_t slot = F0 + i;
         if (i < T && slot < full_cap)
             A.desc[slot] = UnitDesc{(A0_o + j) << kUShift,
-                                    (uint32_t)kU | desc_flags(j == 0, hoff_o, !part1_o && j + 1 == k_o, t_o),
+                                    (uint32_t)kU | (EP ? 0u : desc_flags(j == 0, hoff_o, !part1_o && j + 1 == k_o, t_o)),
                                     j == 0 ? init_o : 0u};
     }
 }
@@ -306,7 +315,7 @@ __device__ __forceinline__ uint64_t lb_wait(unsigned long long* p, uint32_t seq)
 }
 
 // Wave 0 of plan block b: publish the block's full and partial unit counts, sum the counts
-// of the blocks before it (64 per step, newest first, each array until the first block that
+// of the blocks before it (256 per step, newest first, each array until the first block that
 // has published its inclusive total there), publish the inclusive totals and return the
 // exclusive ones (uniform).  Every block it waits for has started (ids are taken in start
 // order) and publishes its own counts before waiting on anything, so the wait ends.
@@ -322,16 +331,34 @@ __device__ void lookback(const RaggedArgs& A, uint64_t b, uint64_t full_b, uint6
             lb_store(lf + b, tag | kLbAgg | full_b);
             lb_store(lp + b, tag | kLbAgg | part_b);
         }
+        // 256 blocks per step: every lane's 4 loads go out together (an inclusive total
+        // travels back 256 blocks per memory round trip instead of 64), then the windows are
+        // taken nearest first; a word is waited for only if its window is reached.
+        constexpr int kLbWin = 4;
         bool doneF = false, doneP = false;
-        for (int64_t j = (int64_t)b - 1; !(doneF && doneP); j -= 64) {
-            const int64_t i = j - (int64_t)lane;
-            uint64_t wf = tag | kLbIncl, wp = tag | kLbIncl;
-            if (i >= 0) {
-                if (!doneF) wf = lb_wait(lf + i, A.lb_seq);
-                if (!doneP) wp = lb_wait(lp + i, A.lb_seq);
+        for (int64_t j = (int64_t)b - 1; !(doneF && doneP); j -= 64 * kLbWin) {
+            uint64_t wf[kLbWin], wp[kLbWin];
+#pragma unroll
+            for (int q = 0; q < kLbWin; ++q) {
+                const int64_t i = j - (int64_t)lane - 64 * q;
+                wf[q] = wp[q] = tag | kLbIncl;  // before block 0: an inclusive total of 0
+                if (i >= 0) {
+                    if (!doneF) wf[q] = lb_load(lf + i);
+                    if (!doneP) wp[q] = lb_load(lp + i);
+                }
             }
-            if (!doneF) doneF = lb_take(wf, exF);
-            if (!doneP) doneP = lb_take(wp, exP);
+#pragma unroll
+            for (int q = 0; q < kLbWin; ++q) {
+                const int64_t i = j - (int64_t)lane - 64 * q;
+                if (!doneF) {
+                    if (i >= 0 && (wf[q] >> 42) != A.lb_seq) wf[q] = lb_wait(lf + i, A.lb_seq);
+                    doneF = lb_take(wf[q], exF);
+                }
+                if (!doneP) {
+                    if (i >= 0 && (wp[q] >> 42) != A.lb_seq) wp[q] = lb_wait(lp + i, A.lb_seq);
+                    doneP = lb_take(wp[q], exP);
+                }
+            }
         }
     }
     if (lane == 0) {
@@ -347,12 +374,16 @@ __device__ void lookback(const RaggedArgs& A, uint64_t b, uint64_t full_b, uint6
 // sorted by chunk count, longest first (the two-pass plan's order, which the units kernel
 // streams 3 % faster on configs[2] than block-interleaved runs).  Replaces k_ragged_scan +
 // k_ragged_desc: one launch, and no block reads every other block's totals.
+template <bool EP = false>
 __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[EP ? kCombCoreWords - kCombZ4 : 4];  // EP: Z4, byte table
     __shared__ unsigned long long cnt[kBuckets];
     __shared__ uint32_t hist[kBuckets];
     __shared__ uint64_t sm[kScanBlock / 64];
     __shared__ uint64_t s_id, s_fbase;
     if (threadIdx.x == 0) s_id = atomicAdd(A.lb, 1ull) - A.lb_base;  // ids in start order
+    if constexpr (EP) copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
     if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t b = s_id;
@@ -385,8 +416,10 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
             }
         }
     }
+    uint32_t h = 0;
+    if (EP && valid && u.k) h = head_register(lds, 0, 1024, A.arena + A.off[r], u.g, A.init ? A.init[r] : A.init_scalar);
     __syncthreads();
-    write_unit_descs(A, u, valid, r, s_fbase + ex, cnt, A.part_base);
+    write_unit_descs<EP>(A, u, valid, r, s_fbase + ex, cnt, A.part_base, h);
 }
 
 // Units of the batch in streaming order: u in [0, U).  Full units are slots [0, F); the
@@ -424,17 +457,18 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
 //   head (kDescFirst): the lane whose chunk-0 window is the body's first one loads the
 //     16-byte block before it (the same cache line unless the body starts on a line), steps
 //     ~init over the head bytes and xors the result into the body's first word;
-//   tail (kDescLast): group lane 0 loads the block at the body end (usually in the unit's
-//     last line) and steps a zero register over the tail bytes: *tail = that register, and
+//   tail (kDescLast): the lane 4 further loads the block at the body end (usually in the
+//     unit's last line) and steps a zero register over the tail bytes: tail (valid where
+//     tail_here) = that register, and
 //     the record's CRC is ~(Z_t(R_b) ^ *tail), R_b its register at the body end
 //     (k_ragged_finalize applies Z_t).
-// The edge loads are issued before the body's, at safe addresses when unused, and the edge
+// The edge loads are issued before the body's, by the lanes that need them, and the edge
 // steps depend on them only, so they run while the body's loads are in flight (vmcnt counts
-// in issue order); the epilogue after the group tree has no extra work.  The results are
+// in issue order); the epilogue after the group tree has no extra work.  The contribution is
 // valid in group lane 0; every lane of the wave must call this.
 template <int PF, bool NT>
 __device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X, uint32_t l, const UnitDesc& d,
-                                                uint32_t& tail) {
+                                                uint32_t& tail, bool& tail_here) {
     const uint8_t* us = reinterpret_cast<const uint8_t*>(d.us);
     const uint8_t* ue = us + (d.span & kDescBytes);
     const bool first = (d.span & kDescFirst) != 0, last = (d.span & kDescLast) != 0;
@@ -442,18 +476,26 @@ __device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X,
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     uint32_t m = kGroupLanes - 1;
     tail = 0;
+    tail_here = false;
     if (ue > us) {
         const uint8_t* base = floor128(us);
         const int64_t nch = (ue - base + kChunk - 1) / kChunk;
         m = (uint32_t)((reinterpret_cast<uintptr_t>(ue) - 16) >> 4) & (kGroupLanes - 1);
         const uint8_t* w = base + 16 * l;
+        const uint8_t* const w0 = w;  // this lane's chunk-0 window
         const uint8_t* wl = base + (nch - 1) * kChunk + 16 * l;
         const bool lok = wl < ue;
         const uint8_t* lclamp = lok ? wl : ue - 16;
-        const bool hl = first && hoff != 0 && w == us;
-        const bool tl = last && t != 0 && l == 0;
-        const u32x4 hv = ld16(hl ? us - 16 : us);
-        const u32x4 tv = ld16(tl ? ue : us);
+        // One lane per edge, and never the same one: the head lane holds the body's first
+        // window, the tail lane sits 4 lanes further, so one load and one (divergent) step
+        // loop serve both edges.  (Lane-masked: an unmasked load at a safe address costs every
+        // lane a 16-byte request per unit, 2.5 % of the kernel on 4 KiB records.)
+        const uint32_t lh = (uint32_t)(reinterpret_cast<uintptr_t>(us) >> 4) & (kGroupLanes - 1);
+        const bool hl = first && hoff != 0 && l == lh;
+        const bool tl = last && t != 0 && l == ((lh + kGroupLanes / 2) & (kGroupLanes - 1));
+        tail_here = tl;
+        u32x4 ev = {0u, 0u, 0u, 0u};
+        if (hl || tl) ev = ld16(hl ? us - 16 : ue);
         const bool ok = w >= us && w < ue;
         u32x4 v = ok ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
         int64_t rem = nch - 1;
@@ -461,25 +503,41 @@ __device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X,
         u32x4 nb[PF];
 #pragma unroll
         for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
-        uint32_t h = ~d.inj;
-        if (hl) h = steps_in_vec(lds, kLZ4, kLT8, h, hv, hoff, 16u);
-        if (tl) tail = steps_in_vec(lds, kLZ4, kLT8, 0u, tv, 0u, t);
-        if (first && w - kChunk == us) v.x ^= h;
-        a0 = v.x;
-        a1 = v.y;
-        a2 = v.z;
-        a3 = v.w;
-        while (rem > PF) {
+        // The edge steps and chunk 0's registers are taken after the next batch's loads are
+        // issued: waiting for chunk 0 (or an edge block) before that issue would leave one
+        // batch fewer in flight at every unit start (measured: 1.7 % on 4 KiB records).
+        auto edges = [&]() {
+            uint32_t r = hl ? ~d.inj : 0u;
+            if (hl || tl) r = steps_in_vec(lds, kLZ4, kLT8, r, ev, hl ? hoff : 0u, hl ? 16u : t);
+            if (tl) tail = r;
+            if (first && w0 == us) v.x ^= hl ? r : ~d.inj;
+            a0 = v.x;
+            a1 = v.y;
+            a2 = v.z;
+            a3 = v.w;
+        };
+        auto batch = [&]() {  // step the PF chunks in flight, with the next PF issued first
             u32x4 cur[PF];
 #pragma unroll
             for (int q = 0; q < PF; ++q) cur[q] = nb[q];
             w += PF * kChunk;
 #pragma unroll
             for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
+            return [&, cur]() {
 #pragma unroll
-            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
-            rem -= PF;
+                for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+                rem -= PF;
+            };
+        };
+        if (rem > PF) {  // the first batch, peeled: the edges go between its issue and its steps
+            auto steps = batch();
+            __builtin_amdgcn_sched_barrier(0);
+            edges();
+            steps();
+        } else {
+            edges();
         }
+        while (rem > PF) batch()();
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
             if (q < rem - 1 || (q == rem - 1 && lok)) step4(lds, X, a0, a1, a2, a3, nb[q]);
@@ -505,7 +563,7 @@ __device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X,
 // records 0.6656 vs 0.6525; 8: no better than 4 -- profiles/r02_ragged_pf_ab.txt).  With one
 // 1024-thread workgroup per CU (the 145 KiB LDS image) the chunks in flight per CU are what
 // keeps HBM busy across the unit boundaries this kernel does not pipeline.
-template <bool BAL = true, int PF = kRaggedUnitsPF>
+template <bool BAL = true, int PF = kRaggedUnitsPF, bool EP = false>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
@@ -540,12 +598,16 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
         }
         const uint64_t un = wb_next * kGroupsPerWave + grp;
         d = un < U ? load_desc(&KB_READ(A.desc, M.slot(un), A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
-        uint32_t tail;
-        const uint32_t R = ragged_unit<PF, kRaggedNT>(lds, X, l, cur, tail);
-        if (valid && l == 0) {
-            KB_WRITE(A.partial, M.slot(u), A.unit_cap, kKbUnit, R);
-            if (cur.span & kDescLast) KB_WRITE(A.tailc, M.slot(u), A.unit_cap, kKbUnit, tail);
+        uint32_t tail = 0, R;
+        bool tail_here = false;
+        if constexpr (EP) {
+            const uint8_t* us = reinterpret_cast<const uint8_t*>(cur.us);
+            R = group_unit<PF, kRaggedNT>(lds, X, l, us, us + cur.span, us, cur.inj);
+        } else {
+            R = ragged_unit<PF, kRaggedNT>(lds, X, l, cur, tail, tail_here);
         }
+        if (valid && l == 0) KB_WRITE(A.partial, M.slot(u), A.unit_cap, kKbUnit, R);
+        if (valid && tail_here) KB_WRITE(A.tailc, M.slot(u), A.unit_cap, kKbUnit, tail);
         wb = wb_next;
         u = un;
     }
@@ -568,6 +630,7 @@ __device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, 
 // One lane per record: Horner fold of the unit contributions (Z_U between unit
 // ends, Z_last before the last unit), the unaligned tail, ~R.  Records of more
 // than 64 units: the whole wave folds all but the last unit with the 64-lane tree.
+template <bool EP = false>
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombWords];
@@ -634,7 +697,9 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
         }
         if (ok && u.k >= 2)  // the last unit: shift by its own length
             acc = shift_last(lds, acc, u.last, U) ^ A.partial[unit_slot(u.k - 1, u.k, fb, ps0, ps1, u.part0, u.part1)];
-        if (ok && u.k > 0 && u.g.e > u.g.b)  // the tail: Z_t, and the tail bytes' register from the units kernel
+        if (EP && ok && u.k > 0)
+            acc = tail_register(lds, kCombZ4, kCombT8, acc, u.g);
+        else if (ok && u.k > 0 && u.g.e > u.g.b)  // the tail: Z_t, and the tail bytes' register from the units kernel
             acc = steps_in_vec(lds, kCombZ4, kCombT8, acc, u32x4{0u, 0u, 0u, 0u}, 0u, (uint32_t)(u.g.e - u.g.b)) ^
                   A.tailc[unit_slot(u.k - 1, u.k, fb, ps0, ps1, u.part0, u.part1)];
         if (valid) {
@@ -968,6 +1033,8 @@ hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool two_pass) {
     if (a.n_rec == 0) return hipSuccess;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
+    // the tools build's KARMA_RAGGED_EDGES=1: head register in the plan, tail in finalize
+    const bool edges_in_plan = KARMA_AB_KNOB("KARMA_RAGGED_EDGES", 0) == 1 && !two_pass;
 #ifdef KARMA_AB
     if (two_pass)
         hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);  // after launch_ragged_scan
@@ -975,12 +1042,19 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
 #endif
     {
         if (two_pass || !a.lb || a.lb_seq == 0 || a.lb_seq >= (1u << 22)) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_ragged_plan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+#ifdef KARMA_AB
+        if (edges_in_plan)
+            hipLaunchKernelGGL(k_ragged_plan<true>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+        else
+#endif
+            hipLaunchKernelGGL(k_ragged_plan<false>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     }
     units_timer_begin(s);
 #ifdef KARMA_AB  // tools build (ab.h): 2 = static wave-steps, 4 / 8 = chunks in flight
     const long v = KARMA_AB_KNOB("KARMA_RAGGED_VARIANT", 0);
-    if (v == 4)
+    if (edges_in_plan)
+        hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 4)
         hipLaunchKernelGGL((k_units_ragged<true, 4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 8)
         hipLaunchKernelGGL((k_units_ragged<true, 8>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
@@ -993,7 +1067,12 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
     const uint64_t cap = 2 * (uint64_t)grid_blocks;
     if (fblocks > cap) fblocks = cap;
-    hipLaunchKernelGGL(k_ragged_finalize, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
+#ifdef KARMA_AB
+    if (edges_in_plan)
+        hipLaunchKernelGGL(k_ragged_finalize<true>, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
+    else
+#endif
+        hipLaunchKernelGGL(k_ragged_finalize<false>, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

@@ -20,6 +20,10 @@ import synth  # noqa: E402
 
 LIBS = {"head": _lib.load(os.path.join(ROOT, "build", "head", "karma_amd", "lib", "libkarma_crc32c.so")),
         "new": _lib.load(_lib.LIB_PATH)}
+ENV = {v: {} for v in LIBS}
+if os.environ.get("WITH_EDGES_IN_PLAN", "1") == "1":  # the tools build: head register in the plan, tail in finalize
+    LIBS["edges-in-plan"] = _lib.load(_lib.AB_LIB_PATH)
+    ENV["edges-in-plan"] = {"KARMA_RAGGED_EDGES": "1"}
 dev = torch.device("cuda:0")
 GB = 4 << 30
 RAW = GB + (64 << 20)
@@ -39,6 +43,10 @@ def ragged_case(lens, offs):
     outs = {v: torch.empty(n, dtype=torch.uint32, device=dev) for v in LIBS}
 
     def run(v):
+        os.environ.update(ENV[v])
+        for k in ("KARMA_RAGGED_EDGES",):
+            if k not in ENV[v]:
+                os.environ.pop(k, None)
         _lib.check("ragged", LIBS[v].karma_crc32c_batch_ragged(raw.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n,
                                                                 total, None, 0, outs[v].data_ptr(), sh))
     return run, total, outs
@@ -96,5 +104,5 @@ for name, (run, nbytes, outs) in cases.items():
     for v in names:
         c, u = np.median(res[(name, v)][0]), np.median(res[(name, v)][1])
         line += f" | {v}: call {c:.4f} ms ({nbytes / c / 8e9:.3f} of 8 TB/s) units {u:.4f}"
-    c0, c1 = (np.median(res[(name, v)][0]) for v in names)
-    print(line + f" | call {100 * (c0 - c1) / c0:+.1f} %", flush=True)
+    c0, c1 = (np.median(res[(name, v)][0]) for v in names[:2])
+    print(line + f" | new vs head: call {100 * (c0 - c1) / c0:+.1f} %", flush=True)
