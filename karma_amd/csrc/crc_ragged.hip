@@ -457,9 +457,9 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
 //   head (kDescFirst): the lane whose chunk-0 window is the body's first one loads the
 //     16-byte block before it (the same cache line unless the body starts on a line), steps
 //     ~init over the head bytes and xors the result into the body's first word;
-//   tail (kDescLast): the lane 4 further loads the block at the body end (usually in the
-//     unit's last line) and steps a zero register over the tail bytes: tail (valid where
-//     tail_here) = that register, and
+//   tail (kDescLast): group lane 0 loads the block at the body end (usually in the unit's
+//     last line) and steps a zero register over the tail bytes: tail (valid where tail_here)
+//     = that register, and
 //     the record's CRC is ~(Z_t(R_b) ^ *tail), R_b its register at the body end
 //     (k_ragged_finalize applies Z_t).
 // The edge loads are issued before the body's, by the lanes that need them, and the edge
@@ -486,16 +486,17 @@ __device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X,
         const uint8_t* wl = base + (nch - 1) * kChunk + 16 * l;
         const bool lok = wl < ue;
         const uint8_t* lclamp = lok ? wl : ue - 16;
-        // One lane per edge, and never the same one: the head lane holds the body's first
-        // window, the tail lane sits 4 lanes further, so one load and one (divergent) step
-        // loop serve both edges.  (Lane-masked: an unmasked load at a safe address costs every
-        // lane a 16-byte request per unit, 2.5 % of the kernel on 4 KiB records.)
-        const uint32_t lh = (uint32_t)(reinterpret_cast<uintptr_t>(us) >> 4) & (kGroupLanes - 1);
-        const bool hl = first && hoff != 0 && l == lh;
-        const bool tl = last && t != 0 && l == ((lh + kGroupLanes / 2) & (kGroupLanes - 1));
+        // The head lane holds the body's first window, the tail lane is group lane 0.  (Putting
+        // the tail 4 lanes from the head, so that one load and one divergent step loop serve
+        // both edges, measured slower: 0.821 vs 0.797 ms units on 1-1.5 KiB records.  The loads
+        // are lane-masked: an unmasked pair at safe addresses costs every lane two 16-byte
+        // requests per unit, 2.5 % of the kernel on 4 KiB records.)
+        const bool hl = first && hoff != 0 && w == us;
+        const bool tl = last && t != 0 && l == 0;
         tail_here = tl;
-        u32x4 ev = {0u, 0u, 0u, 0u};
-        if (hl || tl) ev = ld16(hl ? us - 16 : ue);
+        u32x4 hv = {0u, 0u, 0u, 0u}, tv = {0u, 0u, 0u, 0u};
+        if (hl) hv = ld16(us - 16);
+        if (tl) tv = ld16(ue);
         const bool ok = w >= us && w < ue;
         u32x4 v = ok ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
         int64_t rem = nch - 1;
@@ -507,10 +508,10 @@ __device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X,
         // issued: waiting for chunk 0 (or an edge block) before that issue would leave one
         // batch fewer in flight at every unit start (measured: 1.7 % on 4 KiB records).
         auto edges = [&]() {
-            uint32_t r = hl ? ~d.inj : 0u;
-            if (hl || tl) r = steps_in_vec(lds, kLZ4, kLT8, r, ev, hl ? hoff : 0u, hl ? 16u : t);
-            if (tl) tail = r;
-            if (first && w0 == us) v.x ^= hl ? r : ~d.inj;
+            uint32_t h = ~d.inj;
+            if (hl) h = steps_in_vec(lds, kLZ4, kLT8, h, hv, hoff, 16u);
+            if (tl) tail = steps_in_vec(lds, kLZ4, kLT8, 0u, tv, 0u, t);
+            if (first && w0 == us) v.x ^= h;
             a0 = v.x;
             a1 = v.y;
             a2 = v.z;
