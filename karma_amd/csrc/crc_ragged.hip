@@ -32,6 +32,12 @@ using namespace dev;
 constexpr int kRaggedPF = 4;       // chunk loads in flight per lane: small-record and pipelined kernels
 constexpr int kRaggedUnitsPF = 6;  // ... and the shipped units kernel (k_units_ragged)
 constexpr bool kRaggedNT = true;
+// Where a ragged record's unaligned head and tail bytes are stepped (the EM template argument of
+// k_ragged_plan / k_units_ragged / k_ragged_finalize): bit 0 = the head in the plan, bit 1 = the
+// tail in finalize; 0 = both in the units kernel (ragged_unit, from the lines it loads).  3 is
+// shipped: the units-kernel form saves the plan and finalize 15 us of scattered reads on
+// configs[2] but costs the units kernel as much.
+constexpr int kShipEM = 3;
 
 static_assert(kScanBlock % 64 == 0 && kScanBlock <= 1024 && kScanBlock >= kBuckets, "scan block shape");
 constexpr uint64_t kU = kDefaultUnit;  // ragged units: absolute kU-byte boundaries
@@ -116,10 +122,10 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
 // unit_cap are dropped (a caller's total_len too low: k_ragged_finalize steps those records
 // alone).  The first unit carries the record's init and head offset, the last its tail length
 // (UnitDesc): the plan reads no record bytes.
-// (EP, the tools build's KARMA_RAGGED_EDGES=1: round 2's first form, the entering register h
-// stepped here from the record's head bytes and stored as inj, no edge flags; the tail is then
-// finalize's.)
-template <bool EP = false>
+// (EM, the tools build's KARMA_RAGGED_EDGES: bit 0 = the head in the plan -- the entering
+// register h stepped here from the record's head bytes and stored as inj, no kDescFirst --; bit
+// 1 = the tail in finalize (no kDescLast).  The shipped library has EM = 0.)
+template <int EM = 0>
 __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool valid, uint64_t r, uint64_t fb,
                                  unsigned long long* cnt, uint64_t full_cap, uint32_t h = 0) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -131,23 +137,24 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
         init = A.init ? A.init[r] : A.init_scalar;
         hoff = (uint32_t)(reinterpret_cast<uintptr_t>(A.arena + A.off[r]) & 15u);
         t = (uint32_t)(u.g.e - u.g.b);
-        if (EP) {
+        if (EM & 1) {
             init = h;
-            hoff = t = 0;
+            hoff = 0;
         }
+        if (EM & 2) t = 0;
         if (u.part0) {
             const uint64_t slot = atomicAdd(&cnt[u.c0], 1ull);
             A.pslot[2 * r] = slot;
             const uintptr_t e0 = ((A0 + 1) << kUShift) < b ? ((A0 + 1) << kUShift) : b;
             if (slot < A.unit_cap)
-                A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a) | (EP ? 0u : desc_flags(true, hoff, u.k == 1, t)), init};
+                A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a) | desc_flags(!(EM & 1), hoff, !(EM & 2) && u.k == 1, t), init};
         }
         if (u.part1) {
             const uint64_t slot = atomicAdd(&cnt[u.c1], 1ull);
             A.pslot[2 * r + 1] = slot;
             const uintptr_t s1 = (A0 + u.k - 1) << kUShift;
             if (slot < A.unit_cap)
-                A.desc[slot] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1) | (EP ? 0u : desc_flags(false, 0, true, t)), 0u};
+                A.desc[slot] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1) | desc_flags(false, 0, !(EM & 2), t), 0u};
         }
     }
     // Full units of the wave's 64 records are consecutive slots: the wave writes them together,
@@ -171,7 +178,7 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
         const uint64_t slot = F0 + i;
         if (i < T && slot < full_cap)
             A.desc[slot] = UnitDesc{(A0_o + j) << kUShift,
-                                    (uint32_t)kU | (EP ? 0u : desc_flags(j == 0, hoff_o, !part1_o && j + 1 == k_o, t_o)),
+                                    (uint32_t)kU | desc_flags(!(EM & 1) && j == 0, hoff_o, !(EM & 2) && !part1_o && j + 1 == k_o, t_o),
                                     j == 0 ? init_o : 0u};
     }
 }
@@ -374,16 +381,17 @@ __device__ void lookback(const RaggedArgs& A, uint64_t b, uint64_t full_b, uint6
 // sorted by chunk count, longest first (the two-pass plan's order, which the units kernel
 // streams 3 % faster on configs[2] than block-interleaved runs).  Replaces k_ragged_scan +
 // k_ragged_desc: one launch, and no block reads every other block's totals.
-template <bool EP = false>
+template <int EM = 0>
 __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[EP ? kCombCoreWords - kCombZ4 : 4];  // EP: Z4, byte table
+    constexpr bool HP = (EM & 1) != 0;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[HP ? kCombCoreWords - kCombZ4 : 4];  // HP: Z4, byte table
     __shared__ unsigned long long cnt[kBuckets];
     __shared__ uint32_t hist[kBuckets];
     __shared__ uint64_t sm[kScanBlock / 64];
     __shared__ uint64_t s_id, s_fbase;
     if (threadIdx.x == 0) s_id = atomicAdd(A.lb, 1ull) - A.lb_base;  // ids in start order
-    if constexpr (EP) copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
+    if constexpr (HP) copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
     if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t b = s_id;
@@ -417,9 +425,9 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
         }
     }
     uint32_t h = 0;
-    if (EP && valid && u.k) h = head_register(lds, 0, 1024, A.arena + A.off[r], u.g, A.init ? A.init[r] : A.init_scalar);
+    if (HP && valid && u.k) h = head_register(lds, 0, 1024, A.arena + A.off[r], u.g, A.init ? A.init[r] : A.init_scalar);
     __syncthreads();
-    write_unit_descs<EP>(A, u, valid, r, s_fbase + ex, cnt, A.part_base, h);
+    write_unit_descs<EM>(A, u, valid, r, s_fbase + ex, cnt, A.part_base, h);
 }
 
 // Units of the batch in streaming order: u in [0, U).  Full units are slots [0, F); the
@@ -466,7 +474,7 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
 // steps depend on them only, so they run while the body's loads are in flight (vmcnt counts
 // in issue order); the epilogue after the group tree has no extra work.  The contribution is
 // valid in group lane 0; every lane of the wave must call this.
-template <int PF, bool NT>
+template <int PF, bool NT, bool HP = false>  // HP: the plan stepped the head (inj = the register)
 __device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X, uint32_t l, const UnitDesc& d,
                                                 uint32_t& tail, bool& tail_here) {
     const uint8_t* us = reinterpret_cast<const uint8_t*>(d.us);
@@ -511,7 +519,11 @@ __device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X,
             uint32_t h = ~d.inj;
             if (hl) h = steps_in_vec(lds, kLZ4, kLT8, h, hv, hoff, 16u);
             if (tl) tail = steps_in_vec(lds, kLZ4, kLT8, 0u, tv, 0u, t);
-            if (first && w0 == us) v.x ^= h;
+            if (HP) {
+                if (w0 == us) v.x ^= d.inj;  // (0 for all but a record's first unit)
+            } else if (first && w0 == us) {
+                v.x ^= h;
+            }
             a0 = v.x;
             a1 = v.y;
             a2 = v.z;
@@ -564,7 +576,7 @@ __device__ __forceinline__ uint32_t ragged_unit(const uint32_t* lds, uint32_t X,
 // records 0.6656 vs 0.6525; 8: no better than 4 -- profiles/r02_ragged_pf_ab.txt).  With one
 // 1024-thread workgroup per CU (the 145 KiB LDS image) the chunks in flight per CU are what
 // keeps HBM busy across the unit boundaries this kernel does not pipeline.
-template <bool BAL = true, int PF = kRaggedUnitsPF, bool EP = false>
+template <bool BAL = true, int PF = kRaggedUnitsPF, int EM = kShipEM>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
@@ -601,11 +613,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
         d = un < U ? load_desc(&KB_READ(A.desc, M.slot(un), A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
         uint32_t tail = 0, R;
         bool tail_here = false;
-        if constexpr (EP) {
+        if constexpr (EM == 3) {
             const uint8_t* us = reinterpret_cast<const uint8_t*>(cur.us);
             R = group_unit<PF, kRaggedNT>(lds, X, l, us, us + cur.span, us, cur.inj);
         } else {
-            R = ragged_unit<PF, kRaggedNT>(lds, X, l, cur, tail, tail_here);
+            R = ragged_unit<PF, kRaggedNT, (EM & 1) != 0>(lds, X, l, cur, tail, tail_here);
         }
         if (valid && l == 0) KB_WRITE(A.partial, M.slot(u), A.unit_cap, kKbUnit, R);
         if (valid && tail_here) KB_WRITE(A.tailc, M.slot(u), A.unit_cap, kKbUnit, tail);
@@ -631,7 +643,7 @@ __device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, 
 // One lane per record: Horner fold of the unit contributions (Z_U between unit
 // ends, Z_last before the last unit), the unaligned tail, ~R.  Records of more
 // than 64 units: the whole wave folds all but the last unit with the 64-lane tree.
-template <bool EP = false>
+template <int EM = 0>
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombWords];
@@ -698,7 +710,7 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
         }
         if (ok && u.k >= 2)  // the last unit: shift by its own length
             acc = shift_last(lds, acc, u.last, U) ^ A.partial[unit_slot(u.k - 1, u.k, fb, ps0, ps1, u.part0, u.part1)];
-        if (EP && ok && u.k > 0)
+        if ((EM & 2) && ok && u.k > 0)
             acc = tail_register(lds, kCombZ4, kCombT8, acc, u.g);
         else if (ok && u.k > 0 && u.g.e > u.g.b)  // the tail: Z_t, and the tail bytes' register from the units kernel
             acc = steps_in_vec(lds, kCombZ4, kCombT8, acc, u32x4{0u, 0u, 0u, 0u}, 0u, (uint32_t)(u.g.e - u.g.b)) ^
@@ -1034,27 +1046,41 @@ hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool two_pass) {
     if (a.n_rec == 0) return hipSuccess;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
-    // the tools build's KARMA_RAGGED_EDGES=1: head register in the plan, tail in finalize
-    const bool edges_in_plan = KARMA_AB_KNOB("KARMA_RAGGED_EDGES", 0) == 1 && !two_pass;
+    // Where the record edges are stepped: kShipEM (the plan steps each record's head, finalize
+    // its tail).  The tools build's KARMA_RAGGED_EDGES: 1 = that, 0 = both in the units kernel
+    // (ragged_unit), 2 = head in the plan only, 3 = tail in finalize only.
+    int em = kShipEM;
 #ifdef KARMA_AB
-    if (two_pass)
+    {
+        const long ev = KARMA_AB_KNOB("KARMA_RAGGED_EDGES", 1);
+        em = two_pass ? 0 : ev == 1 ? 3 : ev == 2 ? 1 : ev == 3 ? 2 : 0;
+    }
+    if (two_pass) {
         hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);  // after launch_ragged_scan
-    else
+    } else
 #endif
     {
         if (two_pass || !a.lb || a.lb_seq == 0 || a.lb_seq >= (1u << 22)) return hipErrorInvalidValue;
 #ifdef KARMA_AB
-        if (edges_in_plan)
-            hipLaunchKernelGGL(k_ragged_plan<true>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+        if (em == 0)
+            hipLaunchKernelGGL(k_ragged_plan<0>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+        else if (em == 1)
+            hipLaunchKernelGGL(k_ragged_plan<1>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+        else if (em == 2)
+            hipLaunchKernelGGL(k_ragged_plan<2>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
         else
 #endif
-            hipLaunchKernelGGL(k_ragged_plan<false>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+            hipLaunchKernelGGL(k_ragged_plan<kShipEM>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     }
     units_timer_begin(s);
 #ifdef KARMA_AB  // tools build (ab.h): 2 = static wave-steps, 4 / 8 = chunks in flight
     const long v = KARMA_AB_KNOB("KARMA_RAGGED_VARIANT", 0);
-    if (edges_in_plan)
-        hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    if (em == 0)
+        hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, 0>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (em == 1)
+        hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, 1>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (em == 2)
+        hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, 2>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 4)
         hipLaunchKernelGGL((k_units_ragged<true, 4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 8)
@@ -1068,12 +1094,12 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
     const uint64_t cap = 2 * (uint64_t)grid_blocks;
     if (fblocks > cap) fblocks = cap;
+    if (em & 2)
+        hipLaunchKernelGGL(k_ragged_finalize<2>, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
 #ifdef KARMA_AB
-    if (edges_in_plan)
-        hipLaunchKernelGGL(k_ragged_finalize<true>, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
     else
+        hipLaunchKernelGGL(k_ragged_finalize<0>, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
 #endif
-        hipLaunchKernelGGL(k_ragged_finalize<false>, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

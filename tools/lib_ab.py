@@ -21,9 +21,12 @@ import synth  # noqa: E402
 LIBS = {"head": _lib.load(os.path.join(ROOT, "build", "head", "karma_amd", "lib", "libkarma_crc32c.so")),
         "new": _lib.load(_lib.LIB_PATH)}
 ENV = {v: {} for v in LIBS}
-if os.environ.get("WITH_EDGES_IN_PLAN", "1") == "1":  # the tools build: head register in the plan, tail in finalize
-    LIBS["edges-in-plan"] = _lib.load(_lib.AB_LIB_PATH)
-    ENV["edges-in-plan"] = {"KARMA_RAGGED_EDGES": "1"}
+# tools-build edge placements (KARMA_RAGGED_EDGES): 1 = head in the plan + tail in finalize,
+# 2 = head in the plan only, 3 = tail in finalize only
+_AB = _lib.load(_lib.AB_LIB_PATH)
+for e in os.environ.get("EDGE_VARIANTS", "1").split():
+    LIBS[f"edges{e}"] = _AB
+    ENV[f"edges{e}"] = {"KARMA_RAGGED_EDGES": e}
 dev = torch.device("cuda:0")
 GB = 4 << 30
 RAW = GB + (64 << 20)
@@ -65,10 +68,11 @@ cases["800K uniform 1-8 KiB"] = ragged_case(l2, o2)
 l3 = synth.uniform_lengths(12, 3 << 20, 1025, 1500)
 o3, _ = synth.ragged_layout(l3, header=8)
 cases["3M x 1-1.5 KiB"] = ragged_case(l3, o3)
-l4 = synth.loguniform_lengths(13, 200_000, 64, 1 << 20)
-o4, _ = synth.ragged_layout(l4, header=8)
-keep = int(np.searchsorted(o4 + l4.astype(np.uint64), np.uint64(GB)))
-cases["log-uniform 64B-1MiB"] = ragged_case(l4[:keep].copy(), o4[:keep].copy())
+if os.environ.get("WITH_1MIB", "1") == "1":
+    l4 = synth.loguniform_lengths(13, 200_000, 64, 1 << 20)
+    o4, _ = synth.ragged_layout(l4, header=8)
+    keep = int(np.searchsorted(o4 + l4.astype(np.uint64), np.uint64(GB)))
+    cases["log-uniform 64B-1MiB"] = ragged_case(l4[:keep].copy(), o4[:keep].copy())
 
 names = list(LIBS)
 for name, (run, nbytes, outs) in cases.items():
