@@ -284,7 +284,10 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
     a.fold_k = fold_k;
     if (fold_k) {
         KARMA_RC(comb_blob(ds, unit, &a.comb_maps));
-        KARMA_HIP(launch_fixed(a, ds.cu, s));
+        // (the tools build's KARMA_FIXED_GRID_MULT: that many workgroups per CU, dispatched in
+        // rounds, so the hardware hands the later ones to the CUs that finish first)
+        const long gm = KARMA_AB_KNOB("KARMA_FIXED_GRID_MULT", 1);
+        KARMA_HIP(launch_fixed(a, ds.cu * (int)(gm < 1 ? 1 : gm > 16 ? 16 : gm), s));
         return 0;
     }
     if (k == 1) {
