@@ -34,7 +34,7 @@ constexpr int kRaggedUnitsPF = 6;  // ... and the shipped units kernel (k_units_
 constexpr bool kRaggedNT = true;
 // Where a ragged record's unaligned head and tail bytes are stepped (the EM template argument of
 // k_ragged_plan / k_units_ragged / k_ragged_finalize): bit 0 = the head in the plan, bit 1 = the
-// tail in finalize; 0 = both in the units kernel (ragged_unit, from the lines it loads).  3 is
+// tail in finalize, bit 2 = the head in finalize; 0 = both in the units kernel (ragged_unit, from the lines it loads).  3 is
 // shipped: the units-kernel form saves the plan and finalize 15 us of scattered reads on
 // configs[2] but costs the units kernel as much.
 constexpr int kShipEM = 3;
@@ -141,13 +141,17 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
             init = h;
             hoff = 0;
         }
+        if (EM & 4) {  // the head is finalize's: no entering register in the units
+            init = 0;
+            hoff = 0;
+        }
         if (EM & 2) t = 0;
         if (u.part0) {
             const uint64_t slot = atomicAdd(&cnt[u.c0], 1ull);
             A.pslot[2 * r] = slot;
             const uintptr_t e0 = ((A0 + 1) << kUShift) < b ? ((A0 + 1) << kUShift) : b;
             if (slot < A.unit_cap)
-                A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a) | desc_flags(!(EM & 1), hoff, !(EM & 2) && u.k == 1, t), init};
+                A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a) | desc_flags(!(EM & 5), hoff, !(EM & 2) && u.k == 1, t), init};
         }
         if (u.part1) {
             const uint64_t slot = atomicAdd(&cnt[u.c1], 1ull);
@@ -178,7 +182,7 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
         const uint64_t slot = F0 + i;
         if (i < T && slot < full_cap)
             A.desc[slot] = UnitDesc{(A0_o + j) << kUShift,
-                                    (uint32_t)kU | desc_flags(!(EM & 1) && j == 0, hoff_o, !(EM & 2) && !part1_o && j + 1 == k_o, t_o),
+                                    (uint32_t)kU | desc_flags(!(EM & 5) && j == 0, hoff_o, !(EM & 2) && !part1_o && j + 1 == k_o, t_o),
                                     j == 0 ? init_o : 0u};
     }
 }
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
         d = un < U ? load_desc(&KB_READ(A.desc, M.slot(un), A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
         uint32_t tail = 0, R;
         bool tail_here = false;
-        if constexpr (EM == 3) {
+        if constexpr ((EM & 2) && (EM & 5)) {  // neither edge in the units kernel
             const uint8_t* us = reinterpret_cast<const uint8_t*>(cur.us);
             R = group_unit<PF, kRaggedNT>(lds, X, l, us, us + cur.span, us, cur.inj);
         } else {
@@ -673,9 +677,16 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
                         (!u.part1 || ps1 < A.unit_cap);
         uint32_t acc = 0;
         bool huge = false;
+        // (EM bit 2: the head here -- its register moved to the first unit's end, Z_len0(h))
+        uint32_t hs = 0;
+        if ((EM & 4) && ok && u.k > 0) {
+            const uintptr_t a0 = reinterpret_cast<uintptr_t>(u.g.a);
+            const uint32_t len0 = u.k == 1 ? u.last : u.part0 ? (uint32_t)((((a0 >> kUShift) + 1) << kUShift) - a0) : (uint32_t)U;
+            hs = shift_last(lds, head_register(lds, kCombZ4, kCombT8, p, u.g, init), len0, U);
+        }
         if (ok && u.k > 0) {
             if (u.k <= 64) {
-                acc = A.partial[unit_slot(0, u.k, fb, ps0, ps1, u.part0, u.part1)];
+                acc = A.partial[unit_slot(0, u.k, fb, ps0, ps1, u.part0, u.part1)] ^ hs;
                 for (uint64_t j = 1; j + 1 < u.k; j += 8) {  // middle units: Z_U steps, 8 loads in flight
                     uint32_t s[8];
 #pragma unroll
@@ -694,7 +705,7 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
             hm &= hm - 1;
             const uint64_t hk = __shfl(u.k, h) - 1;  // all units but the last
             const uint64_t hfb = __shfl(fb, h), hps0 = __shfl(ps0, h);
-            const uint32_t hp0 = __shfl(u.part0, h);
+            const uint32_t hp0 = __shfl(u.part0, h), hhs = __shfl(hs, h);
             const uint64_t nb = (hk + 63) / 64;
             const int64_t pad = (int64_t)(nb * 64 - hk);
             uint32_t w = 0;
@@ -702,6 +713,7 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
                 const int64_t idx = (int64_t)(blk * 64 + lane) - pad;
                 uint32_t v = 0;
                 if (idx >= 0) v = A.partial[idx == 0 && hp0 ? hps0 : hfb + idx - hp0];
+                if (idx == 0) v ^= hhs;
                 v = wave_tree(lds, v);
                 w = zmap(lds, 6 * 1024, w) ^ v;
             }
@@ -1048,12 +1060,12 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
     // Where the record edges are stepped: kShipEM (the plan steps each record's head, finalize
     // its tail).  The tools build's KARMA_RAGGED_EDGES: 1 = that, 0 = both in the units kernel
-    // (ragged_unit), 2 = head in the plan only, 3 = tail in finalize only.
+    // (ragged_unit), 2 = head in the plan only, 3 = tail in finalize only, 4 = both in finalize.
     int em = kShipEM;
 #ifdef KARMA_AB
     {
         const long ev = KARMA_AB_KNOB("KARMA_RAGGED_EDGES", 1);
-        em = two_pass ? 0 : ev == 1 ? 3 : ev == 2 ? 1 : ev == 3 ? 2 : 0;
+        em = two_pass ? 0 : ev == 1 ? 3 : ev == 2 ? 1 : ev == 3 ? 2 : ev == 4 ? 6 : 0;
     }
     if (two_pass) {
         hipLaunchKernelGGL(k_ragged_desc, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);  // after launch_ragged_scan
@@ -1068,6 +1080,8 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
             hipLaunchKernelGGL(k_ragged_plan<1>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
         else if (em == 2)
             hipLaunchKernelGGL(k_ragged_plan<2>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+        else if (em == 6)
+            hipLaunchKernelGGL(k_ragged_plan<6>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
         else
 #endif
             hipLaunchKernelGGL(k_ragged_plan<kShipEM>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
@@ -1081,6 +1095,8 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
         hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, 1>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (em == 2)
         hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, 2>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (em == 6)
+        hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, 6>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 4)
         hipLaunchKernelGGL((k_units_ragged<true, 4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 8)
@@ -1094,6 +1110,11 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
     const uint64_t cap = 2 * (uint64_t)grid_blocks;
     if (fblocks > cap) fblocks = cap;
+#ifdef KARMA_AB
+    if (em == 6)
+        hipLaunchKernelGGL(k_ragged_finalize<6>, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
+    else
+#endif
     if (em & 2)
         hipLaunchKernelGGL(k_ragged_finalize<2>, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
 #ifdef KARMA_AB

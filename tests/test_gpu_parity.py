@@ -316,7 +316,7 @@ def test_rejects_bad_arguments(dev):
 
 @pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", v) for v in "127"] +
                          [("KARMA_RAGGED_VARIANT", v) for v in "248"] + [("KARMA_FOLD_MAX_K", "1")] +
-                         [("KARMA_RAGGED_PLAN", "2")] + [("KARMA_RAGGED_EDGES", v) for v in "023"])
+                         [("KARMA_RAGGED_PLAN", "2")] + [("KARMA_RAGGED_EDGES", v) for v in "0234"])
 def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
     """The A/B kernels of the tools build (karma_amd/csrc/ab.h, tools/variant_bench.py) are held to
     the same parity as the shipped ones."""
