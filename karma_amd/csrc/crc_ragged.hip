@@ -1108,7 +1108,9 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
         hipLaunchKernelGGL(k_units_ragged<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
-    const uint64_t cap = 2 * (uint64_t)grid_blocks;
+    // at most 2 per CU (each loads the 73 KiB combine image; the tools build's
+    // KARMA_FINALIZE_PER_CU tries other counts)
+    const uint64_t cap = (uint64_t)KARMA_AB_KNOB("KARMA_FINALIZE_PER_CU", 2) * (uint64_t)grid_blocks;
     if (fblocks > cap) fblocks = cap;
 #ifdef KARMA_AB
     if (em == 6)
