@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
 import sys
@@ -112,13 +113,45 @@ def cgroup_cpu_quota():
         return None
 
 
-def cpu_baseline(workload: str, rec_bytes: int, threads: int, sample=None) -> dict:
+def baseline_threads(affinity) -> int:
+    """Threads of the headline CPU baseline: the CPUs the process may use AND the CPU time the
+    cgroup grants it, min(affinity CPUs, ceil(cgroup quota)).  More threads than the quota only
+    time-slice (the box grants 16 CPUs of 256 visible: 128 threads there measured 23 % below 16)."""
+    q = cgroup_cpu_quota()
+    n = len(affinity)
+    return max(1, min(n, math.ceil(q))) if q else n
+
+
+class Affinity:
+    """Run a block on a given CPU set (the CPU baselines run on the process's original mask, not
+    only the GPU's NUMA node the bench binds to), restoring the current mask afterwards."""
+
+    def __init__(self, cpus):
+        self.cpus = set(cpus) if cpus else None
+
+    def __enter__(self):
+        self.saved = os.sched_getaffinity(0)
+        if self.cpus:
+            os.sched_setaffinity(0, self.cpus)
+        return self
+
+    def __exit__(self, *exc):
+        os.sched_setaffinity(0, self.saved)
+        return False
+
+
+def cpu_baseline(workload: str, rec_bytes: int, threads: int, sample=None, orig_cpus=None, node_cpus=None) -> dict:
     """Reference crc32c (oracle/_ref, built from /root/reference/karma-util/crc32c.cc) on host cores.
 
     A bounded sample of the same workload, at least 1 GiB (larger than the host's last-level
     cache, so it streams from DRAM like the device batch streams from HBM), checksummed for ~2 s
-    on `threads` std::threads (records round-robin; default: every CPU of the affinity mask), on
-    one thread, and on 16 threads (round 1's setting, kept for comparison):
+    per figure, records round-robin over std::threads:
+      value (headline) -- `threads` threads (baseline_threads: min(affinity CPUs, ceil(cgroup
+                          quota))) on the process's ORIGINAL affinity mask `orig_cpus` (before the
+                          bench bound itself to its GPU's NUMA node);
+      single_thread_value, all_affinity_value (one thread per CPU of the original mask: more than
+      the quota, so time-sliced), numa_node_value (the node's CPUs, on the node the bench binds to).
+    Samples:
       fixed/host -- the first 1 GiB of records of the timed batch (`sample`, copied off the device);
       ragged     -- the first ~1 GiB of records of the configs[2] layout (same lengths, seed 7);
       stream     -- 16 distinct 64 MiB segments (one thread per segment at most).
@@ -177,9 +210,15 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int, sample=None) -> di
             if dt > budget:
                 return reps * nbytes / dt / GIB, reps
 
-    multi, reps_m = rate(threads, 2.0)
-    single, reps_s = rate(1, 2.0)
-    sixteen, _ = rate(16, 2.0) if threads != 16 else (multi, reps_m)
+    orig_cpus = set(orig_cpus) if orig_cpus else os.sched_getaffinity(0)
+    with Affinity(orig_cpus):
+        multi, reps_m = rate(threads, 2.0)
+        single, _ = rate(1, 2.0)
+        all_aff = rate(len(orig_cpus), 2.0)[0] if len(orig_cpus) != threads else multi
+    node = None
+    if node_cpus and set(node_cpus) != orig_cpus:
+        with Affinity(node_cpus):
+            node = rate(len(node_cpus), 2.0)[0]
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as f:
@@ -191,9 +230,14 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int, sample=None) -> di
         pass
     return {"value": round(multi, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
             "sample": f"{desc}, crc32c::Value per record, round-robin over {threads} std::threads "
-                      f"(every CPU of the affinity mask), repeated {reps_m}x (~2 s)",
-            "single_thread_value": round(single, 3), "threads16_value": round(sixteen, 3), "cpu_model": cpu,
-            "host_cpus_affinity": host_cpus(), "host_cpus_visible": os.cpu_count(),
+                      f"(min(affinity CPUs, ceil(cgroup quota)), on the process's original CPU mask), "
+                      f"repeated {reps_m}x (~2 s)",
+            "threads_rule": "min(affinity CPUs, ceil(cgroup cpu.max quota))",
+            "single_thread_value": round(single, 3),
+            "all_affinity_value": round(all_aff, 3), "all_affinity_threads": len(orig_cpus),
+            "numa_node_value": round(node, 3) if node is not None else None,
+            "numa_node_threads": len(node_cpus) if node is not None else None,
+            "cpu_model": cpu, "host_cpus_affinity": len(orig_cpus), "host_cpus_visible": os.cpu_count(),
             "cgroup_cpu_quota": cgroup_cpu_quota()}
 
 
@@ -273,22 +317,46 @@ def wal_bench(args, L, rank):
     images[other][:] = wal  # the same image in the other kind of host memory
     step = append if args.workload == "wal_append" else replay
     dev_rate = dir_rate = None
-    if args.workload == "wal_replay":  # the same replay over a copy already in HBM (no upload)
+    dev_single = None
+    if args.workload == "wal_replay":
+        # The same replay over copies already in HBM (no upload).  Four distinct images (payloads
+        # of other seeds, same framing: 4 x ~201 MB > 512 MiB) are replayed in rotation, so no call
+        # finds its image in the 256 MB Infinity Cache the previous call left: the
+        # rotated rate is the HBM figure.  The single reused image is reported beside it.
         import torch
-        d_wal = torch.from_numpy(wal).to(torch.device("cuda", local))
+        d_wals = [torch.from_numpy(wal).to(torch.device("cuda", local))]
+        img_k = np.zeros_like(wal)
+        for k in range(1, 4):
+            src_k = synth.splitmix_np(args.seed + rank + 1000 * k, 0, src.size).copy()
+            cur.value = 0
+            _lib.check("wal_append", L.karma_wal_append_batch(src_k.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                                              n, img_k.ctypes.data, wal_bytes, seg, ctypes.byref(cur),
+                                                              None, ctypes.byref(nf), local))
+            d_wals.append(torch.from_numpy(img_k).to(torch.device("cuda", local)))
+            del src_k
+        del img_k
+        rot = {"i": 0, "k": len(d_wals)}
 
         def replay_dev():
+            d_wal = d_wals[rot["i"] % rot["k"]]
+            rot["i"] += 1
             _lib.check("wal_replay", L.karma_wal_replay(None, d_wal.data_ptr(), wal_bytes, seg, 0, ctypes.byref(nrec),
                                                         ctypes.byref(stop), ctypes.byref(status), None, 0, local))
             assert nrec.value == n
 
-        for _ in range(args.warmup):
-            replay_dev()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            replay_dev()
-        dev_rate = payload / ((time.perf_counter() - t0) / args.steps) / GIB
-        del d_wal
+        for k in (len(d_wals), 1):  # rotated, then the single image
+            rot["k"] = k
+            for _ in range(args.warmup):
+                replay_dev()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                replay_dev()
+            r = payload / ((time.perf_counter() - t0) / args.steps) / GIB
+            if k > 1:
+                dev_rate = r
+            else:
+                dev_single = r
+        del d_wals
         # the same replay from segment files named by their WAL offsets (karma_wal_replay_dir),
         # page-cached: the files are read straight into the pinned staging buffers
         import shutil
@@ -338,6 +406,14 @@ def wal_bench(args, L, rank):
            "records_per_s": round(n / dt, 1), "wal_image": args.wal_image,
            f"{other}_image_value": round(other_rate, 3),
            "device_resident_value": round(dev_rate, 3) if dev_rate is not None else None,
+           "device_resident_image_tbs": round(wal_bytes / (payload / dev_rate / GIB) / 1e12, 3)
+           if dev_rate is not None else None,
+           "device_resident_single_image_value": round(dev_single, 3) if dev_single is not None else None,
+           "device_resident_note": "karma_wal_replay over WAL images already in HBM, 4 distinct ~%d MB images "
+                                   "in rotation (none left in the 256 MB MALL by the previous call); host wall "
+                                   "clock over --steps synchronous calls; image TB/s = wal_bytes / call time; the "
+                                   "single-image value reuses one image every call (MALL-resident)" % (wal_bytes // 10**6)
+           if dev_rate is not None else None,
            "segment_files_value": round(dir_rate, 3) if dir_rate is not None else None,
            "config": {"workload": f"{mix} WAL records, 1 MiB segments, "
                                   f"{'karma_wal_append_batch' if step is append else 'karma_wal_replay'} "
@@ -348,7 +424,9 @@ def wal_bench(args, L, rank):
         import oracle_lib
         ref = oracle_lib.ref()
         if ref is not None:
-            thr = args.cpu_threads or min(16, host_cpus())  # 16 independent WALs (one per sivir io thread)
+            # one independent WAL per thread (one per sivir io thread), as many as the CPU grant
+            # runs at once (baseline_threads), on the process's original CPU mask
+            thr = args.cpu_threads or baseline_threads(args.orig_cpus)
             k = min(n, 1 << 20)
             img = ((k // thr + per_seg - 1) // per_seg + 2) * seg
             imgs = np.zeros(img * thr, dtype=np.uint8)
@@ -370,14 +448,17 @@ def wal_bench(args, L, rank):
             def rep(nthr):
                 return ref.ref_wal_replay_mt(imgs.ctypes.data, img, seg, nthr, nthr)
 
-            app(thr)  # the images the replay baseline reads
             fn = app if step is append else rep
-            _, multi, reps = rate(thr, fn)
-            _, single, _ = rate(1, fn)
+            with Affinity(args.orig_cpus):
+                app(thr)  # the images the replay baseline reads
+                _, multi, reps = rate(thr, fn)
+                _, single, _ = rate(1, fn)
             res["cpu_baseline"] = {"value": round(multi, 3), "unit": "GiB/s", "cores": thr, "kind": "reference",
                                    "sample": f"{k} x {size} B records framed ({'append' if fn is app else 'replay'}) "
                                              f"into {thr} independent WAL images, one per std::thread, reference "
                                              f"crc32c::Value, repeated {reps}x (~2 s)",
+                                   "threads_rule": "min(affinity CPUs, ceil(cgroup cpu.max quota))",
+                                   "cgroup_cpu_quota": cgroup_cpu_quota(),
                                    "single_thread_value": round(single, 3)}
     return res
 
@@ -450,6 +531,23 @@ def records_per_gpu(requested: int, world: int, workload: str):
     return 1 << 20, False
 
 
+def config5_anchor():
+    """The one-GPU rate of configs[4]'s per-GPU shard (33,554,432 x 4 KiB, 128 GiB), measured by
+    `bench.py --records-per-gpu 33554432` and committed under profiles/: the N = 8 line's per-GPU
+    work at N = 1, so a scaling curve can separate shard size from scaling.  Not measured in
+    this run; the source file is named."""
+    for name in ("r03_bench_config5_slice.json", "r02_bench_config5_slice.json"):
+        path = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(path) as f:
+                d = json.loads(f.read().strip().splitlines()[-1])
+            return {"value": d["value"], "unit": d.get("unit", "GiB/s"),
+                    "frac": d.get("roofline", {}).get("frac"), "source": f"profiles/{name}"}
+        except (OSError, ValueError, KeyError, IndexError):
+            continue
+    return None
+
+
 class TorchSync:
     """Streams and events of the GPU run: the compute stream (the caller's), a second stream for
     the gather, torch.cuda events between them."""
@@ -520,7 +618,9 @@ def main():
     local = local % max(ndev, 1)  # one rank per GPU; several ranks per GPU only for plumbing checks
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    args.orig_cpus = os.sched_getaffinity(0)  # before binding: the CPU baselines run on the whole mask
     numa = None if args.no_numa_bind else bind_to_gpu_node(torch, local)
+    args.node_cpus = os.sched_getaffinity(0) if numa else None
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
@@ -672,11 +772,22 @@ def main():
         cur["out"] = o
         kernel_step()
 
+    # the gather of each timed step bracketed by events on the gather stream (its own time per
+    # rank, separate from the batch kernel's: the N > 1 line reports both per rank)
+    gtime = {"i": None}
+    gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)] \
+        if comm is not None else []
+
     def gather(o, gs):
+        i = gtime["i"]
+        if i is not None:
+            gev[i][0].record(gs)
         st = L.karma_crc32c_gather_u32(comm, o.data_ptr(), n_rec,
                                        gather_buf.data_ptr() if gather_buf is not None else None, 0, gs.cuda_stream)
         if st:
             _lib.check("gather_u32", st)
+        if i is not None:
+            gev[i][1].record(gs)
 
     pipe = GatherPipeline(outs, compute, gather if (comm is not None and out is not None) else None,
                           TorchSync(torch, stream))
@@ -724,7 +835,9 @@ def main():
         crc_step()
         if call_events:
             ev[i][1].record(stream)
+        gtime["i"] = i
         gather_step()
+    gtime["i"] = None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -735,10 +848,21 @@ def main():
     kern_ms = kern_ms if kern_ms is not None else call_ms
     kern_avg = float(np.mean(kern_ms))
     call_avg = float(np.mean(call_ms))
+    gather_avg = float(np.mean([a.elapsed_time(b) for a, b in gev])) if gev else None
+    per_rank = None
     if world > 1:
-        t = torch.tensor([elapsed, kern_avg, call_avg], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_max, call_max = float(t[0]), float(t[1]), float(t[2])
+        t = torch.tensor([elapsed, kern_avg, call_avg, gather_avg if gather_avg is not None else 0.0],
+                         dtype=torch.float64, device=dev)
+        rows = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(rows, t)
+        rows = torch.stack(rows).cpu().numpy()
+        elapsed, kern_max, call_max = float(rows[:, 0].max()), float(rows[:, 1].max()), float(rows[:, 2].max())
+        per_rank = {"elapsed_s": [round(float(x), 6) for x in rows[:, 0]],
+                    "kernel_ms_avg": [round(float(x), 4) for x in rows[:, 1]],
+                    "call_ms_avg": [round(float(x), 4) for x in rows[:, 2]],
+                    "gather_ms_avg": [round(float(x), 4) for x in rows[:, 3]],
+                    "gather": "karma_crc32c_gather_u32 on the gather stream, events around each timed step's call; "
+                              "it overlaps the next step's batch (GatherPipeline)"}
     else:
         kern_max, call_max = kern_avg, call_avg
 
@@ -776,6 +900,7 @@ def main():
         value = total_bytes / elapsed / GIB
         achieved = algo_bytes / (kern_avg * 1e-3) / 1e9
         traffic = pmc_traffic(args.pmc, wl, payload) if wl == "fixed" else None
+        traffic_source = os.path.relpath(args.pmc, ROOT) if traffic is not None else None
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -795,6 +920,13 @@ def main():
                                  "host->device pipeline"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_source,
+                         "traffic_note": "HBM bytes per launch from a separate rocprofv3 --pmc pass of the same "
+                                         "workload (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md gfx950 "
+                                         "correction), read from traffic_source: not measured in this run"
+                                         if traffic is not None else None,
+                         "achieved_source": "algorithmic bytes / kernel_ms_avg (HIP events around the "
+                                            "k_units_* launch inside the library, on its stream, this run)",
                          "algorithmic_bytes_per_launch": int(algo_bytes),
                          "kernel_ms_avg": round(kern_avg, 4), "kernel_ms_max_over_ranks": round(kern_max, 4),
                          "call_ms_avg": round(call_avg, 4),
@@ -804,15 +936,22 @@ def main():
             "host_binding": numa,
             "rccl_nranks": rccl_nranks,
         }
+        if per_rank is not None:
+            res["per_rank"] = per_rank
+        if config5:  # the N = 8 default is configs[4]'s shard, not configs[1]'s 1M records per GPU
+            res["config"]["records_per_gpu_n1_equivalent"] = 1 << 20
+            anchor = config5_anchor()
+            if anchor:
+                res["config"]["same_shard_one_gpu_anchor"] = anchor
         res.update(extra)
         if check:
             res["self_check"] = check
         if world == 1 and not args.no_cpu_baseline:
-            thr = args.cpu_threads or host_cpus()
+            thr = args.cpu_threads or baseline_threads(args.orig_cpus)
             sample = None
             if wl in ("fixed", "stream", "ragged") and arena is not None:  # the first 1 GiB of the timed input
                 sample = arena[: min(arena.numel(), (1 << 30) + 16)].cpu().numpy()
-            res["cpu_baseline"] = cpu_baseline(wl, rec, thr, sample)
+            res["cpu_baseline"] = cpu_baseline(wl, rec, thr, sample, args.orig_cpus, args.node_cpus)
         print(json.dumps(res), flush=True)
 
     if comm is not None:

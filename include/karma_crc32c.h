@@ -73,14 +73,22 @@ int karma_crc32c_batch_fixed(const void* d_data, size_t rec_bytes, size_t n_rec,
  * table: pass sum(d_len) (or any upper bound) to stay fully asynchronous;
  * pass 0 when unknown and the call reads the unit count back (one host sync).
  * A total_len below sum(d_len) is not an error and never changes a result: the
- * records whose units do not fit the table are checksummed one lane each. */
+ * records whose units do not fit the table are checksummed one lane each.
+ * Graph capture: a call with total_len > 0 enqueues kernels only, so it may be
+ * captured in a hipGraph and the graph replayed any number of times (the plan's
+ * block counter and look-back tags live on the device), with new bytes and
+ * lengths in the same buffers as long as sum(d_len) stays <= total_len.  Make one
+ * uncaptured call of that size on the stream first (it allocates the stream's
+ * workspace; a capture cannot).  Per-stream state is per calling thread for
+ * hipStreamPerThread. */
 int karma_crc32c_batch_ragged(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
                               size_t total_len, const uint32_t* d_init, uint32_t init, uint32_t* d_out,
                               karma_stream_t stream);
 
 /* The same with an upper bound of every d_len[r] (0 = unknown).  With max_len <= 1 KiB
- * (WAL records, KFP frames) each record is checksummed by one group of 8 lanes with no
- * planning kernels.  The result is exact whatever the bound: a wrong one costs balance. */
+ * (WAL records, KFP frames) each record is checksummed by one small group of lanes (4)
+ * with no planning kernels.  The result is exact whatever the bound: a wrong one costs
+ * balance. */
 int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
                                       size_t total_len, uint32_t max_len, const uint32_t* d_init, uint32_t init,
                                       uint32_t* d_out, karma_stream_t stream);

@@ -82,17 +82,19 @@ std::map<std::pair<int, void*>, Workspace> g_ws;
 
 // The ragged plan's look-back words per (device, stream) (RaggedArgs::lb, crc_ragged.hip):
 // [0] counts started plan blocks, [1 + b] block b's full-unit status and [1 + half + b] its
-// partial-unit status, tagged with the call's seq.
+// partial-unit status, tagged with the call's seq; then the two control words lb_ctl.
 // Calls on one stream run in order, so a call sees only its own tag or older ones.  The
-// words are zeroed when allocated and whenever the 22-bit tag wraps.
+// counter and the tag are kept on the device (k_ragged_plan / k_ragged_finalize), none on the
+// host: a ragged call captured in a hipGraph may be replayed any number of times.  The words
+// are zeroed when allocated; the device clears them when the 22-bit tag wraps.
+// hipStreamPerThread is one handle for many streams: it is keyed per calling thread.
 struct Lookback {
     unsigned long long* words = nullptr;
-    uint64_t cap = 0;   // words: 1 + 2 * half
+    uint64_t cap = 0;   // words: 1 + 2 * half + 2
     uint64_t half = 0;  // plan blocks a call may have
-    uint64_t seq = 0;   // tag of the last call
-    uint64_t ctr = 0;   // value of words[0] after the last call's blocks
 };
 std::map<std::pair<int, void*>, Lookback> g_lb;
+thread_local char t_per_thread_key;  // the look-back key of this thread's hipStreamPerThread
 
 int current_device(int* dev) {
     int n = 0;
@@ -160,13 +162,22 @@ int block_comb_blob(DevState& d, uint64_t unit_bytes, uint64_t per_thread, const
 }
 
 // A per-(device, stream) scratch buffer, grown on demand (*reallocated: it was).
+// Per-stream state is keyed by the stream handle; hipStreamPerThread is one handle for many
+// streams, so it is keyed by the calling thread.
+void* stream_key(hipStream_t s) { return s == hipStreamPerThread ? (void*)&t_per_thread_key : (void*)s; }
+
+// Buffers a stream's workspace or look-back words outgrew.  They are kept, not freed: a ragged
+// call captured in a hipGraph keeps their addresses in its kernel arguments, and a later,
+// larger call on the same stream must not free memory such a graph still uses.  (Growth is
+// by at least 1.25x, so the retired buffers add up to a few times the largest one.)
+std::vector<void*> g_retired;
+
 int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocated = nullptr) {
-    Workspace& w = g_ws[{dev, (void*)s}];
+    Workspace& w = g_ws[{dev, stream_key(s)}];
     if (reallocated) *reallocated = w.bytes < bytes;
     if (w.bytes < bytes) {
         if (w.ptr) {
-            KARMA_HIP(hipStreamSynchronize(s));
-            KARMA_HIP(hipFree(w.ptr));
+            g_retired.push_back(w.ptr);
             w.ptr = nullptr;
             w.bytes = 0;
         }
@@ -178,39 +189,28 @@ int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocate
     return 0;
 }
 
-// Caller holds g_mu.  Binds this call's look-back words, tag and block-id base for nb
-// plan blocks.
+// Caller holds g_mu.  Binds the stream's look-back words for nb plan blocks.
 int bind_lookback(int dev, hipStream_t s, uint64_t nb, RaggedArgs& a) {
-    Lookback& L = g_lb[{dev, (void*)s}];
-    bool clear = false;
+    Lookback& L = g_lb[{dev, stream_key(s)}];
     if (L.half < nb) {
         if (L.words) {
-            KARMA_HIP(hipStreamSynchronize(s));
-            KARMA_HIP(hipFree(L.words));
+            g_retired.push_back(L.words);
             L.words = nullptr;
             L.cap = L.half = 0;
         }
         const uint64_t half = std::max<uint64_t>(2 * nb, 2048);
-        KARMA_HIP(hipMalloc(&L.words, (1 + 2 * half) * sizeof(unsigned long long)));
+        const uint64_t cap = 1 + 2 * half + 2;
+        KARMA_HIP(hipMalloc(&L.words, cap * sizeof(unsigned long long)));
+        KARMA_HIP(hipMemsetAsync(L.words, 0, cap * sizeof(unsigned long long), s));
         L.half = half;
-        L.cap = 1 + 2 * half;
-        clear = true;
-    }
-    // (the tools build can lower the wrap point to test it: KARMA_LB_SEQ_MAX, ab.h)
-    const uint64_t seq_max = (uint64_t)KARMA_AB_KNOB("KARMA_LB_SEQ_MAX", 1l << 22);
-    if (++L.seq >= std::min<uint64_t>(seq_max, 1ull << 22)) {
-        L.seq = 1;
-        clear = true;
-    }
-    if (clear) {
-        KARMA_HIP(hipMemsetAsync(L.words, 0, L.cap * sizeof(unsigned long long), s));
-        L.ctr = 0;
+        L.cap = cap;
     }
     a.lb = L.words;
     a.lbp = L.words + 1 + L.half;
-    a.lb_base = L.ctr;
-    a.lb_seq = (uint32_t)L.seq;
-    L.ctr += nb;
+    a.lb_ctl = L.words + 1 + 2 * L.half;
+    a.lb_words = 2 * L.half;
+    // (the tools build can lower the wrap point to test it: KARMA_LB_SEQ_MAX, ab.h)
+    a.lb_seq_max = (uint32_t)std::min<long>(KARMA_AB_KNOB("KARMA_LB_SEQ_MAX", 1l << 22), 1l << 22);
     return 0;
 }
 

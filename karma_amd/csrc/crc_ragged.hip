@@ -330,10 +330,10 @@ __device__ __forceinline__ uint64_t lb_wait(unsigned long long* p, uint32_t seq)
 // has published its inclusive total there), publish the inclusive totals and return the
 // exclusive ones (uniform).  Every block it waits for has started (ids are taken in start
 // order) and publishes its own counts before waiting on anything, so the wait ends.
-__device__ void lookback(const RaggedArgs& A, uint64_t b, uint64_t full_b, uint64_t part_b, uint64_t& exF,
-                         uint64_t& exP) {
+__device__ void lookback(const RaggedArgs& A, uint32_t seq, uint64_t b, uint64_t full_b, uint64_t part_b,
+                         uint64_t& exF, uint64_t& exP) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t tag = (uint64_t)A.lb_seq << 42;
+    const uint64_t tag = (uint64_t)seq << 42;
     unsigned long long* lf = A.lb + 1;
     unsigned long long* lp = A.lbp;
     exF = exP = 0;
@@ -362,11 +362,11 @@ __device__ void lookback(const RaggedArgs& A, uint64_t b, uint64_t full_b, uint6
             for (int q = 0; q < kLbWin; ++q) {
                 const int64_t i = j - (int64_t)lane - 64 * q;
                 if (!doneF) {
-                    if (i >= 0 && (wf[q] >> 42) != A.lb_seq) wf[q] = lb_wait(lf + i, A.lb_seq);
+                    if (i >= 0 && (wf[q] >> 42) != seq) wf[q] = lb_wait(lf + i, seq);
                     doneF = lb_take(wf[q], exF);
                 }
                 if (!doneP) {
-                    if (i >= 0 && (wp[q] >> 42) != A.lb_seq) wp[q] = lb_wait(lp + i, A.lb_seq);
+                    if (i >= 0 && (wp[q] >> 42) != seq) wp[q] = lb_wait(lp + i, seq);
                     doneP = lb_take(wp[q], exP);
                 }
             }
@@ -375,6 +375,25 @@ __device__ void lookback(const RaggedArgs& A, uint64_t b, uint64_t full_b, uint6
     if (lane == 0) {
         lb_store(lf + b, tag | kLbIncl | (exF + full_b));
         lb_store(lp + b, tag | kLbIncl | (exP + part_b));
+    }
+}
+
+// The single-pass plan's look-back words after the call (the first thing k_ragged_finalize
+// does; the plan has finished, stream order): the block counter back to 0 and the finished
+// call's tag into lb_ctl[0], so the next plan -- also a replay of a captured graph -- takes
+// fresh ids and the next tag.  When the tags run out every status word is cleared (each
+// finalize thread a stride of them) and they restart at 1.  Every block writes the same values.
+__device__ void lookback_retire(const RaggedArgs& A) {
+    const uint32_t seq = (uint32_t)lb_load(A.lb_ctl + 1);
+    const bool wrap = seq + 1u >= A.lb_seq_max;
+    if (wrap) {
+        const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.lb_words; i += stride)
+            lb_store(A.lb + 1 + i, 0ull);
+    }
+    if (threadIdx.x == 0) {
+        lb_store(A.lb, 0ull);
+        lb_store(A.lb_ctl, wrap ? 0ull : (unsigned long long)seq);
     }
 }
 
@@ -394,7 +413,12 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     __shared__ uint32_t hist[kBuckets];
     __shared__ uint64_t sm[kScanBlock / 64];
     __shared__ uint64_t s_id, s_fbase;
-    if (threadIdx.x == 0) s_id = atomicAdd(A.lb, 1ull) - A.lb_base;  // ids in start order
+    __shared__ uint32_t s_seq;
+    if (threadIdx.x == 0) {
+        s_id = atomicAdd(A.lb, 1ull);  // ids in start order (k_ragged_finalize resets the counter)
+        s_seq = (uint32_t)lb_load(A.lb_ctl) + 1u;  // this call's tag (RaggedArgs::lb_ctl)
+        if (s_id == 0) lb_store(A.lb_ctl + 1, s_seq);
+    }
     if constexpr (HP) copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
     if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     __syncthreads();
@@ -414,7 +438,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     const uint64_t full_b = tot >> 16, part_b = tot & 0xffffu;
     if (threadIdx.x < 64) {
         uint64_t exF, exP;
-        lookback(A, b, full_b, part_b, exF, exP);
+        lookback(A, s_seq, b, full_b, part_b, exF, exP);
         if (threadIdx.x == 0) {
             s_fbase = exF;
             unsigned long long s = A.part_base + exP;  // the block's partial run, longest bucket first
@@ -651,6 +675,7 @@ template <int EM = 0>
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombWords];
+    if (A.lb) lookback_retire(A);
     load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -1072,7 +1097,7 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     } else
 #endif
     {
-        if (two_pass || !a.lb || a.lb_seq == 0 || a.lb_seq >= (1u << 22)) return hipErrorInvalidValue;
+        if (two_pass || !a.lb || !a.lb_ctl || a.lb_seq_max < 2 || a.lb_seq_max > (1u << 22)) return hipErrorInvalidValue;
 #ifdef KARMA_AB
         if (em == 0)
             hipLaunchKernelGGL(k_ragged_plan<0>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);

@@ -126,13 +126,18 @@ struct RaggedArgs {
     uint64_t* block_sums;      // per scan block: full-unit offset
     uint64_t* block_psums;     // per scan block: partial units, then the block's first partial slot
     // Single-pass plan (k_ragged_plan): decoupled look-back over per-block status words.
-    // lb[0] counts the blocks that started (plan-block ids in start order, from lb_base on);
-    // lb[1 + b] = seq << 42 | flag << 40 | value (flag 1: block b's own full-unit count, 2:
-    // the full units of blocks 0..b); lbp[b] the same for partial units.  lb_seq (1 .. 2^22 - 1) tags this call's words (capi.cc).
+    // lb[0] counts the blocks that started (plan-block ids in start order); lb[1 + b] =
+    // seq << 42 | flag << 40 | value (flag 1: block b's own full-unit count, 2: the full units
+    // of blocks 0..b); lbp[b] the same for partial units.  The call's tag seq (1 .. lb_seq_max
+    // - 1) and the counter live on the device (lb_ctl), so that a call replayed from a captured
+    // graph gets fresh ids and a fresh tag: the plan takes seq = lb_ctl[0] + 1 and records it
+    // in lb_ctl[1]; k_ragged_finalize (the call's last kernel) resets lb[0] and moves lb_ctl[0]
+    // to seq, or, at lb_seq_max, clears the lb_words status words and restarts the tags at 1.
     unsigned long long* lb;
     unsigned long long* lbp;   // the same for the blocks' partial unit counts
-    uint64_t lb_base;
-    uint32_t lb_seq;
+    unsigned long long* lb_ctl;  // [0] the last finished call's tag, [1] the running call's
+    uint64_t lb_words;         // status words after lb[0] (both arrays)
+    uint32_t lb_seq_max;       // 2^22 (the tools build lowers it to test the wrap)
     UnitDesc* desc;            // unit_cap entries
     uint64_t unit_cap;         // capacity of desc / partial
     uint64_t part_base;        // single-pass plan: first slot of the partial units (full units
@@ -202,12 +207,21 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {
     uint32_t count;  // type-0 records (candidates) the walk found
-    uint32_t kind;   // KARMA_WAL_END / _CORRUPT / _BAD_TYPE
-    uint64_t stop;   // WAL offset where the segment's walk stopped (segment end for END)
+    uint32_t kind;   // KARMA_WAL_END / _CORRUPT / _BAD_TYPE, or kWalSpill
+    uint64_t stop;   // WAL offset where the segment's walk stopped (segment end for END; for
+                     // kWalSpill the offset past the segment end where the chain continues)
     uint32_t max_len;  // an upper bound of the candidates' payload lengths
     uint32_t pad;
 };
 static_assert(sizeof(WalSegMeta) == 24, "one 24-byte record per segment");
+
+// An accepted size-0 record advances replay by 12 bytes, not 8: scan_record appends the 4
+// stale bytes to the record (wal.cc:66) and sivir::open advances by record.size()
+// (sivir.cc:38).  When that carries the chain 1-4 bytes past a segment's end, the next
+// segment is entered at that offset instead of 0; the walk reports the segment with this
+// internal kind, replay stops there (k_wal_plan), and replay_core continues from the
+// reported offset with another device pass (wal.cc).  Never returned to a caller.
+constexpr uint32_t kWalSpill = 16;
 
 // What replay reads, from the segments' metas (k_wal_plan, on the device): segments [0, w1),
 // n_all candidates in them, their largest payload, and the structural stop.

@@ -84,7 +84,7 @@ int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std:
         hipMemcpy(B->len, len.data(), len.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         rc = set_last_error(KARMA_E_HIP, "crc_spans: hipMemcpy H2D");
     else if ((rc = karma_crc32c_batch_ragged_bounded(d_buf, static_cast<uint64_t*>(B->off),
-                                                     static_cast<uint32_t*>(B->len), off.size(), total, max_len,
+                                                     static_cast<uint32_t*>(B->len), off.size(), total, std::max<uint32_t>(max_len, 1),
                                                      nullptr, 0, static_cast<uint32_t*>(B->out), nullptr)))
         ;
     else if (hipMemcpy(out.data(), B->out, out.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
@@ -313,7 +313,9 @@ int encode_pass(EncCtx& C, int dev, const EncFrames& F, size_t f0, size_t m, uin
             hipMemcpyAsync(doff, so + lo, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
             hipMemcpyAsync(dlen, sl + lo, nr * 4, hipMemcpyHostToDevice, s) != hipSuccess)
             return (int)KARMA_E_HIP;
-        if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, doff, dlen, nr, phi - plo, max_len, nullptr, 0,
+        // (max_len 0, every span empty, would read as "no bound" and take the unknown-total plan)
+        if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, doff, dlen, nr, phi - plo,
+                                                             std::max<uint32_t>(max_len, 1), nullptr, 0,
                                                              C.d_crc.as<uint32_t>() + lo, s))
             return rc;
         if (hipMemcpyAsync(hc + lo, C.d_crc.as<uint32_t>() + lo, nr * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||

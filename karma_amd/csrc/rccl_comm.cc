@@ -18,6 +18,7 @@
 #include <new>
 #include <string>
 
+#include "gather_p2p.h"
 #include "karma_crc32c.h"
 
 namespace karma::engine {
@@ -154,21 +155,29 @@ int karma_crc32c_gather_u32(karma_comm_t comm, const uint32_t* d_send, size_t co
         if (e != ncclSuccess) return rfail(std::string("ncclGather: ") + r.getErrorString(e));
         return 0;
     }
-    // grouped point-to-point form: every rank sends, the root receives each shard in rank order
-    ncclResult_t e = r.groupStart();
-    if (e == ncclSuccess && comm->rank == root) {
-        for (int p = 0; p < comm->nranks && e == ncclSuccess; ++p)
-            if (p != root) e = r.recv(d_recv + (size_t)p * count, count, ncclUint32, p, comm->nc, s);
-    } else if (e == ncclSuccess) {
-        e = r.send(d_send, count, ncclUint32, root, comm->nc, s);
-    }
-    const ncclResult_t e2 = r.groupEnd();
-    if (e != ncclSuccess || e2 != ncclSuccess)
-        return rfail(std::string("ncclSend/ncclRecv: ") + r.getErrorString(e != ncclSuccess ? e : e2));
-    if (comm->rank == root && count &&
-        hipMemcpyAsync(d_recv + (size_t)root * count, d_send, count * sizeof(uint32_t), hipMemcpyDeviceToDevice, s) !=
-            hipSuccess)
-        return KARMA_E_HIP;
+    // grouped point-to-point form (gather_p2p.h): every rank sends, the root receives each
+    // shard in rank order and copies its own
+    struct Ops {
+        Rccl& r;
+        karma_comm* c;
+        hipStream_t s;
+        ncclResult_t last = ncclSuccess;
+        int nc(ncclResult_t e) {
+            if (e != ncclSuccess) last = e;
+            return e != ncclSuccess ? KARMA_E_RCCL : 0;
+        }
+        int group_start() { return nc(r.groupStart()); }
+        int group_end() { return nc(r.groupEnd()); }
+        int send(const uint32_t* b, size_t n, int peer) { return nc(r.send(b, n, ncclUint32, peer, c->nc, s)); }
+        int recv(uint32_t* b, size_t n, int peer) { return nc(r.recv(b, n, ncclUint32, peer, c->nc, s)); }
+        int copy(uint32_t* d, const uint32_t* src, size_t n) {
+            return hipMemcpyAsync(d, src, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s) == hipSuccess ? 0
+                                                                                                 : KARMA_E_HIP;
+        }
+    } ops{r, comm, s};
+    const int rc = karma::engine::gather_p2p(ops, comm->rank, comm->nranks, root, d_send, count, d_recv);
+    if (rc == KARMA_E_RCCL) return rfail(std::string("ncclSend/ncclRecv: ") + r.getErrorString(ops.last));
+    if (rc) return karma::engine::set_last_error(rc, "gather_u32: root's own copy");
     return 0;
 }
 

@@ -172,9 +172,44 @@ ReplayCtx& replay_ctx(int dev) {
 // image is streamed into HBM through the library's pinned staging (host_stage.h).
 using ImageFill = karma::engine::HostFill;
 
+int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
+                uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
+                int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned);
+
+// sivir::open's loop (sivir.cc:31-41) as device passes.  One pass replays from `start` until
+// scan_record would return false, or until an accepted size-0 record carries the chain past a
+// segment's end (kWalSpill, engine.h): the reference then enters the next segment 1-4 bytes in
+// (it advances record.size() = 12, wal.cc:66 / sivir.cc:38), so the next pass starts there.
+// The records of all passes are concatenated.  A chain carried past the image's last segment
+// ends replay (scan_record finds no segment, wal.cc:86) with the stop offset past wal_bytes,
+// where sivir::open's start_wal_offset is left.
 int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
-                int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned = nullptr);
+                int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned = nullptr) {
+    uint64_t total = 0;
+    while (true) {
+        uint64_t n = 0, stop = 0;
+        int status = 0;
+        const uint64_t got = std::min<uint64_t>(total, rec_cap);
+        if (const int rc = replay_pass(d_wal, fill, wal_bytes, seg_bytes, start, &n, &stop, &status,
+                                       h_rec_off ? h_rec_off + got : nullptr, rec_cap - got, device, tuning, h_pinned))
+            return rc;
+        total += n;
+        if (status != (int)karma::engine::kWalSpill) {
+            *h_n_records = total;
+            *h_stop = stop;
+            *h_status = status;
+            return 0;
+        }
+        start = stop;  // > the previous start: every pass makes progress
+        if (start >= wal_bytes) {  // carried past the last segment: scan_record finds none
+            *h_n_records = total;
+            *h_stop = start;
+            *h_status = KARMA_WAL_END;
+            return 0;
+        }
+    }
+}
 
 }  // namespace
 
@@ -209,10 +244,10 @@ int karma_wal_replay_tuned(const void* h_wal, const void* d_wal, size_t wal_byte
 
 namespace {
 
-// The replay proper (karma_wal_replay): the image is d_wal, or produced by fill and
-// streamed into HBM (or, h_pinned: the same image in page-locked host memory, one DMA).
-// Offsets in and out are relative to the image start.
-int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
+// One replay pass (replay_core): the image is d_wal, or produced by fill and streamed into
+// HBM (or, h_pinned: the same image in page-locked host memory, one DMA).  Offsets in and
+// out are relative to the image start.
+int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                 int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned) {
     using namespace karma::engine;

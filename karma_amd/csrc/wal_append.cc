@@ -255,8 +255,10 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
             // the small-record kernel reads each record's offset and length once and writes its CRC
             // once: it does so over PCIe, from and into the fine-grained host arrays, so the block's
             // only copy is its payload DMA (the small copies each cost the DMA engine ~10 us)
-            if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, hoff, hl + lo, nr, phi - plo, max_len, nullptr,
-                                                                 0, hc + lo, s))
+            // (a block of empty payloads has max_len 0, which the ABI reads as "no bound": bound it
+            // by 1 so it too takes the small-record kernel and not the unknown-total plan)
+            if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, hoff, hl + lo, nr, phi - plo,
+                                                                 std::max<uint32_t>(max_len, 1), nullptr, 0, hc + lo, s))
                 return rc;
         } else {
             if (hipMemcpyAsync(doff, hoff, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||

@@ -20,7 +20,10 @@
 //
 // The size-0 quirk is kept: read_exact_at returns early for size 0
 // (segment_file.cc:8), so the CRC compared is that of the stale 4-byte len/type
-// word (wal.cc:50-60); the walk checks it in place.
+// word (wal.cc:50-60); the walk checks it in place.  An accepted size-0 record is 12
+// bytes long to sivir::open: scan_record appends the 4 stale bytes (wal.cc:66) and the
+// loop advances by record.size() (sivir.cc:38), so the next header is read at +12
+// (kStaleAdvance); past the segment end the walk reports kWalSpill (engine.h).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,6 +46,9 @@ constexpr uint32_t crc_word_host(uint32_t w) {
 }
 constexpr uint32_t kStaleZero = crc_word_host(0);
 static_assert(kStaleZero == 0x48674BC7u, "crc32c::Value of four zero bytes");
+// sivir::open's advance over an accepted size-0 record: 8 header bytes + the 4 stale bytes
+// scan_record appended to it (wal.cc:47-51, :66; sivir.cc:38).
+constexpr uint32_t kStaleAdvance = 12;
 
 #ifdef KARMA_AB  // k_wal_walk: the workgroup walker, tools build only (ab.h)
 constexpr int kWalkThreads = 256;
@@ -131,7 +137,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
                         llen[b][nc] = 0;
                         lcrc[b][nc] = crc;
                         ++nc;
-                        pos = npos;
+                        pos += kStaleAdvance;  // record.size() = 12 (wal.cc:66, sivir.cc:38)
                         continue;
                     }
                     done = 1;
@@ -172,6 +178,10 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
         }
     }
     if (threadIdx.x == 0) {
+        if (!kind && pos > seg) {  // a size-0 record's advance left the segment (kWalSpill)
+            kind = kWalSpill;
+            stop = pos;
+        }
         A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg), mx, 0u};
         A.span[2 * blockIdx.x] = 0;
         A.span[2 * blockIdx.x + 1] = 0;
@@ -294,7 +304,8 @@ struct WalkEnd {
     uint32_t max_len;  // their largest payload
     uint32_t kind;   // KARMA_WAL_CORRUPT / _BAD_TYPE, or 0
     uint32_t stop;   // where kind was found
-    uint32_t pos;    // where the walk left off (seg after a type-1 padding record)
+    uint32_t pos;    // where the walk left off (seg after a type-1 padding record; up to seg + 4
+                     // after a size-0 record at the segment end: kWalSpill)
 };
 
 // Walk the header chain from pos while pos < hi, with scan_record's checks (wal.cc:34-87):
@@ -413,7 +424,7 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
                 const uint32_t type = st & 0xffu;
                 if (type == 0 && npos <= seg && crc == kStaleZero) {  // size 0: the stale word
                     push(pos, 0u, crc);
-                    pos = npos;
+                    pos += kStaleAdvance;  // record.size() = 12 (wal.cc:66, sivir.cc:38); may pass seg
                     continue;
                 }
                 done = 1;
@@ -466,7 +477,7 @@ __device__ __forceinline__ bool header_ok(uint32_t crc, uint32_t st, uint32_t c,
                                           bool* last) {
     const uint32_t type = st & 0xffu, size = st >> 8;
     *last = false;
-    *next = c + 8 + size;
+    *next = c + (size ? 8 + size : kStaleAdvance);
     if (type == 1) {
         *last = true;
         return crc == 0;
@@ -547,7 +558,9 @@ __global__ __launch_bounds__(64) void k_wal_walk_sub(WalArgs A) {
     const WalkEnd E = walk_range(W, S, lane, first, hi, A, slot, A.sub_cap, start < lo && first < hi ? lo : ~0u);
     if (lane != 0) return;
     if (P == 1) {
-        KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{E.count, E.kind, A.base0 + rel + (E.kind ? E.stop : S.seg), E.max_len, 0u}));
+        const bool spill = !E.kind && E.pos > S.seg;  // a size-0 record's advance left the segment
+        const uint32_t kind = spill ? kWalSpill : E.kind, stop = spill ? E.pos : E.stop;
+        KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{E.count, kind, A.base0 + rel + (kind ? stop : S.seg), E.max_len, 0u}));
         KB_WRITE(A.span, 2 * s, 2 * A.nwork, kKbSpan, 0u);
         KB_WRITE(A.span, 2 * s + 1, 2 * A.nwork, kKbSpan, 0u);
     } else {
@@ -688,6 +701,10 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
             KB_WRITE(A.span, 2 * (s * P + j) + 1, 2 * A.nwork * P, kKbSpan, count);  // candidates before the run
         }
         count += n;
+    }
+    if (!kind && pos > seg) {  // a size-0 record's advance left the segment
+        kind = kWalSpill;
+        stop = pos;
     }
     if (lane == 0) KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg), mx, 0u}));
 }

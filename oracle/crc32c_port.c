@@ -133,6 +133,12 @@ void oracle_splitmix_bytes(uint64_t seed, uint64_t byte_off, uint8_t* dst, size_
     size_t k = 0;
     while (k < n) {
         uint64_t pos = byte_off + k;
+        if ((pos & 7u) == 0 && n - k >= 8) {  /* whole words (little-endian host) */
+            uint64_t w = splitmix_word(seed, pos >> 3);
+            memcpy(dst + k, &w, 8);
+            k += 8;
+            continue;
+        }
         uint64_t w = splitmix_word(seed, pos >> 3);
         unsigned sh = (unsigned)(pos & 7u);
         size_t take = 8 - sh;

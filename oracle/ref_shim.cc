@@ -126,7 +126,7 @@ uint64_t ref_wal_replay_mt(const void* wal, uint64_t wal_bytes, uint64_t seg, in
                     const char* data = reinterpret_cast<const char*>(size ? w + off + 8 : w + off + 4);
                     if (crc32c::Value(data, size ? size : 4) != crc) break;
                     ++cnt;
-                    off += 8 + size;
+                    off += 8 + (size ? size : 4);  // record.size(): + the 4 stale bytes (wal.cc:66, sivir.cc:38)
                 }
             }
             done[t] = cnt;

@@ -10,7 +10,10 @@
 //      corrupted and random buffers;
 //   4. wal_walk_plan's sub-range split for many segment sizes, counts and CU counts;
 //   5. without a device: every C ABI entry point with real arguments runs its host part
-//      (validation, placement, directory scan, structural walks) and refuses cleanly.
+//      (validation, placement, directory scan, structural walks) and refuses cleanly;
+//   6. the grouped point-to-point gather (gather_p2p.h, karma_crc32c_gather_u32 without
+//      ncclGather) through a recording stub of the RCCL calls: every rank's shard lands at
+//      recv + p * count on the root, the root's own by its copy, each slot written once.
 #include <hip/hip_runtime_api.h>
 #include <unistd.h>
 
@@ -23,6 +26,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "gather_p2p.h"
 #include "karma-util/crc32c.h"
 #include "karma_crc32c.h"
 #include "wal_place.h"
@@ -286,6 +290,99 @@ void test_abi_without_device() {
 
 }  // namespace
 
+// A stub of the RCCL calls gather_p2p makes: records them (rank, op, buffer, count, peer).
+struct P2POp {
+    int rank;
+    char op;  // 'S' send, 'R' recv, 'C' root's copy, '[' / ']' group
+    const uint32_t* src;
+    uint32_t* dst;
+    size_t count;
+    int peer;
+};
+struct StubOps {
+    int rank;
+    std::vector<P2POp>* log;
+    int fail_at = -1;  // make the n-th operation of this rank fail (error paths)
+    int n = 0;
+    int rec(P2POp o) {
+        log->push_back(o);
+        return n++ == fail_at ? KARMA_E_RCCL : 0;
+    }
+    int group_start() { return rec({rank, '[', nullptr, nullptr, 0, -1}); }
+    int group_end() { return rec({rank, ']', nullptr, nullptr, 0, -1}); }
+    int send(const uint32_t* b, size_t c, int peer) { return rec({rank, 'S', b, nullptr, c, peer}); }
+    int recv(uint32_t* b, size_t c, int peer) { return rec({rank, 'R', nullptr, b, c, peer}); }
+    int copy(uint32_t* d, const uint32_t* s, size_t c) { return rec({rank, 'C', s, d, c, rank}); }
+};
+
+void test_gather_p2p() {
+    for (int nranks = 1; nranks <= 8; ++nranks)
+        for (int root = 0; root < nranks; ++root)
+            for (size_t count : {size_t(0), size_t(1), size_t(5), size_t(1000)}) {
+                std::vector<std::vector<uint32_t>> shard(nranks);
+                for (int p = 0; p < nranks; ++p)
+                    for (size_t i = 0; i < count; ++i) shard[p].push_back(uint32_t(p) << 24 | uint32_t(i));
+                std::vector<uint32_t> out(nranks * count + 1, 0xDEADBEEFu);  // + a guard word
+                std::vector<P2POp> log;
+                for (int p = 0; p < nranks; ++p) {
+                    StubOps ops{p, &log};
+                    CHECK(gather_p2p(ops, p, nranks, root, shard[p].data(), count,
+                                     p == root ? out.data() : nullptr) == 0);
+                }
+                // match the root's receives with the senders' sends, then apply them and the copy
+                std::vector<int> written(nranks * count, 0);
+                int sends = 0, recvs = 0, copies = 0;
+                for (const P2POp& o : log) {
+                    if (o.op == 'S') {
+                        ++sends;
+                        CHECK(o.rank != root && o.peer == root && o.count == count && o.src == shard[o.rank].data());
+                    } else if (o.op == 'R' || o.op == 'C') {
+                        CHECK(o.rank == root);
+                        const int from = o.op == 'R' ? o.peer : root;
+                        CHECK(o.count == count && from >= 0 && from < nranks);
+                        CHECK(o.dst == out.data() + (size_t)from * count);  // slot p * count
+                        if (o.op == 'R') {
+                            ++recvs;
+                            CHECK(from != root);
+                        } else {
+                            ++copies;
+                            CHECK(o.src == shard[root].data());
+                        }
+                        for (size_t i = 0; i < o.count; ++i) {
+                            const size_t slot = (size_t)(o.dst - out.data()) + i;
+                            CHECK(slot < (size_t)nranks * count);
+                            ++written[slot];
+                            out[slot] = shard[from][i];
+                        }
+                    }
+                }
+                CHECK(sends == nranks - 1 && recvs == nranks - 1 && copies == (count ? 1 : 0));
+                for (size_t i = 0; i < (size_t)nranks * count; ++i) CHECK(written[i] == 1);
+                for (int p = 0; p < nranks; ++p)
+                    for (size_t i = 0; i < count; ++i) CHECK(out[(size_t)p * count + i] == shard[p][i]);
+                CHECK(out.back() == 0xDEADBEEFu);
+                // the root's ops sit inside one group, the copy after it
+                int depth = 0;
+                for (const P2POp& o : log)
+                    if (o.rank == root) {
+                        if (o.op == '[') ++depth;
+                        if (o.op == ']') --depth;
+                        if (o.op == 'R') CHECK(depth == 1);
+                        if (o.op == 'C') CHECK(depth == 0);
+                    }
+            }
+    // a failing receive: the group is still closed, the error returned, no copy made
+    for (int fail = 0; fail < 3; ++fail) {
+        std::vector<uint32_t> a(4, 1), out(16, 0);
+        std::vector<P2POp> log;
+        StubOps ops{0, &log, fail};
+        CHECK(gather_p2p(ops, 0, 4, 0, a.data(), 4, out.data()) == KARMA_E_RCCL);
+        CHECK(!log.empty() && (fail == 0 || log.back().op == ']'));
+        for (const P2POp& o : log) CHECK(o.op != 'C');
+    }
+    std::printf("gather_p2p: slots checked for 1..8 ranks, every root\n");
+}
+
 int main() {
     std::mt19937_64 rng(20260131);
     test_host_crc(rng);
@@ -293,6 +390,7 @@ int main() {
     test_kfp_walk(rng);
     test_walk_plan();
     test_abi_without_device();
+    test_gather_p2p();
     if (g_fail) {
         std::printf("host_logic_test: %d failures\n", g_fail);
         return 1;

@@ -31,7 +31,8 @@ namespace {
 
 constexpr uint32_t kWTile = 4096, kWQV = kWTile / 1024, kChainCheck = 4, kMaxSub = 4096, kWSmall = 1024;
 constexpr uint32_t kStaleZero = 0x48674BC7u;  // crc32c::Value("\0\0\0\0")
-enum { END = 0, CORRUPT = 1, BAD_TYPE = 2 };
+constexpr uint32_t kStaleAdvance = 12;         // an accepted size-0 record: 8 + 4 stale bytes (sivir.cc:38)
+enum { END = 0, CORRUPT = 1, BAD_TYPE = 2, SPILL = 16 };
 
 uint64_t g_reads = 0, g_slots = 0;
 
@@ -200,7 +201,7 @@ WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List&
                 const uint32_t type = st & 0xffu;
                 if (type == 0 && npos <= seg && crc == kStaleZero) {
                     push(pos, 0u, crc);
-                    pos = npos;
+                    pos += kStaleAdvance;
                     continue;
                 }
                 done = 1;
@@ -240,7 +241,7 @@ WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List&
 bool header_ok(uint32_t crc, uint32_t st, uint32_t c, uint32_t seg, uint32_t* next, bool* last) {
     const uint32_t type = st & 0xffu, size = st >> 8;
     *last = false;
-    *next = c + 8 + size;
+    *next = c + (size ? 8 + size : kStaleAdvance);
     if (type == 1) {
         *last = true;
         return crc == 0;
@@ -322,29 +323,15 @@ struct SegMeta {
     uint32_t max_len;
 };
 
-}  // namespace
-
-int main(int argc, char** argv) {
-    if (argc != 6) {
-        std::fprintf(stderr, "usage: %s image seg_bytes start sub_bytes cu\n", argv[0]);
-        return 2;
-    }
-    FILE* f = std::fopen(argv[1], "rb");
-    if (!f) return 2;
-    std::vector<uint8_t> file;
-    uint8_t buf[1 << 16];
-    size_t got;
-    while ((got = std::fread(buf, 1, sizeof buf, f)) > 0) file.insert(file.end(), buf, buf + got);
-    std::fclose(f);
-    const uint64_t wal_bytes = file.size(), seg_bytes = std::strtoull(argv[2], nullptr, 10);
-    const uint64_t start = std::strtoull(argv[3], nullptr, 10), force_sub = std::strtoull(argv[4], nullptr, 10);
-    const int cu = std::atoi(argv[5]);
-    if (!seg_bytes || wal_bytes % seg_bytes || start > wal_bytes || seg_bytes >= (1ull << 31)) return 2;
-    // replay_core (wal.cc)
+// replay_pass (wal.cc): one device pass from start; appends the accepted offsets to recs
+void replay_pass(const std::vector<uint8_t>& file, uint64_t seg_bytes, uint64_t start, uint64_t force_sub, int cu,
+                 std::vector<uint64_t>& recs, uint64_t& end_out, int& status_out) {
+    const uint64_t wal_bytes = file.size();
     const uint64_t nseg = wal_bytes / seg_bytes, s0 = std::min<uint64_t>(start / seg_bytes, nseg), nwork = nseg - s0;
     if (!nwork) {
-        std::printf("%d %llu %d\n", 0, (unsigned long long)start, END);
-        return 0;
+        end_out = start;
+        status_out = END;
+        return;
     }
     const uint64_t base0 = s0 * seg_bytes, first_pos = start - base0;
     // the image as the kernels see it: A.wal = a 256-byte aligned copy of segments s0.. (the
@@ -375,7 +362,9 @@ int main(int argc, char** argv) {
             const WalkEnd E = walk_range(W, S, first, hi, L);
             if (E.count > plan.sub_cap) die("walker list longer than its capacity", E.count, plan.sub_cap);
             if (plan.nsub == 1) {
-                meta[s] = SegMeta{E.count, E.kind, base0 + rel + (E.kind ? E.stop : S.seg), E.max_len};
+                const bool spill = !E.kind && E.pos > S.seg;
+                const uint32_t kind = spill ? (uint32_t)SPILL : E.kind, stop = spill ? E.pos : E.stop;
+                meta[s] = SegMeta{E.count, kind, base0 + rel + (kind ? stop : S.seg), E.max_len};
                 span[2 * s] = 0;
                 span[2 * s + 1] = 0;
             } else {
@@ -437,6 +426,10 @@ int main(int argc, char** argv) {
                 span[2 * (s * P + j) + 1] = count;
                 count += n;
             }
+            if (!kind && pos > seg) {
+                kind = SPILL;
+                stop = pos;
+            }
             meta[s] = SegMeta{count, kind, base0 + rel + (kind ? stop : seg), mx};
         }
     // replay_core: replay enters segment s + 1 only if segment s ended cleanly
@@ -497,10 +490,48 @@ int main(int argc, char** argv) {
         status = CORRUPT;
         end = base0 + off[first_bad];
     }
-    std::printf("%llu %llu %d\n", (unsigned long long)accepted, (unsigned long long)end, status);
-    for (uint64_t g = 0; g < accepted; ++g) std::printf("%llu\n", (unsigned long long)(off[g] + base0));
-    std::fprintf(stderr, "plan nsub=%llu sub_bytes=%llu; checked %llu walker reads, %llu list slots\n",
-                 (unsigned long long)plan.nsub, (unsigned long long)plan.sub_bytes, (unsigned long long)g_reads,
-                 (unsigned long long)g_slots);
+    for (uint64_t g = 0; g < accepted; ++g) recs.push_back(off[g] + base0);
+    end_out = end;
+    status_out = status;
+    std::fprintf(stderr, "pass from %llu: plan nsub=%llu sub_bytes=%llu; checked %llu walker reads, %llu list slots\n",
+                 (unsigned long long)start, (unsigned long long)plan.nsub, (unsigned long long)plan.sub_bytes,
+                 (unsigned long long)g_reads, (unsigned long long)g_slots);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc != 6) {
+        std::fprintf(stderr, "usage: %s image seg_bytes start sub_bytes cu\n", argv[0]);
+        return 2;
+    }
+    FILE* f = std::fopen(argv[1], "rb");
+    if (!f) return 2;
+    std::vector<uint8_t> file;
+    uint8_t buf[1 << 16];
+    size_t got;
+    while ((got = std::fread(buf, 1, sizeof buf, f)) > 0) file.insert(file.end(), buf, buf + got);
+    std::fclose(f);
+    const uint64_t wal_bytes = file.size(), seg_bytes = std::strtoull(argv[2], nullptr, 10);
+    uint64_t start = std::strtoull(argv[3], nullptr, 10);
+    const uint64_t force_sub = std::strtoull(argv[4], nullptr, 10);
+    const int cu = std::atoi(argv[5]);
+    if (!seg_bytes || wal_bytes % seg_bytes || start > wal_bytes || seg_bytes >= (1ull << 31)) return 2;
+    // replay_core (wal.cc): passes until the chain no longer spills past a segment end
+    std::vector<uint64_t> recs;
+    uint64_t end = 0;
+    int status = END;
+    while (true) {
+        replay_pass(file, seg_bytes, start, force_sub, cu, recs, end, status);
+        if (status != SPILL) break;
+        if (end <= start) die("spill pass made no progress", start, end);
+        start = end;
+        if (start >= wal_bytes) {
+            status = END;
+            break;
+        }
+    }
+    std::printf("%llu %llu %d\n", (unsigned long long)recs.size(), (unsigned long long)end, status);
+    for (uint64_t r : recs) std::printf("%llu\n", (unsigned long long)r);
     return 0;
 }

@@ -252,6 +252,35 @@ def test_config5_shards_concatenate_to_whole_batch(dev):
     _eq(np.concatenate(parts), whole)
 
 
+def test_config5_full_shard(dev):
+    """BASELINE configs[4]'s per-GPU work on one GPU: rank 7's shard of 256M x 4 KiB records,
+    33,554,432 records = 128 GiB at first_byte = 7 * shard * 4096 (bench.py's N = 8 default),
+    generated on the device as that rank's slice of the global stream.  Every one of the 33.5M
+    CRCs is checked against the oracle, computed in slices of 4M records on the host threads
+    (SURVEY §8(d) config 5 asks for a 1M-record sample + a rolling digest; the full comparison
+    covers both), and the XOR / 64-bit-sum digests of the two arrays are compared as well.
+    Per-record independence: karma-store/segment_file.cc:22, wal.cc:60."""
+    from karma_amd.shard import shard_range
+    n_total, world, rank, rec = 1 << 28, 8, 7, 4096
+    lo, hi = shard_range(n_total, world, rank)
+    n = hi - lo
+    assert n == 33_554_432
+    buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 42, first_byte=lo * rec)
+    got = K.value_batch_fixed(buf, rec).cpu().numpy()
+    del buf
+    torch.cuda.empty_cache()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    step = 1 << 22
+    want = np.empty(n, np.uint32)
+    for a in range(0, n, step):
+        b = min(n, a + step)
+        want[a:b] = oracle_lib.splitmix_fixed_crcs(42, rec, lo + a, b - a, threads=threads)
+    assert int(np.bitwise_xor.reduce(got)) == int(np.bitwise_xor.reduce(want))
+    assert int(got.astype(np.uint64).sum()) == int(want.astype(np.uint64).sum())
+    _eq(got, want)
+
+
 def test_rccl_gather_world1(dev):
     L = _lib.lib()
     uid = (ctypes.c_char * _lib.UNIQUE_ID_BYTES)()
@@ -371,6 +400,62 @@ def test_ragged_plan_many_blocks_lookback(raw, dev, build, monkeypatch):
         for i in range(7):
             (n, o, want), (d_off, d_len) = cases[i % 2], dl[i % 2]
             _eq(K.extend_batch_ragged(dbuf, d_off, d_len, total_len=int(n.sum())).cpu().numpy(), want)
+
+
+def test_ragged_graph_capture_replays(dev):
+    """A ragged call captured in a hipGraph replays any number of times: the single-pass plan's
+    block ids and look-back tags come from the device (k_ragged_plan / k_ragged_finalize), not
+    from host state baked into the captured arguments.  200K records = 196 plan blocks, replayed
+    three times with new payload bytes AND new lengths / offsets in the same buffers (sum(len) <=
+    total_len), each replay exact against the oracle; uncaptured calls of other sizes run on the
+    same stream between replays (they grow the stream's workspace: the graph's buffers must
+    survive that)."""
+    n, arena_bytes = 200_000, 48 << 20
+    cap_total = 60 << 20
+    arena = torch.empty(arena_bytes, dtype=torch.uint8, device=dev)
+    d_off = torch.empty(n, dtype=torch.int64, device=dev)
+    d_len = torch.empty(n, dtype=torch.int32, device=dev)
+    out = torch.empty(n, dtype=torch.uint32, device=dev)
+
+    def load(seed):
+        rng = np.random.default_rng(seed)
+        lens = np.where(rng.random(n) < 0.01, rng.integers(0, 30000, n), rng.integers(0, 400, n)).astype(np.uint32)
+        offs = rng.integers(0, arena_bytes - 30000, n).astype(np.uint64)
+        host = rng.integers(0, 256, arena_bytes, dtype=np.uint8)
+        assert int(lens.sum()) <= cap_total
+        arena.copy_(torch.from_numpy(host))
+        d_off.copy_(torch.from_numpy(offs.astype(np.int64)))
+        d_len.copy_(torch.from_numpy(lens.astype(np.int32)))
+        return oracle_lib.ragged_crcs(host, offs, lens)
+
+    s = torch.cuda.Stream()
+    want = load(1)
+    with torch.cuda.stream(s):  # the uncaptured call that sizes the stream's workspace
+        K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=cap_total, stream=s)
+    s.synchronize()
+    _eq(out.cpu().numpy(), want)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=cap_total, stream=s)
+    for seed in (2, 3, 4):
+        torch.cuda.synchronize()
+        want = load(seed)
+        torch.cuda.synchronize()
+        out.view(torch.int32).fill_(-0x5A5A5A5B)  # 0xA5A5A5A5: no stale right answer
+        g.replay()
+        torch.cuda.synchronize()
+        _eq(out.cpu().numpy(), want)
+        # an uncaptured, larger call on the same stream between replays
+        rng = np.random.default_rng(seed + 10)
+        m = 3 * n // 2 + seed
+        lens = rng.integers(0, 2000, m).astype(np.uint32)
+        offs = rng.integers(0, arena_bytes - 2000, m).astype(np.uint64)
+        with torch.cuda.stream(s):
+            got = K.extend_batch_ragged(arena, torch.from_numpy(offs.astype(np.int64)).to(dev),
+                                        torch.from_numpy(lens.astype(np.int32)).to(dev), total_len=int(lens.sum()),
+                                        stream=s)
+        s.synchronize()
+        _eq(got.cpu().numpy(), oracle_lib.ragged_crcs(arena.cpu().numpy(), offs, lens))
 
 
 def test_ragged_unknown_total_workspace_growth(raw, dev):

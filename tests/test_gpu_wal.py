@@ -452,3 +452,33 @@ def test_replay_segment_counts_around_the_fused_plan(lib, nseg):
     got = _replay(lib, wal, seg=seg)
     w = wal_model.replay(wal.tobytes(), seg)
     assert got == (list(w[0]), w[1], w[2]) and len(got[0]) == k
+
+
+@pytest.mark.parametrize("walk", list(WALKS))
+@pytest.mark.parametrize("seg", [65536, 16384 + 4, 1 << 20])
+def test_replay_accepted_size0_records_advance_12(lib, seg, walk, monkeypatch):
+    """An empty record whose stored CRC is Value("\\0\\0\\0\\0") = 0x48674BC7 passes scan_record's
+    stale-word check (wal.cc:47-60) and is returned 12 bytes long (wal.cc:66); sivir::open then
+    reads the next header 12 bytes on (sivir.cc:38), into the next segment when the record sits in
+    a segment's last 11 bytes, and past the image end at the last segment (tests/wal_images.py
+    stale_empty: such records mid-run, around every tile / sub-range edge, at seg-8..seg-13 and at
+    the image end).  Every walk plan must give scan_record's result, from the start and from
+    checkpoints on such records, over the host image and the device copy alone."""
+    import wal_images
+    _walk_env(monkeypatch, walk)
+    nseg = 3 if seg == (1 << 20) else 6
+    spills = 0
+    for seed in range(3):
+        wal, heads = wal_images.stale_empty(seg, nseg, seed * 7 + (seg & 0xFF) + len(walk))
+        w = wal_model.replay(wal.tobytes(), seg)
+        assert w[0] == heads[: len(w[0])]
+        zs = [h for h in w[0] if int.from_bytes(wal[h + 4: h + 8].tobytes(), "little") == 0]
+        assert zs, "the image must hold accepted size-0 records"
+        spills += sum(1 for h in zs if h % seg + 12 > seg)
+        assert _replay(lib, wal, seg=seg) == (list(w[0]), w[1], w[2])
+        d = torch.from_numpy(wal).cuda()
+        assert _replay(lib, wal, d_wal=d, host=False, seg=seg) == (list(w[0]), w[1], w[2])
+        for start in (zs[len(zs) // 2], zs[-1], zs[-1] + 12 if zs[-1] + 12 <= wal.size else zs[-1]):
+            ws = wal_model.replay(wal.tobytes(), seg, start)
+            assert _replay(lib, wal, start=start, seg=seg) == (list(ws[0]), ws[1], ws[2]), start
+    assert spills > 0, "some size-0 record must carry the chain into the next segment"

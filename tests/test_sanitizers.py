@@ -114,3 +114,18 @@ def test_emulated_walk_zero_image_and_end(san_build):
     wal = np.zeros(4 * (64 << 10), np.uint8)
     _check(san_build, wal, 64 << 10, 0)
     assert _emulate(san_build, wal, 64 << 10, wal.nbytes, 0) == ([], wal.nbytes, wal_model.END)
+
+
+@pytest.mark.parametrize("seg", [65536, 16384 + 4])
+def test_emulated_walk_accepted_size0_records(san_build, seg):
+    """Accepted size-0 records (stored CRC Value("\\0\\0\\0\\0")) advance the chain by 12 bytes
+    (wal.cc:66, sivir.cc:38), across tile / sub-range edges and into the next segment
+    (tests/wal_images.py stale_empty): the emulated walk matches scan_record, every access in
+    bounds, from the start and from checkpoints on such records."""
+    for seed in range(3):
+        wal, heads = wal_images.stale_empty(seg, 6, 100 + seed)
+        want = wal_model.replay(wal.tobytes(), seg)
+        zs = [h for h in want[0] if int.from_bytes(wal[h + 4: h + 8].tobytes(), "little") == 0]
+        assert zs
+        for start in (0, zs[len(zs) // 2], zs[-1]):
+            _check(san_build, wal, seg, start)

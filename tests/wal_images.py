@@ -122,3 +122,99 @@ def uniform_runs(seg, seed=5):
     nseg = int((lens.astype(np.int64) + 8).sum() // (seg - 4096) + 3)
     wal, rec = frame(src, offs, lens, seg, nseg)
     return wal, seg, rec, lens
+
+
+STALE_ZERO = 0x48674BC7  # crc32c::Value("\0\0\0\0"): the stored CRC a size-0 record needs to pass
+
+
+def stale_empty(seg, nseg, seed):
+    """Images with ACCEPTED size-0 records ("Z": header [0x48674BC7][len 0 | type 0]).  scan_record
+    checks such a record against the stale len/type word (wal.cc:47-60, segment_file.cc:8) and
+    returns it 12 bytes long (wal.cc:66), so sivir::open reads the next header 12 bytes on
+    (sivir.cc:38); the 4 bytes after the header are never looked at (random here).  Z records are
+    placed
+      * inside uniform runs of one record size (the walker's speculative header rounds),
+      * at every offset from 14 bytes before to 2 bytes after a 4 KiB tile edge (the tile edges
+        are the sub-range edges of the split plans), so the header or the 12-byte advance
+        straddles it,
+      * at a segment's last header positions seg-8-d (d = 0..5): for d <= 3 the advance carries
+        the chain 4-d bytes into the next segment, which the writer here continues at that
+        offset (the skipped bytes are random); d = 4 ends exactly at the segment end,
+      * at the image end (the chain leaves the image: replay ends past wal_bytes), or followed
+        by the never-written zero tail.
+    Returns (image, header offsets of every record and Z, in WAL order)."""
+    rng = np.random.default_rng(seed)
+    wal = np.zeros(nseg * seg, np.uint8)
+    heads = []
+    c = 0
+
+    def rec(n):
+        nonlocal c
+        p = rng.integers(0, 256, n, dtype=np.uint8)
+        crc = wal_model.oracle_lib.extend(0, p.tobytes())
+        wal[c: c + 8] = np.frombuffer(np.array([crc, n << 8], "<u4").tobytes(), np.uint8)
+        wal[c + 8: c + 8 + n] = p
+        heads.append(c)
+        c += 8 + n
+
+    def z():
+        nonlocal c
+        wal[c: c + 8] = np.frombuffer(np.array([STALE_ZERO, 0], "<u4").tobytes(), np.uint8)
+        e = min(c + 12, wal.size)
+        wal[c + 8: e] = rng.integers(0, 256, e - c - 8, dtype=np.uint8)
+        heads.append(c)
+        c += 12
+
+    def goto(t):  # one record from c to exactly t (same segment, t - c >= 9), or False
+        if t - c < 9:
+            return False
+        rec(t - c - 8)
+        return True
+
+    def pad():  # append_footer (segment_file.cc:33-49)
+        nonlocal c
+        end = (c // seg + 1) * seg
+        if end - c >= 8:
+            wal[c: c + 8] = np.frombuffer(np.array([0, ((end - c - 8) << 8) | 1], "<u4").tobytes(), np.uint8)
+            wal[c + 8: end] = ord("0")
+        else:
+            wal[c: end] = ord("0")
+        c = end
+
+    for s in range(nseg):
+        base, end = s * seg, (s + 1) * seg
+        if c >= end:
+            continue
+        size = int(rng.choice([1, 24, 180, 500]))
+        edge_k = list(range(-14, 3))
+        rng.shuffle(edge_k)
+        tail_d = int(rng.integers(0, 6)) if s < nseg - 1 else int(rng.choice([0, 1, 3, 7]))
+        while True:
+            pos = c - base
+            room = seg - pos
+            if room < 2 * (8 + size) + 64:
+                break
+            t_edge = (pos // 4096 + 1) * 4096
+            r = rng.random()
+            if r < 0.06:
+                z()
+            elif r < 0.12 and edge_k and t_edge + 3 < seg - 64:  # a Z around the next tile edge
+                if goto(base + t_edge + edge_k[-1]):
+                    edge_k.pop()
+                    z()
+            else:
+                rec(size)
+        if s == nseg - 1 and tail_d == 7:  # the zero tail after a Z (stored CRC 0: "Corrupt record")
+            z()
+            break
+        # the segment end: a Z at seg - 8 - tail_d (d <= 3: spill 4 - d bytes; d = 4: exact end)
+        zpos = base + seg - 8 - tail_d
+        if goto(zpos):
+            z()
+            if end < c <= wal.size:  # the next segment is entered at c - end; its first bytes are skipped
+                wal[end: c] = rng.integers(0, 256, c - end, dtype=np.uint8)
+            elif c < end:
+                pad()
+        else:
+            pad()
+    return wal, heads

@@ -6,7 +6,8 @@ karma_wal_append_batch / karma_wal_replay).
              append_record (:21-31)
 * replay  -- sivir::open's loop (sivir.cc:31-41) over wal::scan_record (wal.cc:34-87),
              including the size-0 quirk: read_exact_at returns early for size 0
-             (segment_file.cc:8), so the CRC is taken over the stale len/type word (wal.cc:50-60)
+             (segment_file.cc:8), so the CRC is taken over the stale len/type word (wal.cc:50-60),
+             and an accepted size-0 record is 12 bytes long to the loop (wal.cc:66, sivir.cc:38)
 CRCs come from the oracle (oracle/crc32c_port.c).
 """
 from __future__ import annotations
@@ -64,7 +65,9 @@ def replay(wal: bytes, seg: int, start: int = 0):
             if oracle_lib.extend(0, bytes(data)) != crc:
                 return recs, off, CORRUPT
             recs.append(off)
-            off += HEADER + size
+            # sivir.cc:38 advances record.size(): for size 0 that is the 8 header bytes plus the 4
+            # stale bytes scan_record appended (wal.cc:66), so 12 -- possibly into the next segment
+            off += HEADER + size if size else HEADER + 4
         elif typ == 1:
             off = base + seg
         else:

@@ -18,6 +18,12 @@ copy for each variant in interleaved rounds (same process, same image):
 
 Every call's result is checked (record count).  Prints ms per call and GB/s of image bytes per
 variant (median over rounds).
+
+--images K (default 4): K distinct images (different payload seeds, same framing) are copied
+into HBM and the calls rotate over them, so that (K x ~201 MB > 512 MiB) no call finds its image
+in the 256 MB Infinity Cache (MALL) left behind by the previous one (SURVEY.md §7 measurement
+trap); --images 1 is the single reused image of round 2.  --single also times each variant on
+image 0 alone, printed beside the rotated rate.
 """
 import argparse
 import ctypes
@@ -38,6 +44,8 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--calls", type=int, default=20)
     p.add_argument("--variants", default="shipped,direct4,direct_v1,sub=24576,sub=32768,sub=40960")
+    p.add_argument("--images", type=int, default=4)
+    p.add_argument("--single", action="store_true")
     a = p.parse_args()
     import torch
     import synth
@@ -52,21 +60,28 @@ def main():
         lens = np.full(count, size, dtype=np.uint32)
         wal_bytes = ((count + seg // (size + 8) - 1) // (seg // (size + 8)) + 1) * seg
     offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
-    src = synth.splitmix_np(42, 0, int(lens.sum()) + 16).copy()
-    wal = np.zeros(wal_bytes, dtype=np.uint8)
     L = _lib.lib()
     cur, nf = ctypes.c_uint64(0), ctypes.c_size_t()
-    _lib.check("append", L.karma_wal_append_batch(src.ctypes.data, offs.ctypes.data, lens.ctypes.data, count,
-                                                  wal.ctypes.data, wal_bytes, seg, ctypes.byref(cur), None,
-                                                  ctypes.byref(nf), 0))
-    assert nf.value == count
-    d_wal = torch.from_numpy(wal).cuda()
+    d_wals = []
+    for k in range(a.images):
+        src = synth.splitmix_np(42 + k, 0, int(lens.sum()) + 16).copy()
+        wal = np.zeros(wal_bytes, dtype=np.uint8)
+        cur.value = 0
+        _lib.check("append", L.karma_wal_append_batch(src.ctypes.data, offs.ctypes.data, lens.ctypes.data, count,
+                                                      wal.ctypes.data, wal_bytes, seg, ctypes.byref(cur), None,
+                                                      ctypes.byref(nf), 0))
+        assert nf.value == count
+        d_wals.append(torch.from_numpy(wal).cuda())
+        del src, wal
     torch.cuda.synchronize()
+    rot = {"i": 0, "single": False}
     AB = _lib.load(_lib.AB_LIB_PATH)
     n, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
 
     def call(lib, sub, batch):
         t = _lib.WalTuning(sub, batch, 0)
+        d_wal = d_wals[0] if rot["single"] else d_wals[rot["i"] % len(d_wals)]
+        rot["i"] += 1
         st = lib.karma_wal_replay_tuned(None, d_wal.data_ptr(), wal_bytes, seg, 0, ctypes.byref(n), ctypes.byref(stop),
                                         ctypes.byref(status), None, 0, 0, ctypes.byref(t))
         assert st == 0 and n.value == count, (st, n.value)
@@ -90,23 +105,38 @@ def main():
         elif v.startswith("sub="):
             variants[v] = (L, int(v[4:]), 0, None)
     res = {v: [] for v in variants}
+    res1 = {v: [] for v in variants}
+
+    def timed(lib, sub, batch, single):
+        rot["single"] = single
+        for _ in range(3):
+            call(lib, sub, batch)
+        t0 = time.perf_counter()
+        for _ in range(a.calls):
+            call(lib, sub, batch)
+        rot["single"] = False
+        return (time.perf_counter() - t0) / a.calls * 1e3
+
     for r in range(a.rounds):
         for v, (lib, sub, batch, env) in variants.items():
             if env:
                 os.environ[env[0]] = env[1]
-            for _ in range(3):
-                call(lib, sub, batch)
-            t0 = time.perf_counter()
-            for _ in range(a.calls):
-                call(lib, sub, batch)
-            res[v].append((time.perf_counter() - t0) / a.calls * 1e3)
+            res[v].append(timed(lib, sub, batch, False))
+            if a.single:
+                res1[v].append(timed(lib, sub, batch, True))
             if env:
                 del os.environ[env[0]]
-        print(f"round {r}: " + "  ".join(f"{v} {res[v][-1]:.4f}" for v in variants), flush=True)
+        print(f"round {r}: " + "  ".join(f"{v} {res[v][-1]:.4f}" + (f" (single {res1[v][-1]:.4f})" if a.single else "")
+                                         for v in variants), flush=True)
+    print(f"images: {len(d_wals)} x {wal_bytes / 1e6:.1f} MB rotated ({len(d_wals) * wal_bytes / 2**20:.0f} MiB)")
     for v in variants:
         ms = float(np.median(res[v]))
-        print(f"{v:>14}: {ms:.4f} ms/call  {wal_bytes / ms / 1e6:.1f} GB/s image  "
-              f"{int(lens.sum()) / ms / 1e6:.1f} GB/s payload", flush=True)
+        line = (f"{v:>14}: {ms:.4f} ms/call  {wal_bytes / ms / 1e6:.1f} GB/s image  "
+                f"{int(lens.sum()) / ms / 1e6:.1f} GB/s payload (rotated)")
+        if a.single:
+            m1 = float(np.median(res1[v]))
+            line += f"   single image: {m1:.4f} ms/call  {wal_bytes / m1 / 1e6:.1f} GB/s image"
+        print(line, flush=True)
 
 
 if __name__ == "__main__":
