@@ -90,10 +90,16 @@ std::map<std::pair<int, void*>, Workspace> g_ws;
 // hipStreamPerThread is one handle for many streams: it is keyed per calling thread.
 struct Lookback {
     unsigned long long* words = nullptr;
-    uint64_t cap = 0;   // words: 1 + 2 * half + 2
+    uint64_t cap = 0;   // words: 1 + 2 * half + 3
     uint64_t half = 0;  // plan blocks a call may have
 };
 std::map<std::pair<int, void*>, Lookback> g_lb;
+
+// The fused record combine's words per (device, stream) (FixedArgs::fctl, k_units_fixed FUSE):
+// [0] workgroups finished, [1] the last finished call's tag, then kBlockCombMaxPerThread * 1024
+// tagged wave states.  Allocated and zeroed once and never moved: the tags only grow, so no
+// state a later call could read carries its tag before that call wrote it.
+std::map<std::pair<int, void*>, unsigned long long*> g_fused;
 thread_local char t_per_thread_key;  // the look-back key of this thread's hipStreamPerThread
 
 int current_device(int* dev) {
@@ -189,6 +195,18 @@ int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocate
     return 0;
 }
 
+// Caller holds g_mu.
+int fused_words(int dev, hipStream_t s, unsigned long long** out) {
+    unsigned long long*& w = g_fused[{dev, stream_key(s)}];
+    if (!w) {
+        const size_t bytes = (2 + kBlockCombMaxPerThread * 1024) * sizeof(unsigned long long);
+        KARMA_HIP(hipMalloc(&w, bytes));
+        KARMA_HIP(hipMemsetAsync(w, 0, bytes, s));
+    }
+    *out = w;
+    return 0;
+}
+
 // Caller holds g_mu.  Binds the stream's look-back words for nb plan blocks.
 int bind_lookback(int dev, hipStream_t s, uint64_t nb, RaggedArgs& a) {
     Lookback& L = g_lb[{dev, stream_key(s)}];
@@ -199,7 +217,7 @@ int bind_lookback(int dev, hipStream_t s, uint64_t nb, RaggedArgs& a) {
             L.cap = L.half = 0;
         }
         const uint64_t half = std::max<uint64_t>(2 * nb, 2048);
-        const uint64_t cap = 1 + 2 * half + 2;
+        const uint64_t cap = 1 + 2 * half + 3;
         KARMA_HIP(hipMalloc(&L.words, cap * sizeof(unsigned long long)));
         KARMA_HIP(hipMemsetAsync(L.words, 0, cap * sizeof(unsigned long long), s));
         L.half = half;
@@ -282,6 +300,9 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
     a.blob = ds.blob;
     a.comb_maps = nullptr;
     a.fold_k = fold_k;
+    a.fctl = nullptr;
+    a.block_blob = nullptr;
+    a.comb_m = 0;
     if (fold_k) {
         KARMA_RC(comb_blob(ds, unit, &a.comb_maps));
         // (the tools build's KARMA_FIXED_GRID_MULT: that many workgroups per CU, dispatched in
@@ -295,6 +316,19 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
         return 0;
     }
     KARMA_RC(comb_blob(ds, unit, &a.comb_maps));  // Z_U, Z_2U, Z_4U lead the unit's combine blob
+    if (n_rec == 1 && k / kGroupsPerWave <= kBlockCombMaxPerThread * 1024) {
+        // one record (a segment scan): the units kernel's last workgroup folds the wave states
+        // itself (k_units_fixed FUSE), one launch instead of two
+        const uint64_t k_in = k / kGroupsPerWave;
+        a.comb_m = ceil_div(k_in, 1024);
+        KARMA_RC(block_comb_blob(ds, unit * kGroupsPerWave, a.comb_m, &a.block_blob));
+        unsigned long long* w = nullptr;
+        KARMA_RC(fused_words(dev, s, &w));
+        a.fctl = w;
+        a.partial = reinterpret_cast<uint32_t*>(w + 2);
+        KARMA_HIP(launch_fixed(a, ds.cu, s));
+        return 0;
+    }
     const size_t part_bytes = align256(n_rec * k * sizeof(uint32_t));
     const size_t lvl_bytes = align256(n_rec * ceil_div(k, 64) * sizeof(uint32_t));
     void* ws = nullptr;
@@ -431,6 +465,7 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         if (fresh && two_pass) KARMA_HIP(launch_ragged_scan(a, s));
     }
     a.part_base = two_pass ? 0 : cap_full;
+    a.tail_blocks = (uint64_t)KARMA_AB_KNOB("KARMA_RAGGED_TAIL_BLOCKS", 32);
     if (!two_pass) KARMA_RC(bind_lookback(dev, s, ragged_scan_blocks(n_rec), a));
     KARMA_HIP(launch_ragged_main(a, ds.cu, s, two_pass));
     return 0;
@@ -480,6 +515,18 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
 namespace {
 thread_local hipEvent_t t_units_start = nullptr, t_units_stop = nullptr;
 }
+#ifdef KARMA_AB
+}  // namespace karma::engine
+// Tools build only (wavelog.h): the units kernels log one WaveLogRec per wave into d_buf
+// (cap records); d_buf = NULL stops the log.
+extern "C" int karma_ab_wave_log(void* d_buf, uint64_t cap) {
+    using namespace karma::engine;
+    if (set_wave_log_ragged(d_buf, d_buf ? cap : 0) != hipSuccess || set_wave_log_fixed(d_buf, d_buf ? cap : 0) != hipSuccess)
+        return KARMA_E_HIP;
+    return 0;
+}
+namespace karma::engine {
+#endif
 void units_timer_begin(hipStream_t s) {
     if (t_units_start) (void)hipEventRecord(t_units_start, s);
 }

@@ -12,6 +12,7 @@
 #include "ab.h"
 #include "crc_device.h"
 #include "engine.h"
+#include "wavelog.h"
 
 namespace karma {
 namespace engine {
@@ -68,13 +69,59 @@ __device__ __forceinline__ FixedPlan fixed_plan(const FixedArgs& A, uint64_t u, 
 // a wave hold units 8i..8i+7 of one record, end-aligned; a 3-level tree over
 // the groups (Z_U, Z_2U, Z_4U) leaves one state per 8 units, so the combine
 // kernels start one level up (a 64 MiB segment: 32768 -> 4096 states here).
-template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0, bool BAL = true, int KW = 1>
+// The fused combine of FUSE (one record, its wave states folded by the workgroup that ends last):
+// thread t folds states [t m, t m + m) with Z_D (leading zero states pad k_in to 1024 m), reading
+// each tagged state with an agent-scope atomic load until it carries this call's tag (a state
+// whose store is not visible yet is waited for; no release fence or L2 write-back is needed);
+// then the 64-lane tree and thread 0's fold of the 16 wave results, as k_combine_block.
+__device__ void fused_record_fold(const FixedArgs& A, uint32_t* lds, uint32_t* wv, uint64_t k_in, uint32_t tag) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t m = A.comb_m;
+    const int64_t pad = (int64_t)(m * 1024 - k_in);
+    const int64_t i0 = (int64_t)(threadIdx.x * m) - pad;
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(A.partial);
+    copy_to_lds<kBlockCombWords, kBlockThreads>(lds, A.block_blob);
+    __syncthreads();
+    uint32_t acc = 0;
+    for (uint64_t q = 0; q < m; ++q) {
+        uint32_t v = 0;
+        if (i0 + (int64_t)q >= 0) {
+            unsigned long long w = __hip_atomic_load(st + i0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while ((uint32_t)(w >> 32) != tag) {
+                __builtin_amdgcn_s_sleep(1);
+                w = __hip_atomic_load(st + i0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            v = (uint32_t)w;
+        }
+        acc = zmap(lds, kBcZD, acc) ^ v;
+    }
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        const uint32_t t = __shfl_down(acc, 1u << d, 64);
+        acc = zmap(lds, kBcTree + d * 1024, acc) ^ t;
+    }
+    if (lane == 0) wv[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t v = wv[0];
+        for (int w = 1; w < 16; ++w) v = zmap(lds, kBcWave, v) ^ wv[w];
+        A.out[0] = ~tail_register(lds, kBcZ4, kBcT8, v, geom(A.arena, A.rec_bytes));
+    }
+}
+
+template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0, bool BAL = true, int KW = 1, bool FUSE = false>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
+    static_assert(!FUSE || WAVE_COMB, "the fused combine folds wave states");
     KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
                  (reinterpret_cast<uintptr_t>(A.arena + A.n_rec * A.rec_bytes) + 15) & ~uintptr_t(15));
     constexpr bool kMaps = WAVE_COMB || KW > 1;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kMaps ? kLdsWordsComb : kLdsWords];
     __shared__ uint32_t blk_next;  // BAL: the block's next wave-step (an LDS counter, lgkmcnt only)
+    __shared__ uint32_t s_tag, s_last;  // FUSE: this call's tag; this block ends last
+    if (FUSE && threadIdx.x == 0) {
+        const uint32_t t = (uint32_t)__hip_atomic_load(A.fctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        s_tag = t ? t : 1u;
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & (kGroupLanes - 1);
     const uint32_t grp = lane / kGroupLanes;
@@ -102,6 +149,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     load_stream_tables(lds, A.blob);
     if constexpr (kMaps) copy_to_lds<3 * 1024, kBlockThreads>(lds + kCombLdsBase, A.comb_maps);
     __syncthreads();
+    WLOG_DECL;
+    WLOG_START();
+    const uint64_t wlog_id = wb;
+    (void)wlog_id;
     for (; wb < nws; ) {
         uint32_t inj = 0;
         if (P.inj_at) inj = P.hfrom < 16 ? steps_in_vec(lds, kLZ4, kLT8, ~iv, hv, P.hfrom, 16u) : ~iv;
@@ -131,7 +182,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
             R = zmap(lds, kCombLdsBase + 1024, R) ^ t;
             t = __shfl_down(R, 32, 64);
             R = zmap(lds, kCombLdsBase + 2048, R) ^ t;
-            if (P.valid && lane == 0) A.partial[wb] = R;  // state wb = units 8wb .. 8wb+7
+            if constexpr (FUSE) {  // tagged, visible to the last workgroup without a fence
+                if (P.valid && lane == 0)
+                    __hip_atomic_store(reinterpret_cast<unsigned long long*>(A.partial) + wb,
+                                       ((unsigned long long)s_tag << 32) | R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (P.valid && lane == 0) {
+                A.partial[wb] = R;  // state wb = units 8wb .. 8wb+7
+            }
         } else if constexpr (KW > 1) {
             // the record's KW units sit in groups KW*i .. KW*i+KW-1 of this wave (end-aligned: all
             // but the first are full); fold them into the last group, whose lanes hold the tail:
@@ -154,9 +211,28 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
             else
                 A.partial[u] = R;
         }
+        WLOG_STEP();
+        WLOG_UNIT(P.valid && l == 0, A.unit_bytes);
         P = N;
         wb = wb_next;
         u = wb * kGroupsPerWave + grp;
+    }
+    WLOG_END(wlog_id);
+    if constexpr (FUSE) {  // the workgroup that ends last folds the record's wave states
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long done =
+                __hip_atomic_fetch_add(A.fctl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = done + 1 == gridDim.x;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __shared__ uint32_t wv[16];
+        fused_record_fold(A, lds, wv, A.units_per_rec / kGroupsPerWave, s_tag);
+        if (threadIdx.x == 0) {  // ready for the next call (stream order): counter 0, tag retired
+            __hip_atomic_store(A.fctl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.fctl + 1, (unsigned long long)s_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -177,8 +253,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed_v1(FixedArgs A) {
     const uint64_t k = A.units_per_rec;
     const uint64_t U = A.n_rec * k;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    WLOG_DECL;
+    WLOG_START();
     for (uint64_t wb = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); wb * kGroupsPerWave < U;
          wb += nwaves) {
+        WLOG_STEP();
         const uint64_t u = wb * kGroupsPerWave + grp;
         const bool valid = u < U;
         uint64_t r = 0, j = 0;
@@ -209,6 +288,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed_v1(FixedArgs A) {
             }
         }
         uint32_t R = group_unit<PF, NT>(lds, X, l, us, ue, inj_at, inj);
+        WLOG_UNIT(valid && l == 0, ue - us);
         if (valid && l == 0) {
             if (g.is_short) {
                 A.out[r] = short_record(lds, kLZ4, kLT8, p, A.rec_bytes, init);
@@ -219,6 +299,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed_v1(FixedArgs A) {
             }
         }
     }
+    WLOG_END((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
 }
 
 // One combine level: record r's k_in states (end-aligned, D bytes each) ->
@@ -362,6 +443,11 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     else hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, true, KW>), grid, blk, 0, s, a);
         if (a.fold_k == 2) { KARMA_FOLD(2) } else if (a.fold_k == 4) { KARMA_FOLD(4) } else { KARMA_FOLD(8) }
 #undef KARMA_FOLD
+    } else if (a.comb_maps && a.fctl) {  // one record, its wave states folded by the last workgroup
+        if (a.n_rec != 1 || !a.block_blob || a.comb_m == 0 || a.units_per_rec / kGroupsPerWave > a.comb_m * 1024)
+            return hipErrorInvalidValue;
+        if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true, 0, true, 1, true>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_units_fixed<4, true, false, true, 0, true, 1, true>), grid, blk, 0, s, a);
     } else if (a.comb_maps) {  // k % 8 == 0, units >= 2 KiB (planner)
         if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true>), grid, blk, 0, s, a);
         else hipLaunchKernelGGL((k_units_fixed<4, true, false, true>), grid, blk, 0, s, a);
@@ -394,6 +480,9 @@ hipError_t launch_combine_block(const FixedArgs& a, const uint32_t* in_states, u
 }
 
 KB_DEFINE_COLLECT(fixed)
+#ifdef KARMA_AB
+WLOG_SETTER(fixed)
+#endif
 
 }  // namespace engine
 }  // namespace karma

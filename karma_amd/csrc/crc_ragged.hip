@@ -22,6 +22,7 @@
 #include "ab.h"
 #include "crc_device.h"
 #include "engine.h"
+#include "wavelog.h"
 
 namespace karma {
 namespace engine {
@@ -394,6 +395,7 @@ __device__ void lookback_retire(const RaggedArgs& A) {
     if (threadIdx.x == 0) {
         lb_store(A.lb, 0ull);
         lb_store(A.lb_ctl, wrap ? 0ull : (unsigned long long)seq);
+        lb_store(A.lb_ctl + 2, 0ull);  // the longest partial run (k_ragged_plan's atomicMax)
     }
 }
 
@@ -450,6 +452,10 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
                 A.fbase[A.n_rec] = exF + full_b + exP + part_b;  // total units
                 A.fbase[A.n_rec + 1] = exF + full_b;             // full units
             }
+            // the block's partial run (first slot after part_base, length) and the longest run:
+            // the units kernel's rank-major order (k_units_ragged_pipe, RM)
+            A.block_psums[b] = (exP << 16) | part_b;
+            atomicMax(A.lb_ctl + 2, (unsigned long long)part_b);
         }
     }
     uint32_t h = 0;
@@ -612,6 +618,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     if (BAL && threadIdx.x == 0) blk_next = kWavesPerBlock;
     load_stream_tables(lds, A.blob);
     __syncthreads();
+    WLOG_DECL;
+    WLOG_START();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & (kGroupLanes - 1);
     const uint32_t grp = lane / kGroupLanes;
@@ -649,11 +657,142 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
         }
         if (valid && l == 0) KB_WRITE(A.partial, M.slot(u), A.unit_cap, kKbUnit, R);
         if (valid && tail_here) KB_WRITE(A.tailc, M.slot(u), A.unit_cap, kKbUnit, tail);
+        WLOG_STEP();
+        WLOG_UNIT(valid && l == 0, cur.span & kDescBytes);
         wb = wb_next;
         u = un;
     }
+    WLOG_END(bw0 + (threadIdx.x >> 6));
 }
 
+
+// The units kernel, software-pipelined across units (stream_unit, as k_units_fixed): the
+// next wave-step's descriptor is loaded when the current unit starts (its slot taken from
+// the block's LDS counter), and that unit's first chunk loads go out before the current
+// unit's last batch is stepped, so a wave never drains its loads at a unit boundary.  The
+// per-wave log (tools/ragged_gap.py) showed the unpipelined kernel streaming configs[2] at
+// 6.85 TB/s in steady state against 7.52 for the pipelined fixed kernel (and 6.73 for the
+// fixed kernel without pipelining, k_units_fixed_v1).  Edges as kShipEM: the plan steps each
+// record's head (desc.inj), finalize its tail.  Units past the table point at the table blob
+// (always mapped, 16-byte aligned): every load is issued unconditionally.
+// Rank-major order of the partial units (RM): the plan leaves each plan block's partial run
+// sorted longest first; the units kernel takes rank 0 of every block's run, then rank 1, ...
+// (unit Fc + k is rank k / nb of block k % nb; ranks past a run's end are empty), so the
+// wave-steps come in nearly descending cost and the static round robin over the CUs ends
+// with the shortest units everywhere.  In slot order (block after block) the last steps held
+// the last plan blocks' longest partial units: the per-wave log on configs[2] showed the wave
+// end times spread over 126 us against 51 for fixed records (tools/ragged_gap.py).
+// RM 2 (tail only): slot order up to the partial runs of the last `tail_blocks` plan blocks,
+// rank-major over those (b0 = their first block, T0 = the partial slots before them, L their
+// longest run): the locality of slot order everywhere but in the last few percent of the work.
+struct RankMap {
+    uint64_t Fc, nb, U;  // full units streamed, plan blocks in the rank-major part, units in streaming order
+    uint64_t b0, T0;     // first rank-major block, partial units before it (slot order)
+    __device__ __forceinline__ bool slot(const RaggedArgs& A, uint64_t u, uint64_t& s) const {
+        if (u < Fc + T0) {
+            s = u < Fc ? u : A.part_base + (u - Fc);
+            return u < Fc || s < A.unit_cap;
+        }
+        const uint64_t k = u - Fc - T0, i = k / nb, b = b0 + (k - i * nb);
+        const uint64_t run = __ldg(reinterpret_cast<const unsigned long long*>(A.block_psums) + b);
+        s = A.part_base + (run >> 16) + i;
+        return i < (run & 0xffffu) && s < A.unit_cap;
+    }
+};
+template <int RM>
+__device__ __forceinline__ RankMap rank_map(const RaggedArgs& A, uint64_t tail_blocks) {
+    RankMap m;
+    const uint64_t F = A.fbase[A.n_rec + 1];
+    m.Fc = F < A.part_base ? F : A.part_base;
+    const uint64_t nb = (A.n_rec + kScanBlock - 1) / kScanBlock;
+    if (RM == 1 || tail_blocks >= nb) {
+        m.b0 = 0;
+        m.T0 = 0;
+        m.nb = nb;
+        m.U = m.Fc + m.nb * __hip_atomic_load(A.lb_ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return m;
+    }
+    m.nb = tail_blocks;
+    m.b0 = nb - tail_blocks;
+    const unsigned long long* pr = reinterpret_cast<const unsigned long long*>(A.block_psums);
+    m.T0 = pr[m.b0] >> 16;
+    uint64_t L = 0;
+    for (uint64_t b = m.b0; b < nb; ++b) L = (pr[b] & 0xffffu) > L ? (pr[b] & 0xffffu) : L;  // uniform: scalar loads
+    m.U = m.Fc + m.T0 + m.nb * L;
+    return m;
+}
+
+template <int PF = kRaggedPF, int RM = 0>
+__global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs A) {
+    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.blob, A.blob + kBlobWords);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    __shared__ uint32_t blk_next;
+    if (threadIdx.x == 0) blk_next = kWavesPerBlock;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const UnitMap M = unit_map(A);
+    const RankMap RMap = RM ? rank_map<RM>(A, A.tail_blocks) : RankMap{0, 1, 0, 0, 0};
+    const uint64_t U = RM ? RMap.U : M.U;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
+    const uint32_t nidx = (uint32_t)((nws + nwaves - 1) / nwaves) * kWavesPerBlock;
+    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(A.blob);
+    uint64_t wb = bw0 + (threadIdx.x >> 6);
+    uint64_t u = wb * kGroupsPerWave + grp;
+    auto unit_of = [&](const UnitDesc& d, bool valid) {
+        const uint8_t* us = valid ? reinterpret_cast<const uint8_t*>(d.us) : safe;
+        return lane_unit(us, valid ? us + d.span : safe, l);
+    };
+    // unit u's slot (valid: a unit of the table, else an empty step)
+    auto slot_of = [&](uint64_t uu, uint64_t& s) {
+        if (uu >= U) return false;
+        if constexpr (RM) return RMap.slot(A, uu, s);
+        s = M.slot(uu);
+        return true;
+    };
+    // the first unit: its descriptor, then its loads in flight over the table fill
+    uint64_t su = 0;
+    bool valid = slot_of(u, su);
+    UnitDesc d = valid ? load_desc(A.desc + su) : UnitDesc{0, 0, 0};
+    LaneUnit L = unit_of(d, valid);
+    UnitLoads<PF> Ld;
+    issue_unit_loads<PF, kRaggedNT>(L, Ld);
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    WLOG_DECL;
+    WLOG_START();
+    while (wb < nws) {
+        uint64_t wb_next;
+        {
+            uint32_t i = 0;
+            if (lane == 0) i = atomicAdd(&blk_next, 1u);
+            i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
+            wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
+        }
+        const uint64_t un = wb_next * kGroupsPerWave + grp;
+        uint64_t sn = 0;
+        const bool vn = slot_of(un, sn);
+        const UnitDesc dn = vn ? load_desc(&KB_READ(A.desc, sn, A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
+        LaneUnit N = L;
+        const uint32_t R = stream_unit<PF, kRaggedNT>(lds, X, l, L, Ld, L.us, d.inj, [&](UnitLoads<PF>& nx) {
+            N = unit_of(dn, vn);
+            issue_unit_loads<PF, kRaggedNT>(N, nx);
+        });
+        if (valid && l == 0) KB_WRITE(A.partial, su, A.unit_cap, kKbUnit, R);
+        WLOG_STEP();
+        WLOG_UNIT(valid && l == 0, d.span);
+        wb = wb_next;
+        u = un;
+        su = sn;
+        valid = vn;
+        d = dn;
+        L = N;
+    }
+    WLOG_END(bw0 + (threadIdx.x >> 6));
+}
 
 // Slot of unit j of a record (full units from fb in order, partial ones bucketed).
 __device__ __forceinline__ uint64_t unit_slot(uint64_t j, uint64_t k, uint64_t fb, uint64_t ps0, uint64_t ps1,
@@ -1112,9 +1251,21 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
             hipLaunchKernelGGL(k_ragged_plan<kShipEM>, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     }
     units_timer_begin(s);
-#ifdef KARMA_AB  // tools build (ab.h): 2 = static wave-steps, 4 / 8 = chunks in flight
+#ifdef KARMA_AB  // tools build (ab.h): 2 = static wave-steps, 4 / 8 = chunks in flight, 1 / 6 = pipelined (PF 4 / 6)
     const long v = KARMA_AB_KNOB("KARMA_RAGGED_VARIANT", 0);
-    if (em == 0)
+    if (em == 3 && v == 1)
+        hipLaunchKernelGGL(k_units_ragged_pipe<4>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (em == 3 && v == 6)
+        hipLaunchKernelGGL(k_units_ragged_pipe<6>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (em == 3 && v == 11)
+        hipLaunchKernelGGL((k_units_ragged_pipe<4, 1>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (em == 3 && v == 16)
+        hipLaunchKernelGGL((k_units_ragged_pipe<6, 1>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (em == 3 && v == 21)
+        hipLaunchKernelGGL((k_units_ragged_pipe<4, 2>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (em == 3 && v == 26)
+        hipLaunchKernelGGL((k_units_ragged_pipe<6, 2>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (em == 0)
         hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, 0>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (em == 1)
         hipLaunchKernelGGL((k_units_ragged<true, kRaggedUnitsPF, 1>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
@@ -1152,6 +1303,9 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
 }
 
 KB_DEFINE_COLLECT(ragged)
+#ifdef KARMA_AB
+WLOG_SETTER(ragged)
+#endif
 
 }  // namespace engine
 }  // namespace karma

@@ -80,6 +80,14 @@ struct FixedArgs {
                                // wave fold their 8 consecutive units into one state (else nullptr)
     uint32_t fold_k;           // 2, 4 or 8: k == fold_k units of a record sit in one wave, which folds
                                // them with comb_maps and writes out[] itself (0: not used)
+    // Fused record combine (one record, WAVE_COMB; k_units_fixed FUSE): the wave states go out
+    // tagged, (tag << 32 | state), as agent-scope atomic stores into partial (as uint64); the
+    // workgroup that finishes last (fctl[0] counts them) folds them like k_combine_block with
+    // block_blob and writes the CRC.  fctl[1] = the last finished call's tag (device-resident,
+    // so a captured graph replays correctly).  nullptr: not fused.
+    unsigned long long* fctl;
+    const uint32_t* block_blob; // kBlockCombWords (block_comb_blob for D = 8 units, m states per thread)
+    uint64_t comb_m;            // states per thread of the fused fold
 };
 
 // One unit of a ragged batch: the 16-aligned span [us, us + span) of a record
@@ -124,7 +132,8 @@ struct RaggedArgs {
                                //   [n_rec] = total units, [n_rec+1] = full units
     uint64_t* pslot;           // 2 * n_rec: slots of the record's partial first / last unit
     uint64_t* block_sums;      // per scan block: full-unit offset
-    uint64_t* block_psums;     // per scan block: partial units, then the block's first partial slot
+    uint64_t* block_psums;     // per scan block: partial units, then the block's first partial slot (two-pass);
+                               //   single-pass plan: first partial slot (after part_base) << 16 | run length
     // Single-pass plan (k_ragged_plan): decoupled look-back over per-block status words.
     // lb[0] counts the blocks that started (plan-block ids in start order); lb[1 + b] =
     // seq << 42 | flag << 40 | value (flag 1: block b's own full-unit count, 2: the full units
@@ -135,9 +144,11 @@ struct RaggedArgs {
     // to seq, or, at lb_seq_max, clears the lb_words status words and restarts the tags at 1.
     unsigned long long* lb;
     unsigned long long* lbp;   // the same for the blocks' partial unit counts
-    unsigned long long* lb_ctl;  // [0] the last finished call's tag, [1] the running call's
+    unsigned long long* lb_ctl;  // [0] the last finished call's tag, [1] the running call's,
+                                 // [2] the longest plan block's partial run (reset by finalize)
     uint64_t lb_words;         // status words after lb[0] (both arrays)
     uint32_t lb_seq_max;       // 2^22 (the tools build lowers it to test the wrap)
+    uint64_t tail_blocks;      // units kernel: plan blocks whose partial runs are taken rank-major
     UnitDesc* desc;            // unit_cap entries
     uint64_t unit_cap;         // capacity of desc / partial
     uint64_t part_base;        // single-pass plan: first slot of the partial units (full units
@@ -162,6 +173,10 @@ struct RaggedArgs {
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
 // recorded on `s` immediately around the next units kernel launched by this thread.
+#ifdef KARMA_AB
+hipError_t set_wave_log_ragged(void* p, uint64_t cap);  // wavelog.h (tools build)
+hipError_t set_wave_log_fixed(void* p, uint64_t cap);
+#endif
 void units_timer_begin(hipStream_t s);
 void units_timer_end(hipStream_t s);
 

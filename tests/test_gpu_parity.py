@@ -196,6 +196,48 @@ def test_stream_1gib_with_init(dev):
     assert got == want
 
 
+def test_stream_fused_combine_segments_and_graph_replay(dev):
+    """One record per call (a segment scan) takes the fused combine: the units kernel's last
+    workgroup folds the wave states, read through per-call tags (k_units_fixed FUSE).  64 distinct
+    64 MiB segments back to back on one stream, sizes from one wave state to the 64 Ki states one
+    launch folds (1 GiB), a second stream interleaved, and the call captured in a hipGraph and
+    replayed with new bytes in the buffer: every CRC against the oracle."""
+    seg, nseg = 64 << 20, 64
+    buf = torch.empty(seg * nseg, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 99)
+    out = torch.empty(nseg, dtype=torch.uint32, device=dev)
+    for i in range(nseg):
+        K.extend_stream(0, buf[i * seg:(i + 1) * seg], out=out[i:i + 1])
+    _eq(out.cpu().numpy(), oracle_lib.splitmix_fixed_crcs(99, seg, 0, nseg, threads=16))
+    # sizes: 16 KiB (one wave state) .. 1 GiB, unaligned starts, two streams alternating
+    s2 = torch.cuda.Stream()
+    host = buf[: (1 << 30) + 64].cpu().numpy()
+    for i, (off, n) in enumerate([(0, 16 << 10), (3, (16 << 10) + 5), (100, 1 << 20), (7, (8 << 20) + 77),
+                                  (0, 64 << 20), (1, (1 << 30) - 1), (0, 1 << 30)]):
+        st = s2 if i % 2 else torch.cuda.current_stream()
+        with torch.cuda.stream(st):
+            got = K.extend_stream(0x1234567, buf[off: off + n], stream=st)
+        st.synchronize()
+        assert int(got.item()) == oracle_lib.extend(0x1234567, host[off: off + n].tobytes()), (off, n)
+    # captured once, replayed with new bytes (the tags come from the device)
+    s = torch.cuda.Stream()
+    part = buf[:seg]
+    o1 = torch.empty(1, dtype=torch.uint32, device=dev)
+    with torch.cuda.stream(s):
+        K.extend_stream(0, part, out=o1, stream=s)
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        K.extend_stream(0, part, out=o1, stream=s)
+    for seed in (5, 6, 7):
+        torch.cuda.synchronize()
+        K.fill_splitmix64(part, seed)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(o1.item()) == int(oracle_lib.splitmix_fixed_crcs(seed, seg, 0, 1, threads=16)[0])
+
+
 def test_config2_full_1m_x_4k(dev):
     n, rec = 1 << 20, 4096
     buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)
@@ -411,7 +453,7 @@ def test_ragged_graph_capture_replays(dev):
     same stream between replays (they grow the stream's workspace: the graph's buffers must
     survive that)."""
     n, arena_bytes = 200_000, 48 << 20
-    cap_total = 60 << 20
+    cap_total = 96 << 20
     arena = torch.empty(arena_bytes, dtype=torch.uint8, device=dev)
     d_off = torch.empty(n, dtype=torch.int64, device=dev)
     d_len = torch.empty(n, dtype=torch.int32, device=dev)
