@@ -160,6 +160,8 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
 #define KARMA_WAL_CRC_PLAN 0    /* one-record-per-group batch when every payload <= 1 KiB, else the unit plan */
 #define KARMA_WAL_CRC_DIRECT 1  /* always the one-record-per-group batch */
 #define KARMA_WAL_CRC_UNITS 2   /* always the unit plan (karma_crc32c_batch_ragged) */
+#define KARMA_WAL_CRC_SEPARATE 3 /* as PLAN, but the walk first, then one batch over the gathered lists
+                                    (PLAN checksums payloads <= 1 KiB inside the walk) */
 typedef struct karma_wal_tuning {
     uint64_t walk_sub_bytes; /* header-walk sub-range size, rounded down to a 4 KiB multiple (>= 4 KiB);
                                 >= seg_bytes: one walker per segment; 0 = planned */

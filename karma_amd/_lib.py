@@ -74,7 +74,7 @@ SIGNATURES = {
 }
 
 
-KARMA_WAL_CRC_PLAN, KARMA_WAL_CRC_DIRECT, KARMA_WAL_CRC_UNITS = 0, 1, 2
+KARMA_WAL_CRC_PLAN, KARMA_WAL_CRC_DIRECT, KARMA_WAL_CRC_UNITS, KARMA_WAL_CRC_SEPARATE = 0, 1, 2, 3
 
 
 class WalTuning(ctypes.Structure):

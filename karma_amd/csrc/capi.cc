@@ -485,6 +485,13 @@ struct Locked {
 }  // namespace
 
 namespace karma::engine {
+int device_quad_blob(int dev, const uint32_t** out) {
+    (void)dev;  // the current device (the caller set it)
+    Locked L;
+    if (L.rc) return L.rc;
+    *out = L.ds->quad_blob;
+    return 0;
+}
 int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
                        uint32_t* d_out, hipStream_t s) {
     return karma_crc32c_batch_ragged_bounded(d_arena, d_off, d_len, n_rec, 0, 1, nullptr, 0, d_out, s);

@@ -61,6 +61,24 @@ __device__ __forceinline__ uint32_t stride_step(const uint32_t* lds, uint32_t X,
     return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
 }
 
+// The half-replicated image (16 copies, 64 KiB; the fused WAL walker, which also needs LDS
+// for its walkers' tiles): row e (256 bytes) holds entry e of the four tables, 16 copies
+// each: byte address of table k, entry e, for lane L = e<<8 | k<<6 | (L&15)<<2, so one
+// v_perm_b32 per table builds it from acc byte k and byte k of the lane constant
+// (lane_const16).  Lanes L and L+16 share a bank: random data costs 2-way conflicts.
+constexpr int kRep16Words = 16384;
+__device__ __forceinline__ uint32_t lane_const16() {
+    const uint32_t c = (threadIdx.x & 15u) << 2;
+    return c | ((64u + c) << 8) | ((128u + c) << 16) | ((192u + c) << 24);
+}
+__device__ __forceinline__ uint32_t stride_step16(const uint32_t* lds, uint32_t X, uint32_t acc, uint32_t w) {
+    const uint32_t i0 = __builtin_amdgcn_perm(X, acc, 0x0c0c0004u);  // {X.b0, acc.b0, 0, 0}
+    const uint32_t i1 = __builtin_amdgcn_perm(X, acc, 0x0c0c0105u);  // {X.b1, acc.b1, 0, 0}
+    const uint32_t i2 = __builtin_amdgcn_perm(X, acc, 0x0c0c0206u);  // {X.b2, acc.b2, 0, 0}
+    const uint32_t i3 = __builtin_amdgcn_perm(X, acc, 0x0c0c0307u);  // {X.b3, acc.b3, 0, 0}
+    return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
+}
+
 // Z(x) for a map stored as four plain 256-entry tables at word `base`.
 __device__ __forceinline__ uint32_t zmap(const uint32_t* lds, int base, uint32_t x) {
     return lds[base + (x & 255u)] ^ lds[base + 256 + ((x >> 8) & 255u)] ^ lds[base + 512 + ((x >> 16) & 255u)] ^
@@ -191,9 +209,17 @@ __device__ __forceinline__ uint32_t tail_register(const uint32_t* lds, int z4, i
 // MODE (timing experiments of the tools build only, wrong results): bit 0 = main-loop
 // steps without the LDS lookups (KARMA_CRC_VARIANT=6, ab.h), bit 1 = stream_unit without
 // the lane fold and group tree.  The shipped library instantiates MODE 0 only.
+// MODE bit 3: the 16-copy stride image (stride_step16, lane_const16).
 template <int MODE = 0>
 __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
                                       uint32_t& a3, const u32x4& v) {
+    if constexpr (MODE & 8) {
+        a0 = stride_step16(lds, X, a0, v.x);
+        a1 = stride_step16(lds, X, a1, v.y);
+        a2 = stride_step16(lds, X, a2, v.z);
+        a3 = stride_step16(lds, X, a3, v.w);
+        return;
+    }
     if constexpr (MODE & 1) {
         a0 = ((a0 << 1) | (a0 >> 31)) ^ v.x;
         a1 = ((a1 << 1) | (a1 >> 31)) ^ v.y;
@@ -401,6 +427,59 @@ __device__ __forceinline__ uint32_t stream_unit(const uint32_t* lds, uint32_t X,
     return c;
 }
 
+// One batch of up to 64 small records, one per lane (this lane's record: pi, ni bytes, init
+// initi, vi = a real record), checksummed by groups of G lanes: the small-record kernel's body
+// (k_ragged_direct4; also the fused WAL walker's list pass, wal_device.hip).  The head and tail
+// byte steps run for the 64 records at once (lane i: record i, serial steps with per-record
+// trip counts); the bodies stream in 64 / (64 / G) rounds of 64 / G groups, registers passed in
+// and out by shuffles, each round's loads issued before the previous round's last chunks are
+// stepped (stream_unit).  A group with no body in a round streams an empty unit at `safe`
+// (16-byte aligned, always mapped): every load is issued unconditionally.  Returns this
+// lane's CRC (valid when vi); every lane of the wave must call it.
+template <int G, int PF, bool NT, int MODE>
+__device__ __forceinline__ uint32_t direct_batch(const uint32_t* lds, uint32_t X, const uint8_t* safe,
+                                                 const uint8_t* pi, uint32_t ni, uint32_t initi, bool vi) {
+    constexpr int NG = 64 / G, NR = 64 / NG;  // groups per wave, rounds
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const Geom gi = geom(pi, ni);
+    const bool body = vi && !gi.is_short;
+    const uint64_t ai = reinterpret_cast<uintptr_t>(body ? gi.a : safe);
+    const uint64_t bi = reinterpret_cast<uintptr_t>(body ? gi.b : safe);
+    auto unit_of = [&](uint32_t r) {  // round r's record of this group: NG r + grp
+        const int src = (int)(r * NG + grp);
+        const uint8_t* us = reinterpret_cast<const uint8_t*>((uintptr_t)__shfl((long long)ai, src));
+        const uint8_t* ue = reinterpret_cast<const uint8_t*>((uintptr_t)__shfl((long long)bi, src));
+        return lane_unit<G>(us, ue, l);
+    };
+    LaneUnit L = unit_of(0);
+    UnitLoads<PF> Ld;
+    issue_unit_loads<PF, NT, G>(L, Ld);
+    const bool tail = body && gi.e > gi.b;
+    const u32x4 tv = ld16(tail ? gi.b : safe);
+    const uint32_t hi = body ? ((MODE & 4) ? initi : head_register(lds, kLZ4, kLT8, pi, gi, initi)) : 0u;
+    uint32_t Ri = 0;
+#pragma unroll 1
+    for (uint32_t round = 0; round < NR; ++round) {
+        const uint32_t sh = __shfl(hi, (int)(round * NG + grp));
+        LaneUnit N = L;
+        const uint32_t R = stream_unit<PF, NT, MODE, G>(lds, X, l, L, Ld, L.us, sh, [&](UnitLoads<PF>& nx) {
+            if (round + 1 < NR) {
+                N = unit_of(round + 1);
+                issue_unit_loads<PF, NT, G>(N, nx);
+            }
+        });
+        const uint32_t Rr = __shfl(R, (int)((lane % NG) * G));  // group (lane % NG)'s register
+        if (lane / NG == round) Ri = Rr;
+        L = N;
+    }
+    if (!vi) return 0u;
+    return gi.is_short ? short_record(lds, kLZ4, kLT8, pi, ni, initi)
+           : (MODE & 4) ? Ri ^ tv.x
+                        : ~steps_in_vec(lds, kLZ4, kLT8, Ri, tv, 0u, tail ? (uint32_t)(gi.e - gi.b) : 0u);
+}
+
 // Copy WORDS words (WORDS % 4 == 0, both pointers 16-byte aligned) from global
 // memory into LDS with THREADS threads: every thread issues all of its 16-byte
 // loads before its first LDS store, so the copy costs about one memory latency
@@ -443,6 +522,29 @@ __device__ __forceinline__ void load_stream_tables(uint32_t* lds, const uint32_t
     u32x4* l4 = reinterpret_cast<u32x4*>(lds);
 #pragma unroll
     for (int q = 0; q < IT; ++q) l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e[q], e[q], e[q], e[q]};
+}
+
+// The 16-copy image of a stream / quad blob for THREADS threads: [0, kRep16Words) the
+// stride tables (stride_step16), the small tables at kSmallBase as in load_stream_tables.
+template <int THREADS>
+__device__ __forceinline__ void load_stream_tables16(uint32_t* lds, const uint32_t* __restrict__ blob) {
+    // vector v of row e: table k = (v >> 2) & 3, copies 4 (v & 3) .. +3
+    constexpr int NV = kRep16Words / 4;
+    constexpr int IT = (NV + THREADS - 1) / THREADS;
+    uint32_t e[IT];
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int v = (int)threadIdx.x + q * THREADS;
+        const int row = v >> 4, k = (v >> 2) & 3;
+        e[q] = v < NV ? *(const __attribute__((address_space(1))) uint32_t*)(blob + kBlobStride + k * 256 + row) : 0u;
+    }
+    copy_to_lds<kSmallWords, THREADS>(lds + kSmallBase, blob + 1024);
+    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int v = (int)threadIdx.x + q * THREADS;
+        if (v < NV) l4[v] = u32x4{e[q], e[q], e[q], e[q]};
+    }
 }
 
 // Per-lane constant of the replicated-table address (see the LDS image above).

@@ -924,7 +924,6 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
 template <int G, int MODE = 0>  // MODE != 0: timing-only variants of the tools build (bits 0-1:
                                  // stream_unit's, crc_device.h; bit 2: no head / tail steps)
 __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) {
-    constexpr int NG = 64 / G, NR = 64 / NG;  // groups per wave, rounds
     uint64_t n_rec = A.n_rec;
     if (A.n_dev) {  // a device-sized batch: the count is known on the device only
         if (*A.gate_len > A.gate_max) return;
@@ -935,8 +934,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
     load_stream_tables(lds, A.blob);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t l = lane & (G - 1);
-    const uint32_t grp = lane / G;
     const uint32_t X = lane_const();
     const uint8_t* safe = reinterpret_cast<const uint8_t*>(A.blob);  // 16-aligned, always mapped
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
@@ -947,42 +944,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
         const uint8_t* pi = vi ? A.arena + A.off[ri] : A.arena;
         const uint32_t ni = vi ? A.len[ri] : 0u;
         const uint32_t initi = vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
-        const Geom gi = geom(pi, ni);
-        const bool body = vi && !gi.is_short;
-        const uint64_t ai = reinterpret_cast<uintptr_t>(body ? gi.a : safe);
-        const uint64_t bi = reinterpret_cast<uintptr_t>(body ? gi.b : safe);
-        auto unit_of = [&](uint32_t r) {  // round r's record of this group: base + NG r + grp
-            const int src = (int)(r * NG + grp);
-            const uint8_t* us = reinterpret_cast<const uint8_t*>((uintptr_t)__shfl((long long)ai, src));
-            const uint8_t* ue = reinterpret_cast<const uint8_t*>((uintptr_t)__shfl((long long)bi, src));
-            return lane_unit<G>(us, ue, l);
-        };
-        LaneUnit L = unit_of(0);
-        UnitLoads<kRaggedPF> Ld;
-        issue_unit_loads<kRaggedPF, kRaggedNT, G>(L, Ld);
-        const bool tail = body && gi.e > gi.b;
-        const u32x4 tv = ld16(tail ? gi.b : safe);
-        const uint32_t hi = body ? ((MODE & 4) ? initi : head_register(lds, kLZ4, kLT8, pi, gi, initi)) : 0u;
-        uint32_t Ri = 0;
-#pragma unroll 1
-        for (uint32_t round = 0; round < NR; ++round) {
-            const uint32_t sh = __shfl(hi, (int)(round * NG + grp));
-            LaneUnit N = L;
-            const uint32_t R = stream_unit<kRaggedPF, kRaggedNT, MODE, G>(lds, X, l, L, Ld, L.us, sh,
-                                                                       [&](UnitLoads<kRaggedPF>& nx) {
-                if (round + 1 < NR) {
-                    N = unit_of(round + 1);
-                    issue_unit_loads<kRaggedPF, kRaggedNT, G>(N, nx);
-                }
-            });
-            const uint32_t Rr = __shfl(R, (int)((lane % NG) * G));  // group (lane % NG)'s register
-            if (lane / NG == round) Ri = Rr;
-            L = N;
-        }
+        const uint32_t res = direct_batch<G, kRaggedPF, kRaggedNT, MODE>(lds, X, safe, pi, ni, initi, vi);
         if (vi) {
-            const uint32_t res = gi.is_short ? short_record(lds, kLZ4, kLT8, pi, ni, initi)
-                                 : (MODE & 4) ? Ri ^ tv.x
-                                              : ~steps_in_vec(lds, kLZ4, kLT8, Ri, tv, 0u, tail ? (uint32_t)(gi.e - gi.b) : 0u);
             A.out[ri] = res;
             if (A.cmp_stored && ni && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
         }

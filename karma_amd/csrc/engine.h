@@ -215,6 +215,8 @@ int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_
 // *d_gate_len <= gate_max (else the kernel does nothing).
 // With d_stored set it is also the CRC check: the first record whose CRC differs from
 // d_stored[r] (length 0 excepted) goes to *d_first_bad (atomicMin).
+// The 4-lane small-record kernel's table blob on the current device (k_wal_walk_crc's tables).
+int device_quad_blob(int dev, const uint32_t** out);
 int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
                            uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
                            const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s);
@@ -226,7 +228,8 @@ struct WalSegMeta {
     uint64_t stop;   // WAL offset where the segment's walk stopped (segment end for END; for
                      // kWalSpill the offset past the segment end where the chain continues)
     uint32_t max_len;  // an upper bound of the candidates' payload lengths
-    uint32_t pad;
+    uint32_t first_bad;  // inline CRCs: ordinal of the first mismatching candidate (~0u: none;
+                         // ~0u - 1: not all checksummed); other walks: ~0u - 1
 };
 static_assert(sizeof(WalSegMeta) == 24, "one 24-byte record per segment");
 
@@ -246,10 +249,11 @@ struct WalSummary {
     uint32_t w1;
     uint32_t status;     // KARMA_WAL_END / _CORRUPT / _BAD_TYPE (structural)
     uint32_t max_len;    // an upper bound of the payload lengths
-    uint32_t pad;
+    uint32_t crc_unknown;  // inline CRCs (k_wal_walk_crc): 1 = some candidate of [0, w1) was not checksummed
     uint64_t first_bad;  // the first candidate whose payload CRC differs (~0: none), set by the CRC check
+    uint64_t bad_off;    // inline CRCs: that candidate's header offset relative to wal (k_wal_plan)
 };
-static_assert(sizeof(WalSummary) == 40, "one 40-byte summary, read back in one copy");
+static_assert(sizeof(WalSummary) == 48, "one 48-byte summary, read back in one copy");
 
 // One sub-range walker's result: where it started (a header it found, or the
 // sub-range end: none), its list length, its stop kind / offset and where it left
@@ -284,16 +288,20 @@ struct WalArgs {
     uint64_t n_all;            // capacity of the contiguous lists (bounds build checks)
     WalSummary* sum;           // k_wal_plan's result
     uint64_t wal_end;          // WAL offset of the image end
+    const uint32_t* crc_blob;  // k_wal_walk_crc: the quad blob (its tables' LDS image; empty units' address)
+    uintptr_t kb_lo, kb_hi;    // bounds build: the image's allocation (the inline CRC loads)
 };
 constexpr uint32_t kWalkTile = 4096;  // the one-wave walker's LDS tile (wal_device.hip)
 constexpr uint32_t kMaxSub = 4096;    // sub-ranges per segment (k_wal_gather stages their runs in LDS)
 struct WalWalkPlan {
     uint64_t nsub, sub_bytes, sub_cap, cand_cap;
-    int kernel;  // 0: sub-range walkers (+ resolve when nsub > 1), 1: one workgroup per segment
+    int kernel;  // 0: sub-range walkers (+ resolve when nsub > 1), 1: one workgroup per segment,
+                 // 2: sub-range walkers with the CRCs inline (k_wal_walk_crc, + resolve)
 };
 // Host planner (wal.cc).  sub_bytes: 0 = the planner's split, else the forced sub-range
 // size (karma_wal_tuning).
-WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes);
+WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes, bool inline_crc = false);
+constexpr int kWalFuseWaves = 15;  // walkers per workgroup of k_wal_walk_crc (wal_device.hip)
 hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s);
 // The replay plan on the device: a.sum, a.cand_base (first list slot per segment) and
 // *a.first_bad = ~0, from the walk's metas of nseg segments.

@@ -50,18 +50,20 @@ int set_last_error(int code, const std::string& what);  // capi.cc
 // k_wal_resolve stitches their lists.  Many segments: one walker per segment.
 // sub_bytes != 0 forces the sub-range size (karma_wal_tuning: tests, tuning);
 // the tools build's KARMA_WALK_VARIANT=1 (ab.h) selects k_wal_walk instead.
-WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes) {
-    WalWalkPlan p{1, 0, 0, 0, 0};
+WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes, bool inline_crc) {
+    WalWalkPlan p{1, 0, 0, 0, inline_crc ? 2 : 0};
     const uint64_t tiles = (seg_bytes + kWalkTile - 1) / kWalkTile;
     uint64_t sub_tiles = tiles;
-    if (KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 1) {
+    if (!inline_crc && KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 1) {
         p.kernel = 1;
     } else if (sub_bytes) {
         sub_tiles = std::max<uint64_t>(1, sub_bytes / kWalkTile);
     } else {
         // walkers: 20 per CU (1M x 180 B in 188 segments of 1 MiB: 40 KiB sub-ranges; 24-40 KiB
-        // measured 11 us faster per replay call than 48 KiB)
-        const uint64_t want = 20 * (uint64_t)(cu > 0 ? cu : 1);
+        // measured 11 us faster per replay call than 48 KiB); with the CRCs
+        // inline, one workgroup of kWalFuseWaves walkers per CU
+        const uint64_t per_cu = inline_crc ? (uint64_t)kWalFuseWaves : 20;
+        const uint64_t want = per_cu * (uint64_t)(cu > 0 ? cu : 1);
         if (nseg > 0 && nseg < want) {
             const uint64_t per = (want + nseg - 1) / nseg;  // sub-ranges per segment
             sub_tiles = std::max<uint64_t>(4, (tiles + per - 1) / per);
@@ -227,7 +229,7 @@ int karma_wal_replay_tuned(const void* h_wal, const void* d_wal, size_t wal_byte
                            int device, const karma_wal_tuning* tuning) {
     if ((!h_wal && !d_wal) || !h_n_records || !h_stop || !h_status || seg_bytes < 1 || wal_bytes % seg_bytes ||
         start > wal_bytes || seg_bytes >= (uint64_t(1) << 31) ||
-        (tuning && (tuning->crc_batch < 0 || tuning->crc_batch > 2)))
+        (tuning && (tuning->crc_batch < 0 || tuning->crc_batch > KARMA_WAL_CRC_SEPARATE)))
         return fail(KARMA_E_INVALID, "wal_replay");
     const uint8_t* src = static_cast<const uint8_t*>(h_wal);
     const ImageFill copy = [src](uint8_t* dst, uint64_t off, size_t n) {
@@ -291,8 +293,33 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     A.nwork = nwork;
     A.seg_bytes = seg_bytes;
     A.first_pos = start - base0;
+    const int batch = tuning ? tuning->crc_batch : KARMA_WAL_CRC_PLAN;
+    // Images up to kDevicePlanMax take a device-planned path (one host round trip): with the
+    // default plan the walkers checksum the candidates inline (k_wal_walk_crc); the tools
+    // build's other walk / small-record kernels, and KARMA_WAL_CRC_SEPARATE, walk first and
+    // then run one small-record batch over the gathered lists (the round-2 path).
+    const bool dev_plan = img_bytes <= kDevicePlanMax && batch != KARMA_WAL_CRC_UNITS &&
+                          KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 0;
+    const bool inline_crc =
+        dev_plan && batch == KARMA_WAL_CRC_PLAN && KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 0;
+    if (inline_crc) {
+        if (const int rc = device_quad_blob(dev, &A.crc_blob)) return rc;
+#ifdef KARMA_BOUNDS
+        hipDeviceptr_t lo = nullptr;
+        size_t sz = 0;
+        if (hipMemGetAddressRange(&lo, &sz, (hipDeviceptr_t)A.wal) == hipSuccess) {
+            A.kb_lo = reinterpret_cast<uintptr_t>(lo);
+            A.kb_hi = A.kb_lo + sz;
+        } else {
+            (void)hipGetLastError();
+            A.kb_lo = 0;
+            A.kb_hi = ~uintptr_t(0);
+        }
+#endif
+    }
     // 1. segment-parallel header walk (sub-range walkers when there are few segments)
-    const WalWalkPlan plan = wal_walk_plan(seg_bytes, nwork, c.cu, tuning ? tuning->walk_sub_bytes : 0);
+    const WalWalkPlan plan =
+        wal_walk_plan(seg_bytes, nwork, c.cu, tuning ? tuning->walk_sub_bytes : 0, inline_crc);
     A.nsub = plan.nsub;
     A.sub_bytes = plan.sub_bytes;
     A.sub_cap = plan.sub_cap;
@@ -316,7 +343,6 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     A.sum = c.sum.as<WalSummary>();
     A.first_bad = &A.sum->first_bad;
     A.wal_end = wal_bytes;
-    const int batch = tuning ? tuning->crc_batch : KARMA_WAL_CRC_PLAN;
     const uint32_t direct_max = batch == KARMA_WAL_CRC_DIRECT ? ~0u : kSmallRecordMax;  // the device-side gate
     auto bind_lists = [&](uint64_t cap) {  // the contiguous lists for up to cap candidates
         if (const int rc = c.off.ensure(cap * 8)) return rc;
@@ -331,22 +357,20 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         return 0;
     };
     // 2. the replay plan on the device (k_wal_plan: the segments replay enters, their list
-    //    offsets, the summary).  Images up to kDevicePlanMax take the device-planned path: the
-    //    lists are sized for the most candidates the image can hold (a header every 8 bytes),
-    //    and the gather, the small-record CRC batch and the compare are enqueued right behind
-    //    the walk; the two CRC kernels check the summary themselves and do nothing when a payload
-    //    is over 1 KiB.  One host round trip then reads the summary and the first mismatch, and
-    //    only WALs with larger records need a second one (the ragged plan is sized on the host).
+    //    offsets, the summary).  Device-planned path, separate batch: the lists are sized for the
+    //    most candidates the image can hold (a header every 8 bytes), and the gather, the
+    //    small-record CRC batch and the compare are enqueued right behind the walk; the CRC
+    //    kernel checks the summary itself and does nothing when a payload is over 1 KiB.  Inline
+    //    CRCs: the plan also finds the first mismatch the walkers reported.  One host round trip
+    //    then reads the summary; only WALs with larger records (or, inline, a run the walkers
+    //    could not checksum) need a second one (the ragged plan is sized on the host).
     const uint64_t cap_all = img_bytes / 8 + nwork;
-    // (the tools build's other small-record kernels, KARMA_DIRECT_VARIANT, take the host-sized path)
-    const bool dev_plan = img_bytes <= kDevicePlanMax && batch != KARMA_WAL_CRC_UNITS &&
-                          KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 0;
     // (up to 1024 segments the device-planned gather reduces the metas itself: no plan launch)
-    const bool fused_plan = dev_plan && nwork <= 1024;
+    const bool fused_plan = dev_plan && !inline_crc && nwork <= 1024;
     if (launch_wal_walk(A, nwork, plan, c.st) != hipSuccess ||
         (!fused_plan && launch_wal_plan(A, nwork, c.st) != hipSuccess))
         return fail(KARMA_E_HIP, "wal_replay: header walk");
-    if (dev_plan) {
+    if (dev_plan && !inline_crc) {
         if (const int rc = bind_lists(cap_all)) return rc;
         if (launch_wal_gather(A, nwork, fused_plan, c.st) != hipSuccess)
             return fail(KARMA_E_HIP, "wal_replay: gather");
@@ -359,18 +383,28 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     if (hipMemcpyAsync(S, A.sum, sizeof(WalSummary), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
         hipStreamSynchronize(c.st) != hipSuccess)
         return fail(KARMA_E_HIP, "wal_replay: walk + plan");
-    T.mark(dev_plan ? "walk + plan + gather + CRCs (device)" : "walk + plan (device)");
+    T.mark(inline_crc ? "walk + inline CRCs + plan (device)"
+                      : dev_plan ? "walk + plan + gather + CRCs (device)" : "walk + plan (device)");
     // replay enters segment s+1 only if segment s ended cleanly (k_wal_plan)
     int status = (int)S->status;
     uint64_t end = S->end;
     const uint64_t w1 = S->w1, n_all = S->n_all;
     const uint32_t max_len = S->max_len;
-    const bool small = batch == KARMA_WAL_CRC_DIRECT || (batch == KARMA_WAL_CRC_PLAN && max_len <= kSmallRecordMax);
+    const bool small = batch == KARMA_WAL_CRC_DIRECT ||
+                       ((batch == KARMA_WAL_CRC_PLAN || batch == KARMA_WAL_CRC_SEPARATE) && max_len <= kSmallRecordMax);
+    // inline CRCs complete: the first mismatch is known (no gathered lists exist yet)
+    const bool inline_done = inline_crc && !S->crc_unknown;
+    const bool lists = dev_plan && !inline_crc;  // the device-planned gather wrote them
     uint64_t accepted = n_all;
-    if (n_all && !(dev_plan && small)) {
-        // 3. the host-sized CRC batch: large payloads (the ragged plan), or an image too large
-        //    for the device-planned lists
-        if (!dev_plan) {
+    if (inline_done && S->first_bad < n_all) {
+        accepted = S->first_bad;
+        status = KARMA_WAL_CORRUPT;
+        end = base0 + S->bad_off;
+    }
+    if (n_all && !inline_done && !(lists && small)) {
+        // 3. the host-sized CRC batch: large payloads (the ragged plan), an image too large for
+        //    the device-planned lists, or runs the inline walk could not checksum
+        if (!lists) {
             if (const int rc = bind_lists(n_all)) return rc;
             if (launch_wal_gather(A, nwork, false, c.st) != hipSuccess)
                 return fail(KARMA_E_HIP, "wal_replay: gather");
@@ -387,13 +421,18 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         T.mark("CRC batch + compare");
     }
     if (n_all) {
-        if (S->first_bad < n_all) {  // the first mismatch in WAL order is where scan_record logs "Corrupt record"
+        if (!inline_done && S->first_bad < n_all) {  // the first mismatch in WAL order: "Corrupt record"
             accepted = S->first_bad;
             status = KARMA_WAL_CORRUPT;
             uint64_t at = 0;
             if (hipMemcpy(&at, A.off + accepted, 8, hipMemcpyDeviceToHost) != hipSuccess)
                 return fail(KARMA_E_HIP, "wal_replay: D2H");
             end = base0 + at;
+        }
+        if (h_rec_off && rec_cap && accepted && inline_done) {  // the offsets: the lists are gathered now
+            if (const int rc = bind_lists(n_all)) return rc;
+            if (launch_wal_gather(A, nwork, false, c.st) != hipSuccess)
+                return fail(KARMA_E_HIP, "wal_replay: gather");
         }
         if (h_rec_off && rec_cap && accepted) {
             const uint64_t k = std::min<uint64_t>(accepted, rec_cap);

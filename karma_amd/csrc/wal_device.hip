@@ -30,12 +30,14 @@
 
 #include "ab.h"
 #include "bounds.h"
+#include "crc_device.h"
 #include "engine.h"
 #include "karma_crc32c.h"
 
 namespace karma {
 namespace engine {
 namespace {
+using namespace dev;
 
 // crc32c::Value of the stale len/type word of a size-0 record.  A type-0 record
 // of size 0 has the word 0, so the value is a constant: Value("\0\0\0\0").
@@ -46,6 +48,10 @@ constexpr uint32_t crc_word_host(uint32_t w) {
 }
 constexpr uint32_t kStaleZero = crc_word_host(0);
 static_assert(kStaleZero == 0x48674BC7u, "crc32c::Value of four zero bytes");
+// Inline CRC results (k_wal_walk_crc) in WalSubMeta::pad[0] / WalSegMeta::first_bad.
+constexpr uint32_t kNoBad = ~0u;           // no mismatch
+constexpr uint32_t kCrcUnknown = ~0u - 1;  // some candidate was not checksummed inline
+
 // sivir::open's advance over an accepted size-0 record: 8 header bytes + the 4 stale bytes
 // scan_record appended to it (wal.cc:47-51, :66; sivir.cc:38).
 constexpr uint32_t kStaleAdvance = 12;
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_wal_walk(WalArgs A) {
             kind = kWalSpill;
             stop = pos;
         }
-        A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg), mx, 0u};
+        A.meta[blockIdx.x] = WalSegMeta{count, kind, base + (kind ? stop : seg), mx, kCrcUnknown};
         A.span[2 * blockIdx.x] = 0;
         A.span[2 * blockIdx.x + 1] = 0;
     }
@@ -204,6 +210,22 @@ constexpr uint32_t kChainCheck = 4;  // headers a sub-range walker's start must 
 struct WaveLds {
     uint32_t tile[kWTile / 4 + 4];  // + a header's slack
 };
+
+// Orders one walker's LDS tile accesses (its tile writes before its header reads, and the
+// reverse).  A walker alone in its workgroup (k_wal_walk_sub, k_wal_resolve): a barrier.
+// WG: the fused kernel's workgroup of kFuseWaves independent walkers (k_wal_walk_crc): only
+// this wave's LDS accesses are waited for -- a workgroup barrier would tie the walkers together.
+template <bool WG>
+__device__ __forceinline__ void wave_sync() {
+    if constexpr (WG) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
 
 struct Seg {  // one segment as a walker sees it
     const uint8_t* img;
@@ -259,11 +281,12 @@ __device__ __forceinline__ void wtile_fetch(const Seg& S, uint32_t lane, uint32_
     }
 }
 
+template <bool WG = false>
 __device__ __forceinline__ void wtile_store(WaveLds& W, uint32_t lane, const uint4 (&r)[kWQV + 1]) {
 #pragma unroll
     for (int q = 0; q < kWQV; ++q) reinterpret_cast<uint4*>(W.tile)[lane + 64u * q] = r[q];
     if (lane == 0) reinterpret_cast<uint4*>(W.tile)[kWTile / 16] = r[kWQV];
-    __syncthreads();  // one wave: orders the tile writes before the walker's reads
+    wave_sync<WG>();  // orders the tile writes before the walker's reads
 }
 
 // A 1 KiB window at t (16-byte aligned): one vector per lane + the slack, for a
@@ -285,10 +308,11 @@ __device__ __forceinline__ void wsmall_fetch(const Seg& S, uint32_t lane, uint32
     slack = uint4{w[4], w[5], w[6], w[7]};
 }
 
+template <bool WG = false>
 __device__ __forceinline__ void wsmall_store(WaveLds& W, uint32_t lane, const uint4& v, const uint4& slack) {
     reinterpret_cast<uint4*>(W.tile)[lane] = v;
     if (lane == 0) reinterpret_cast<uint4*>(W.tile)[kWSmall / 16] = slack;
-    __syncthreads();
+    wave_sync<WG>();
 }
 
 // The header at segment offset c, read from the tile at t0 (c - t0 < kWTile).
@@ -299,6 +323,15 @@ __device__ __forceinline__ void tile_header(const WaveLds& W, uint32_t c, uint32
     st = __builtin_amdgcn_alignbyte(w2, w1, sh);
 }
 
+// The fused walker's inline CRCs (k_wal_walk_crc): the LDS image (16-copy stride tables of the
+// quad blob, small tables at kSmallBase), its lane constant and the safe address of empty units.
+struct CrcCtx {
+    const uint32_t* lds;
+    uint32_t X;
+    const uint8_t* safe;
+};
+constexpr uint32_t kCrcInlineMax = 1024;  // payloads the walker checksums itself (4-lane groups)
+
 struct WalkEnd {
     uint32_t count;  // candidates written
     uint32_t max_len;  // their largest payload
@@ -308,12 +341,43 @@ struct WalkEnd {
                      // after a size-0 record at the segment end: kWalSpill)
 };
 
+// The fused kernel's second phase: the walker's own list [slot0, slot0 + count), 64 entries at
+// a time (read back from the slots it just wrote), checksummed by groups of 4 lanes
+// (direct_batch, the small-record kernel's body, through the 16-copy tables) and compared with
+// the stored CRCs.  Returns the first mismatching entry (kNoBad: none), or kCrcUnknown when a
+// payload is over kCrcInlineMax (the replay then takes the unit plan).
+__device__ uint32_t crc_list(const CrcCtx& C, const Seg& S, const WalArgs& A, uint32_t lane, uint64_t slot0,
+                             uint32_t count, uint32_t max_len) {
+    if (!count) return kNoBad;
+    if (max_len > kCrcInlineMax) return kCrcUnknown;
+    const uint64_t total = A.nwork * A.cand_cap;
+    (void)total;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the list writes before their reads
+    __builtin_amdgcn_s_waitcnt(0);
+    for (uint32_t i0 = 0; i0 < count; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool v = i < count;
+        uint32_t rec = 0, n = 0, st = 0;
+        if (v) {
+            rec = KB_READ(A.cand_rec, slot0 + i, total, kKbCand);
+            n = KB_READ(A.cand_len, slot0 + i, total, kKbCand);
+            st = KB_READ(A.cand_crc, slot0 + i, total, kKbCand);
+        }
+        const uint8_t* p = v ? S.img + rec + 8 : C.safe;
+        const uint32_t res = direct_batch<4, 4, true, 8>(C.lds, C.X, C.safe, p, n, 0u, v);
+        const uint64_t bm = __ballot(v && n != 0 && res != st);  // size 0: checked by the walk
+        if (bm) return i0 + (uint32_t)__builtin_ctzll(bm);
+    }
+    return kNoBad;
+}
+
 // Walk the header chain from pos while pos < hi, with scan_record's checks (wal.cc:34-87):
 // a rest shorter than a header ends the segment, type 0 with a payload that fits
 // is a candidate, a size-0 record compares the stored CRC with Value of the stale
 // len/type word (wal.cc:50-60), type 1 skips to the segment end, anything else
 // stops the walk.  Candidates go to crec / clen (cap slots).
 // resident: the tile start W already holds (find_start's tile), or ~0u.
+template <bool WG = false>
 __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t pos, uint32_t hi, const WalArgs& A,
                               uint64_t slot0, uint64_t cap, uint32_t resident = ~0u) {
     const uint64_t total = A.nwork * A.cand_cap;  // every list slot (bounds build)
@@ -370,7 +434,7 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
     uint4 r[kWQV + 1];
     if (t0 != resident) {  // else find_start left this tile in W: no second load of it
         wtile_fetch(S, lane, t0, r);
-        wtile_store(W, lane, r);
+        wtile_store<WG>(W, lane, r);
     }
     while (true) {
         const bool more = tsz == kWTile && (uint64_t)t0 + kWTile < tlim;
@@ -442,20 +506,20 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
         }
         if (done || (uint64_t)pos + 8 > seg || pos >= hi) break;
         const uint32_t nt0 = pos / kWTile * kWTile;
-        __syncthreads();  // the walk's tile reads are done before the next tile is stored
+        wave_sync<WG>();  // the walk's tile reads are done before the next tile is stored
         if (more && nt0 == t0 + kWTile) {  // the prefetched tile
-            wtile_store(W, lane, r);
+            wtile_store<WG>(W, lane, r);
             t0 = nt0;
         } else if (pos - t0 < 2 * tsz) {  // just past a window (or a tile at the segment end): tiles again
             wtile_fetch(S, lane, nt0, r);
-            wtile_store(W, lane, r);
+            wtile_store<WG>(W, lane, r);
             t0 = nt0;
             tsz = kWTile;
         } else {  // a jump: the window at the header
             uint4 v, sl;
             t0 = pos & ~15u;
             wsmall_fetch(S, lane, t0, v, sl);
-            wsmall_store(W, lane, v, sl);
+            wsmall_store<WG>(W, lane, v, sl);
             tsz = kWSmall;
         }
     }
@@ -493,12 +557,13 @@ __device__ __forceinline__ bool header_ok(uint32_t crc, uint32_t st, uint32_t c,
 // One tile is enough: where headers are further apart, k_wal_resolve walks the
 // sub-range itself in a few steps.  A wrong start only costs time: k_wal_resolve
 // accepts a walker's list only where the authoritative chain meets it.
+template <bool WG = false>
 __device__ uint32_t find_start(WaveLds& W, const Seg& S, uint32_t lane, uint32_t lo, uint32_t hi) {
     const uint32_t seg = S.seg;
     uint4 r[kWQV + 1];
     for (uint32_t t0 = lo; t0 < hi && t0 < lo + kWTile; t0 += kWTile) {  // lo is tile-aligned
         wtile_fetch(S, lane, t0, r);
-        wtile_store(W, lane, r);
+        wtile_store<WG>(W, lane, r);
         const uint32_t tend = t0 + kWTile < hi ? t0 + kWTile : hi;
         for (uint32_t c0 = t0; c0 < tend; c0 += 64) {
             const uint32_t c = c0 + lane;
@@ -526,7 +591,7 @@ __device__ uint32_t find_start(WaveLds& W, const Seg& S, uint32_t lane, uint32_t
             const uint64_t m = __ballot(ok);
             if (m) return c0 + (uint32_t)(__ffsll((long long)m) - 1);
         }
-        __syncthreads();  // everyone is done with the tile before the next store
+        wave_sync<WG>();  // everyone is done with the tile before the next store
     }
     return hi;
 }
@@ -560,11 +625,60 @@ __global__ __launch_bounds__(64) void k_wal_walk_sub(WalArgs A) {
     if (P == 1) {
         const bool spill = !E.kind && E.pos > S.seg;  // a size-0 record's advance left the segment
         const uint32_t kind = spill ? kWalSpill : E.kind, stop = spill ? E.pos : E.stop;
-        KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{E.count, kind, A.base0 + rel + (kind ? stop : S.seg), E.max_len, 0u}));
+        KB_WRITE(A.meta, s, A.nwork, kKbMeta,
+                 (WalSegMeta{E.count, kind, A.base0 + rel + (kind ? stop : S.seg), E.max_len, kCrcUnknown}));
         KB_WRITE(A.span, 2 * s, 2 * A.nwork, kKbSpan, 0u);
         KB_WRITE(A.span, 2 * s + 1, 2 * A.nwork, kKbSpan, 0u);
     } else {
-        KB_WRITE(A.sub, blockIdx.x, A.nwork * P, kKbSubMeta, (WalSubMeta{first, E.count, E.kind, E.stop, E.pos, E.max_len, {0u, 0u}}));
+        KB_WRITE(A.sub, blockIdx.x, A.nwork * P, kKbSubMeta,
+                 (WalSubMeta{first, E.count, E.kind, E.stop, E.pos, E.max_len, {kCrcUnknown, 0u}}));
+    }
+}
+
+// The walk with the CRCs in the same kernel (the device-planned replay of small records):
+// kFuseWaves walkers per workgroup, each exactly k_wal_walk_sub's walker (its own sub-range,
+// its own 4 KiB tile, no workgroup barriers between them), sharing one LDS image of the quad
+// blob's tables (16 copies).  After its walk each walker checksums its own list (crc_list):
+// the payloads it just read through its tiles (L2 / Infinity Cache hits), no gathered lists,
+// no separate gather and CRC launches.  Reports per walker the first
+// mismatching list entry (kNoBad: none) or kCrcUnknown.
+constexpr int kFuseWaves = kWalFuseWaves;
+static_assert(kRep16Words + kFuseWaves * (int)(sizeof(WaveLds) / 4) <= kSmallBase, "the walkers' tiles fit");
+__global__ __launch_bounds__(kFuseWaves * 64) void k_wal_walk_crc(WalArgs A) {
+    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.crc_blob, A.crc_blob + kBlobWords);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];  // 16-copy image | tiles | small tables
+    load_stream_tables16<kFuseWaves * 64>(lds, A.crc_blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t P = A.nsub, w = (uint64_t)blockIdx.x * kFuseWaves + wave;
+    if (w >= A.nwork * P) return;
+    WaveLds& W = reinterpret_cast<WaveLds*>(lds + kRep16Words)[wave];
+    const CrcCtx C{lds, lane_const16(), reinterpret_cast<const uint8_t*>(A.crc_blob)};
+    const uint64_t s = w / P, j = w % P;
+    const uint64_t rel = s * A.seg_bytes;
+    const Seg S = make_seg(A, s);
+    const uint32_t lo = (uint32_t)(j * A.sub_bytes);
+    const uint32_t hi = (uint64_t)lo + A.sub_bytes < S.seg ? lo + (uint32_t)A.sub_bytes : S.seg;
+    const uint32_t start = s == 0 ? (uint32_t)A.first_pos : 0u;
+    uint32_t first;
+    if (start >= hi)
+        first = hi;
+    else if (start >= lo)
+        first = start;
+    else
+        first = find_start<true>(W, S, lane, lo, hi);
+    const uint64_t slot = s * A.cand_cap + j * A.sub_cap;
+    const WalkEnd E = walk_range<true>(W, S, lane, first, hi, A, slot, A.sub_cap, start < lo && first < hi ? lo : ~0u);
+    const uint32_t fb = crc_list(C, S, A, lane, slot, E.count < A.sub_cap ? E.count : (uint32_t)A.sub_cap, E.max_len);
+    if (lane != 0) return;
+    if (P == 1) {
+        const bool spill = !E.kind && E.pos > S.seg;
+        const uint32_t kind = spill ? kWalSpill : E.kind, stop = spill ? E.pos : E.stop;
+        KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{E.count, kind, A.base0 + rel + (kind ? stop : S.seg), E.max_len, fb}));
+        KB_WRITE(A.span, 2 * s, 2 * A.nwork, kKbSpan, 0u);
+        KB_WRITE(A.span, 2 * s + 1, 2 * A.nwork, kKbSpan, 0u);
+    } else {
+        KB_WRITE(A.sub, w, A.nwork * P, kKbSubMeta, (WalSubMeta{first, E.count, E.kind, E.stop, E.pos, E.max_len, {fb, 0u}}));
     }
 }
 
@@ -585,6 +699,12 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
     (void)total;
     uint32_t pos = s == 0 ? (uint32_t)A.first_pos : 0u;
     uint32_t count = 0, kind = 0, stop = seg, mx = 0;
+    // the walkers' inline CRCs (k_wal_walk_crc; WalSubMeta::pad[0]): the segment's first
+    // mismatching candidate (ordinal among its accepted ones), or kCrcUnknown when a run the
+    // chain accepts was not checksummed whole (a walker with a long payload, a run taken from
+    // past a mismatch in the walker's own rejected prefix, or a sub-range walked here)
+    uint32_t sfb = kNoBad;
+    bool sunk = false;
     // Fast pass, 64 sub-ranges at a time (lane l: sub-range j0 + l): when every walker started
     // exactly where the one before it left off (the usual case: find_start lands on the real
     // chain), each run is accepted whole, and the spans are a prefix sum.  Lane l takes the
@@ -625,6 +745,18 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
             vmx = o > vmx ? o : vmx;
         }
         mx = vmx > mx ? vmx : mx;
+        {
+            const uint32_t f0 = m.pad[0];
+            const bool unk = take && n != 0 && f0 == kCrcUnknown;
+            uint32_t ord = take && f0 < kCrcUnknown ? count + pre - n + f0 : kNoBad;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                const uint32_t o = __shfl_xor(ord, d);
+                ord = o < ord ? o : ord;
+            }
+            if (__ballot(unk)) sunk = true;
+            sfb = ord < sfb ? ord : sfb;
+        }
         const uint64_t kt = __ballot(take && m.kind != 0);
         if (kt) {
             const int l = __builtin_ctzll(kt);
@@ -658,6 +790,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
             m.stop = __builtin_amdgcn_readlane(mine.stop, src);
             m.exit = __builtin_amdgcn_readlane(mine.exit, src);
             m.max_len = __builtin_amdgcn_readlane(mine.max_len, src);
+            m.pad[0] = __builtin_amdgcn_readlane(mine.pad[0], src);
             int64_t idx = -1;
             if (m.first == pos) {
                 idx = 0;
@@ -679,6 +812,9 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
             if (idx >= 0) {
                 st += (uint32_t)idx;
                 n = m.count - (uint32_t)idx;
+                if (n && (m.pad[0] == kCrcUnknown || (m.pad[0] != kNoBad && m.pad[0] < (uint32_t)idx))) sunk = true;
+                else if (m.pad[0] < kCrcUnknown && count + (m.pad[0] - (uint32_t)idx) < sfb)
+                    sfb = count + (m.pad[0] - (uint32_t)idx);
                 pos = m.exit;
                 mx = m.max_len > mx ? m.max_len : mx;  // of the walker's whole list: an upper bound
                 if (m.kind) {
@@ -688,6 +824,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
             } else {
                 const WalkEnd E = walk_range(W, S, lane, pos, hi, A, c0 + st, A.sub_cap);
                 n = E.count;
+                if (n) sunk = true;  // no inline CRCs for this run
                 pos = E.pos;
                 mx = E.max_len > mx ? E.max_len : mx;
                 if (E.kind) {
@@ -706,7 +843,9 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
         kind = kWalSpill;
         stop = pos;
     }
-    if (lane == 0) KB_WRITE(A.meta, s, A.nwork, kKbMeta, (WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg), mx, 0u}));
+    if (lane == 0)
+        KB_WRITE(A.meta, s, A.nwork, kKbMeta,
+                 (WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg), mx, sunk ? kCrcUnknown : sfb}));
 }
 
 // The replay plan on the device (one block): replay enters segment s + 1 only when segment s
@@ -751,12 +890,39 @@ __global__ __launch_bounds__(1024) void k_wal_plan(WalArgs A) {
         __syncthreads();  // s_wsum is rewritten by the next chunk
     }
     atomicMax(&s_max, mx);
+    // the inline CRCs' first mismatch in WAL order (k_wal_walk_crc): min over the segments replay
+    // enters of list offset + the segment's ordinal, packed with the segment; or unknown
+    __shared__ unsigned long long s_bad;
+    __shared__ uint32_t s_unk;
+    if (tid == 0) {
+        s_bad = ~0ull;
+        s_unk = 0;
+    }
+    __syncthreads();
+    for (uint64_t w = tid; w < w1; w += blockDim.x) {
+        const uint32_t fb = A.meta[w].first_bad;
+        if (fb == kCrcUnknown) s_unk = 1;
+        else if (fb != kNoBad) atomicMin(&s_bad, ((A.cand_base[w] + fb) << 24) | w);  // < 2^40 candidates, < 2^24 segments
+    }
     __syncthreads();
     if (tid == 0) {
-        WalSummary S{carry, A.wal_end, w1, KARMA_WAL_END, s_max, 0u, ~0ull};
+        WalSummary S{carry, A.wal_end, w1, KARMA_WAL_END, s_max, s_unk, ~0ull, 0ull};
         if (w1 > 0 && A.meta[w1 - 1].kind != KARMA_WAL_END) {
             S.status = A.meta[w1 - 1].kind;
             S.end = A.meta[w1 - 1].stop;
+        }
+        if (!s_unk && s_bad != ~0ull) {  // its header offset: the segment's run holding the ordinal
+            const uint64_t g = s_bad >> 24, w = s_bad & 0xffffffu, o = g - A.cand_base[w];
+            const uint32_t* sp = A.span + 2 * w * A.nsub;
+            uint32_t a = 0, b = (uint32_t)A.nsub;  // the last run whose prefix is <= o
+            while (b - a > 1) {
+                const uint32_t mid = (a + b) / 2;
+                if (sp[2 * mid + 1] <= o) a = mid;
+                else b = mid;
+            }
+            const uint64_t slot = sp[2 * a] + (o - sp[2 * a + 1]);
+            S.first_bad = g;
+            S.bad_off = w * A.seg_bytes + KB_READ(A.cand_rec, w * A.cand_cap + slot, A.nwork * A.cand_cap, kKbCand);
         }
         *A.sum = S;
     }
@@ -816,7 +982,7 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
             n_all += s_all[v];
         }
         if (blockIdx.x == 0 && tid == 0) {
-            WalSummary S{n_all, A.wal_end, w1, KARMA_WAL_END, s_max, 0u, ~0ull};
+            WalSummary S{n_all, A.wal_end, w1, KARMA_WAL_END, s_max, 1u, ~0ull, 0ull};
             if (A.meta[w1 - 1].kind != KARMA_WAL_END) {
                 S.status = A.meta[w1 - 1].kind;
                 S.end = A.meta[w1 - 1].stop;
@@ -893,10 +1059,15 @@ hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& p
         return hipGetLastError();
     }
 #endif
-    {
+    if (plan.kernel == 2) {
+        if (!a.crc_blob) return hipErrorInvalidValue;
+        const uint64_t walkers = nseg * plan.nsub;
+        hipLaunchKernelGGL(k_wal_walk_crc, dim3((unsigned)((walkers + kFuseWaves - 1) / kFuseWaves)),
+                           dim3(kFuseWaves * 64), 0, s, a);
+    } else {
         hipLaunchKernelGGL(k_wal_walk_sub, dim3((unsigned)(nseg * plan.nsub)), dim3(64), 0, s, a);
-        if (plan.nsub > 1) hipLaunchKernelGGL(k_wal_resolve, dim3((unsigned)nseg), dim3(64), 0, s, a);
     }
+    if (plan.nsub > 1) hipLaunchKernelGGL(k_wal_resolve, dim3((unsigned)nseg), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

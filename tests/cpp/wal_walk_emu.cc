@@ -296,7 +296,9 @@ Plan walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes) {
     if (sub_bytes) {
         sub_tiles = std::max<uint64_t>(1, sub_bytes / kWTile);
     } else {
-        const uint64_t want = 20 * (uint64_t)(cu > 0 ? cu : 1);
+        // the default replay plan walks with the CRCs in the same kernel: 15 walkers per CU
+        // (k_wal_walk_crc, kFuseWaves; the walk itself is k_wal_walk_sub's, restated here)
+        const uint64_t want = 15 * (uint64_t)(cu > 0 ? cu : 1);
         if (nseg > 0 && nseg < want) {
             const uint64_t per = (want + nseg - 1) / nseg;
             sub_tiles = std::max<uint64_t>(4, (tiles + per - 1) / per);

@@ -15,6 +15,8 @@ copy for each variant in interleaved rounds (same process, same image):
     direct4              tools build, KARMA_DIRECT_VARIANT=4 (= the shipped k_ragged_direct4<4>)
     direct2              tools build, KARMA_DIRECT_VARIANT=5 (k_ragged_direct4<2>: pairs of lanes)
     units                the shipped library, ragged plan instead of the direct kernel (crc_batch)
+    sep                  the shipped library, KARMA_WAL_CRC_SEPARATE: walk, gather, one batch (round 2's path;
+                         the default now checksums inside the walk kernel, k_wal_walk_crc)
 
 Every call's result is checked (record count).  Prints ms per call and GB/s of image bytes per
 variant (median over rounds).
@@ -102,6 +104,8 @@ def main():
             variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "5"))
         elif v == "units":
             variants[v] = (L, 0, 2, None)
+        elif v == "sep":  # the walk, then one small-record batch over the gathered lists (round 2's path)
+            variants[v] = (L, 0, 3, None)
         elif v.startswith("sub="):
             variants[v] = (L, int(v[4:]), 0, None)
     res = {v: [] for v in variants}
