@@ -425,7 +425,8 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
             accepted = S->first_bad;
             status = KARMA_WAL_CORRUPT;
             uint64_t at = 0;
-            if (hipMemcpy(&at, A.off + accepted, 8, hipMemcpyDeviceToHost) != hipSuccess)
+            if (hipMemcpyAsync(&at, A.off + accepted, 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+                hipStreamSynchronize(c.st) != hipSuccess)
                 return fail(KARMA_E_HIP, "wal_replay: D2H");
             end = base0 + at;
         }
@@ -436,7 +437,10 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         }
         if (h_rec_off && rec_cap && accepted) {
             const uint64_t k = std::min<uint64_t>(accepted, rec_cap);
-            if (hipMemcpy(h_rec_off, A.off, k * 8, hipMemcpyDeviceToHost) != hipSuccess)
+            // (on the replay's stream: it is non-blocking, so a legacy-stream copy would not wait
+            // for the gather just enqueued there)
+            if (hipMemcpyAsync(h_rec_off, A.off, k * 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+                hipStreamSynchronize(c.st) != hipSuccess)
                 return fail(KARMA_E_HIP, "wal_replay: D2H offsets");
             parallel_for(0, k, 1 << 16, [&](uint64_t i) { h_rec_off[i] += base0; });
         }

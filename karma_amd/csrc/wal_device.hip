@@ -737,15 +737,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
             KB_WRITE(A.span, 2 * (s * P + jj), 2 * A.nwork * P, kKbSpan, (uint32_t)(jj * A.sub_cap));
             KB_WRITE(A.span, 2 * (s * P + jj) + 1, 2 * A.nwork * P, kKbSpan, count + pre - n);
         }
-        count += __shfl(pre, 63);
-        uint32_t vmx = take ? m.max_len : 0u;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            const uint32_t o = __shfl_xor(vmx, d);
-            vmx = o > vmx ? o : vmx;
-        }
-        mx = vmx > mx ? vmx : mx;
-        {
+        {  // (count: the candidates before this batch of runs)
             const uint32_t f0 = m.pad[0];
             const bool unk = take && n != 0 && f0 == kCrcUnknown;
             uint32_t ord = take && f0 < kCrcUnknown ? count + pre - n + f0 : kNoBad;
@@ -757,6 +749,14 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
             if (__ballot(unk)) sunk = true;
             sfb = ord < sfb ? ord : sfb;
         }
+        count += __shfl(pre, 63);
+        uint32_t vmx = take ? m.max_len : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t o = __shfl_xor(vmx, d);
+            vmx = o > vmx ? o : vmx;
+        }
+        mx = vmx > mx ? vmx : mx;
         const uint64_t kt = __ballot(take && m.kind != 0);
         if (kt) {
             const int l = __builtin_ctzll(kt);

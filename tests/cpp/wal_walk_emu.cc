@@ -8,6 +8,10 @@
 //                                  tile_header), k_wal_resolve,
 //                                  k_wal_gather, k_wal_compare
 //   karma_amd/csrc/wal.cc          replay_core's planning around them
+//   k_wal_walk_crc / k_wal_resolve / k_wal_plan's inline CRCs: each walker's first mismatching
+//                                  list entry, the resolver's per-segment ordinal, the plan's
+//                                  minimum -- which must equal the gathered batch's first
+//                                  mismatch whenever every accepted run was checksummed
 //   karma_amd/csrc/crc_ragged.hip  the 16-byte blocks k_ragged_direct reads per record
 // and checks, on every access:
 //   * each global read of a walker lies inside its own segment ([0, seg) of segment s);
@@ -34,7 +38,7 @@ constexpr uint32_t kStaleZero = 0x48674BC7u;  // crc32c::Value("\0\0\0\0")
 constexpr uint32_t kStaleAdvance = 12;         // an accepted size-0 record: 8 + 4 stale bytes (sivir.cc:38)
 enum { END = 0, CORRUPT = 1, BAD_TYPE = 2, SPILL = 16 };
 
-uint64_t g_reads = 0, g_slots = 0;
+uint64_t g_reads = 0, g_slots = 0, g_inline_known = 0, g_inline_unknown = 0;
 
 [[noreturn]] void die(const char* what, uint64_t a, uint64_t b) {
     std::fprintf(stderr, "VIOLATION: %s (%llu, %llu)\n", what, (unsigned long long)a, (unsigned long long)b);
@@ -317,13 +321,14 @@ Plan walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes) {
 }
 
 struct SubMeta {
-    uint32_t first, count, kind, stop, exit, max_len;
+    uint32_t first, count, kind, stop, exit, max_len, fb;  // fb: the walker's inline-CRC result
 };
 struct SegMeta {
     uint32_t count, kind;
     uint64_t stop;
-    uint32_t max_len;
+    uint32_t max_len, first_bad;  // first_bad: the segment's inline-CRC ordinal / unknown
 };
+constexpr uint32_t kNoBad = ~0u, kCrcUnknown = ~0u - 1, kCrcInlineMax = 1024;
 
 // replay_pass (wal.cc): one device pass from start; appends the accepted offsets to recs
 void replay_pass(const std::vector<uint8_t>& file, uint64_t seg_bytes, uint64_t start, uint64_t force_sub, int cu,
@@ -363,14 +368,28 @@ void replay_pass(const std::vector<uint8_t>& file, uint64_t seg_bytes, uint64_t 
             const List L{&crec, &clen, &ccrc, s * plan.cand_cap + j * plan.sub_cap, plan.sub_cap};
             const WalkEnd E = walk_range(W, S, first, hi, L);
             if (E.count > plan.sub_cap) die("walker list longer than its capacity", E.count, plan.sub_cap);
+            // k_wal_walk_crc's crc_list: the walker's own list, the first entry whose payload CRC
+            // differs (size 0: checked by the walk), or unknown when a payload is over 1 KiB
+            uint32_t fb = kNoBad;
+            if (E.count && E.max_len > kCrcInlineMax) {
+                fb = kCrcUnknown;
+            } else {
+                for (uint32_t i = 0; i < E.count; ++i) {
+                    const uint64_t slot = L.base + i;
+                    if (clen[slot] && crc32c(S.img + crec[slot] + 8, clen[slot]) != ccrc[slot]) {
+                        fb = i;
+                        break;
+                    }
+                }
+            }
             if (plan.nsub == 1) {
                 const bool spill = !E.kind && E.pos > S.seg;
                 const uint32_t kind = spill ? (uint32_t)SPILL : E.kind, stop = spill ? E.pos : E.stop;
-                meta[s] = SegMeta{E.count, kind, base0 + rel + (kind ? stop : S.seg), E.max_len};
+                meta[s] = SegMeta{E.count, kind, base0 + rel + (kind ? stop : S.seg), E.max_len, fb};
                 span[2 * s] = 0;
                 span[2 * s + 1] = 0;
             } else {
-                sub[s * plan.nsub + j] = SubMeta{first, E.count, E.kind, E.stop, E.pos, E.max_len};
+                sub[s * plan.nsub + j] = SubMeta{first, E.count, E.kind, E.stop, E.pos, E.max_len, fb};
             }
         }
     // k_wal_resolve: one wave per segment, along the real chain
@@ -380,6 +399,8 @@ void replay_pass(const std::vector<uint8_t>& file, uint64_t seg_bytes, uint64_t 
             const Seg S{wal + rel, (uint32_t)seg_bytes, ((reinterpret_cast<uintptr_t>(wal + rel)) & 15u) == 0};
             const uint32_t seg = S.seg;
             uint32_t pos = s == 0 ? (uint32_t)first_pos : 0u, count = 0, kind = 0, stop = seg, mx = 0;
+            uint32_t sfb = kNoBad;  // k_wal_resolve's inline-CRC ordinal of the segment
+            bool sunk = false;
             for (uint64_t j = 0; j < P; ++j) {
                 const uint32_t lo = (uint32_t)(j * plan.sub_bytes);
                 const uint32_t hi = (uint64_t)lo + plan.sub_bytes < seg ? lo + (uint32_t)plan.sub_bytes : seg;
@@ -406,6 +427,8 @@ void replay_pass(const std::vector<uint8_t>& file, uint64_t seg_bytes, uint64_t 
                     if (idx >= 0) {
                         st += (uint32_t)idx;
                         n = m.count - (uint32_t)idx;
+                        if (n && (m.fb == kCrcUnknown || (m.fb != kNoBad && m.fb < (uint32_t)idx))) sunk = true;
+                        else if (m.fb < kCrcUnknown) sfb = std::min(sfb, count + (m.fb - (uint32_t)idx));
                         pos = m.exit;
                         mx = std::max(mx, m.max_len);
                         if (m.kind) {
@@ -416,6 +439,7 @@ void replay_pass(const std::vector<uint8_t>& file, uint64_t seg_bytes, uint64_t 
                         const List L{&crec, &clen, &ccrc, cbase + st, plan.sub_cap};
                         const WalkEnd E = walk_range(W, S, pos, hi, L);
                         n = E.count;
+                        if (n) sunk = true;  // walked by the resolver: no inline CRCs
                         pos = E.pos;
                         mx = std::max(mx, E.max_len);
                         if (E.kind) {
@@ -432,7 +456,7 @@ void replay_pass(const std::vector<uint8_t>& file, uint64_t seg_bytes, uint64_t 
                 kind = SPILL;
                 stop = pos;
             }
-            meta[s] = SegMeta{count, kind, base0 + rel + (kind ? stop : seg), mx};
+            meta[s] = SegMeta{count, kind, base0 + rel + (kind ? stop : seg), mx, sunk ? kCrcUnknown : sfb};
         }
     // replay_core: replay enters segment s + 1 only if segment s ended cleanly
     int status = END;
@@ -486,6 +510,22 @@ void replay_pass(const std::vector<uint8_t>& file, uint64_t seg_bytes, uint64_t 
             break;
         }
     }
+    // k_wal_plan with the inline CRCs: the first mismatch = min over the segments entered of
+    // list offset + ordinal, unless some segment is unknown (the replay then runs the batch
+    // above); when known it must be the batch's answer
+    bool unknown = false;
+    uint64_t inline_bad = ~0ull;
+    for (uint64_t w = 0; w < w1; ++w) {
+        if (meta[w].first_bad == kCrcUnknown) unknown = true;
+        else if (meta[w].first_bad != kNoBad) inline_bad = std::min<uint64_t>(inline_bad, cb[w] + meta[w].first_bad);
+    }
+    if (!unknown) {
+        const uint64_t want = first_bad < n_all ? first_bad : ~0ull;
+        if (inline_bad != want) die("inline CRC first mismatch differs from the batch's", inline_bad, want);
+        ++g_inline_known;
+    } else {
+        ++g_inline_unknown;
+    }
     uint64_t accepted = n_all;
     if (first_bad < n_all) {
         accepted = first_bad;
@@ -495,9 +535,11 @@ void replay_pass(const std::vector<uint8_t>& file, uint64_t seg_bytes, uint64_t 
     for (uint64_t g = 0; g < accepted; ++g) recs.push_back(off[g] + base0);
     end_out = end;
     status_out = status;
-    std::fprintf(stderr, "pass from %llu: plan nsub=%llu sub_bytes=%llu; checked %llu walker reads, %llu list slots\n",
+    std::fprintf(stderr,
+                 "pass from %llu: plan nsub=%llu sub_bytes=%llu; checked %llu walker reads, %llu list slots; inline "
+                 "CRCs %s\n",
                  (unsigned long long)start, (unsigned long long)plan.nsub, (unsigned long long)plan.sub_bytes,
-                 (unsigned long long)g_reads, (unsigned long long)g_slots);
+                 (unsigned long long)g_reads, (unsigned long long)g_slots, unknown ? "unknown (batch)" : "known");
 }
 
 }  // namespace
