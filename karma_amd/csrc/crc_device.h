@@ -436,7 +436,10 @@ __device__ __forceinline__ uint32_t stream_unit(const uint32_t* lds, uint32_t X,
 // stepped (stream_unit).  A group with no body in a round streams an empty unit at `safe`
 // (16-byte aligned, always mapped): every load is issued unconditionally.  Returns this
 // lane's CRC (valid when vi); every lane of the wave must call it.
-template <int G, int PF, bool NT, int MODE>
+// ALL: every round's first 1 + PF chunk loads are issued at once, before the head steps
+// (records of up to 16 G (1 + PF) bytes then wait on memory once per batch instead of once per
+// round; longer ones stream the rest within their round).
+template <int G, int PF, bool NT, int MODE, bool ALL = false>
 __device__ __forceinline__ uint32_t direct_batch(const uint32_t* lds, uint32_t X, const uint8_t* safe,
                                                  const uint8_t* pi, uint32_t ni, uint32_t initi, bool vi) {
     constexpr int NG = 64 / G, NR = 64 / NG;  // groups per wave, rounds
@@ -453,13 +456,33 @@ __device__ __forceinline__ uint32_t direct_batch(const uint32_t* lds, uint32_t X
         const uint8_t* ue = reinterpret_cast<const uint8_t*>((uintptr_t)__shfl((long long)bi, src));
         return lane_unit<G>(us, ue, l);
     };
+    uint32_t Ri = 0;
+    if constexpr (ALL) {
+        UnitLoads<PF> Ld[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) issue_unit_loads<PF, NT, G>(unit_of(r), Ld[r]);
+        const bool tail = body && gi.e > gi.b;
+        const u32x4 tv = ld16(tail ? gi.b : safe);
+        const uint32_t hi = body ? ((MODE & 4) ? initi : head_register(lds, kLZ4, kLT8, pi, gi, initi)) : 0u;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const uint32_t sh = __shfl(hi, (int)(r * NG + grp));
+            const LaneUnit L = unit_of(r);
+            const uint32_t R = stream_unit<PF, NT, MODE, G>(lds, X, l, L, Ld[r], L.us, sh, [](UnitLoads<PF>&) {});
+            const uint32_t Rr = __shfl(R, (int)((lane % NG) * G));  // group (lane % NG)'s register
+            if (lane / NG == (uint32_t)r) Ri = Rr;
+        }
+        if (!vi) return 0u;
+        return gi.is_short ? short_record(lds, kLZ4, kLT8, pi, ni, initi)
+               : (MODE & 4) ? Ri ^ tv.x
+                            : ~steps_in_vec(lds, kLZ4, kLT8, Ri, tv, 0u, tail ? (uint32_t)(gi.e - gi.b) : 0u);
+    }
     LaneUnit L = unit_of(0);
     UnitLoads<PF> Ld;
     issue_unit_loads<PF, NT, G>(L, Ld);
     const bool tail = body && gi.e > gi.b;
     const u32x4 tv = ld16(tail ? gi.b : safe);
     const uint32_t hi = body ? ((MODE & 4) ? initi : head_register(lds, kLZ4, kLT8, pi, gi, initi)) : 0u;
-    uint32_t Ri = 0;
 #pragma unroll 1
     for (uint32_t round = 0; round < NR; ++round) {
         const uint32_t sh = __shfl(hi, (int)(round * NG + grp));

@@ -80,20 +80,31 @@ __device__ void fused_record_fold(const FixedArgs& A, uint32_t* lds, uint32_t* w
     const int64_t pad = (int64_t)(m * 1024 - k_in);
     const int64_t i0 = (int64_t)(threadIdx.x * m) - pad;
     unsigned long long* st = reinterpret_cast<unsigned long long*>(A.partial);
+    // 8 states per thread in flight at once (the first 8 before the table copy), then checked
+    constexpr int kQ = 8;
+    auto load8 = [&](uint64_t q0, unsigned long long (&w)[kQ]) {
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+            w[q] = q0 + q < m && i0 + (int64_t)(q0 + q) >= 0
+                       ? __hip_atomic_load(st + i0 + q0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : ((unsigned long long)tag << 32);
+    };
+    unsigned long long w[kQ];
+    load8(0, w);
     copy_to_lds<kBlockCombWords, kBlockThreads>(lds, A.block_blob);
     __syncthreads();
     uint32_t acc = 0;
-    for (uint64_t q = 0; q < m; ++q) {
-        uint32_t v = 0;
-        if (i0 + (int64_t)q >= 0) {
-            unsigned long long w = __hip_atomic_load(st + i0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while ((uint32_t)(w >> 32) != tag) {
+    for (uint64_t q0 = 0; q0 < m; q0 += kQ) {
+        if (q0) load8(q0, w);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            if (q0 + q >= m) break;
+            while ((uint32_t)(w[q] >> 32) != tag) {  // a store not visible yet: wait for it
                 __builtin_amdgcn_s_sleep(1);
-                w = __hip_atomic_load(st + i0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                w[q] = __hip_atomic_load(st + i0 + q0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            v = (uint32_t)w;
+            acc = zmap(lds, kBcZD, acc) ^ (uint32_t)w[q];
         }
-        acc = zmap(lds, kBcZD, acc) ^ v;
     }
 #pragma unroll
     for (int d = 0; d < 6; ++d) {

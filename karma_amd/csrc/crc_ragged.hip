@@ -921,8 +921,8 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
 // replay call of 1M x 180 B, 4: 0.202, 2: 0.222 -- their loads then spread over 32 cache
 // lines per instruction; one record per lane: 0.327).  G = 2 is the tools
 // build's KARMA_DIRECT_VARIANT=5 (the pair blob, Z_32).
-template <int G, int MODE = 0>  // MODE != 0: timing-only variants of the tools build (bits 0-1:
-                                 // stream_unit's, crc_device.h; bit 2: no head / tail steps)
+template <int G, int MODE = 0, int PF = kRaggedPF, bool ALL = false>  // MODE != 0: timing-only variants of the
+                                 // tools build (bits 0-1: stream_unit's, crc_device.h; bit 2: no head / tail steps)
 __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) {
     uint64_t n_rec = A.n_rec;
     if (A.n_dev) {  // a device-sized batch: the count is known on the device only
@@ -944,7 +944,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
         const uint8_t* pi = vi ? A.arena + A.off[ri] : A.arena;
         const uint32_t ni = vi ? A.len[ri] : 0u;
         const uint32_t initi = vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
-        const uint32_t res = direct_batch<G, kRaggedPF, kRaggedNT, MODE>(lds, X, safe, pi, ni, initi, vi);
+        const uint32_t res = direct_batch<G, PF, kRaggedNT, MODE, ALL>(lds, X, safe, pi, ni, initi, vi);
         if (vi) {
             A.out[ri] = res;
             if (A.cmp_stored && ni && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
@@ -1161,6 +1161,12 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL((k_ragged_direct4<4, 4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 10)
         hipLaunchKernelGGL((k_ragged_direct4<4, 7>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 11)  // every round's first loads at once (direct_batch ALL), 2 / 4 chunks each
+        hipLaunchKernelGGL((k_ragged_direct4<4, 0, 2, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 12)
+        hipLaunchKernelGGL((k_ragged_direct4<4, 0, 4, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 13)  // one round ahead (the shipped form) with 2 chunks
+        hipLaunchKernelGGL((k_ragged_direct4<4, 0, 2, false>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else
 #endif
         hipLaunchKernelGGL(k_ragged_direct4<4>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);

@@ -7,7 +7,9 @@ n payloads of --size bytes at a 188-byte stride (+8: the WAL image's header offs
 karma_crc32c_batch_ragged_bounded(max_len 1024) through the tools build with
 KARMA_DIRECT_VARIANT = each variant, interleaved rounds; kernel time from HIP events around
 --calls calls.  Variants 6-10 are timing-only (wrong CRCs): 6 no body lookups, 7 no lane fold
-and group tree, 8 neither, 9 no head / tail steps, 10 none of these.
+and group tree, 8 neither, 9 no head / tail steps, 10 none of these.  11 / 12: every round's
+first 2 / 4 chunk loads issued at once (direct_batch ALL); 13: the shipped pipeline with 2 chunks
+(11-13 are exact: checked against the shipped kernel's CRCs; list "0" first).
 """
 import argparse
 import ctypes
@@ -63,6 +65,10 @@ def main():
             res[v].append(e0.elapsed_time(e1) / a.calls * 1e3)
             if v == "0" and ref is None:
                 ref = out.clone()
+            elif r == 0 and v in ("11", "12", "13") and ref is not None:  # exact variants: the same CRCs
+                bad = int((out != ref).sum().item())
+                print(f"variant {v}: {bad} CRCs differ from the shipped kernel's", flush=True)
+                assert bad == 0
         print(f"round {r}: " + "  ".join(f"v{v} {res[v][-1]:.2f}" for v in variants), flush=True)
     if ref is not None:  # the shipped kernel against the oracle's first records
         sys.path.insert(0, os.path.join(ROOT, "tests"))
