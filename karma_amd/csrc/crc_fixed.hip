@@ -69,7 +69,7 @@ __device__ __forceinline__ FixedPlan fixed_plan(const FixedArgs& A, uint64_t u, 
 // a wave hold units 8i..8i+7 of one record, end-aligned; a 3-level tree over
 // the groups (Z_U, Z_2U, Z_4U) leaves one state per 8 units, so the combine
 // kernels start one level up (a 64 MiB segment: 32768 -> 4096 states here).
-// The fused combine of FUSE (one record, its wave states folded by the workgroup that ends last):
+// The fused combine of FUSE (one record, its wave states folded by the grid's last workgroup):
 // thread t folds states [t m, t m + m) with Z_D (leading zero states pad k_in to 1024 m), reading
 // each tagged state with an agent-scope atomic load until it carries this call's tag (a state
 // whose store is not visible yet is waited for; no release fence or L2 write-back is needed);
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     constexpr bool kMaps = WAVE_COMB || KW > 1;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kMaps ? kLdsWordsComb : kLdsWords];
     __shared__ uint32_t blk_next;  // BAL: the block's next wave-step (an LDS counter, lgkmcnt only)
-    __shared__ uint32_t s_tag, s_last;  // FUSE: this call's tag; this block ends last
+    __shared__ uint32_t s_tag;  // FUSE: this call's tag
     if (FUSE && threadIdx.x == 0) {
         const uint32_t t = (uint32_t)__hip_atomic_load(A.fctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
         s_tag = t ? t : 1u;
@@ -229,21 +229,17 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
         u = wb * kGroupsPerWave + grp;
     }
     WLOG_END(wlog_id);
-    if constexpr (FUSE) {  // the workgroup that ends last folds the record's wave states
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned long long done =
-                __hip_atomic_fetch_add(A.fctl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = done + 1 == gridDim.x;
-        }
-        __syncthreads();
-        if (!s_last) return;
+    if constexpr (FUSE) {  // the grid's last workgroup folds the record's wave states
+        // (no completion counter: 256 workgroups' atomics on one word serialise at the memory
+        // side; the fold waits on each state's tag instead.  Every workgroup reads the tag at
+        // its start, before its states exist, so the fold -- which waits for all of them --
+        // retires the tag only after every workgroup has read it.)
+        if (blockIdx.x + 1 != gridDim.x) return;
+        __syncthreads();  // this workgroup's waves are done with the stream tables
         __shared__ uint32_t wv[16];
         fused_record_fold(A, lds, wv, A.units_per_rec / kGroupsPerWave, s_tag);
-        if (threadIdx.x == 0) {  // ready for the next call (stream order): counter 0, tag retired
-            __hip_atomic_store(A.fctl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0)  // retired: the next call (stream order) takes the next tag
             __hip_atomic_store(A.fctl + 1, (unsigned long long)s_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 

@@ -82,9 +82,9 @@ struct FixedArgs {
                                // them with comb_maps and writes out[] itself (0: not used)
     // Fused record combine (one record, WAVE_COMB; k_units_fixed FUSE): the wave states go out
     // tagged, (tag << 32 | state), as agent-scope atomic stores into partial (as uint64); the
-    // workgroup that finishes last (fctl[0] counts them) folds them like k_combine_block with
-    // block_blob and writes the CRC.  fctl[1] = the last finished call's tag (device-resident,
-    // so a captured graph replays correctly).  nullptr: not fused.
+    // grid's last workgroup folds them like k_combine_block with block_blob, waiting on each
+    // state's tag, and writes the CRC.  fctl[1] = the last finished call's tag (device-resident,
+    // so a captured graph replays correctly; fctl[0] unused).  nullptr: not fused.
     unsigned long long* fctl;
     const uint32_t* block_blob; // kBlockCombWords (block_comb_blob for D = 8 units, m states per thread)
     uint64_t comb_m;            // states per thread of the fused fold
