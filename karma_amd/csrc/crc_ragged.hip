@@ -392,10 +392,12 @@ __device__ void lookback_retire(const RaggedArgs& A) {
         for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.lb_words; i += stride)
             lb_store(A.lb + 1 + i, 0ull);
     }
-    if (threadIdx.x == 0) {
+    // one workgroup writes the control words: hundreds of workgroups storing the same words
+    // queue at the memory side (it cost the call ~30 us)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         lb_store(A.lb, 0ull);
         lb_store(A.lb_ctl, wrap ? 0ull : (unsigned long long)seq);
-        lb_store(A.lb_ctl + 2, 0ull);  // the longest partial run (k_ragged_plan's atomicMax)
+        lb_store(A.lb_ctl + 2, 0ull);  // the longest partial run (the tools build's rank-major order)
     }
 }
 
@@ -455,7 +457,9 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
             // the block's partial run (first slot after part_base, length) and the longest run:
             // the units kernel's rank-major order (k_units_ragged_pipe, RM)
             A.block_psums[b] = (exP << 16) | part_b;
+#ifdef KARMA_AB  // (the rank-major variants' longest run: one atomic per plan block, tools build only)
             atomicMax(A.lb_ctl + 2, (unsigned long long)part_b);
+#endif
         }
     }
     uint32_t h = 0;
