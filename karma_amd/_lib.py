@@ -19,6 +19,9 @@ AB_LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "lib", "libkarma_crc
 # The bounds-checked debug build (karma_amd/csrc/bounds.h): the same C ABI plus
 # karma_debug_bounds_report; the GPU suite runs on it under `pytest --karma-lib bounds`.
 BOUNDS_LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "lib", "libkarma_crc32c_bounds.so")
+# The tools build with the bounds checks (`make abbounds`): `pytest --karma-lib abbounds` runs the
+# variant tests on it (and the rest of the suite on BOUNDS_LIB_PATH).
+ABBOUNDS_LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "lib", "libkarma_crc32c_abbounds.so")
 KB_SITES = {1: "WAL image byte outside the image", 2: "WAL image byte outside the walker's segment",
             3: "candidate slot outside the segment's lists", 4: "candidate write dropped by the cap guard",
             5: "sub-range report index", 6: "span index", 7: "segment meta index", 8: "gathered list index",
@@ -117,6 +120,10 @@ def load(path: str) -> ctypes.CDLL:
             handle.karma_debug_bounds_report.argtypes = [_vp, _i]
         _LOADED[path] = handle
     return _LOADED[path]
+
+
+def is_loaded(path: str) -> bool:
+    return path in _LOADED
 
 
 def lib() -> ctypes.CDLL:

@@ -89,12 +89,16 @@ __device__ __forceinline__ uint32_t zmap(const uint32_t* lds, int base, uint32_t
 // (crc32c.cc:312-319): Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0)))).  (The expanded form
 // Z16(a0)^Z12(a1)^Z8(a2)^Z4(a3), one LDS round trip instead of four, measured
 // no faster and costs 8 KiB of LDS: DESIGN.md §4.)
+__device__ __forceinline__ uint32_t lane_fold_at(const uint32_t* lds, int z4, uint32_t a0, uint32_t a1, uint32_t a2,
+                                                 uint32_t a3) {
+    uint32_t c = zmap(lds, z4, a0);
+    c = zmap(lds, z4, c ^ a1);
+    c = zmap(lds, z4, c ^ a2);
+    return zmap(lds, z4, c ^ a3);
+}
 __device__ __forceinline__ uint32_t lane_fold(const uint32_t* lds, uint32_t a0, uint32_t a1, uint32_t a2,
                                               uint32_t a3) {
-    uint32_t c = zmap(lds, kLZ4, a0);
-    c = zmap(lds, kLZ4, c ^ a1);
-    c = zmap(lds, kLZ4, c ^ a2);
-    return zmap(lds, kLZ4, c ^ a3);
+    return lane_fold_at(lds, kLZ4, a0, a1, a2, a3);
 }
 
 // One data byte (STEP1).
@@ -547,10 +551,11 @@ __device__ __forceinline__ void load_stream_tables(uint32_t* lds, const uint32_t
     for (int q = 0; q < IT; ++q) l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e[q], e[q], e[q], e[q]};
 }
 
-// The 16-copy image of a stream / quad blob for THREADS threads: [0, kRep16Words) the
-// stride tables (stride_step16), the small tables at kSmallBase as in load_stream_tables.
-template <int THREADS>
-__device__ __forceinline__ void load_stream_tables16(uint32_t* lds, const uint32_t* __restrict__ blob) {
+// The 16-copy image of a blob's stride tables for THREADS threads, [0, kRep16Words)
+// (stride_step16, lane_const16); `between` runs after the table loads are issued and
+// before they are stored (the caller's other copies overlap them).
+template <int THREADS, typename Between>
+__device__ __forceinline__ void load_rep16_stride(uint32_t* lds, const uint32_t* __restrict__ blob, Between&& between) {
     // vector v of row e: table k = (v >> 2) & 3, copies 4 (v & 3) .. +3
     constexpr int NV = kRep16Words / 4;
     constexpr int IT = (NV + THREADS - 1) / THREADS;
@@ -561,13 +566,20 @@ __device__ __forceinline__ void load_stream_tables16(uint32_t* lds, const uint32
         const int row = v >> 4, k = (v >> 2) & 3;
         e[q] = v < NV ? *(const __attribute__((address_space(1))) uint32_t*)(blob + kBlobStride + k * 256 + row) : 0u;
     }
-    copy_to_lds<kSmallWords, THREADS>(lds + kSmallBase, blob + 1024);
+    between();
     u32x4* l4 = reinterpret_cast<u32x4*>(lds);
 #pragma unroll
     for (int q = 0; q < IT; ++q) {
         const int v = (int)threadIdx.x + q * THREADS;
         if (v < NV) l4[v] = u32x4{e[q], e[q], e[q], e[q]};
     }
+}
+
+// The 16-copy image of a stream / quad blob for THREADS threads: [0, kRep16Words) the
+// stride tables (stride_step16, lane_const16), the small tables at kSmallBase as in load_stream_tables.
+template <int THREADS>
+__device__ __forceinline__ void load_stream_tables16(uint32_t* lds, const uint32_t* __restrict__ blob) {
+    load_rep16_stride<THREADS>(lds, blob, [&] { copy_to_lds<kSmallWords, THREADS>(lds + kSmallBase, blob + 1024); });
 }
 
 // Per-lane constant of the replicated-table address (see the LDS image above).
@@ -599,6 +611,45 @@ __device__ __forceinline__ uint32_t wave_tree(const uint32_t* lds, uint32_t v) {
         v = zmap(lds, d * 1024, v) ^ t;
     }
     return v;
+}
+
+// LDS writes of a wave visible to its own later LDS reads (and its reads done before its
+// next writes): the wave's LDS operations complete in order, so a wait for them and a
+// compiler barrier suffice (no workgroup barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One record per lane: [p, p + n) with init, its aligned 16-byte blocks read through
+// src(address) (16-aligned absolute address; LDS staging or global memory).  The reference's
+// own structure (crc32c.cc:323-370): the unaligned head byte steps, four word slots striding
+// 16 bytes through the aligned body (Z_16 stride tables in the 16-copy image: stride_step16),
+// the STEP4W lane fold and the unaligned tail; records with no aligned 16-byte block inside
+// are stepped word by word.  n must be > 0 (an empty record's CRC is init).
+template <typename Src>
+__device__ __forceinline__ uint32_t lane_record(const uint32_t* lds, uint32_t X, int z4, int t8, uintptr_t p,
+                                                uint32_t n, uint32_t init, Src&& src) {
+    uint32_t r = ~init;
+    const uintptr_t e = p + n;
+    const uintptr_t a = (p + 15) & ~uintptr_t(15), b = e & ~uintptr_t(15);
+    if (b < a + 16) {  // short: the one or two blocks it touches, step by step
+        for (uintptr_t blk = p & ~uintptr_t(15); blk < e; blk += 16) {
+            const uint32_t from = p > blk ? (uint32_t)(p - blk) : 0u;
+            const uint32_t to = e - blk < 16 ? (uint32_t)(e - blk) : 16u;
+            r = steps_in_vec(lds, z4, t8, r, src(blk), from, to);
+        }
+        return ~r;
+    }
+    if (p < a) r = steps_in_vec(lds, z4, t8, r, src(a - 16), (uint32_t)(p - (a - 16)), 16u);
+    const u32x4 v0 = src(a);
+    uint32_t a0 = v0.x ^ r, a1 = v0.y, a2 = v0.z, a3 = v0.w;
+    for (uintptr_t w = a + 16; w < b; w += 16) step4<8>(lds, X, a0, a1, a2, a3, src(w));
+    r = lane_fold_at(lds, z4, a0, a1, a2, a3);
+    if (e > b) r = steps_in_vec(lds, z4, t8, r, src(b), 0u, (uint32_t)(e - b));
+    return ~r;
 }
 
 }  // namespace dev

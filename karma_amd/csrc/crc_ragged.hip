@@ -956,6 +956,153 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
     }
 }
 
+// Batches of small records staged through LDS, one record per lane: a wave takes 64 records,
+// and when their aligned extent [lo, hi) fits its kStgBytes of LDS (64 WAL records of up to
+// ~190 bytes; consecutive records of any smaller size) it copies that extent in with whole
+// 1 KiB wave loads (every cache line read once, by one instruction), then each lane steps its
+// own record out of LDS with the reference's 4-slot structure (lane_record: no shuffles, no
+// per-round unit geometry, no group tree).  A batch whose extent does not fit (records far
+// apart or long) reads its blocks from global memory instead -- exact, only slower.
+// PIPE: the next batch's extent is loaded into registers while this batch is stepped.
+constexpr uint32_t kStgBytes = 12800;        // staging per wave
+constexpr int kStgVecs = (int)((kStgBytes / 16 + 63) / 64);  // 16-byte loads per lane and batch
+constexpr int kStgZ4 = kRep16Words;          // [0, 64 KiB) the 16-copy Z_16 stride tables
+constexpr int kStgT8 = kStgZ4 + 1024;
+constexpr int kStgBuf = kStgT8 + 256;
+constexpr int kStgLdsWords = kStgBuf + kStgWaves * (int)(kStgBytes / 4);  // 160,256 bytes
+static_assert(kStgLdsWords * 4 <= 160 * 1024, "LDS of one workgroup");
+
+// A wave-uniform 64-bit value into scalar registers (readfirstlane is int -> int: each half is
+// taken as uint32_t before widening, or a low word >= 2^31 would sign-extend into the high one).
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    return ((uint64_t)h << 32) | l;
+}
+
+struct StgBatch {
+    uintptr_t p;    // this lane's record
+    uint32_t n, init;
+    bool vi;
+    uintptr_t lo;   // the batch's aligned extent (wave-uniform); hi == 0: no live record
+    uintptr_t hi;
+};
+
+__device__ __forceinline__ StgBatch stg_meta(const RaggedArgs& A, uint64_t n_rec, uint64_t base, uint32_t lane) {
+    StgBatch B;
+    const uint64_t ri = base + lane;
+    B.vi = ri < n_rec;
+    B.p = B.vi ? reinterpret_cast<uintptr_t>(A.arena + A.off[ri]) : 0;
+    B.n = B.vi ? A.len[ri] : 0u;
+    B.init = B.vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
+    const bool live = B.vi && B.n;
+    uint64_t lo = live ? (B.p & ~uintptr_t(15)) : ~0ull, hi = live ? ((B.p + B.n + 15) & ~uintptr_t(15)) : 0ull;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t ol = (uint64_t)__shfl_xor((long long)lo, d), oh = (uint64_t)__shfl_xor((long long)hi, d);
+        lo = ol < lo ? ol : lo;
+        hi = oh > hi ? oh : hi;
+    }
+    B.lo = uniform64(lo);
+    B.hi = uniform64(hi);
+    return B;
+}
+__device__ __forceinline__ bool stg_fits(const StgBatch& B) { return B.hi != 0 && B.hi - B.lo <= kStgBytes; }
+
+__device__ __forceinline__ void stg_issue(const StgBatch& B, uint32_t lane, u32x4 (&v)[kStgVecs]) {
+    const uint32_t nv = (uint32_t)((B.hi - B.lo) / 16);
+#pragma unroll
+    for (int q = 0; q < kStgVecs; ++q) {
+        const uint32_t j = lane + 64u * q;
+        if (j < nv) v[q] = ldg<true>(reinterpret_cast<const uint8_t*>(B.lo + 16ull * j));
+    }
+}
+__device__ __forceinline__ void stg_store(const StgBatch& B, uint32_t lane, const u32x4 (&v)[kStgVecs], uint8_t* stage) {
+    const uint32_t nv = (uint32_t)((B.hi - B.lo) / 16);
+#pragma unroll
+    for (int q = 0; q < kStgVecs; ++q) {
+        const uint32_t j = lane + 64u * q;
+        if (j < nv) *reinterpret_cast<u32x4*>(stage + 16u * j) = v[q];
+    }
+}
+
+template <bool PIPE>
+__global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) {
+    uint64_t n_rec = A.n_rec;
+    if (A.n_dev) {  // a device-sized batch (as k_ragged_direct4)
+        if (*A.gate_len > A.gate_max) return;
+        n_rec = *A.n_dev;
+    }
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kStgLdsWords];
+    load_rep16_stride<kStgWaves * 64>(lds, A.blob, [&] {
+        copy_to_lds<1024, kStgWaves * 64>(lds + kStgZ4, A.blob + kBlobZ4);
+        copy_to_lds<256, kStgWaves * 64>(lds + kStgT8, A.blob + kBlobT8);
+    });
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t X = lane_const16();
+    uint8_t* stage = reinterpret_cast<uint8_t*>(lds + kStgBuf) + wave * kStgBytes;
+    const uint64_t step = (uint64_t)gridDim.x * kStgWaves * 64;
+    uint64_t base = ((uint64_t)blockIdx.x * kStgWaves + wave) * 64;
+    if (base >= n_rec) return;
+    auto one = [&](const StgBatch& B, bool staged) {
+        uint32_t res = B.init;
+        if (B.vi && B.n) {
+            if (staged)
+                res = lane_record(lds, X, kStgZ4, kStgT8, B.p, B.n, B.init,
+                                  [&](uintptr_t a) { return *reinterpret_cast<const u32x4*>(stage + (uint32_t)(a - B.lo)); });
+            else
+                res = lane_record(lds, X, kStgZ4, kStgT8, B.p, B.n, B.init,
+                                  [&](uintptr_t a) { return ld16(reinterpret_cast<const uint8_t*>(a)); });
+        }
+        if (B.vi) {
+            const uint64_t ri = base + lane;
+            A.out[ri] = res;
+            if (A.cmp_stored && B.n && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
+        }
+    };
+    u32x4 v[kStgVecs];
+    if constexpr (!PIPE) {
+        for (; base < n_rec; base += step) {
+            const StgBatch B = stg_meta(A, n_rec, base, lane);
+            const bool staged = stg_fits(B);
+            if (staged) {
+                stg_issue(B, lane, v);
+                stg_store(B, lane, v, stage);
+                wave_lds_sync();
+            }
+            one(B, staged);
+            wave_lds_sync();  // this batch's reads before the next batch's stores
+        }
+    } else {
+        StgBatch B = stg_meta(A, n_rec, base, lane);
+        bool staged = stg_fits(B);
+        if (staged) stg_issue(B, lane, v);
+        for (;;) {
+            if (staged) {
+                stg_store(B, lane, v, stage);
+                wave_lds_sync();
+            }
+            const uint64_t nb = base + step;
+            const bool more = nb < n_rec;
+            StgBatch N = B;
+            bool nstaged = false;
+            if (more) {  // the next batch's extent in flight while this one is stepped
+                N = stg_meta(A, n_rec, nb, lane);
+                nstaged = stg_fits(N);
+                if (nstaged) stg_issue(N, lane, v);
+            }
+            one(B, staged);
+            wave_lds_sync();
+            if (!more) break;
+            base = nb;
+            B = N;
+            staged = nstaged;
+        }
+    }
+}
+
 #ifdef KARMA_AB
 // Tools build (KARMA_DIRECT_VARIANT=1, ab.h): small records one per group of 8 lanes, the
 // shipped kernel before k_ragged_direct4 (0.237 vs 0.202 ms per 1M x 180 B replay call,
@@ -1171,6 +1318,10 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL((k_ragged_direct4<4, 0, 4, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (v == 13)  // one round ahead (the shipped form) with 2 chunks
         hipLaunchKernelGGL((k_ragged_direct4<4, 0, 2, false>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (v == 14)  // staged through LDS, one record per lane (the lane blob)
+        hipLaunchKernelGGL(k_ragged_staged<false>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (v == 15)  // ... with the next batch's extent loaded while this one is stepped
+        hipLaunchKernelGGL(k_ragged_staged<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else
 #endif
         hipLaunchKernelGGL(k_ragged_direct4<4>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);

@@ -17,6 +17,7 @@ constexpr int kChunk = 16 * kGroupLanes;       // bytes a group consumes per ste
 constexpr int kBlockThreads = 1024;            // one workgroup per CU
 constexpr int kWavesPerBlock = kBlockThreads / 64;
 constexpr int kGroupsPerWave = 64 / kGroupLanes;
+constexpr int kStgWaves = 7;  // k_ragged_staged: one 448-thread workgroup per CU (LDS-bound)
 #ifndef KARMA_RAGGED_UNIT
 #define KARMA_RAGGED_UNIT 8192  // a build-time A/B knob (tools/ragged_unit_ab.sh)
 #endif

@@ -21,17 +21,20 @@ for p in (ROOT, HERE):
 
 
 def pytest_addoption(parser):
-    parser.addoption("--karma-lib", default="shipped", choices=["shipped", "bounds"],
+    parser.addoption("--karma-lib", default="shipped", choices=["shipped", "bounds", "abbounds"],
                      help="bounds: run on the bounds-checked debug build (karma_amd/csrc/bounds.h); every GPU "
-                          "test then also fails on any out-of-bounds access its kernels attempted")
+                          "test then also fails on any out-of-bounds access its kernels attempted; abbounds: "
+                          "the same, and the variant tests on the tools build with the bounds checks")
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
-    if config.getoption("--karma-lib") == "bounds":
+    if config.getoption("--karma-lib") in ("bounds", "abbounds"):
         import torch  # noqa: F401  (torch's HIP runtime first, as in every other run: the library binds to it)
         from karma_amd import _lib
         _lib.select(_lib.BOUNDS_LIB_PATH)
+        if config.getoption("--karma-lib") == "abbounds":
+            _lib.AB_LIB_PATH = _lib.ABBOUNDS_LIB_PATH
 
 
 @pytest.fixture(autouse=True)
@@ -39,16 +42,22 @@ def _bounds_report(request):
     """Under --karma-lib bounds: after each GPU test, no kernel of the test may have attempted an
     access outside its buffers."""
     yield
-    if request.config.getoption("--karma-lib") != "bounds" or request.node.get_closest_marker("gpu") is None:
+    mode = request.config.getoption("--karma-lib")
+    if mode not in ("bounds", "abbounds") or request.node.get_closest_marker("gpu") is None:
         return
     import ctypes
     import numpy as np
     from karma_amd import _lib
-    rep = np.zeros(4, np.uint64)
-    L = _lib.load(_lib.BOUNDS_LIB_PATH)
-    assert L.karma_debug_bounds_report(rep.ctypes.data_as(ctypes.c_void_p), 1) == 0
-    n, site, index, cap = (int(x) for x in rep)
-    assert n == 0, f"{n} out-of-bounds accesses; first: {_lib.KB_SITES.get(site, site)} (index {index}, cap {cap})"
+    paths = [_lib.BOUNDS_LIB_PATH] + ([_lib.ABBOUNDS_LIB_PATH] if mode == "abbounds" else [])
+    for path in paths:
+        if path != _lib.BOUNDS_LIB_PATH and not _lib.is_loaded(path):
+            continue
+        rep = np.zeros(4, np.uint64)
+        L = _lib.load(path)
+        assert L.karma_debug_bounds_report(rep.ctypes.data_as(ctypes.c_void_p), 1) == 0
+        n, site, index, cap = (int(x) for x in rep)
+        assert n == 0, (f"{os.path.basename(path)}: {n} out-of-bounds accesses; first: "
+                        f"{_lib.KB_SITES.get(site, site)} (index {index}, cap {cap})")
 
 
 @pytest.fixture(scope="session")

@@ -531,13 +531,14 @@ def test_ragged_low_total_len_is_still_exact(raw, dev):
         _eq(got, want)
 
 
-@pytest.mark.parametrize("variant", ["shipped", "1", "2", "3", "4", "5"])
+@pytest.mark.parametrize("variant", ["shipped", "1", "2", "3", "4", "5", "14", "15"])
 @pytest.mark.parametrize("bound", [0, 64, 1024, 1 << 20])
 def test_ragged_bounded_direct_path(raw, dev, bound, variant, monkeypatch):
     """karma_crc32c_batch_ragged_bounded: with max_len <= 1 KiB one record per group (no plan
     kernels); any bound -- too low included -- gives the exact CRCs, with per-record inits.
     Variants 1-5 are the tools build's small-record kernels (KARMA_DIRECT_VARIANT: 8-lane groups
-    pipelined / un-pipelined, one record per lane, the shipped 4-lane groups, 2-lane groups)."""
+    pipelined / un-pipelined, one record per lane, the shipped 4-lane groups, 2-lane groups);
+    14 / 15 the LDS-staged kernel (here every batch is too spread out to stage: its global path)."""
     host, dbuf = raw
     if variant == "shipped":
         L = _lib.lib()
@@ -559,3 +560,50 @@ def test_ragged_bounded_direct_path(raw, dev, bound, variant, monkeypatch):
     assert st == 0, L.karma_crc32c_last_error()
     _eq(out.cpu().numpy().view(np.uint32), oracle_lib.ragged_crcs(host, offs, lens, init))
 
+
+
+@pytest.mark.parametrize("variant", ["shipped", "4", "14", "15"])
+@pytest.mark.parametrize("shape", ["wal180", "mixed", "tiny", "unaligned_arena"])
+def test_ragged_bounded_consecutive_records(raw, dev, shape, variant, monkeypatch):
+    """Consecutive small records (a WAL image's payloads, a writer's block) through the bounded
+    ABI: the LDS-staged kernel (14 / 15) stages a wave's 64 records when their extent fits its
+    12,800 bytes and steps the rest from global memory; both paths against the oracle, with
+    per-record inits, empty records, every alignment, and batches that straddle the limit."""
+    host, dbuf = raw
+    if variant == "shipped":
+        L = _lib.lib()
+    else:
+        monkeypatch.setenv("KARMA_DIRECT_VARIANT", variant)
+        L = _lib.load(_lib.AB_LIB_PATH)
+    rng = np.random.default_rng(["wal180", "mixed", "tiny", "unaligned_arena"].index(shape) + 77)
+    n = 40000
+    if shape == "wal180":
+        lens = np.full(n, 180, np.uint32)
+        gaps = np.full(n, 8, np.uint64)
+    elif shape == "mixed":  # mostly small, some records of up to 1 KiB: some batches do not fit
+        lens = rng.integers(0, 260, n).astype(np.uint32)
+        big = rng.random(n) < 0.01
+        lens[big] = rng.integers(500, 1025, int(big.sum()))
+        lens[rng.random(n) < 0.02] = 0
+        gaps = rng.integers(0, 24, n).astype(np.uint64)
+    elif shape == "tiny":
+        lens = rng.integers(0, 20, n).astype(np.uint32)
+        gaps = rng.integers(0, 3, n).astype(np.uint64)
+    else:
+        lens = rng.integers(1, 200, n).astype(np.uint32)
+        gaps = np.full(n, 8, np.uint64)
+    start = 3 if shape == "unaligned_arena" else 0
+    offs = (np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])]) + gaps[0]).astype(np.uint64)
+    end = int(offs[-1]) + int(lens[-1])
+    assert start + end <= host.size
+    init = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    d_ini = torch.from_numpy(init.view(np.int32)).to(dev)
+    out = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    arena = dbuf[start:]
+    st = L.karma_crc32c_batch_ragged_bounded(arena.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n,
+                                             int(lens.sum()), 1024, d_ini.data_ptr(), 0, out.data_ptr(),
+                                             torch.cuda.current_stream().cuda_stream)
+    assert st == 0, L.karma_crc32c_last_error()
+    _eq(out.cpu().numpy().view(np.uint32), oracle_lib.ragged_crcs(host[start:], offs, lens, init))

@@ -10,6 +10,7 @@ KARMA_DIRECT_VARIANT = each variant, interleaved rounds; kernel time from HIP ev
 and group tree, 8 neither, 9 no head / tail steps, 10 none of these.  11 / 12: every round's
 first 2 / 4 chunk loads issued at once (direct_batch ALL); 13: the shipped pipeline with 2 chunks
 (11-13 are exact: checked against the shipped kernel's CRCs; list "0" first).
+14 / 15: the LDS-staged one-record-per-lane kernel, un-pipelined / next batch in flight (exact).
 """
 import argparse
 import ctypes
@@ -65,7 +66,7 @@ def main():
             res[v].append(e0.elapsed_time(e1) / a.calls * 1e3)
             if v == "0" and ref is None:
                 ref = out.clone()
-            elif r == 0 and v in ("11", "12", "13") and ref is not None:  # exact variants: the same CRCs
+            elif r == 0 and v in ("11", "12", "13", "14", "15") and ref is not None:  # exact variants: the same CRCs
                 bad = int((out != ref).sum().item())
                 print(f"variant {v}: {bad} CRCs differ from the shipped kernel's", flush=True)
                 assert bad == 0
