@@ -124,13 +124,13 @@ int dev_state(int dev, DevState** out) {
         build_quad_blob(host.data());
         KARMA_HIP(hipMalloc(&d.quad_blob, kBlobWords * sizeof(uint32_t)));
         KARMA_HIP(hipMemcpy(d.quad_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+        build_lane_blob(host.data());
+        KARMA_HIP(hipMalloc(&d.lane_blob, kBlobWords * sizeof(uint32_t)));
+        KARMA_HIP(hipMemcpy(d.lane_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
 #ifdef KARMA_AB
         build_pair_blob(host.data());
         KARMA_HIP(hipMalloc(&d.pair_blob, kBlobWords * sizeof(uint32_t)));
         KARMA_HIP(hipMemcpy(d.pair_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
-        build_lane_blob(host.data());
-        KARMA_HIP(hipMalloc(&d.lane_blob, kBlobWords * sizeof(uint32_t)));
-        KARMA_HIP(hipMemcpy(d.lane_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
 #endif
         d.ready = true;
     }
@@ -492,6 +492,13 @@ int device_quad_blob(int dev, const uint32_t** out) {
     *out = L.ds->quad_blob;
     return 0;
 }
+int device_lane_blob(int dev, const uint32_t** out) {
+    (void)dev;
+    Locked L;
+    if (L.rc) return L.rc;
+    *out = L.ds->lane_blob;
+    return 0;
+}
 int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
                        uint32_t* d_out, hipStream_t s) {
     return karma_crc32c_batch_ragged_bounded(d_arena, d_off, d_len, n_rec, 0, 1, nullptr, 0, d_out, s);
@@ -633,11 +640,11 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
         a.init_scalar = init;
         a.out = d_out;
         const long dv = KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0);  // tools build: the other kernels
-        a.blob = dv == 1 || dv == 2 ? L.ds->blob : dv == 3 || dv == 14 || dv == 15 ? L.ds->lane_blob : dv == 5 ? L.ds->pair_blob : L.ds->quad_blob;
+        a.blob = dv == 1 || dv == 2 ? L.ds->blob : dv == 3 || (dv >= 14 && dv <= 20) ? L.ds->lane_blob : dv == 5 ? L.ds->pair_blob : L.ds->quad_blob;
         bind_arena_bounds(a);
         // a wave takes 64 records (lanes variant: a workgroup 1024): no more workgroups than
         // the batch fills (each one loads the 145 KiB table image into its LDS first)
-        const uint64_t per_block = dv == 3 ? kBlockThreads : dv == 14 || dv == 15 ? 64 * kStgWaves : 64 * kWavesPerBlock;
+        const uint64_t per_block = dv == 3 ? kBlockThreads : dv >= 14 && dv <= 20 ? 64 * kStgWaves : 64 * kWavesPerBlock;
         const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_rec, per_block));
         KARMA_HIP(launch_ragged_direct(a, (int)blocks, (hipStream_t)stream));
         return KARMA_OK;

@@ -613,6 +613,184 @@ __device__ __forceinline__ uint32_t wave_tree(const uint32_t* lds, uint32_t v) {
     return v;
 }
 
+// ---- small records staged through LDS (k_ragged_staged, k_wal_list_crc) ----------------
+constexpr uint32_t kStgBytes = 12288;        // staging per wave: kStgVecs whole-wave 1 KiB loads (64 x 188 B)
+constexpr int kStgVecs = (int)(kStgBytes / 1024);  // 16-byte loads per lane and batch
+static_assert(kStgBytes % 1024 == 0, "every lane's loads land inside the stage: no guard per load");
+constexpr int kStgZ4 = kRep16Words;          // [0, 64 KiB) the 16-copy Z_16 stride tables
+constexpr int kStgT8 = kStgZ4 + 1024;
+constexpr int kStgBuf = kStgT8 + 256;
+constexpr int kStgLdsWords = kStgBuf + kStgWaves * (int)(kStgBytes / 4);  // 160,256 bytes
+static_assert(kStgLdsWords * 4 <= 160 * 1024, "LDS of one workgroup");
+
+// A wave-uniform 64-bit value into scalar registers (readfirstlane is int -> int: each half is
+// taken as uint32_t before widening, or a low word >= 2^31 would sign-extend into the high one).
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    return ((uint64_t)h << 32) | l;
+}
+
+struct StgBatch {
+    uintptr_t p;    // this lane's record
+    uint32_t n, init;
+    bool vi;
+    uintptr_t lo;   // the batch's aligned extent (wave-uniform); hi == 0: no live record
+    uintptr_t hi;
+};
+
+__device__ __forceinline__ StgBatch stg_meta(const RaggedArgs& A, uint64_t n_rec, uint64_t base, uint32_t lane) {
+    StgBatch B;
+    const uint64_t ri = base + lane;
+    B.vi = ri < n_rec;
+    B.p = B.vi ? reinterpret_cast<uintptr_t>(A.arena + A.off[ri]) : 0;
+    B.n = B.vi ? A.len[ri] : 0u;
+    B.init = B.vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
+    const bool live = B.vi && B.n;
+    uint64_t lo = live ? (B.p & ~uintptr_t(15)) : ~0ull, hi = live ? ((B.p + B.n + 15) & ~uintptr_t(15)) : 0ull;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t ol = (uint64_t)__shfl_xor((long long)lo, d), oh = (uint64_t)__shfl_xor((long long)hi, d);
+        lo = ol < lo ? ol : lo;
+        hi = oh > hi ? oh : hi;
+    }
+    B.lo = uniform64(lo);
+    B.hi = uniform64(hi);
+    return B;
+}
+__device__ __forceinline__ bool stg_fits(const StgBatch& B) { return B.hi != 0 && B.hi - B.lo <= kStgBytes; }
+
+__device__ __forceinline__ void stg_issue(const StgBatch& B, uint32_t lane, u32x4 (&v)[kStgVecs]) {
+    const uint32_t nv = (uint32_t)((B.hi - B.lo) / 16);
+#pragma unroll
+    for (int q = 0; q < kStgVecs; ++q) {
+        const uint32_t j = lane + 64u * q;  // past the extent: its first block again (no branch)
+        v[q] = ldg<true>(reinterpret_cast<const uint8_t*>(B.lo + 16ull * (j < nv ? j : 0u)));
+    }
+}
+__device__ __forceinline__ void stg_store(const StgBatch& B, uint32_t lane, const u32x4 (&v)[kStgVecs], uint8_t* stage) {
+#pragma unroll
+    for (int q = 0; q < kStgVecs; ++q) {
+        const uint32_t j = lane + 64u * q;  // every slot of the stage (past the extent: unused)
+        *reinterpret_cast<u32x4*>(stage + 16u * j) = v[q];
+    }
+}
+
+// The staged kernels' table image: the lane blob's Z_16 stride tables in 16 copies, Z4 and the
+// byte table.
+template <int THREADS>
+__device__ __forceinline__ void load_stg_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
+    load_rep16_stride<THREADS>(lds, blob, [&] {
+        copy_to_lds<1024, THREADS>(lds + kStgZ4, blob + kBlobZ4);
+        copy_to_lds<256, THREADS>(lds + kStgT8, blob + kBlobT8);
+    });
+}
+
+// Records in lane order (this lane's: [p, p + n), live = a record with bytes): the longest
+// prefix of lanes whose aligned extent fits kStgBytes -- cnt lanes (wave-uniform, >= 1) and
+// the extent [lo, hi).  cnt == 1 with hi == 0 and a live lane 0: that one record alone does
+// not fit (it is read from global memory).  Lanes whose prefix holds no live record fit
+// with an empty extent.
+struct StgSpan {
+    uintptr_t lo, hi;
+    uint32_t cnt;
+};
+__device__ __forceinline__ StgSpan stg_prefix(uintptr_t p, uint32_t n, bool live, uint32_t lane) {
+    uint64_t lo = live ? (p & ~uintptr_t(15)) : ~0ull, hi = live ? ((p + n + 15) & ~uintptr_t(15)) : 0ull;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {  // inclusive prefix min / max
+        const uint64_t ol = (uint64_t)__shfl_up((long long)lo, d), oh = (uint64_t)__shfl_up((long long)hi, d);
+        if (lane >= (uint32_t)d) {
+            lo = ol < lo ? ol : lo;
+            hi = oh > hi ? oh : hi;
+        }
+    }
+    const bool fits = hi == 0 || hi - lo <= kStgBytes;  // monotonic in the lane
+    const uint32_t cnt = (uint32_t)__popcll(__ballot(fits));
+    StgSpan S;
+    if (cnt == 0) {
+        S.lo = S.hi = 0;
+        S.cnt = 1;
+        return S;
+    }
+    S.lo = uniform64((uint64_t)__shfl((long long)lo, (int)cnt - 1));
+    S.hi = uniform64((uint64_t)__shfl((long long)hi, (int)cnt - 1));
+    S.cnt = cnt;
+    if (S.hi == 0) S.lo = 0;
+    return S;
+}
+// Copy [lo, hi) (hi - lo <= kStgBytes, 16-aligned) into the wave's stage: every load issued
+// before the first store.
+__device__ __forceinline__ void stg_copy(uintptr_t lo, uintptr_t hi, uint32_t lane, uint8_t* stage) {
+    const uint32_t nv = (uint32_t)((hi - lo) / 16);
+    u32x4 v[kStgVecs];
+#pragma unroll
+    for (int q = 0; q < kStgVecs; ++q) {
+        const uint32_t j = lane + 64u * q;
+        v[q] = ldg<true>(reinterpret_cast<const uint8_t*>(lo + 16ull * (j < nv ? j : 0u)));
+    }
+#pragma unroll
+    for (int q = 0; q < kStgVecs; ++q) {
+        const uint32_t j = lane + 64u * q;  // every slot of the stage (past the extent: unused)
+        *reinterpret_cast<u32x4*>(stage + 16u * j) = v[q];
+    }
+}
+
+// One record per lane out of the LDS stage, its 16-byte windows aligned to the record's END:
+// the record [sp, sp + n) of the stage (byte offsets; 16 <= sp is not required, but the 15
+// bytes before sp must be stage bytes too) is read as W = ceil(n / 16) windows ending at
+// sp + n, the first window front-padded with h0 = 16 W - n bytes that are masked to zero.
+// Zero bytes entering a zero register leave it zero, so the padded span steps from a zero
+// register once ~init is xored into the record's first 4 bytes (the register a word step
+// xors in, crc32c.cc:293-299): no head or tail byte steps, one dependent chain of W stride
+// steps and the STEP4W fold.  Needs n >= 4 (the injected word lies inside the record).
+// rd(q): dword q of the stage (q = byte offset / 4; the windows are read as dwords and
+// funnel-shifted, v_alignbyte_b32).
+template <typename Rd>
+__device__ __forceinline__ uint32_t lane_record_end(const uint32_t* lds, uint32_t X, int z4, uint32_t sp, uint32_t n,
+                                                    uint32_t init, Rd&& rd) {
+    const uint32_t W = (n + 15) >> 4, h0 = 16 * W - n;
+    const uint32_t s0 = sp - h0, sh = s0 & 3;
+    uint32_t q = s0 >> 2;
+    uint32_t d0 = rd(q), d1 = rd(q + 1), d2 = rd(q + 2), d3 = rd(q + 3), d4 = rd(q + 4);
+    uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh), w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+    // window 0: bytes [0, h0) are not the record's
+    auto keep = [&](uint32_t k) {
+        const int r = (int)h0 - 4 * (int)k;
+        return r <= 0 ? ~0u : r >= 4 ? 0u : (~0u << (8 * r));
+    };
+    w0 &= keep(0);
+    w1 &= keep(1);
+    w2 &= keep(2);
+    w3 &= keep(3);
+    // ~init into bytes [h0, h0 + 4): word k0 and (unaligned) the next one, or window 1's first
+    const uint32_t inj = ~init, b = h0 & 3, k0 = h0 >> 2;
+    const uint32_t lo32 = inj << (8 * b), hi32 = b ? inj >> (32 - 8 * b) : 0u;
+    w0 ^= k0 == 0 ? lo32 : 0u;
+    w1 ^= (k0 == 1 ? lo32 : 0u) ^ (k0 == 0 ? hi32 : 0u);
+    w2 ^= (k0 == 2 ? lo32 : 0u) ^ (k0 == 1 ? hi32 : 0u);
+    w3 ^= (k0 == 3 ? lo32 : 0u) ^ (k0 == 2 ? hi32 : 0u);
+    uint32_t carry = k0 == 3 ? hi32 : 0u;
+    uint32_t a0 = w0, a1 = w1, a2 = w2, a3 = w3;
+    for (uint32_t j = 1; j < W; ++j) {
+        q += 4;
+        d0 = d4;
+        d1 = rd(q + 1);
+        d2 = rd(q + 2);
+        d3 = rd(q + 3);
+        d4 = rd(q + 4);
+        u32x4 v;
+        v.x = __builtin_amdgcn_alignbyte(d1, d0, sh) ^ carry;
+        v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+        v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+        carry = 0u;
+        step4<8>(lds, X, a0, a1, a2, a3, v);
+    }
+    return ~lane_fold_at(lds, z4, a0, a1, a2, a3);
+}
+
 // LDS writes of a wave visible to its own later LDS reads (and its reads done before its
 // next writes): the wave's LDS operations complete in order, so a wait for them and a
 // compiler barrier suffice (no workgroup barrier).

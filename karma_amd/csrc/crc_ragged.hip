@@ -964,69 +964,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // per-round unit geometry, no group tree).  A batch whose extent does not fit (records far
 // apart or long) reads its blocks from global memory instead -- exact, only slower.
 // PIPE: the next batch's extent is loaded into registers while this batch is stepped.
-constexpr uint32_t kStgBytes = 12800;        // staging per wave
-constexpr int kStgVecs = (int)((kStgBytes / 16 + 63) / 64);  // 16-byte loads per lane and batch
-constexpr int kStgZ4 = kRep16Words;          // [0, 64 KiB) the 16-copy Z_16 stride tables
-constexpr int kStgT8 = kStgZ4 + 1024;
-constexpr int kStgBuf = kStgT8 + 256;
-constexpr int kStgLdsWords = kStgBuf + kStgWaves * (int)(kStgBytes / 4);  // 160,256 bytes
-static_assert(kStgLdsWords * 4 <= 160 * 1024, "LDS of one workgroup");
-
-// A wave-uniform 64-bit value into scalar registers (readfirstlane is int -> int: each half is
-// taken as uint32_t before widening, or a low word >= 2^31 would sign-extend into the high one).
-__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
-    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
-    const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
-    return ((uint64_t)h << 32) | l;
-}
-
-struct StgBatch {
-    uintptr_t p;    // this lane's record
-    uint32_t n, init;
-    bool vi;
-    uintptr_t lo;   // the batch's aligned extent (wave-uniform); hi == 0: no live record
-    uintptr_t hi;
-};
-
-__device__ __forceinline__ StgBatch stg_meta(const RaggedArgs& A, uint64_t n_rec, uint64_t base, uint32_t lane) {
-    StgBatch B;
-    const uint64_t ri = base + lane;
-    B.vi = ri < n_rec;
-    B.p = B.vi ? reinterpret_cast<uintptr_t>(A.arena + A.off[ri]) : 0;
-    B.n = B.vi ? A.len[ri] : 0u;
-    B.init = B.vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
-    const bool live = B.vi && B.n;
-    uint64_t lo = live ? (B.p & ~uintptr_t(15)) : ~0ull, hi = live ? ((B.p + B.n + 15) & ~uintptr_t(15)) : 0ull;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t ol = (uint64_t)__shfl_xor((long long)lo, d), oh = (uint64_t)__shfl_xor((long long)hi, d);
-        lo = ol < lo ? ol : lo;
-        hi = oh > hi ? oh : hi;
-    }
-    B.lo = uniform64(lo);
-    B.hi = uniform64(hi);
-    return B;
-}
-__device__ __forceinline__ bool stg_fits(const StgBatch& B) { return B.hi != 0 && B.hi - B.lo <= kStgBytes; }
-
-__device__ __forceinline__ void stg_issue(const StgBatch& B, uint32_t lane, u32x4 (&v)[kStgVecs]) {
-    const uint32_t nv = (uint32_t)((B.hi - B.lo) / 16);
-#pragma unroll
-    for (int q = 0; q < kStgVecs; ++q) {
-        const uint32_t j = lane + 64u * q;
-        if (j < nv) v[q] = ldg<true>(reinterpret_cast<const uint8_t*>(B.lo + 16ull * j));
-    }
-}
-__device__ __forceinline__ void stg_store(const StgBatch& B, uint32_t lane, const u32x4 (&v)[kStgVecs], uint8_t* stage) {
-    const uint32_t nv = (uint32_t)((B.hi - B.lo) / 16);
-#pragma unroll
-    for (int q = 0; q < kStgVecs; ++q) {
-        const uint32_t j = lane + 64u * q;
-        if (j < nv) *reinterpret_cast<u32x4*>(stage + 16u * j) = v[q];
-    }
-}
-
-template <bool PIPE>
+template <bool PIPE, int MODE = 0>  // MODE (tools build timing only, wrong CRCs): 1 no CRC steps, 2 no staging copy
 __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) {
     uint64_t n_rec = A.n_rec;
     if (A.n_dev) {  // a device-sized batch (as k_ragged_direct4)
@@ -1035,10 +973,7 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) 
     }
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kStgLdsWords];
-    load_rep16_stride<kStgWaves * 64>(lds, A.blob, [&] {
-        copy_to_lds<1024, kStgWaves * 64>(lds + kStgZ4, A.blob + kBlobZ4);
-        copy_to_lds<256, kStgWaves * 64>(lds + kStgT8, A.blob + kBlobT8);
-    });
+    load_stg_tables<kStgWaves * 64>(lds, A.blob);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t X = lane_const16();
@@ -1048,7 +983,9 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) 
     if (base >= n_rec) return;
     auto one = [&](const StgBatch& B, bool staged) {
         uint32_t res = B.init;
-        if (B.vi && B.n) {
+        if constexpr ((MODE & 1) != 0) {
+            if (B.vi && B.n && staged) res ^= *reinterpret_cast<const uint32_t*>(stage + (uint32_t)((B.p & ~uintptr_t(15)) - B.lo));
+        } else if (B.vi && B.n) {
             if (staged)
                 res = lane_record(lds, X, kStgZ4, kStgT8, B.p, B.n, B.init,
                                   [&](uintptr_t a) { return *reinterpret_cast<const u32x4*>(stage + (uint32_t)(a - B.lo)); });
@@ -1067,7 +1004,7 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) 
         for (; base < n_rec; base += step) {
             const StgBatch B = stg_meta(A, n_rec, base, lane);
             const bool staged = stg_fits(B);
-            if (staged) {
+            if (staged && (MODE & 2) == 0) {
                 stg_issue(B, lane, v);
                 stg_store(B, lane, v, stage);
                 wave_lds_sync();
@@ -1100,6 +1037,117 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) 
             B = N;
             staged = nstaged;
         }
+    }
+}
+
+// The staged kernel software-pipelined across batches: batch k + 1's extent and batch k + 2's
+// offsets / lengths are in flight while batch k is stepped (a wave's batches are otherwise one
+// chain of three memory latencies and the steps: DESIGN.md §8a), plain scalars across the loop.
+// END: the records' windows aligned to their ends (lane_record_end: no head or tail steps);
+// the stage then holds the extent 16 bytes in, after a slack the first window may read.
+template <bool END>
+__global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArgs A) {
+    constexpr uint32_t kLead = END ? 16u : 0u, kFit = END ? kStgBytes - 32u : kStgBytes;
+    uint64_t n_rec = A.n_rec;
+    if (A.n_dev) {
+        if (*A.gate_len > A.gate_max) return;
+        n_rec = *A.n_dev;
+    }
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kStgLdsWords];
+    load_stg_tables<kStgWaves * 64>(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t X = lane_const16();
+    uint8_t* stage = reinterpret_cast<uint8_t*>(lds + kStgBuf) + wave * kStgBytes;
+    const uint64_t step = (uint64_t)gridDim.x * kStgWaves * 64;
+    uint64_t base = ((uint64_t)blockIdx.x * kStgWaves + wave) * 64;
+    if (base >= n_rec) return;
+    auto ld_meta = [&](uint64_t b, uint64_t& o, uint32_t& n, uint32_t& ini) {
+        const uint64_t ri = b + lane;
+        const bool v = ri < n_rec;
+        o = v ? A.off[ri] : 0;
+        n = v ? A.len[ri] : 0u;
+        ini = v ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
+    };
+    auto extent = [&](uint64_t o, uint32_t n, uintptr_t& lo, uintptr_t& hi) {
+        const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
+        uint64_t l = n ? (p & ~uintptr_t(15)) : ~0ull, h = n ? ((p + n + 15) & ~uintptr_t(15)) : 0ull;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t ol = (uint64_t)__shfl_xor((long long)l, d), oh = (uint64_t)__shfl_xor((long long)h, d);
+            l = ol < l ? ol : l;
+            h = oh > h ? oh : h;
+        }
+        lo = uniform64(l);
+        hi = uniform64(h);
+    };
+    u32x4 v[kStgVecs];
+    auto issue = [&](uintptr_t lo, uintptr_t hi) {
+        const uint32_t nv = (uint32_t)((hi - lo) / 16);
+#pragma unroll
+        for (int q = 0; q < kStgVecs; ++q) {
+            const uint32_t j = lane + 64u * q;  // past the extent: its first block again (no branch)
+            v[q] = ldg<true>(reinterpret_cast<const uint8_t*>(lo + 16ull * (j < nv ? j : 0u)));
+        }
+    };
+    // batch `base`: meta (o, n, ini), extent; batch base + step: meta (o2, n2, ini2)
+    uint64_t o, o2;
+    uint32_t n, ini, n2, ini2;
+    uintptr_t lo, hi;
+    ld_meta(base, o, n, ini);
+    ld_meta(base + step, o2, n2, ini2);
+    extent(o, n, lo, hi);
+    bool fits = hi != 0 && hi - lo <= kFit;
+    if (fits) issue(lo, hi);
+    for (;;) {
+        if (fits) {
+#pragma unroll
+            for (int q = 0; q < kStgVecs; ++q) {
+                uint32_t at = kLead + 16u * (lane + 64u * q);
+                at = at >= kStgBytes ? 0u : at;  // (END) the last slot, past any extent, into the slack
+                *reinterpret_cast<u32x4*>(stage + at) = v[q];
+            }
+            wave_lds_sync();
+        }
+        const uint64_t nb = base + step;
+        const bool more = nb < n_rec;
+        uintptr_t lo2 = 0, hi2 = 0;
+        bool fits2 = false;
+        uint64_t o3 = 0;
+        uint32_t n3 = 0, ini3 = 0;
+        if (more) {
+            extent(o2, n2, lo2, hi2);
+            fits2 = hi2 != 0 && hi2 - lo2 <= kFit;
+            if (fits2) issue(lo2, hi2);
+            ld_meta(nb + step, o3, n3, ini3);
+        }
+        const uint64_t ri = base + lane;
+        if (ri < n_rec) {
+            uint32_t res = ini;
+            const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
+            if (n) {
+                if (fits && END && n >= 4)
+                    res = lane_record_end(lds, X, kStgZ4, kLead + (uint32_t)(p - lo), n, ini, [&](uint32_t q) {
+                        return *reinterpret_cast<const uint32_t*>(stage + 4u * q);
+                    });
+                else if (fits)
+                    res = lane_record(lds, X, kStgZ4, kStgT8, p, n, ini, [&](uintptr_t a) {
+                        return *reinterpret_cast<const u32x4*>(stage + kLead + (uint32_t)(a - lo));
+                    });
+                else
+                    res = lane_record(lds, X, kStgZ4, kStgT8, p, n, ini,
+                                      [&](uintptr_t a) { return ld16(reinterpret_cast<const uint8_t*>(a)); });
+            }
+            A.out[ri] = res;
+            if (A.cmp_stored && n && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
+        }
+        wave_lds_sync();
+        if (!more) break;
+        base = nb;
+        o = o2; n = n2; ini = ini2;
+        o2 = o3; n2 = n3; ini2 = ini3;
+        lo = lo2; hi = hi2; fits = fits2;
     }
 }
 
@@ -1322,6 +1370,16 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL(k_ragged_staged<false>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else if (v == 15)  // ... with the next batch's extent loaded while this one is stepped
         hipLaunchKernelGGL(k_ragged_staged<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (v == 19)  // staged, software-pipelined across batches (k_ragged_staged_pipe)
+        hipLaunchKernelGGL(k_ragged_staged_pipe<false>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (v == 20)  // ... with the windows aligned to the record ends (no head / tail steps)
+        hipLaunchKernelGGL(k_ragged_staged_pipe<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (v == 16)  // timing only: staging copy without the CRC steps / 17 the steps without the copy / 18 neither
+        hipLaunchKernelGGL((k_ragged_staged<false, 1>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (v == 17)
+        hipLaunchKernelGGL((k_ragged_staged<false, 2>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (v == 18)
+        hipLaunchKernelGGL((k_ragged_staged<false, 3>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else
 #endif
         hipLaunchKernelGGL(k_ragged_direct4<4>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);

@@ -218,6 +218,8 @@ int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_
 // d_stored[r] (length 0 excepted) goes to *d_first_bad (atomicMin).
 // The 4-lane small-record kernel's table blob on the current device (k_wal_walk_crc's tables).
 int device_quad_blob(int dev, const uint32_t** out);
+// The staged kernels' blob (Z_16 stride tables: k_ragged_staged, k_wal_list_crc).
+int device_lane_blob(int dev, const uint32_t** out);
 int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
                            uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
                            const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s);
@@ -297,11 +299,14 @@ constexpr uint32_t kMaxSub = 4096;    // sub-ranges per segment (k_wal_gather st
 struct WalWalkPlan {
     uint64_t nsub, sub_bytes, sub_cap, cand_cap;
     int kernel;  // 0: sub-range walkers (+ resolve when nsub > 1), 1: one workgroup per segment,
-                 // 2: sub-range walkers with the CRCs inline (k_wal_walk_crc, + resolve)
+                 // 2: sub-range walkers with the CRCs inline (k_wal_walk_crc, + resolve),
+                 // 3: sub-range walkers, then their lists checksummed (k_wal_list_crc, + resolve)
+    int cu;      // CUs of the device (the list kernel's grid)
 };
 // Host planner (wal.cc).  sub_bytes: 0 = the planner's split, else the forced sub-range
 // size (karma_wal_tuning).
-WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes, bool inline_crc = false);
+WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes, bool inline_crc = false,
+                          bool list_crc = false);
 constexpr int kWalFuseWaves = 15;  // walkers per workgroup of k_wal_walk_crc (wal_device.hip)
 hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s);
 // The replay plan on the device: a.sum, a.cand_base (first list slot per segment) and

@@ -50,8 +50,10 @@ int set_last_error(int code, const std::string& what);  // capi.cc
 // k_wal_resolve stitches their lists.  Many segments: one walker per segment.
 // sub_bytes != 0 forces the sub-range size (karma_wal_tuning: tests, tuning);
 // the tools build's KARMA_WALK_VARIANT=1 (ab.h) selects k_wal_walk instead.
-WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes, bool inline_crc) {
-    WalWalkPlan p{1, 0, 0, 0, inline_crc ? 2 : 0};
+WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes, bool inline_crc,
+                          bool list_crc) {
+    WalWalkPlan p{1, 0, 0, 0, list_crc ? 3 : inline_crc ? 2 : 0, cu};
+    if (list_crc) inline_crc = false;  // the walkers are k_wal_walk_sub's
     const uint64_t tiles = (seg_bytes + kWalkTile - 1) / kWalkTile;
     uint64_t sub_tiles = tiles;
     if (!inline_crc && KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 1) {
@@ -302,8 +304,12 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
                           KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 0;
     const bool inline_crc =
         dev_plan && batch == KARMA_WAL_CRC_PLAN && KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 0;
+    // the walkers' lists checksummed after the walk by the LDS-staged kernel (k_wal_list_crc)
+    // instead of by the walkers themselves (k_wal_walk_crc)
+    const bool list_crc = inline_crc && KARMA_AB_KNOB("KARMA_WAL_LIST_CRC", 0) != 0;
     if (inline_crc) {
-        if (const int rc = device_quad_blob(dev, &A.crc_blob)) return rc;
+        if (const int rc = list_crc ? device_lane_blob(dev, &A.crc_blob) : device_quad_blob(dev, &A.crc_blob))
+            return rc;
 #ifdef KARMA_BOUNDS
         hipDeviceptr_t lo = nullptr;
         size_t sz = 0;
@@ -319,7 +325,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     }
     // 1. segment-parallel header walk (sub-range walkers when there are few segments)
     const WalWalkPlan plan =
-        wal_walk_plan(seg_bytes, nwork, c.cu, tuning ? tuning->walk_sub_bytes : 0, inline_crc);
+        wal_walk_plan(seg_bytes, nwork, c.cu, tuning ? tuning->walk_sub_bytes : 0, inline_crc, list_crc);
     A.nsub = plan.nsub;
     A.sub_bytes = plan.sub_bytes;
     A.sub_cap = plan.sub_cap;

@@ -682,6 +682,90 @@ __global__ __launch_bounds__(kFuseWaves * 64) void k_wal_walk_crc(WalArgs A) {
     }
 }
 
+// The walkers' lists checksummed after the walk (plan kernel 3: k_wal_walk_sub, then this,
+// then k_wal_resolve): the same per-walker report as k_wal_walk_crc's crc_list (the first
+// mismatching entry of the walker's own list, kNoBad, or kCrcUnknown over kCrcInlineMax), but
+// computed by the small-record kernel staged through LDS (crc_device.h: stg_prefix, lane_record):
+// a wave takes a walker, and each step the longest run of its next 64 entries whose bytes fit
+// the wave's stage is copied in with whole-wave loads and checksummed one record per lane.
+// The walk keeps its occupancy (no CRC state in the walker) and the CRC pass its own.
+__global__ __launch_bounds__(kStgWaves * 64) void k_wal_list_crc(WalArgs A) {
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kStgLdsWords];
+    load_stg_tables<kStgWaves * 64>(lds, A.crc_blob);  // the lane blob
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t X = lane_const16();
+    uint8_t* stage = reinterpret_cast<uint8_t*>(lds + kStgBuf) + wave * kStgBytes;
+    const uint64_t P = A.nsub, nw = A.nwork * P, total = A.nwork * A.cand_cap;
+    (void)total;
+    for (uint64_t w = (uint64_t)blockIdx.x * kStgWaves + wave; w < nw; w += (uint64_t)gridDim.x * kStgWaves) {
+        const uint64_t s = w / P, j = w % P;
+        const Seg S = make_seg(A, s);
+        uint32_t count, max_len;
+        if (P == 1) {
+            const WalSegMeta M = KB_READ(A.meta, s, A.nwork, kKbMeta);
+            count = M.count;
+            max_len = M.max_len;
+        } else {
+            const WalSubMeta M = KB_READ(A.sub, w, nw, kKbSubMeta);
+            count = M.count;
+            max_len = M.max_len;
+        }
+        if (count > A.sub_cap) count = (uint32_t)A.sub_cap;
+        const uint64_t slot0 = s * A.cand_cap + j * A.sub_cap;
+        uint32_t fb = kNoBad;
+        if (max_len > kCrcInlineMax) {
+            fb = kCrcUnknown;
+        } else {
+            for (uint32_t i0 = 0; i0 < count;) {
+                const uint32_t i = i0 + lane;
+                const bool v = i < count;
+                uint32_t rec = 0, n = 0, st = 0;
+                if (v) {
+                    rec = KB_READ(A.cand_rec, slot0 + i, total, kKbCand);
+                    n = KB_READ(A.cand_len, slot0 + i, total, kKbCand);
+                    st = KB_READ(A.cand_crc, slot0 + i, total, kKbCand);
+                }
+                const uintptr_t p = reinterpret_cast<uintptr_t>(S.img) + rec + 8;
+                const StgSpan SP = stg_prefix(p, n, v && n, lane);
+                const bool staged = SP.hi != 0;
+                if (staged) {
+                    stg_copy(SP.lo, SP.hi, lane, stage);
+                    wave_lds_sync();
+                }
+                uint32_t res = 0;
+                const bool mine = v && n && lane < SP.cnt;  // size 0: checked by the walk
+                if (mine) {
+                    if (staged)
+                        res = lane_record(lds, X, kStgZ4, kStgT8, p, n, 0u, [&](uintptr_t a) {
+                            return *reinterpret_cast<const u32x4*>(stage + (uint32_t)(a - SP.lo));
+                        });
+                    else
+                        res = lane_record(lds, X, kStgZ4, kStgT8, p, n, 0u,
+                                          [&](uintptr_t a) { return ld16(reinterpret_cast<const uint8_t*>(a)); });
+                }
+                const uint64_t bm = __ballot(mine && res != st);
+                if (bm) {
+                    fb = i0 + (uint32_t)__builtin_ctzll(bm);
+                    break;
+                }
+                i0 += SP.cnt;
+                wave_lds_sync();  // this step's reads before the next step's stores
+            }
+        }
+        if (lane == 0) {
+#ifdef KARMA_BOUNDS
+            if (!KB_IDX(P == 1 ? s : w, P == 1 ? A.nwork : nw, P == 1 ? kKbMeta : kKbSubMeta)) continue;
+#endif
+            if (P == 1)
+                A.meta[s].first_bad = fb;
+            else
+                A.sub[w].pad[0] = fb;
+        }
+    }
+}
+
 // One wave per segment: follow the authoritative chain through the sub-ranges.
 // Entering sub-range j at pos, the chain continues exactly as walker j's list
 // from the entry equal to pos on (the walk is a function of the position), so
@@ -1066,6 +1150,13 @@ hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& p
                            dim3(kFuseWaves * 64), 0, s, a);
     } else {
         hipLaunchKernelGGL(k_wal_walk_sub, dim3((unsigned)(nseg * plan.nsub)), dim3(64), 0, s, a);
+    }
+    if (plan.kernel == 3) {  // the walkers' lists checksummed after the walk (the lane blob)
+        if (!a.crc_blob) return hipErrorInvalidValue;
+        const uint64_t walkers = nseg * plan.nsub;
+        uint64_t blocks = (walkers + kStgWaves - 1) / kStgWaves;
+        if (blocks > (uint64_t)plan.cu) blocks = (uint64_t)plan.cu;
+        hipLaunchKernelGGL(k_wal_list_crc, dim3((unsigned)blocks), dim3(kStgWaves * 64), 0, s, a);
     }
     if (plan.nsub > 1) hipLaunchKernelGGL(k_wal_resolve, dim3((unsigned)nseg), dim3(64), 0, s, a);
     return hipGetLastError();

@@ -15,6 +15,9 @@ copy for each variant in interleaved rounds (same process, same image):
     direct4              tools build, KARMA_DIRECT_VARIANT=4 (= the shipped k_ragged_direct4<4>)
     direct2              tools build, KARMA_DIRECT_VARIANT=5 (k_ragged_direct4<2>: pairs of lanes)
     units                the shipped library, ragged plan instead of the direct kernel (crc_batch)
+    ab                   tools build, default plan (k_wal_walk_crc)
+    listcrc              tools build, KARMA_WAL_LIST_CRC=1: the walk, then the walkers' lists checksummed by
+                         the LDS-staged one-record-per-lane kernel (k_wal_list_crc)
     sep                  the shipped library, KARMA_WAL_CRC_SEPARATE: walk, gather, one batch (round 2's path;
                          the default now checksums inside the walk kernel, k_wal_walk_crc)
 
@@ -102,6 +105,10 @@ def main():
             variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "4"))
         elif v == "direct2":
             variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "5"))
+        elif v == "listcrc":  # the walk, then the walkers' lists by the LDS-staged kernel (k_wal_list_crc)
+            variants[v] = (AB, 0, 0, ("KARMA_WAL_LIST_CRC", "1"))
+        elif v == "ab":  # the tools build's default plan (same-library reference for listcrc)
+            variants[v] = (AB, 0, 0, None)
         elif v == "units":
             variants[v] = (L, 0, 2, None)
         elif v == "sep":  # the walk, then one small-record batch over the gathered lists (round 2's path)
@@ -123,6 +130,8 @@ def main():
 
     for r in range(a.rounds):
         for v, (lib, sub, batch, env) in variants.items():
+            for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC"):
+                os.environ.pop(k, None)
             if env:
                 os.environ[env[0]] = env[1]
             res[v].append(timed(lib, sub, batch, False))
