@@ -522,6 +522,20 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
     a.cmp_stored = d_stored;
     a.cmp_bad = reinterpret_cast<unsigned long long*>(d_first_bad);
     bind_arena_bounds(a);
+    // Two gated launches split the range of the batch's largest payload (known on the device
+    // only): up to kStgGateLen the LDS-staged kernel (64 consecutive WAL payloads per wave's
+    // stage, windows aligned to the record ends: k_ragged_staged_pipe), above it the 4-lane
+    // groups (k_ragged_direct4); the other one returns at once.
+    const uint32_t stg_max = std::min<uint32_t>(gate_max, kStgGateLen);
+    if (KARMA_AB_KNOB("KARMA_SMALL_STAGED", 1)) {
+        RaggedArgs b = a;
+        b.blob = L.ds->lane_blob;
+        b.gate_max = stg_max;
+        const uint64_t sblocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_cap, 64 * kStgWaves));
+        KARMA_HIP(launch_ragged_staged_dev(b, (int)sblocks, s));
+        if (gate_max <= stg_max) return 0;
+        a.gate_min = stg_max + 1;
+    }
     const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_cap, 64 * kWavesPerBlock));
     KARMA_HIP(launch_ragged_direct_dev(a, (int)blocks, s));
     return 0;
@@ -640,11 +654,11 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
         a.init_scalar = init;
         a.out = d_out;
         const long dv = KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0);  // tools build: the other kernels
-        a.blob = dv == 1 || dv == 2 ? L.ds->blob : dv == 3 || (dv >= 14 && dv <= 20) ? L.ds->lane_blob : dv == 5 ? L.ds->pair_blob : L.ds->quad_blob;
+        a.blob = dv == 1 || dv == 2 ? L.ds->blob : dv == 3 || (dv >= 14 && dv <= 20) ? L.ds->lane_blob : dv == 5 || dv == 21 ? L.ds->pair_blob : L.ds->quad_blob;
         bind_arena_bounds(a);
         // a wave takes 64 records (lanes variant: a workgroup 1024): no more workgroups than
         // the batch fills (each one loads the 145 KiB table image into its LDS first)
-        const uint64_t per_block = dv == 3 ? kBlockThreads : dv >= 14 && dv <= 20 ? 64 * kStgWaves : 64 * kWavesPerBlock;
+        const uint64_t per_block = dv == 3 ? kBlockThreads : dv >= 14 && dv <= 20 ? 64 * kStgWaves : dv == 21 ? 32 * 14 : 64 * kWavesPerBlock;
         const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_rec, per_block));
         KARMA_HIP(launch_ragged_direct(a, (int)blocks, (hipStream_t)stream));
         return KARMA_OK;

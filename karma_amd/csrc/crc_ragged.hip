@@ -930,7 +930,7 @@ template <int G, int MODE = 0, int PF = kRaggedPF, bool ALL = false>  // MODE !=
 __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) {
     uint64_t n_rec = A.n_rec;
     if (A.n_dev) {  // a device-sized batch: the count is known on the device only
-        if (*A.gate_len > A.gate_max) return;
+        if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
         n_rec = *A.n_dev;
     }
     KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.blob, A.blob + kBlobWords);  // the blob: empty units' address
@@ -968,7 +968,7 @@ template <bool PIPE, int MODE = 0>  // MODE (tools build timing only, wrong CRCs
 __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) {
     uint64_t n_rec = A.n_rec;
     if (A.n_dev) {  // a device-sized batch (as k_ragged_direct4)
-        if (*A.gate_len > A.gate_max) return;
+        if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
         n_rec = *A.n_dev;
     }
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
@@ -1050,7 +1050,7 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
     constexpr uint32_t kLead = END ? 16u : 0u, kFit = END ? kStgBytes - 32u : kStgBytes;
     uint64_t n_rec = A.n_rec;
     if (A.n_dev) {
-        if (*A.gate_len > A.gate_max) return;
+        if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
         n_rec = *A.n_dev;
     }
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
@@ -1152,6 +1152,168 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
 }
 
 #ifdef KARMA_AB
+// Pairs of lanes per record (tools build, KARMA_DIRECT_VARIANT=21): half the stage per wave
+// (32 records, 6 KiB) so twice the waves per CU, and half the dependent chain per lane.  The
+// windows are aligned to the record's end (lane_record_end) and dealt from the end: lane 1 of
+// the pair takes windows W-1, W-3, ..., lane 0 takes W-2, W-4, ..., each striding 32 bytes
+// (the pair blob's Z_32 tables); the record's register is R1 ^ Z16(R0).
+constexpr int kPairWaves = 14;
+constexpr uint32_t kPairStg = 6144;                     // extent bytes per wave (32 records)
+constexpr uint32_t kPairStride = kPairStg + 16;         // + the first window's lead-in slack
+constexpr int kPairVecs = (int)(kPairStg / 1024);
+constexpr int kPairZ4 = kRep16Words, kPairZ16 = kPairZ4 + 1024, kPairT8 = kPairZ16 + 1024, kPairBuf = kPairT8 + 256;
+constexpr int kPairLdsWords = kPairBuf + kPairWaves * (int)(kPairStride / 4);
+static_assert(kPairLdsWords * 4 <= 160 * 1024, "LDS of one workgroup");
+
+// This lane's half of the record [sp, sp + n) of the stage (n >= 4): its windows' register,
+// ending at the record end (l = 1) or 16 bytes before it (l = 0; 0 when it has none).
+template <typename Rd>
+__device__ __forceinline__ uint32_t pair_record_end(const uint32_t* lds, uint32_t X, uint32_t sp, uint32_t n,
+                                                    uint32_t init, uint32_t l, Rd&& rd) {
+    const uint32_t W = (n + 15) >> 4, h0 = 16 * W - n;
+    const uint32_t s0 = sp - h0, sh = s0 & 3, q0 = s0 >> 2;
+    const uint32_t inj = ~init, b = h0 & 3, k0 = h0 >> 2;
+    const uint32_t lo32 = inj << (8 * b), hi32 = b ? inj >> (32 - 8 * b) : 0u;
+    auto keep = [&](uint32_t k) {
+        const int r = (int)h0 - 4 * (int)k;
+        return r <= 0 ? ~0u : r >= 4 ? 0u : (~0u << (8 * r));
+    };
+    auto window = [&](uint32_t j) {
+        const uint32_t q = q0 + 4 * j;
+        const uint32_t d0 = rd(q), d1 = rd(q + 1), d2 = rd(q + 2), d3 = rd(q + 3), d4 = rd(q + 4);
+        u32x4 v;
+        v.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+        v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+        v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+        if (j == 0) {  // the lead-in bytes masked, ~init into the record's first 4 bytes
+            v.x = (v.x & keep(0)) ^ (k0 == 0 ? lo32 : 0u);
+            v.y = (v.y & keep(1)) ^ (k0 == 1 ? lo32 : 0u) ^ (k0 == 0 ? hi32 : 0u);
+            v.z = (v.z & keep(2)) ^ (k0 == 2 ? lo32 : 0u) ^ (k0 == 1 ? hi32 : 0u);
+            v.w = (v.w & keep(3)) ^ (k0 == 3 ? lo32 : 0u) ^ (k0 == 2 ? hi32 : 0u);
+        } else if (j == 1 && k0 == 3) {
+            v.x ^= hi32;
+        }
+        return v;
+    };
+    uint32_t j = l ? ((W - 1) & 1u) : (W & 1u);
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    if (j < W) {
+        const u32x4 v = window(j);
+        a0 = v.x;
+        a1 = v.y;
+        a2 = v.z;
+        a3 = v.w;
+        j += 2;
+    }
+    for (; j < W; j += 2) step4<8>(lds, X, a0, a1, a2, a3, window(j));
+    return lane_fold_at(lds, kPairZ4, a0, a1, a2, a3);
+}
+
+__global__ __launch_bounds__(kPairWaves * 64) void k_ragged_staged_pair(RaggedArgs A) {
+    uint64_t n_rec = A.n_rec;
+    if (A.n_dev) {
+        if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
+        n_rec = *A.n_dev;
+    }
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kPairLdsWords];
+    load_rep16_stride<kPairWaves * 64>(lds, A.blob, [&] {  // the pair blob: Z_32 stride tables
+        copy_to_lds<1024, kPairWaves * 64>(lds + kPairZ4, A.blob + kBlobZ4);
+        copy_to_lds<1024, kPairWaves * 64>(lds + kPairZ16, A.blob + kBlobZ16);
+        copy_to_lds<256, kPairWaves * 64>(lds + kPairT8, A.blob + kBlobT8);
+    });
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, l = lane & 1u, rl = lane >> 1;
+    const uint32_t X = lane_const16();
+    uint8_t* stage = reinterpret_cast<uint8_t*>(lds + kPairBuf) + wave * kPairStride;  // data from stage + 16
+    const uint64_t step = (uint64_t)gridDim.x * kPairWaves * 32;
+    uint64_t base = ((uint64_t)blockIdx.x * kPairWaves + wave) * 32;
+    if (base >= n_rec) return;
+    auto ld_meta = [&](uint64_t b, uint64_t& o, uint32_t& n, uint32_t& ini) {
+        const uint64_t ri = b + rl;
+        const bool v = ri < n_rec;
+        o = v ? A.off[ri] : 0;
+        n = v ? A.len[ri] : 0u;
+        ini = v ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
+    };
+    auto extent = [&](uint64_t o, uint32_t n, uintptr_t& lo, uintptr_t& hi) {
+        const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
+        uint64_t lw = n ? (p & ~uintptr_t(15)) : ~0ull, h = n ? ((p + n + 15) & ~uintptr_t(15)) : 0ull;
+#pragma unroll
+        for (int d = 2; d < 64; d <<= 1) {  // (the two lanes of a pair hold the same record)
+            const uint64_t ol = (uint64_t)__shfl_xor((long long)lw, d), oh = (uint64_t)__shfl_xor((long long)h, d);
+            lw = ol < lw ? ol : lw;
+            h = oh > h ? oh : h;
+        }
+        lo = uniform64(lw);
+        hi = uniform64(h);
+    };
+    u32x4 v[kPairVecs];
+    auto issue = [&](uintptr_t lo, uintptr_t hi) {
+        const uint32_t nv = (uint32_t)((hi - lo) / 16);
+#pragma unroll
+        for (int q = 0; q < kPairVecs; ++q) {
+            const uint32_t j = lane + 64u * q;
+            v[q] = ldg<true>(reinterpret_cast<const uint8_t*>(lo + 16ull * (j < nv ? j : 0u)));
+        }
+    };
+    constexpr uint32_t kFit = kPairStg - 16u;  // the last window may read 3 bytes past the extent
+    uint64_t o, o2;
+    uint32_t n, ini, n2, ini2;
+    uintptr_t lo, hi;
+    ld_meta(base, o, n, ini);
+    ld_meta(base + step, o2, n2, ini2);
+    extent(o, n, lo, hi);
+    bool fits = hi != 0 && hi - lo <= kFit;
+    if (fits) issue(lo, hi);
+    for (;;) {
+        if (fits) {
+#pragma unroll
+            for (int q = 0; q < kPairVecs; ++q) *reinterpret_cast<u32x4*>(stage + 16u + 16u * (lane + 64u * q)) = v[q];
+            wave_lds_sync();
+        }
+        const uint64_t nb = base + step;
+        const bool more = nb < n_rec;
+        uintptr_t lo2 = 0, hi2 = 0;
+        bool fits2 = false;
+        uint64_t o3 = 0;
+        uint32_t n3 = 0, ini3 = 0;
+        if (more) {
+            extent(o2, n2, lo2, hi2);
+            fits2 = hi2 != 0 && hi2 - lo2 <= kFit;
+            if (fits2) issue(lo2, hi2);
+            ld_meta(nb + step, o3, n3, ini3);
+        }
+        const uint64_t ri = base + rl;
+        const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
+        uint32_t part = 0;
+        const bool pair = fits && n >= 4 && ri < n_rec;
+        if (pair)
+            part = pair_record_end(lds, X, 16u + (uint32_t)(p - lo), n, ini, l, [&](uint32_t q) {
+                return *reinterpret_cast<const uint32_t*>(stage + 4u * q);
+            });
+        const uint32_t other = __shfl_xor(part, 1);
+        if (l == 1 && ri < n_rec) {
+            uint32_t res;
+            if (pair)
+                res = ~(part ^ zmap(lds, kPairZ16, other));
+            else if (n)  // a short record or an extent that does not fit: byte / word steps from memory
+                res = short_record(lds, kPairZ4, kPairT8, reinterpret_cast<const uint8_t*>(p), n, ini);
+            else
+                res = ini;
+            A.out[ri] = res;
+            if (A.cmp_stored && n && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
+        }
+        wave_lds_sync();
+        if (!more) break;
+        base = nb;
+        o = o2; n = n2; ini = ini2;
+        o2 = o3; n2 = n3; ini2 = ini3;
+        lo = lo2; hi = hi2; fits = fits2;
+    }
+}
+
 // Tools build (KARMA_DIRECT_VARIANT=1, ab.h): small records one per group of 8 lanes, the
 // shipped kernel before k_ragged_direct4 (0.237 vs 0.202 ms per 1M x 180 B replay call,
 // DESIGN.md §8a).  Batches of small records: one record per group, its whole body one unit, no plan kernels (scan, descriptors and
@@ -1374,6 +1536,8 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL(k_ragged_staged_pipe<false>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else if (v == 20)  // ... with the windows aligned to the record ends (no head / tail steps)
         hipLaunchKernelGGL(k_ragged_staged_pipe<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (v == 21)  // ... and two lanes per record (32 records per wave, 14 waves per CU)
+        hipLaunchKernelGGL(k_ragged_staged_pair, dim3(grid_blocks), dim3(kPairWaves * 64), 0, s, a);
     else if (v == 16)  // timing only: staging copy without the CRC steps / 17 the steps without the copy / 18 neither
         hipLaunchKernelGGL((k_ragged_staged<false, 1>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else if (v == 17)
@@ -1384,6 +1548,12 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
 #endif
         hipLaunchKernelGGL(k_ragged_direct4<4>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
+    return hipGetLastError();
+}
+
+hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
+    if (a.n_rec == 0 || !a.n_dev || !a.gate_len) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ragged_staged_pipe<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -18,6 +18,9 @@ constexpr int kBlockThreads = 1024;            // one workgroup per CU
 constexpr int kWavesPerBlock = kBlockThreads / 64;
 constexpr int kGroupsPerWave = 64 / kGroupLanes;
 constexpr int kStgWaves = 7;  // k_ragged_staged: one 448-thread workgroup per CU (LDS-bound)
+// Consecutive payloads up to this length (with 8-byte WAL headers between them) put 64 records
+// in one wave's 12 KiB stage (crc_device.h kStgBytes: (12288 - 64) / 64 - 8).
+constexpr uint32_t kStgGateLen = 183;
 #ifndef KARMA_RAGGED_UNIT
 #define KARMA_RAGGED_UNIT 8192  // a build-time A/B knob (tools/ragged_unit_ab.sh)
 #endif
@@ -162,10 +165,12 @@ struct RaggedArgs {
     const uint32_t* comb_blob; // kCombWords for unit_bytes
     uintptr_t kb_lo, kb_hi;    // bounds build only: the arena's allocation (bounds.h); else 0
     // Device-sized batches (WAL replay's small-record path): when n_dev is set the kernel reads
-    // n_rec there, and does nothing unless *gate_len <= gate_max.  (k_ragged_direct4 only.)
+    // n_rec there, and does nothing unless gate_min <= *gate_len <= gate_max.  (k_ragged_direct4 and
+// k_ragged_staged_pipe only.)
     const uint64_t* n_dev;
     const uint32_t* gate_len;
     uint32_t gate_max;
+    uint32_t gate_min;         // ... and *gate_len >= gate_min (the staged and 4-lane kernels split the range)
     // ... and, when cmp_stored is set, the kernel also compares each record's CRC with
     // cmp_stored[r] (records of length 0 excepted) and keeps the first mismatch in *cmp_bad.
     const uint32_t* cmp_stored;
@@ -207,6 +212,7 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
 hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // k_ragged_direct4 with a device-sized batch (a.n_dev / a.gate_len set): WAL replay's
 // device-planned path, whatever the tools build's variant.
+hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 hipError_t launch_ragged_direct_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // Library-internal entry (capi.cc) for callers that know every record is small
 // (WAL replay): CRCs of arena[off[r], off[r] + len[r]) with Value's init.

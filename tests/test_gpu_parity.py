@@ -531,7 +531,7 @@ def test_ragged_low_total_len_is_still_exact(raw, dev):
         _eq(got, want)
 
 
-@pytest.mark.parametrize("variant", ["shipped", "1", "2", "3", "4", "5", "14", "15", "19", "20"])
+@pytest.mark.parametrize("variant", ["shipped", "1", "2", "3", "4", "5", "14", "15", "19", "20", "21"])
 @pytest.mark.parametrize("bound", [0, 64, 1024, 1 << 20])
 def test_ragged_bounded_direct_path(raw, dev, bound, variant, monkeypatch):
     """karma_crc32c_batch_ragged_bounded: with max_len <= 1 KiB one record per group (no plan
@@ -562,7 +562,7 @@ def test_ragged_bounded_direct_path(raw, dev, bound, variant, monkeypatch):
 
 
 
-@pytest.mark.parametrize("variant", ["shipped", "4", "14", "15", "19", "20"])
+@pytest.mark.parametrize("variant", ["shipped", "4", "14", "15", "19", "20", "21"])
 @pytest.mark.parametrize("shape", ["wal180", "mixed", "tiny", "unaligned_arena"])
 def test_ragged_bounded_consecutive_records(raw, dev, shape, variant, monkeypatch):
     """Consecutive small records (a WAL image's payloads, a writer's block) through the bounded

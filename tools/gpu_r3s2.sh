@@ -1,5 +1,5 @@
 set -e
 mkdir -p gpurun_out/r3s
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "consecutive or bounded_direct" --karma-lib abbounds > gpurun_out/r3s/tests_abbounds.log 2>&1
-timeout -k 10 240 python3 -u tools/direct_study.py --variants 0,19,20 --rounds 3 > gpurun_out/r3s/direct5.txt 2>&1
+timeout -k 10 240 python3 -u tools/direct_study.py --variants 0,20,21 --rounds 3 > gpurun_out/r3s/direct6.txt 2>&1
 echo done

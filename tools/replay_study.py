@@ -18,6 +18,7 @@ copy for each variant in interleaved rounds (same process, same image):
     ab                   tools build, default plan (k_wal_walk_crc)
     listcrc              tools build, KARMA_WAL_LIST_CRC=1: the walk, then the walkers' lists checksummed by
                          the LDS-staged one-record-per-lane kernel (k_wal_list_crc)
+    sepdirect4           tools build, KARMA_WAL_CRC_SEPARATE with KARMA_SMALL_STAGED=0 (the 4-lane batch)
     sep                  the shipped library, KARMA_WAL_CRC_SEPARATE: walk, gather, one batch (round 2's path;
                          the default now checksums inside the walk kernel, k_wal_walk_crc)
 
@@ -107,6 +108,8 @@ def main():
             variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "5"))
         elif v == "listcrc":  # the walk, then the walkers' lists by the LDS-staged kernel (k_wal_list_crc)
             variants[v] = (AB, 0, 0, ("KARMA_WAL_LIST_CRC", "1"))
+        elif v == "sepdirect4":  # the separate path with the 4-lane small-record kernel only (round 2's)
+            variants[v] = (AB, 0, 3, ("KARMA_SMALL_STAGED", "0"))
         elif v == "ab":  # the tools build's default plan (same-library reference for listcrc)
             variants[v] = (AB, 0, 0, None)
         elif v == "units":
@@ -130,7 +133,7 @@ def main():
 
     for r in range(a.rounds):
         for v, (lib, sub, batch, env) in variants.items():
-            for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC"):
+            for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC", "KARMA_SMALL_STAGED"):
                 os.environ.pop(k, None)
             if env:
                 os.environ[env[0]] = env[1]
