@@ -157,11 +157,14 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
 /* Plan overrides of karma_wal_replay_tuned.  Every setting gives the same result (the
  * replay is exact whatever the plan); they exist for tests and tuning.  Zero = the
  * planner's choice. */
-#define KARMA_WAL_CRC_PLAN 0    /* one-record-per-group batch when every payload <= 1 KiB, else the unit plan */
-#define KARMA_WAL_CRC_DIRECT 1  /* always the one-record-per-group batch */
+#define KARMA_WAL_CRC_PLAN 0    /* the walk, then one small-record batch over the gathered lists when every
+                                   payload <= 1 KiB (LDS-staged up to 183 B, 4-lane groups above), else the
+                                   unit plan */
+#define KARMA_WAL_CRC_DIRECT 1  /* always the small-record batch */
 #define KARMA_WAL_CRC_UNITS 2   /* always the unit plan (karma_crc32c_batch_ragged) */
-#define KARMA_WAL_CRC_SEPARATE 3 /* as PLAN, but the walk first, then one batch over the gathered lists
-                                    (PLAN checksums payloads <= 1 KiB inside the walk) */
+#define KARMA_WAL_CRC_SEPARATE 3 /* = PLAN (kept for callers of round 2's ABI) */
+#define KARMA_WAL_CRC_INLINE 4  /* as PLAN, but payloads <= 1 KiB checksummed inside the walk kernel
+                                   (k_wal_walk_crc: faster when the image is cache-resident, slower from HBM) */
 typedef struct karma_wal_tuning {
     uint64_t walk_sub_bytes; /* header-walk sub-range size, rounded down to a 4 KiB multiple (>= 4 KiB);
                                 >= seg_bytes: one walker per segment; 0 = planned */

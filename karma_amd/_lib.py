@@ -77,7 +77,7 @@ SIGNATURES = {
 }
 
 
-KARMA_WAL_CRC_PLAN, KARMA_WAL_CRC_DIRECT, KARMA_WAL_CRC_UNITS, KARMA_WAL_CRC_SEPARATE = 0, 1, 2, 3
+KARMA_WAL_CRC_PLAN, KARMA_WAL_CRC_DIRECT, KARMA_WAL_CRC_UNITS, KARMA_WAL_CRC_SEPARATE, KARMA_WAL_CRC_INLINE = 0, 1, 2, 3, 4
 
 
 class WalTuning(ctypes.Structure):

@@ -231,7 +231,7 @@ int karma_wal_replay_tuned(const void* h_wal, const void* d_wal, size_t wal_byte
                            int device, const karma_wal_tuning* tuning) {
     if ((!h_wal && !d_wal) || !h_n_records || !h_stop || !h_status || seg_bytes < 1 || wal_bytes % seg_bytes ||
         start > wal_bytes || seg_bytes >= (uint64_t(1) << 31) ||
-        (tuning && (tuning->crc_batch < 0 || tuning->crc_batch > KARMA_WAL_CRC_SEPARATE)))
+        (tuning && (tuning->crc_batch < 0 || tuning->crc_batch > KARMA_WAL_CRC_INLINE)))
         return fail(KARMA_E_INVALID, "wal_replay");
     const uint8_t* src = static_cast<const uint8_t*>(h_wal);
     const ImageFill copy = [src](uint8_t* dst, uint64_t off, size_t n) {
@@ -303,7 +303,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     const bool dev_plan = img_bytes <= kDevicePlanMax && batch != KARMA_WAL_CRC_UNITS &&
                           KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 0;
     const bool inline_crc =
-        dev_plan && batch == KARMA_WAL_CRC_PLAN && KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 0;
+        dev_plan && batch == KARMA_WAL_CRC_INLINE && KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 0;
     // the walkers' lists checksummed after the walk by the LDS-staged kernel (k_wal_list_crc)
     // instead of by the walkers themselves (k_wal_walk_crc)
     const bool list_crc = inline_crc && KARMA_AB_KNOB("KARMA_WAL_LIST_CRC", 0) != 0;
@@ -397,7 +397,8 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     const uint64_t w1 = S->w1, n_all = S->n_all;
     const uint32_t max_len = S->max_len;
     const bool small = batch == KARMA_WAL_CRC_DIRECT ||
-                       ((batch == KARMA_WAL_CRC_PLAN || batch == KARMA_WAL_CRC_SEPARATE) && max_len <= kSmallRecordMax);
+                       ((batch == KARMA_WAL_CRC_PLAN || batch == KARMA_WAL_CRC_SEPARATE || batch == KARMA_WAL_CRC_INLINE) &&
+                        max_len <= kSmallRecordMax);
     // inline CRCs complete: the first mismatch is known (no gathered lists exist yet)
     const bool inline_done = inline_crc && !S->crc_unknown;
     const bool lists = dev_plan && !inline_crc;  // the device-planned gather wrote them

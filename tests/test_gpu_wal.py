@@ -50,8 +50,10 @@ WALKS = {
     "octet": (True, 4096, _lib.KARMA_WAL_CRC_DIRECT),     # the same with the tools build's 8-lane groups
     "sep": (False, 0, _lib.KARMA_WAL_CRC_SEPARATE),       # the walk, the gathered lists, one small-record batch
     "sepdirect4": (True, 0, _lib.KARMA_WAL_CRC_SEPARATE),  # the same with the 4-lane kernel only (tools build)
-    "listcrc": (True, 0, _lib.KARMA_WAL_CRC_PLAN),        # the walk, then the walkers' lists checksummed by
-    "listcrc4k": (True, 4096, _lib.KARMA_WAL_CRC_PLAN),   # the LDS-staged kernel (k_wal_list_crc; tools build)
+    "inline": (False, 0, _lib.KARMA_WAL_CRC_INLINE),      # the CRCs inside the walk kernel (k_wal_walk_crc)
+    "inline4k": (False, 4096, _lib.KARMA_WAL_CRC_INLINE),
+    "listcrc": (True, 0, _lib.KARMA_WAL_CRC_INLINE),      # the walk, then the walkers' lists checksummed by
+    "listcrc4k": (True, 4096, _lib.KARMA_WAL_CRC_INLINE), # the LDS-staged kernel (k_wal_list_crc; tools build)
 }
 _DIRECT_VARIANT = {"octet": "1"}  # KARMA_DIRECT_VARIANT of the tools-build plans
 _LIST_CRC = ("listcrc", "listcrc4k")  # KARMA_WAL_LIST_CRC=1
@@ -261,7 +263,7 @@ def test_replay_large_records_jumps(lib, seg, walk, monkeypatch):
         assert got == (list(w[0]), w[1], w[2])
 
 
-@pytest.mark.parametrize("walk", ["split", "split4k", "octet", "sep", "listcrc", "listcrc4k"])
+@pytest.mark.parametrize("walk", ["split", "split4k", "octet", "sep", "inline", "inline4k", "listcrc", "listcrc4k"])
 def test_replay_payloads_that_look_like_wal_records(lib, walk, monkeypatch):
     """Payloads that are themselves WAL images (valid header chains inside records): a sub-range
     walker can start on a header inside a payload, and the resolver must then walk the sub-range
@@ -402,13 +404,13 @@ def test_replay_randomized_against_model(lib, monkeypatch):
             wal[int(rec[k]) + int(rng.choice([5, 8]))] ^= 0x10
         start = int(rec[int(rng.integers(0, len(rec)))]) if case % 2 and len(rec) else 0
         want = wal_model.replay(wal.tobytes(), seg, start)
-        for walk in ("whole", "split", "split4k", "sep", "listcrc4k"):
+        for walk in ("whole", "split", "split4k", "inline", "inline4k", "listcrc4k"):
             _walk_env(monkeypatch, walk)
             got = _replay(lib, wal, start=start, seg=seg)
             assert got == (list(want[0]), want[1], want[2]), (case, walk, seg, mix)
 
 
-@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "sep", "listcrc"])
+@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc"])
 @pytest.mark.parametrize("seg", [4096 + 4, 65536, 1 << 20])
 def test_replay_uniform_runs_speculative_walk(lib, seg, walk, monkeypatch):
     """Runs of one record size (the walker reads a round of headers at the last stride, lane j at

@@ -15,8 +15,9 @@ copy for each variant in interleaved rounds (same process, same image):
     direct4              tools build, KARMA_DIRECT_VARIANT=4 (= the shipped k_ragged_direct4<4>)
     direct2              tools build, KARMA_DIRECT_VARIANT=5 (k_ragged_direct4<2>: pairs of lanes)
     units                the shipped library, ragged plan instead of the direct kernel (crc_batch)
-    ab                   tools build, default plan (k_wal_walk_crc)
-    listcrc              tools build, KARMA_WAL_LIST_CRC=1: the walk, then the walkers' lists checksummed by
+    ab                   tools build, default plan
+    inline               the shipped library, KARMA_WAL_CRC_INLINE: the CRCs inside the walk (k_wal_walk_crc)
+    listcrc              tools build, KARMA_WAL_CRC_INLINE + KARMA_WAL_LIST_CRC=1: the walk, then the walkers' lists checksummed by
                          the LDS-staged one-record-per-lane kernel (k_wal_list_crc)
     sepdirect4           tools build, KARMA_WAL_CRC_SEPARATE with KARMA_SMALL_STAGED=0 (the 4-lane batch)
     sep                  the shipped library, KARMA_WAL_CRC_SEPARATE: walk, gather, one batch (round 2's path;
@@ -107,7 +108,9 @@ def main():
         elif v == "direct2":
             variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "5"))
         elif v == "listcrc":  # the walk, then the walkers' lists by the LDS-staged kernel (k_wal_list_crc)
-            variants[v] = (AB, 0, 0, ("KARMA_WAL_LIST_CRC", "1"))
+            variants[v] = (AB, 0, 4, ("KARMA_WAL_LIST_CRC", "1"))
+        elif v == "inline":  # the shipped library, KARMA_WAL_CRC_INLINE (k_wal_walk_crc)
+            variants[v] = (L, 0, 4, None)
         elif v == "sepdirect4":  # the separate path with the 4-lane small-record kernel only (round 2's)
             variants[v] = (AB, 0, 3, ("KARMA_SMALL_STAGED", "0"))
         elif v == "ab":  # the tools build's default plan (same-library reference for listcrc)
