@@ -79,6 +79,21 @@ __device__ __forceinline__ uint32_t stride_step16(const uint32_t* lds, uint32_t 
     return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
 }
 
+// The same lookups with lanes 16-31 of each 32-lane half taking the tables in the order 1, 0, 3, 2:
+// one ds_read_b32 then reads table k in lanes 0-15 and table k ^ 1 in lanes 16-31, whose bank
+// columns differ by 16 (k << 6 bytes), so the 16-copy image is read without bank conflicts
+// (the four lookups are xored, in any order).
+__device__ __forceinline__ uint32_t stride_step16s(const uint32_t* lds, uint32_t X, uint32_t acc, uint32_t w) {
+    const bool sw = (threadIdx.x & 16u) != 0;
+    const uint32_t s0 = sw ? 0x0c0c0105u : 0x0c0c0004u, s1 = sw ? 0x0c0c0004u : 0x0c0c0105u;
+    const uint32_t s2 = sw ? 0x0c0c0307u : 0x0c0c0206u, s3 = sw ? 0x0c0c0206u : 0x0c0c0307u;
+    const uint32_t i0 = __builtin_amdgcn_perm(X, acc, s0);
+    const uint32_t i1 = __builtin_amdgcn_perm(X, acc, s1);
+    const uint32_t i2 = __builtin_amdgcn_perm(X, acc, s2);
+    const uint32_t i3 = __builtin_amdgcn_perm(X, acc, s3);
+    return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
+}
+
 // Z(x) for a map stored as four plain 256-entry tables at word `base`.
 __device__ __forceinline__ uint32_t zmap(const uint32_t* lds, int base, uint32_t x) {
     return lds[base + (x & 255u)] ^ lds[base + 256 + ((x >> 8) & 255u)] ^ lds[base + 512 + ((x >> 16) & 255u)] ^
@@ -214,9 +229,17 @@ __device__ __forceinline__ uint32_t tail_register(const uint32_t* lds, int z4, i
 // steps without the LDS lookups (KARMA_CRC_VARIANT=6, ab.h), bit 1 = stream_unit without
 // the lane fold and group tree.  The shipped library instantiates MODE 0 only.
 // MODE bit 3: the 16-copy stride image (stride_step16, lane_const16).
+// MODE bit 4 (with bit 3): the conflict-free lane order of the 16-copy image (stride_step16s).
 template <int MODE = 0>
 __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
                                       uint32_t& a3, const u32x4& v) {
+    if constexpr ((MODE & 24) == 24) {
+        a0 = stride_step16s(lds, X, a0, v.x);
+        a1 = stride_step16s(lds, X, a1, v.y);
+        a2 = stride_step16s(lds, X, a2, v.z);
+        a3 = stride_step16s(lds, X, a3, v.w);
+        return;
+    }
     if constexpr (MODE & 8) {
         a0 = stride_step16(lds, X, a0, v.x);
         a1 = stride_step16(lds, X, a1, v.y);
@@ -746,7 +769,7 @@ __device__ __forceinline__ void stg_copy(uintptr_t lo, uintptr_t hi, uint32_t la
 // steps and the STEP4W fold.  Needs n >= 4 (the injected word lies inside the record).
 // rd(q): dword q of the stage (q = byte offset / 4; the windows are read as dwords and
 // funnel-shifted, v_alignbyte_b32).
-template <typename Rd>
+template <int SMODE = 24, typename Rd>
 __device__ __forceinline__ uint32_t lane_record_end(const uint32_t* lds, uint32_t X, int z4, uint32_t sp, uint32_t n,
                                                     uint32_t init, Rd&& rd) {
     const uint32_t W = (n + 15) >> 4, h0 = 16 * W - n;
@@ -786,7 +809,7 @@ __device__ __forceinline__ uint32_t lane_record_end(const uint32_t* lds, uint32_
         v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
         v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
         carry = 0u;
-        step4<8>(lds, X, a0, a1, a2, a3, v);
+        step4<SMODE>(lds, X, a0, a1, a2, a3, v);
     }
     return ~lane_fold_at(lds, z4, a0, a1, a2, a3);
 }

@@ -1045,7 +1045,7 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) 
 // chain of three memory latencies and the steps: DESIGN.md §8a), plain scalars across the loop.
 // END: the records' windows aligned to their ends (lane_record_end: no head or tail steps);
 // the stage then holds the extent 16 bytes in, after a slack the first window may read.
-template <bool END>
+template <bool END, int SMODE = 24>  // SMODE 8: the 16-copy image in plain lane order (2-way conflicts; A/B)
 __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     constexpr uint32_t kLead = END ? 16u : 0u, kFit = END ? kStgBytes - 32u : kStgBytes;
     uint64_t n_rec = A.n_rec;
@@ -1128,7 +1128,7 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
             const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
             if (n) {
                 if (fits && END && n >= 4)
-                    res = lane_record_end(lds, X, kStgZ4, kLead + (uint32_t)(p - lo), n, ini, [&](uint32_t q) {
+                    res = lane_record_end<SMODE>(lds, X, kStgZ4, kLead + (uint32_t)(p - lo), n, ini, [&](uint32_t q) {
                         return *reinterpret_cast<const uint32_t*>(stage + 4u * q);
                     });
                 else if (fits)
@@ -1536,6 +1536,8 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL(k_ragged_staged_pipe<false>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else if (v == 20)  // ... with the windows aligned to the record ends (no head / tail steps)
         hipLaunchKernelGGL(k_ragged_staged_pipe<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (v == 22)  // variant 20 with the plain lane order of the 16-copy image (2-way bank conflicts)
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 8>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else if (v == 21)  // ... and two lanes per record (32 records per wave, 14 waves per CU)
         hipLaunchKernelGGL(k_ragged_staged_pair, dim3(grid_blocks), dim3(kPairWaves * 64), 0, s, a);
     else if (v == 16)  // timing only: staging copy without the CRC steps / 17 the steps without the copy / 18 neither

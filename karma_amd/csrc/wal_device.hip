@@ -364,7 +364,7 @@ __device__ uint32_t crc_list(const CrcCtx& C, const Seg& S, const WalArgs& A, ui
             st = KB_READ(A.cand_crc, slot0 + i, total, kKbCand);
         }
         const uint8_t* p = v ? S.img + rec + 8 : C.safe;
-        const uint32_t res = direct_batch<4, 4, true, 8>(C.lds, C.X, C.safe, p, n, 0u, v);
+        const uint32_t res = direct_batch<4, 4, true, 24>(C.lds, C.X, C.safe, p, n, 0u, v);
         const uint64_t bm = __ballot(v && n != 0 && res != st);  // size 0: checked by the walk
         if (bm) return i0 + (uint32_t)__builtin_ctzll(bm);
     }
