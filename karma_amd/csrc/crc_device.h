@@ -94,6 +94,38 @@ __device__ __forceinline__ uint32_t stride_step16s(const uint32_t* lds, uint32_t
     return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
 }
 
+// The 8-copy image (32 KiB: entry e, table t, copy c at byte e<<7 | t<<5 | c<<2): lane L reads
+// copy L & 7, and the four lane octets of each 32-lane half take the tables in rotated order
+// (octet q: t = (i + q) & 3 in lookup i), so each ds_read_b32 touches 32 distinct bank columns
+// (t<<3 | c).  The index needs a bit-field extract and a shift-or (the 16- and 32-copy images'
+// 256-byte rows take one v_perm_b32), for half the LDS of the 16-copy image.
+constexpr int kRep8Words = 8192;
+__device__ __forceinline__ uint32_t stride_step8(const uint32_t* lds, uint32_t acc, uint32_t w) {
+    const uint32_t q = (threadIdx.x >> 3) & 3u, c4 = (threadIdx.x & 7u) << 2;
+    uint32_t r = w;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t t = (i + q) & 3u;
+        r ^= lds_at_byte(lds, (__builtin_amdgcn_ubfe(acc, 8u * t, 8u) << 7) | (t << 5) | c4);
+    }
+    return r;
+}
+template <int THREADS>
+__device__ __forceinline__ void load_rep8_stride(uint32_t* lds, const uint32_t* __restrict__ blob) {
+    constexpr int NV = kRep8Words / 4;  // vector v: words 4v..4v+3 = copies 4(v&1)..+3 of (e, t)
+    constexpr int IT = (NV + THREADS - 1) / THREADS;
+    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int v = (int)threadIdx.x + q * THREADS;
+        if (v < NV) {
+            const int e = v >> 3, t = (v >> 1) & 3;
+            const uint32_t x = *(const __attribute__((address_space(1))) uint32_t*)(blob + kBlobStride + t * 256 + e);
+            l4[v] = u32x4{x, x, x, x};
+        }
+    }
+}
+
 // Z(x) for a map stored as four plain 256-entry tables at word `base`.
 __device__ __forceinline__ uint32_t zmap(const uint32_t* lds, int base, uint32_t x) {
     return lds[base + (x & 255u)] ^ lds[base + 256 + ((x >> 8) & 255u)] ^ lds[base + 512 + ((x >> 16) & 255u)] ^
@@ -233,6 +265,13 @@ __device__ __forceinline__ uint32_t tail_register(const uint32_t* lds, int z4, i
 template <int MODE = 0>
 __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
                                       uint32_t& a3, const u32x4& v) {
+    if constexpr ((MODE & 32) != 0) {  // the 8-copy image (stride_step8)
+        a0 = stride_step8(lds, a0, v.x);
+        a1 = stride_step8(lds, a1, v.y);
+        a2 = stride_step8(lds, a2, v.z);
+        a3 = stride_step8(lds, a3, v.w);
+        return;
+    }
     if constexpr ((MODE & 24) == 24) {
         a0 = stride_step16s(lds, X, a0, v.x);
         a1 = stride_step16s(lds, X, a1, v.y);

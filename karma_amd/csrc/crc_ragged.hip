@@ -1045,8 +1045,11 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) 
 // chain of three memory latencies and the steps: DESIGN.md §8a), plain scalars across the loop.
 // END: the records' windows aligned to their ends (lane_record_end: no head or tail steps);
 // the stage then holds the extent 16 bytes in, after a slack the first window may read.
-template <bool END, int SMODE = 24>  // SMODE 8: the 16-copy image in plain lane order (2-way conflicts; A/B)
-__global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArgs A) {
+template <bool END, int SMODE = 24, int NW = kStgWaves>  // SMODE 8: the 16-copy image in plain lane order
+                                                         // (2-way conflicts); NW < kStgWaves: fewer waves (A/B)
+__global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
+    // SMODE 32: the 8-copy stride image (32 KiB), so more waves fit beside their stages
+    constexpr int TW = (SMODE & 32) ? kRep8Words : kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
     constexpr uint32_t kLead = END ? 16u : 0u, kFit = END ? kStgBytes - 32u : kStgBytes;
     uint64_t n_rec = A.n_rec;
     if (A.n_dev) {
@@ -1054,14 +1057,20 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
         n_rec = *A.n_dev;
     }
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kStgLdsWords];
-    load_stg_tables<kStgWaves * 64>(lds, A.blob);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BUF + NW * (int)(kStgBytes / 4)];
+    if constexpr ((SMODE & 32) != 0) {
+        load_rep8_stride<NW * 64>(lds, A.blob);
+        copy_to_lds<1024, NW * 64>(lds + Z4, A.blob + kBlobZ4);
+        copy_to_lds<256, NW * 64>(lds + T8, A.blob + kBlobT8);
+    } else {
+        load_stg_tables<NW * 64>(lds, A.blob);
+    }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t X = lane_const16();
-    uint8_t* stage = reinterpret_cast<uint8_t*>(lds + kStgBuf) + wave * kStgBytes;
-    const uint64_t step = (uint64_t)gridDim.x * kStgWaves * 64;
-    uint64_t base = ((uint64_t)blockIdx.x * kStgWaves + wave) * 64;
+    uint8_t* stage = reinterpret_cast<uint8_t*>(lds + BUF) + wave * kStgBytes;
+    const uint64_t step = (uint64_t)gridDim.x * NW * 64;
+    uint64_t base = ((uint64_t)blockIdx.x * NW + wave) * 64;
     if (base >= n_rec) return;
     auto ld_meta = [&](uint64_t b, uint64_t& o, uint32_t& n, uint32_t& ini) {
         const uint64_t ri = b + lane;
@@ -1128,15 +1137,15 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
             const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
             if (n) {
                 if (fits && END && n >= 4)
-                    res = lane_record_end<SMODE>(lds, X, kStgZ4, kLead + (uint32_t)(p - lo), n, ini, [&](uint32_t q) {
+                    res = lane_record_end<SMODE>(lds, X, Z4, kLead + (uint32_t)(p - lo), n, ini, [&](uint32_t q) {
                         return *reinterpret_cast<const uint32_t*>(stage + 4u * q);
                     });
                 else if (fits)
-                    res = lane_record(lds, X, kStgZ4, kStgT8, p, n, ini, [&](uintptr_t a) {
+                    res = lane_record(lds, X, Z4, T8, p, n, ini, [&](uintptr_t a) {
                         return *reinterpret_cast<const u32x4*>(stage + kLead + (uint32_t)(a - lo));
                     });
                 else
-                    res = lane_record(lds, X, kStgZ4, kStgT8, p, n, ini,
+                    res = lane_record(lds, X, Z4, T8, p, n, ini,
                                       [&](uintptr_t a) { return ld16(reinterpret_cast<const uint8_t*>(a)); });
             }
             A.out[ri] = res;
@@ -1538,6 +1547,14 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL(k_ragged_staged_pipe<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else if (v == 22)  // variant 20 with the plain lane order of the 16-copy image (2-way bank conflicts)
         hipLaunchKernelGGL((k_ragged_staged_pipe<true, 8>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (v == 23)  // variant 20 with 4 / 5 waves per CU (LDS left for other kernels' workgroups)
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 24, 4>), dim3(grid_blocks), dim3(4 * 64), 0, s, a);
+    else if (v == 24)
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 24, 5>), dim3(grid_blocks), dim3(5 * 64), 0, s, a);
+    else if (v == 25)  // variant 20 on the 8-copy stride image, 10 / 9 waves per CU
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 32, 10>), dim3(grid_blocks), dim3(10 * 64), 0, s, a);
+    else if (v == 26)
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 32, 9>), dim3(grid_blocks), dim3(9 * 64), 0, s, a);
     else if (v == 21)  // ... and two lanes per record (32 records per wave, 14 waves per CU)
         hipLaunchKernelGGL(k_ragged_staged_pair, dim3(grid_blocks), dim3(kPairWaves * 64), 0, s, a);
     else if (v == 16)  // timing only: staging copy without the CRC steps / 17 the steps without the copy / 18 neither

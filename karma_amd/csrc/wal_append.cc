@@ -33,6 +33,7 @@
 #include <string>
 #include <vector>
 
+#include "ab.h"
 #include "engine.h"
 #include "host_stage.h"
 #include "host_trace.h"
@@ -403,7 +404,9 @@ extern "C" int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_o
     uint8_t* wal = static_cast<uint8_t*>(h_wal);
     uint64_t cur = *h_cursor;
     size_t done = 0;
-    while (done < n) {  // passes of at most kCallBytes of payload (at least one record)
+    // (the tools build's KARMA_APPEND_CALL_BYTES lowers the pass size, so tests cross passes)
+    const uint64_t call_bytes = (uint64_t)KARMA_AB_KNOB("KARMA_APPEND_CALL_BYTES", (long)kCallBytes);
+    while (done < n) {  // passes of at most call_bytes of payload (at least one record)
         size_t m = 1;
         uint64_t bytes = h_len[done];
         uint32_t max_len = h_len[done];
@@ -418,12 +421,12 @@ extern "C" int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_o
                 s += l[k];
                 mx = std::max(mx, l[k]);
             }
-            if (bytes + s > kCallBytes) break;
+            if (bytes + s > call_bytes) break;
             bytes += s;
             max_len = std::max(max_len, mx);
             m += kSumRun;
         }
-        for (; done + m < n && bytes + h_len[done + m] <= kCallBytes; ++m) {
+        for (; done + m < n && bytes + h_len[done + m] <= call_bytes; ++m) {
             bytes += h_len[done + m];
             max_len = std::max(max_len, h_len[done + m]);
         }

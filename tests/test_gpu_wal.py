@@ -108,6 +108,29 @@ def test_append_matches_reference_framing(lib):
     assert wal.tobytes() == bytes(model)
 
 
+@pytest.mark.parametrize("call_bytes", [1, 20000, 1 << 20])
+def test_append_in_several_passes_matches_reference_framing(call_bytes, monkeypatch):
+    """A batch whose payload exceeds one pass (kCallBytes, 1 GiB in the shipped library; lowered
+    here through the tools build's KARMA_APPEND_CALL_BYTES): the cursor, the record offsets and
+    the image bytes carry across passes exactly as one pass over the model, including an image
+    that fills up during a later pass."""
+    monkeypatch.setenv("KARMA_APPEND_CALL_BYTES", str(call_bytes))
+    ab = _lib.load(_lib.AB_LIB_PATH)
+    src, offs, lens = _payloads(5, 4000, 1, 3000)
+    for nseg in (200, 17):  # 17 segments: the image fills up after a few passes
+        wal = np.zeros(nseg * SEG, np.uint8)
+        for cursor in (0, 5 * SEG + 1000):
+            if cursor:  # a writer resuming from a checkpoint: the image before the cursor as framed
+                wal[:] = 0
+            cur, rec = _append(ab, src, offs, lens, wal, cursor=cursor)
+            model = bytearray(nseg * SEG)
+            payloads = [src[int(o): int(o) + int(n)] for o, n in zip(offs, lens)]
+            mcur, mrec = wal_model.append(payloads, model, SEG, cursor)
+            assert cur == mcur and list(rec) == mrec, (call_bytes, nseg, cursor)
+            assert wal.tobytes() == bytes(model), (call_bytes, nseg, cursor)
+            assert (len(rec) == lens.size) == (nseg == 200)
+
+
 @pytest.mark.parametrize("mix", ["small", "mixed", "large"])
 def test_append_into_pinned_image_matches_pageable(lib, mix):
     """A page-locked image (a writer's own buffer): append gives the pageable image's bytes and the
