@@ -298,6 +298,8 @@ struct WalArgs {
     WalSummary* sum;           // k_wal_plan's result
     uint64_t wal_end;          // WAL offset of the image end
     const uint32_t* crc_blob;  // k_wal_walk_crc: the quad blob (its tables' LDS image; empty units' address)
+    uint32_t direct_streak;    // the walkers read headers straight from global memory after a fast round
+                               // of at least this many headers (0: tiles only; wal.cc kDirectStreak)
     uintptr_t kb_lo, kb_hi;    // bounds build: the image's allocation (the inline CRC loads)
 };
 constexpr uint32_t kWalkTile = 4096;  // the one-wave walker's LDS tile (wal_device.hip)

@@ -143,6 +143,8 @@ struct DevBuf {
     }
 };
 
+// Walkers switch to direct header rounds after a fast round of this many headers.
+constexpr uint32_t kDirectStreak = 8;
 constexpr uint32_t kSmallRecordMax = 1024;      // payloads up to this take the one-record-per-group batch
 constexpr uint64_t kDevicePlanMax = uint64_t(256) << 20;  // images up to this: the device-planned path
 struct ReplayCtx {
@@ -295,6 +297,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     A.nwork = nwork;
     A.seg_bytes = seg_bytes;
     A.first_pos = start - base0;
+    A.direct_streak = (uint32_t)KARMA_AB_KNOB("KARMA_WALK_DIRECT", kDirectStreak);
     const int batch = tuning ? tuning->crc_batch : KARMA_WAL_CRC_PLAN;
     // Images up to kDevicePlanMax take a device-planned path (one host round trip): with the
     // default plan the walkers checksum the candidates inline (k_wal_walk_crc); the tools

@@ -426,6 +426,7 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
     };
     auto push = [&](uint32_t p, uint32_t n, uint32_t c) { push_many(p, n, c, 1u); };  // uniform values
     uint32_t g = 0;  // the guessed header stride: 8 + the last record's size
+    uint32_t streak = 0;  // headers the last fast round took (direct rounds from A.direct_streak on)
     const uint32_t tlim = hi < seg ? hi : seg;  // tiles from here on hold no header before hi
     // Sequential headers go through 4 KiB tiles with the next one prefetched; after a
     // jump past the prefetched tile the walk reads a 1 KiB window at the header, and
@@ -440,6 +441,41 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
         const bool more = tsz == kWTile && (uint64_t)t0 + kWTile < tlim;
         if (more) wtile_fetch(S, lane, t0 + kWTile, r);  // in flight while the walk runs
         uint32_t done = 0;
+        // Direct rounds: while the records repeat their size (the last fast round took at least
+        // A.direct_streak headers), lane j reads the header at pos + j*g straight from global
+        // memory -- 64 headers per memory latency instead of a 4 KiB tile per latency, and the
+        // payload bytes between the headers are not read by the walk at all.  A size change keeps
+        // them going while rounds stay long; a header the fast path does not take (size 0,
+        // padding, a bad type or length, the sub-range end) hands pos back to the tile path.
+        if (A.direct_streak) {
+            const uint32_t dend = hi < seg - 7 ? hi : seg - 7;  // a header at pos needs pos + 8 <= seg
+            while (streak >= A.direct_streak && g >= 8 && pos < dend) {
+                const uint32_t pj = pos + lane * g;  // < 2^32: pos < 2^31, 63 g < 2^30
+                const bool inwin = pj < dend;
+                const uint32_t hp = inwin ? pj : pos;
+                const uint8_t* h = seg_at(S, hp, 8);
+                const uint32_t c_ = uint32_t(h[0]) | uint32_t(h[1]) << 8 | uint32_t(h[2]) << 16 | uint32_t(h[3]) << 24;
+                const uint32_t s_ = uint32_t(h[4]) | uint32_t(h[5]) << 8 | uint32_t(h[6]) << 16 | uint32_t(h[7]) << 24;
+                const uint32_t nx = hp + 8 + (s_ >> 8);
+                const bool ok = inwin && (s_ & 0xffu) == 0 && s_ >= 256u && nx <= seg;
+                const uint64_t brk = __ballot(!(ok && nx == pj + g));
+                const uint32_t f = brk ? (uint32_t)__builtin_ctzll(brk) : 64u;
+                const uint32_t okf = f < 64 ? __builtin_amdgcn_readlane((uint32_t)ok, f) : 0u;
+                const uint32_t na = f + okf;
+                if (na) push_many(hp, s_ >> 8, c_, na);
+                streak = na;
+                if (f == 64) {
+                    pos = __builtin_amdgcn_readlane(nx, 63);
+                } else if (okf) {
+                    pos = __builtin_amdgcn_readlane(nx, f);
+                    g = __builtin_amdgcn_readlane(s_ >> 8, f) + 8;
+                } else {  // lane f's header: the tile path takes it (or the sub-range ends there)
+                    pos += f * g;
+                    streak = 0;
+                    break;
+                }
+            }
+        }
         {
             const uint32_t tend = t0 + tsz < hi ? t0 + tsz : hi, lim = seg - 8;
             const uint32_t fend = lim + 1 < tend ? lim + 1 : tend;  // a header at pos needs pos < fend
@@ -467,6 +503,7 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
                     const uint32_t okf = f < 64 ? __builtin_amdgcn_readlane((uint32_t)ok, f) : 0u;
                     const uint32_t na = f + okf;  // lane f's header is real too (lanes < f led to it)
                     if (na) push_many(hp, s_ >> 8, c_, na);
+                    streak = na;
                     if (f == 64) {
                         pos = __builtin_amdgcn_readlane(nx, 63);
                     } else if (okf) {

@@ -133,13 +133,15 @@ struct WalkEnd {
 // walk_range (wal_device.hip): the 64-entry runs are flushed lane by lane.  The fast path
 // reads a round of 64 headers, lane j at pos + j * g (g: the last record's stride), and takes
 // the lanes up to the first one whose next header is not the next lane's position.
+constexpr uint32_t kDirectStreak = 8;  // wal.cc: direct header rounds after a fast round this long
+
 WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List& out) {
     const uint32_t seg = S.seg;
     WalkEnd E;
     E.stop = seg;
     E.pos = pos;
     if ((uint64_t)pos + 8 > seg || pos >= hi) return E;
-    uint32_t run[64][3], k = 0, g = 0;
+    uint32_t run[64][3], k = 0, g = 0, streak = 0;
     auto push = [&](uint32_t p, uint32_t n, uint32_t c) {
         E.max_len = std::max(E.max_len, n);
         run[k][0] = p, run[k][1] = n, run[k][2] = c;
@@ -157,6 +159,45 @@ WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List&
         const bool more = tsz == kWTile && (uint64_t)t0 + kWTile < tlim;
         if (more) tile_fetch(next, S, t0 + kWTile);
         uint32_t done = 0;
+        {  // direct rounds (kDirectStreak, wal.cc): 64 headers read from the segment, not the tile
+            const uint32_t dend = hi < seg - 7 ? hi : seg - 7;
+            while (streak >= kDirectStreak && g >= 8 && pos < dend) {
+                uint32_t hc[64], hs[64], hn[64];
+                bool ok[64], chain[64];
+                for (uint32_t lane = 0; lane < 64; ++lane) {
+                    const uint32_t pj = pos + lane * g;
+                    const bool inwin = pj < dend;
+                    const uint32_t hp = inwin ? pj : pos;
+                    uint8_t h[8];
+                    for (uint32_t b = 0; b < 8; ++b) h[b] = rd(S, hp + b);  // checked: inside the segment
+                    hc[lane] = uint32_t(h[0]) | uint32_t(h[1]) << 8 | uint32_t(h[2]) << 16 | uint32_t(h[3]) << 24;
+                    hs[lane] = uint32_t(h[4]) | uint32_t(h[5]) << 8 | uint32_t(h[6]) << 16 | uint32_t(h[7]) << 24;
+                    hn[lane] = hp + 8 + (hs[lane] >> 8);
+                    ok[lane] = inwin && (hs[lane] & 0xffu) == 0 && hs[lane] >= 256u && hn[lane] <= seg;
+                    chain[lane] = ok[lane] && hn[lane] == pj + g;
+                }
+                uint32_t f = 64;
+                for (uint32_t lane = 0; lane < 64; ++lane)
+                    if (!chain[lane]) {
+                        f = lane;
+                        break;
+                    }
+                const bool okf = f < 64 && ok[f];
+                const uint32_t na = f + (okf ? 1 : 0);
+                for (uint32_t j = 0; j < na; ++j) push(pos + j * g, hs[j] >> 8, hc[j]);
+                streak = na;
+                if (f == 64) {
+                    pos = hn[63];
+                } else if (okf) {
+                    pos = hn[f];
+                    g = (hs[f] >> 8) + 8;
+                } else {
+                    pos += f * g;
+                    streak = 0;
+                    break;
+                }
+            }
+        }
         {
             const uint32_t tend = t0 + tsz < hi ? t0 + tsz : hi, lim = seg - 8;
             const uint32_t fend = lim + 1 < tend ? lim + 1 : tend;
@@ -184,6 +225,7 @@ WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List&
                     const bool okf = f < 64 && ok[f];
                     const uint32_t na = f + (okf ? 1 : 0);
                     for (uint32_t j = 0; j < na; ++j) push(pos + j * g, hs[j] >> 8, hc[j]);
+                    streak = na;
                     if (f == 64) {
                         pos = hn[63];
                     } else if (okf) {

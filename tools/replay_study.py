@@ -16,6 +16,8 @@ copy for each variant in interleaved rounds (same process, same image):
     direct2              tools build, KARMA_DIRECT_VARIANT=5 (k_ragged_direct4<2>: pairs of lanes)
     units                the shipped library, ragged plan instead of the direct kernel (crc_batch)
     ab                   tools build, default plan
+    nodirect             tools build, KARMA_WALK_DIRECT=0: the walkers read tiles only (no direct header rounds)
+    direct=<k>           tools build, direct header rounds after a fast round of k headers
     inline               the shipped library, KARMA_WAL_CRC_INLINE: the CRCs inside the walk (k_wal_walk_crc)
     listcrc              tools build, KARMA_WAL_CRC_INLINE + KARMA_WAL_LIST_CRC=1: the walk, then the walkers' lists checksummed by
                          the LDS-staged one-record-per-lane kernel (k_wal_list_crc)
@@ -113,6 +115,10 @@ def main():
             variants[v] = (L, 0, 4, None)
         elif v == "sepdirect4":  # the separate path with the 4-lane small-record kernel only (round 2's)
             variants[v] = (AB, 0, 3, ("KARMA_SMALL_STAGED", "0"))
+        elif v == "nodirect":  # the walkers on tiles only (no direct header rounds)
+            variants[v] = (AB, 0, 0, ("KARMA_WALK_DIRECT", "0"))
+        elif v.startswith("direct="):  # direct header rounds after a fast round of this many headers
+            variants[v] = (AB, 0, 0, ("KARMA_WALK_DIRECT", v[7:]))
         elif v == "ab":  # the tools build's default plan (same-library reference for listcrc)
             variants[v] = (AB, 0, 0, None)
         elif v == "units":
@@ -136,7 +142,7 @@ def main():
 
     for r in range(a.rounds):
         for v, (lib, sub, batch, env) in variants.items():
-            for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC", "KARMA_SMALL_STAGED"):
+            for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC", "KARMA_SMALL_STAGED", "KARMA_WALK_DIRECT"):
                 os.environ.pop(k, None)
             if env:
                 os.environ[env[0]] = env[1]
