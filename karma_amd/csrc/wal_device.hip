@@ -447,15 +447,25 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
         // payload bytes between the headers are not read by the walk at all.  A size change keeps
         // them going while rounds stay long; a header the fast path does not take (size 0,
         // padding, a bad type or length, the sub-range end) hands pos back to the tile path.
-        if (A.direct_streak) {
+        if (A.direct_streak && streak >= A.direct_streak && g >= 8) {
             const uint32_t dend = hi < seg - 7 ? hi : seg - 7;  // a header at pos needs pos + 8 <= seg
-            while (streak >= A.direct_streak && g >= 8 && pos < dend) {
-                const uint32_t pj = pos + lane * g;  // < 2^32: pos < 2^31, 63 g < 2^30
-                const bool inwin = pj < dend;
+            // lane j's header of the round at base b: (crc, size/type), its position and window
+            auto hdr = [&](uint32_t b, uint32_t& c, uint32_t& st, uint32_t& pj, bool& inwin) {
+                pj = b + lane * g;  // < 2^32: b < 2^31 + 2^30, 63 g < 2^30
+                inwin = pj < dend;
+                const uint8_t* h = seg_at(S, inwin ? pj : pos, 8);
+                c = uint32_t(h[0]) | uint32_t(h[1]) << 8 | uint32_t(h[2]) << 16 | uint32_t(h[3]) << 24;
+                st = uint32_t(h[4]) | uint32_t(h[5]) << 8 | uint32_t(h[6]) << 16 | uint32_t(h[7]) << 24;
+            };
+            uint32_t c_, s_, pj;
+            bool inwin;
+            hdr(pos, c_, s_, pj, inwin);
+            while (pos < dend) {
+                // the next round's headers, assuming this one chains all 64 lanes at stride g
+                uint32_t c2, s2, pj2;
+                bool inwin2;
+                hdr(pos + 64 * g, c2, s2, pj2, inwin2);
                 const uint32_t hp = inwin ? pj : pos;
-                const uint8_t* h = seg_at(S, hp, 8);
-                const uint32_t c_ = uint32_t(h[0]) | uint32_t(h[1]) << 8 | uint32_t(h[2]) << 16 | uint32_t(h[3]) << 24;
-                const uint32_t s_ = uint32_t(h[4]) | uint32_t(h[5]) << 8 | uint32_t(h[6]) << 16 | uint32_t(h[7]) << 24;
                 const uint32_t nx = hp + 8 + (s_ >> 8);
                 const bool ok = inwin && (s_ & 0xffu) == 0 && s_ >= 256u && nx <= seg;
                 const uint64_t brk = __ballot(!(ok && nx == pj + g));
@@ -464,16 +474,23 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
                 const uint32_t na = f + okf;
                 if (na) push_many(hp, s_ >> 8, c_, na);
                 streak = na;
-                if (f == 64) {
+                if (f == 64) {  // pos + 64 g: the round already in flight is the next one
                     pos = __builtin_amdgcn_readlane(nx, 63);
-                } else if (okf) {
-                    pos = __builtin_amdgcn_readlane(nx, f);
-                    g = __builtin_amdgcn_readlane(s_ >> 8, f) + 8;
-                } else {  // lane f's header: the tile path takes it (or the sub-range ends there)
+                    c_ = c2;
+                    s_ = s2;
+                    pj = pj2;
+                    inwin = inwin2;
+                    continue;
+                }
+                if (!okf) {  // lane f's header: the tile path takes it (or the sub-range ends there)
                     pos += f * g;
                     streak = 0;
                     break;
                 }
+                pos = __builtin_amdgcn_readlane(nx, f);  // a size change: the round at the new stride
+                g = __builtin_amdgcn_readlane(s_ >> 8, f) + 8;
+                if (streak < A.direct_streak || pos >= dend) break;
+                hdr(pos, c_, s_, pj, inwin);
             }
         }
         {

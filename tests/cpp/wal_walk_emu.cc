@@ -182,6 +182,11 @@ WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List&
                         f = lane;
                         break;
                     }
+                for (uint32_t lane = 0; lane < 64; ++lane) {  // the next round, read speculatively
+                    const uint32_t pj2 = pos + (64 + lane) * g;
+                    const uint32_t hp2 = pj2 < dend ? pj2 : pos;
+                    for (uint32_t b = 0; b < 8; ++b) (void)rd(S, hp2 + b);
+                }
                 const bool okf = f < 64 && ok[f];
                 const uint32_t na = f + (okf ? 1 : 0);
                 for (uint32_t j = 0; j < na; ++j) push(pos + j * g, hs[j] >> 8, hc[j]);
@@ -191,6 +196,7 @@ WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List&
                 } else if (okf) {
                     pos = hn[f];
                     g = (hs[f] >> 8) + 8;
+                    if (streak < kDirectStreak) break;
                 } else {
                     pos += f * g;
                     streak = 0;
