@@ -850,7 +850,14 @@ __device__ __forceinline__ uint32_t lane_record_end(const uint32_t* lds, uint32_
         carry = 0u;
         step4<SMODE>(lds, X, a0, a1, a2, a3, v);
     }
-    return ~lane_fold_at(lds, z4, a0, a1, a2, a3);
+    // the STEP4W fold Z4(a3 ^ Z4(a2 ^ Z4(a1 ^ Z4(a0)))) as Z16(a0) ^ Z4(a3 ^ Z4(a2 ^ Z4(a1))): Z16 is
+    // the stride map, read from the replicated image beside the three-step chain
+    const uint32_t z16 = (SMODE & 32) ? stride_step8(lds, a0, 0u)
+                         : (SMODE & 16) ? stride_step16s(lds, X, a0, 0u)
+                                        : stride_step16(lds, X, a0, 0u);
+    uint32_t c = zmap(lds, z4, a1);
+    c = zmap(lds, z4, c ^ a2);
+    return ~(z16 ^ zmap(lds, z4, c ^ a3));
 }
 
 // LDS writes of a wave visible to its own later LDS reads (and its reads done before its
