@@ -654,11 +654,11 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
         a.init_scalar = init;
         a.out = d_out;
         const long dv = KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0);  // tools build: the other kernels
-        a.blob = dv == 1 || dv == 2 ? L.ds->blob : dv == 3 || (dv >= 14 && dv <= 26 && dv != 21) ? L.ds->lane_blob : dv == 5 || dv == 21 ? L.ds->pair_blob : L.ds->quad_blob;
+        a.blob = dv == 1 || dv == 2 ? L.ds->blob : dv == 3 || (dv >= 14 && dv <= 27 && dv != 21) ? L.ds->lane_blob : dv == 5 || dv == 21 ? L.ds->pair_blob : L.ds->quad_blob;
         bind_arena_bounds(a);
         // a wave takes 64 records (lanes variant: a workgroup 1024): no more workgroups than
         // the batch fills (each one loads the 145 KiB table image into its LDS first)
-        const uint64_t per_block = dv == 3 ? kBlockThreads : dv == 23 ? 64 * 4 : dv == 24 ? 64 * 5 : dv == 25 ? 64 * 10 : dv == 26 ? 64 * 9 : dv >= 14 && dv <= 22 && dv != 21 ? 64 * kStgWaves : dv == 21 ? 32 * 14 : 64 * kWavesPerBlock;
+        const uint64_t per_block = dv == 3 ? kBlockThreads : dv == 23 ? 64 * 4 : dv == 24 ? 64 * 5 : dv == 25 ? 64 * 10 : dv == 26 ? 64 * 9 : (dv >= 14 && dv <= 22 && dv != 21) || dv == 27 ? 64 * kStgWaves : dv == 21 ? 32 * 14 : 64 * kWavesPerBlock;
         const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_rec, per_block));
         KARMA_HIP(launch_ragged_direct(a, (int)blocks, (hipStream_t)stream));
         return KARMA_OK;

@@ -1045,19 +1045,24 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged(RaggedArgs A) 
 // chain of three memory latencies and the steps: DESIGN.md §8a), plain scalars across the loop.
 // END: the records' windows aligned to their ends (lane_record_end: no head or tail steps);
 // the stage then holds the extent 16 bytes in, after a slack the first window may read.
-template <bool END, int SMODE = 24, int NW = kStgWaves>  // SMODE 8: the 16-copy image in plain lane order
+// SKEW (with END): the stage is bank-skewed, one pad dword after every 128 bytes (dword q at
+// q + q / 32), so records whose stride is a multiple of 32 bytes (120-B payloads + 8-B headers
+// put every lane on one bank) read their windows without conflicts; stores go out as dwords.
+template <bool END, int SMODE = 24, int NW = kStgWaves, bool SKEW = true>  // SMODE 8: the 16-copy image in plain lane order
                                                          // (2-way conflicts); NW < kStgWaves: fewer waves (A/B)
 __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     // SMODE 32: the 8-copy stride image (32 KiB), so more waves fit beside their stages
     constexpr int TW = (SMODE & 32) ? kRep8Words : kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
     constexpr uint32_t kLead = END ? 16u : 0u, kFit = END ? kStgBytes - 32u : kStgBytes;
+    constexpr bool SK = END && SKEW;
+    constexpr uint32_t kStride = SK ? kStgBytes + kStgBytes / 32 : kStgBytes;  // bytes per wave's stage
     uint64_t n_rec = A.n_rec;
     if (A.n_dev) {
         if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
         n_rec = *A.n_dev;
     }
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[BUF + NW * (int)(kStgBytes / 4)];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BUF + NW * (int)(kStride / 4)];
     if constexpr ((SMODE & 32) != 0) {
         load_rep8_stride<NW * 64>(lds, A.blob);
         copy_to_lds<1024, NW * 64>(lds + Z4, A.blob + kBlobZ4);
@@ -1068,7 +1073,8 @@ __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t X = lane_const16();
-    uint8_t* stage = reinterpret_cast<uint8_t*>(lds + BUF) + wave * kStgBytes;
+    uint8_t* stage = reinterpret_cast<uint8_t*>(lds + BUF) + wave * kStride;
+    uint32_t* stage32 = reinterpret_cast<uint32_t*>(stage);
     const uint64_t step = (uint64_t)gridDim.x * NW * 64;
     uint64_t base = ((uint64_t)blockIdx.x * NW + wave) * 64;
     if (base >= n_rec) return;
@@ -1115,7 +1121,15 @@ __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
             for (int q = 0; q < kStgVecs; ++q) {
                 uint32_t at = kLead + 16u * (lane + 64u * q);
                 at = at >= kStgBytes ? 0u : at;  // (END) the last slot, past any extent, into the slack
-                *reinterpret_cast<u32x4*>(stage + at) = v[q];
+                if constexpr (SK) {  // 4 dwords in one 128-byte line: contiguous after the skew
+                    const uint32_t d = at / 4 + at / 128;
+                    stage32[d] = v[q].x;
+                    stage32[d + 1] = v[q].y;
+                    stage32[d + 2] = v[q].z;
+                    stage32[d + 3] = v[q].w;
+                } else {
+                    *reinterpret_cast<u32x4*>(stage + at) = v[q];
+                }
             }
             wave_lds_sync();
         }
@@ -1138,11 +1152,17 @@ __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
             if (n) {
                 if (fits && END && n >= 4)
                     res = lane_record_end<SMODE>(lds, X, Z4, kLead + (uint32_t)(p - lo), n, ini, [&](uint32_t q) {
+                        if constexpr (SK) return stage32[q + (q >> 5)];
                         return *reinterpret_cast<const uint32_t*>(stage + 4u * q);
                     });
                 else if (fits)
                     res = lane_record(lds, X, Z4, T8, p, n, ini, [&](uintptr_t a) {
-                        return *reinterpret_cast<const u32x4*>(stage + kLead + (uint32_t)(a - lo));
+                        const uint32_t at = kLead + (uint32_t)(a - lo);
+                        if constexpr (SK) {
+                            const uint32_t d = at / 4 + at / 128;
+                            return u32x4{stage32[d], stage32[d + 1], stage32[d + 2], stage32[d + 3]};
+                        }
+                        return *reinterpret_cast<const u32x4*>(stage + at);
                     });
                 else
                     res = lane_record(lds, X, Z4, T8, p, n, ini,
@@ -1551,10 +1571,12 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL((k_ragged_staged_pipe<true, 24, 4>), dim3(grid_blocks), dim3(4 * 64), 0, s, a);
     else if (v == 24)
         hipLaunchKernelGGL((k_ragged_staged_pipe<true, 24, 5>), dim3(grid_blocks), dim3(5 * 64), 0, s, a);
+    else if (v == 27)  // variant 20 without the bank-skewed stage
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 24, kStgWaves, false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else if (v == 25)  // variant 20 on the 8-copy stride image, 10 / 9 waves per CU
-        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 32, 10>), dim3(grid_blocks), dim3(10 * 64), 0, s, a);
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 32, 10, false>), dim3(grid_blocks), dim3(10 * 64), 0, s, a);
     else if (v == 26)
-        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 32, 9>), dim3(grid_blocks), dim3(9 * 64), 0, s, a);
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true, 32, 9, false>), dim3(grid_blocks), dim3(9 * 64), 0, s, a);
     else if (v == 21)  // ... and two lanes per record (32 records per wave, 14 waves per CU)
         hipLaunchKernelGGL(k_ragged_staged_pair, dim3(grid_blocks), dim3(kPairWaves * 64), 0, s, a);
     else if (v == 16)  // timing only: staging copy without the CRC steps / 17 the steps without the copy / 18 neither

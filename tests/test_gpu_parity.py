@@ -562,7 +562,7 @@ def test_ragged_bounded_direct_path(raw, dev, bound, variant, monkeypatch):
 
 
 
-@pytest.mark.parametrize("variant", ["shipped", "4", "14", "15", "19", "20", "21", "22", "25"])
+@pytest.mark.parametrize("variant", ["shipped", "4", "14", "15", "19", "20", "21", "22", "25", "27"])
 @pytest.mark.parametrize("shape", ["wal180", "mixed", "tiny", "unaligned_arena"])
 def test_ragged_bounded_consecutive_records(raw, dev, shape, variant, monkeypatch):
     """Consecutive small records (a WAL image's payloads, a writer's block) through the bounded
