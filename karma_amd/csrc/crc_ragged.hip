@@ -1114,6 +1114,16 @@ __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     ld_meta(base + step, o2, n2, ini2);
     extent(o, n, lo, hi);
     bool fits = hi != 0 && hi - lo <= kFit;
+    // does the batch at (o, n, lo) need the skewed stage?  (banks of the records' first dwords)
+    auto skewed = [&](uint64_t o, uint32_t n, uintptr_t lo) {
+        if constexpr (!SK) return false;
+        const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
+        uint32_t bits = n ? 1u << (((uint32_t)(p - lo) >> 2) & 31u) : 0u;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) bits |= (uint32_t)__shfl_xor((int)bits, d);
+        return __builtin_popcount(__builtin_amdgcn_readfirstlane(bits)) < 24;
+    };
+    bool sk = fits && skewed(o, n, lo);
     if (fits) issue(lo, hi);
     for (;;) {
         if (fits) {
@@ -1121,7 +1131,7 @@ __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
             for (int q = 0; q < kStgVecs; ++q) {
                 uint32_t at = kLead + 16u * (lane + 64u * q);
                 at = at >= kStgBytes ? 0u : at;  // (END) the last slot, past any extent, into the slack
-                if constexpr (SK) {  // 4 dwords in one 128-byte line: contiguous after the skew
+                if (sk) {  // 4 dwords in one 128-byte line: contiguous after the skew
                     const uint32_t d = at / 4 + at / 128;
                     stage32[d] = v[q].x;
                     stage32[d + 1] = v[q].y;
@@ -1136,12 +1146,13 @@ __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
         const uint64_t nb = base + step;
         const bool more = nb < n_rec;
         uintptr_t lo2 = 0, hi2 = 0;
-        bool fits2 = false;
+        bool fits2 = false, sk2 = false;
         uint64_t o3 = 0;
         uint32_t n3 = 0, ini3 = 0;
         if (more) {
             extent(o2, n2, lo2, hi2);
             fits2 = hi2 != 0 && hi2 - lo2 <= kFit;
+            sk2 = fits2 && skewed(o2, n2, lo2);
             if (fits2) issue(lo2, hi2);
             ld_meta(nb + step, o3, n3, ini3);
         }
@@ -1150,15 +1161,17 @@ __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
             uint32_t res = ini;
             const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
             if (n) {
-                if (fits && END && n >= 4)
+                if (fits && END && n >= 4 && sk)
+                    res = lane_record_end<SMODE>(lds, X, Z4, kLead + (uint32_t)(p - lo), n, ini,
+                                                 [&](uint32_t q) { return stage32[q + (q >> 5)]; });
+                else if (fits && END && n >= 4)
                     res = lane_record_end<SMODE>(lds, X, Z4, kLead + (uint32_t)(p - lo), n, ini, [&](uint32_t q) {
-                        if constexpr (SK) return stage32[q + (q >> 5)];
                         return *reinterpret_cast<const uint32_t*>(stage + 4u * q);
                     });
                 else if (fits)
                     res = lane_record(lds, X, Z4, T8, p, n, ini, [&](uintptr_t a) {
                         const uint32_t at = kLead + (uint32_t)(a - lo);
-                        if constexpr (SK) {
+                        if (sk) {
                             const uint32_t d = at / 4 + at / 128;
                             return u32x4{stage32[d], stage32[d + 1], stage32[d + 2], stage32[d + 3]};
                         }
@@ -1176,7 +1189,7 @@ __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
         base = nb;
         o = o2; n = n2; ini = ini2;
         o2 = o3; n2 = n3; ini2 = ini3;
-        lo = lo2; hi = hi2; fits = fits2;
+        lo = lo2; hi = hi2; fits = fits2; sk = sk2;
     }
 }
 
