@@ -1121,7 +1121,7 @@ __global__ __launch_bounds__(NW * 64) void k_ragged_staged_pipe(RaggedArgs A) {
         uint32_t bits = n ? 1u << (((uint32_t)(p - lo) >> 2) & 31u) : 0u;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) bits |= (uint32_t)__shfl_xor((int)bits, d);
-        return __builtin_popcount(__builtin_amdgcn_readfirstlane(bits)) < 24;
+        return __builtin_popcount(__builtin_amdgcn_readfirstlane(bits)) < 12;
     };
     bool sk = fits && skewed(o, n, lo);
     if (fits) issue(lo, hi);
