@@ -447,7 +447,9 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
         // payload bytes between the headers are not read by the walk at all.  A size change keeps
         // them going while rounds stay long; a header the fast path does not take (size 0,
         // padding, a bad type or length, the sub-range end) hands pos back to the tile path.
-        if (A.direct_streak && streak >= A.direct_streak && g >= 8) {
+        // (a round the tile cut short counts as long: records of more than kWTile / direct_streak
+        // bytes never put direct_streak headers in one tile)
+        if (A.direct_streak && g >= 8 && (streak >= A.direct_streak || (streak >= 2 && g * (streak + 1) > kWTile))) {
             const uint32_t dend = hi < seg - 7 ? hi : seg - 7;  // a header at pos needs pos + 8 <= seg
             // lane j's header of the round at base b: (crc, size/type), its position and window
             auto hdr = [&](uint32_t b, uint32_t& c, uint32_t& st, uint32_t& pj, bool& inwin) {
@@ -489,7 +491,7 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
                 }
                 pos = __builtin_amdgcn_readlane(nx, f);  // a size change: the round at the new stride
                 g = __builtin_amdgcn_readlane(s_ >> 8, f) + 8;
-                if (streak < A.direct_streak || pos >= dend) break;
+                if (streak < (g * (streak + 1) > kWTile ? 2u : A.direct_streak) || pos >= dend) break;
                 hdr(pos, c_, s_, pj, inwin);
             }
         }

@@ -161,7 +161,7 @@ WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List&
         uint32_t done = 0;
         {  // direct rounds (kDirectStreak, wal.cc): 64 headers read from the segment, not the tile
             const uint32_t dend = hi < seg - 7 ? hi : seg - 7;
-            while (streak >= kDirectStreak && g >= 8 && pos < dend) {
+            while (g >= 8 && (streak >= kDirectStreak || (streak >= 2 && g * (streak + 1) > kWTile)) && pos < dend) {
                 uint32_t hc[64], hs[64], hn[64];
                 bool ok[64], chain[64];
                 for (uint32_t lane = 0; lane < 64; ++lane) {
@@ -196,7 +196,7 @@ WalkEnd walk_range(Tile& W, const Seg& S, uint32_t pos, uint32_t hi, const List&
                 } else if (okf) {
                     pos = hn[f];
                     g = (hs[f] >> 8) + 8;
-                    if (streak < kDirectStreak) break;
+                    if (streak < (g * (streak + 1) > kWTile ? 2u : kDirectStreak)) break;
                 } else {
                     pos += f * g;
                     streak = 0;

@@ -55,6 +55,8 @@ def main():
     p.add_argument("--variants", default="shipped,direct4,direct_v1,sub=24576,sub=32768,sub=40960")
     p.add_argument("--images", type=int, default=4)
     p.add_argument("--single", action="store_true")
+    p.add_argument("--size", type=int, default=180, help="--mix fixed: payload bytes")
+    p.add_argument("--count", type=int, default=1 << 20, help="--mix fixed: records")
     a = p.parse_args()
     import torch
     import synth
@@ -65,7 +67,7 @@ def main():
         lens = synth.loguniform_lengths(7, count, 64, 65536).astype(np.uint32)
         wal_bytes = ((int(lens.sum()) + 8 * count) // (seg - 65544) + 2) * seg
     else:
-        count, size = 1 << 20, 180
+        count, size = a.count, a.size
         lens = np.full(count, size, dtype=np.uint32)
         wal_bytes = ((count + seg // (size + 8) - 1) // (seg // (size + 8)) + 1) * seg
     offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64)
