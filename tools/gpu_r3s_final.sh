@@ -1,7 +1,7 @@
 # Round-3 session-2 final validation of the committed tree: GPU suite (shipped + bounds builds), smoke,
 # the default bench line and a driver-style bench line.  Each GPU step has its own limit.
 set -e
-O=gpurun_out/r3sfinal4
+O=gpurun_out/r3sfinal5
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=10 > $O/gpu_tests.log 2>&1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --karma-lib abbounds > $O/gpu_tests_bounds.log 2>&1
