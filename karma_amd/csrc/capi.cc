@@ -62,9 +62,8 @@ struct DevState {
     bool ready = false;
     int cu = 0;
     uint32_t* blob = nullptr;       // the streaming kernels' tables (stride 128)
-    uint32_t* lane_blob = nullptr;  // the tools build's k_ragged_lanes tables (stride 16)
+    uint32_t* lane_blob = nullptr;  // the LDS-staged kernel's tables (stride 16: one record per lane)
     uint32_t* quad_blob = nullptr;  // k_ragged_direct4's tables (stride 64)
-    uint32_t* pair_blob = nullptr;  // the tools build's 2-lane groups (stride 32)
     std::map<uint64_t, uint32_t*> comb;  // unit bytes -> combine blob
     std::map<std::pair<uint64_t, uint64_t>, uint32_t*> bcomb;  // (unit bytes, states per thread) -> block blob
 };
@@ -127,11 +126,6 @@ int dev_state(int dev, DevState** out) {
         build_lane_blob(host.data());
         KARMA_HIP(hipMalloc(&d.lane_blob, kBlobWords * sizeof(uint32_t)));
         KARMA_HIP(hipMemcpy(d.lane_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
-#ifdef KARMA_AB
-        build_pair_blob(host.data());
-        KARMA_HIP(hipMalloc(&d.pair_blob, kBlobWords * sizeof(uint32_t)));
-        KARMA_HIP(hipMemcpy(d.pair_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
-#endif
         d.ready = true;
     }
     *out = &d;
@@ -363,7 +357,7 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 
 // ---- ragged records -------------------------------------------------------
 struct RaggedLayout {
-    size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off, tail_off, total;
+    size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off, total;
 };
 
 RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
@@ -375,8 +369,7 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     L.psums_off = L.sums_off + align256(nb * sizeof(uint64_t));
     L.desc_off = L.psums_off + align256(nb * sizeof(uint64_t));
     L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
-    L.tail_off = L.part_off + align256(cap * sizeof(uint32_t));
-    L.total = L.tail_off + align256(cap * sizeof(uint32_t));
+    L.total = L.part_off + align256(cap * sizeof(uint32_t));
     return L;
 }
 
@@ -388,7 +381,6 @@ void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
     a.block_psums = reinterpret_cast<uint64_t*>(b + L.psums_off);
     a.desc = reinterpret_cast<UnitDesc*>(b + L.desc_off);
     a.partial = reinterpret_cast<uint32_t*>(b + L.part_off);
-    a.tailc = reinterpret_cast<uint32_t*>(b + L.tail_off);
     a.unit_cap = cap;
 }
 
@@ -425,8 +417,6 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
     a.blob = ds.blob;
     bind_arena_bounds(a);
     KARMA_RC(comb_blob(ds, kDefaultUnit, &a.comb_blob));
-    // the tools build's KARMA_RAGGED_PLAN=2: round 1's two-pass plan (scan + k_ragged_desc)
-    const bool two_pass = KARMA_AB_KNOB("KARMA_RAGGED_PLAN", 1) == 2;
     // Unit table: full units in [0, cap_full), partial units (at most 2 per record) after them.
     uint64_t cap_full, cap;
     void* ws = nullptr;
@@ -436,7 +426,6 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         const RaggedLayout L = ragged_layout(n_rec, cap);
         KARMA_RC(workspace(dev, s, L.total, &ws));
         bind_ragged(a, ws, L, cap);
-        if (two_pass) KARMA_HIP(launch_ragged_scan(a, s));
     } else {
         // Unknown total: count the units (k_ragged_scan), read the block totals back and size
         // the unit table.
@@ -458,16 +447,12 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         cap_full = std::max<uint64_t>(full, 1);
         cap = cap_full + parts;
         L = ragged_layout(n_rec, cap);
-        bool fresh = false;
-        KARMA_RC(workspace(dev, s, L.total, &ws, &fresh));
+        KARMA_RC(workspace(dev, s, L.total, &ws));
         bind_ragged(a, ws, L, cap);
-        // (a new allocation holds none of the scan's results, even at the old address)
-        if (fresh && two_pass) KARMA_HIP(launch_ragged_scan(a, s));
     }
-    a.part_base = two_pass ? 0 : cap_full;
-    a.tail_blocks = (uint64_t)KARMA_AB_KNOB("KARMA_RAGGED_TAIL_BLOCKS", 32);
-    if (!two_pass) KARMA_RC(bind_lookback(dev, s, ragged_scan_blocks(n_rec), a));
-    KARMA_HIP(launch_ragged_main(a, ds.cu, s, two_pass));
+    a.part_base = cap_full;
+    KARMA_RC(bind_lookback(dev, s, ragged_scan_blocks(n_rec), a));
+    KARMA_HIP(launch_ragged_main(a, ds.cu, s));
     return 0;
 }
 
@@ -653,12 +638,12 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
         a.init = d_init;
         a.init_scalar = init;
         a.out = d_out;
-        const long dv = KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0);  // tools build: the other kernels
-        a.blob = dv == 1 || dv == 2 ? L.ds->blob : dv == 3 || (dv >= 14 && dv <= 27 && dv != 21) ? L.ds->lane_blob : dv == 5 || dv == 21 ? L.ds->pair_blob : L.ds->quad_blob;
+        const bool staged = KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 20;  // tools build: the LDS-staged kernel
+        a.blob = staged ? L.ds->lane_blob : L.ds->quad_blob;
         bind_arena_bounds(a);
-        // a wave takes 64 records (lanes variant: a workgroup 1024): no more workgroups than
-        // the batch fills (each one loads the 145 KiB table image into its LDS first)
-        const uint64_t per_block = dv == 3 ? kBlockThreads : dv == 23 ? 64 * 4 : dv == 24 ? 64 * 5 : dv == 25 ? 64 * 10 : dv == 26 ? 64 * 9 : (dv >= 14 && dv <= 22 && dv != 21) || dv == 27 ? 64 * kStgWaves : dv == 21 ? 32 * 14 : 64 * kWavesPerBlock;
+        // a wave takes 64 records: no more workgroups than the batch fills (each one loads its
+        // table image into LDS first)
+        const uint64_t per_block = 64 * (staged ? kStgWaves : kWavesPerBlock);
         const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_rec, per_block));
         KARMA_HIP(launch_ragged_direct(a, (int)blocks, (hipStream_t)stream));
         return KARMA_OK;

@@ -65,7 +65,6 @@ void build_stream_blob(uint32_t* out /*kBlobWords*/);
 void build_lane_blob(uint32_t* out /*kBlobWords*/);
 // ... and with Z_64: k_ragged_direct4, one record per group of 4 lanes.
 void build_quad_blob(uint32_t* out /*kBlobWords*/);
-void build_pair_blob(uint32_t* out /*kBlobWords*/);  // Z_32: the tools build's 2-lane groups
 void build_combine_blob(uint64_t unit_bytes, uint32_t* out /*kCombWords*/);
 void build_block_combine_blob(uint64_t unit_bytes, uint64_t per_thread, uint32_t* out /*kBlockCombWords*/);
 
@@ -94,27 +93,15 @@ struct FixedArgs {
     uint64_t comb_m;            // states per thread of the fused fold
 };
 
-// One unit of a ragged batch: the 16-aligned span [us, us + span) of a record
-// body and what the units kernel does at the record's edges, so that no other
-// kernel reads record bytes (the head and tail blocks share the unit's first and
-// last cache lines, or the neighbouring ones):
-//   kDescFirst (the record's first unit): the record starts hoff bytes into the
-//     16-byte block before us (hoff 0: at us); the register entering the body is
-//     ~init stepped over those head bytes, xored into the body's first word.
-//   kDescLast (the record's last unit): the record ends t bytes after us + span;
-//     the units kernel also steps a zero register over those tail bytes (tailc).
+// One unit of a ragged batch: the 16-aligned span [us, us + span) of a record body; inj is
+// xored into the span's first word: for the record's first unit the register entering the
+// body (~init stepped over the unaligned head bytes by the plan), else 0.
 struct UnitDesc {
     uint64_t us;
-    uint32_t span;  // bytes (low 16 bits) | kDescFirst | hoff << 17 | kDescLast | t << 22
-    uint32_t inj;   // init (kDescFirst), else 0
+    uint32_t span;  // bytes
+    uint32_t inj;
 };
 static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
-constexpr uint32_t kDescBytes = 0xffffu;
-constexpr uint32_t kDescFirst = 1u << 16;
-constexpr uint32_t kDescLast = 1u << 21;
-constexpr uint32_t desc_flags(bool first, uint32_t hoff, bool last, uint32_t t) {
-    return (first ? kDescFirst | (hoff << 17) : 0u) | (last ? kDescLast | (t << 22) : 0u);
-}
 
 // Ragged batches cut record bodies at absolute unit_bytes boundaries (so full
 // units are unit-aligned and every chunk is a whole cache line) and order the
@@ -136,8 +123,7 @@ struct RaggedArgs {
                                //   [n_rec] = total units, [n_rec+1] = full units
     uint64_t* pslot;           // 2 * n_rec: slots of the record's partial first / last unit
     uint64_t* block_sums;      // per scan block: full-unit offset
-    uint64_t* block_psums;     // per scan block: partial units, then the block's first partial slot (two-pass);
-                               //   single-pass plan: first partial slot (after part_base) << 16 | run length
+    uint64_t* block_psums;     // per scan block: partial units (k_ragged_scan)
     // Single-pass plan (k_ragged_plan): decoupled look-back over per-block status words.
     // lb[0] counts the blocks that started (plan-block ids in start order); lb[1 + b] =
     // seq << 42 | flag << 40 | value (flag 1: block b's own full-unit count, 2: the full units
@@ -148,19 +134,14 @@ struct RaggedArgs {
     // to seq, or, at lb_seq_max, clears the lb_words status words and restarts the tags at 1.
     unsigned long long* lb;
     unsigned long long* lbp;   // the same for the blocks' partial unit counts
-    unsigned long long* lb_ctl;  // [0] the last finished call's tag, [1] the running call's,
-                                 // [2] the longest plan block's partial run (reset by finalize)
+    unsigned long long* lb_ctl;  // [0] the last finished call's tag, [1] the running call's
     uint64_t lb_words;         // status words after lb[0] (both arrays)
     uint32_t lb_seq_max;       // 2^22 (the tools build lowers it to test the wrap)
-    uint64_t tail_blocks;      // units kernel: plan blocks whose partial runs are taken rank-major
     UnitDesc* desc;            // unit_cap entries
     uint64_t unit_cap;         // capacity of desc / partial
-    uint64_t part_base;        // single-pass plan: first slot of the partial units (full units
-                               //   take [0, part_base)); 0: the two-pass plan (partial units
-                               //   follow the full ones)
+    uint64_t part_base;        // first slot of the partial units (full units take [0, part_base))
     uint32_t* out;
     uint32_t* partial;         // register contribution per unit slot
-    uint32_t* tailc;           // per unit slot of a record's last unit: its tail bytes' register
     const uint32_t* blob;      // stream blob (kBlobWords)
     const uint32_t* comb_blob; // kCombWords for unit_bytes
     uintptr_t kb_lo, kb_hi;    // bounds build only: the arena's allocation (bounds.h); else 0
@@ -203,12 +184,12 @@ inline uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock 
 // Ragged: the plan (one pass: unit slots, descriptors and the entering registers; total
 // units at fbase[n_rec]), then the unit kernel and the per-record finalize.
 // launch_ragged_scan only counts units (block_sums / block_psums), for callers that must size
-// the unit table first.  two_pass (tools build only): scan + k_ragged_desc instead of the
-// single-pass plan.
+// the unit table first.
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
-hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool two_pass = false);
+hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // One record per group of 4 lanes, no plan kernels (uses arena, off, len, n_rec, init, out, and
-// blob = build_quad_blob's; the tools build's KARMA_DIRECT_VARIANT picks the alternatives).
+// blob = build_quad_blob's; the tools build's KARMA_DIRECT_VARIANT=20 runs the LDS-staged
+// kernel instead, with blob = build_lane_blob's).
 hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // k_ragged_direct4 with a device-sized batch (a.n_dev / a.gate_len set): WAL replay's
 // device-planned path, whatever the tools build's variant.

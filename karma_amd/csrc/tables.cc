@@ -20,11 +20,6 @@ void build_lane_blob(uint32_t* out) {
     gf2::slicing_tables(gf2::Map::zero_bytes(16), out + kBlobStride);  // one lane's 4 word slots: stride 16
 }
 
-void build_pair_blob(uint32_t* out) {
-    build_stream_blob(out);
-    gf2::slicing_tables(gf2::Map::zero_bytes(32), out + kBlobStride);  // groups of 2 lanes: stride 32
-}
-
 void build_quad_blob(uint32_t* out) {
     build_stream_blob(out);
     gf2::slicing_tables(gf2::Map::zero_bytes(64), out + kBlobStride);  // groups of 4 lanes: stride 64

@@ -303,8 +303,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     // default plan the walkers checksum the candidates inline (k_wal_walk_crc); the tools
     // build's other walk / small-record kernels, and KARMA_WAL_CRC_SEPARATE, walk first and
     // then run one small-record batch over the gathered lists (the round-2 path).
-    const bool dev_plan = img_bytes <= kDevicePlanMax && batch != KARMA_WAL_CRC_UNITS &&
-                          KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 0;
+    const bool dev_plan = img_bytes <= kDevicePlanMax && batch != KARMA_WAL_CRC_UNITS;
     const bool inline_crc =
         dev_plan && batch == KARMA_WAL_CRC_INLINE && KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 0;
     // the walkers' lists checksummed after the walk by the LDS-staged kernel (k_wal_list_crc)

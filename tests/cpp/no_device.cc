@@ -20,7 +20,7 @@ hipError_t launch_combine_block(const FixedArgs&, const uint32_t*, uint64_t, uin
     return hipErrorNoDevice;
 }
 hipError_t launch_ragged_scan(const RaggedArgs&, hipStream_t) { return hipErrorNoDevice; }
-hipError_t launch_ragged_main(const RaggedArgs&, int, hipStream_t, bool) { return hipErrorNoDevice; }
+hipError_t launch_ragged_main(const RaggedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_ragged_direct(const RaggedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_wal_walk(const WalArgs&, uint64_t, const WalWalkPlan&, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_ragged_direct_dev(const RaggedArgs&, int, hipStream_t) { return hipErrorNoDevice; }

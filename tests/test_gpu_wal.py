@@ -47,7 +47,6 @@ WALKS = {
     "split": (False, 0, _lib.KARMA_WAL_CRC_PLAN),         # the plan: few segments -> sub-range walkers
     "split4k": (False, 4096, _lib.KARMA_WAL_CRC_DIRECT),  # one-tile sub-ranges + k_wal_resolve, and every
                                                           # CRC batch one record per group (any length)
-    "octet": (True, 4096, _lib.KARMA_WAL_CRC_DIRECT),     # the same with the tools build's 8-lane groups
     "sep": (False, 0, _lib.KARMA_WAL_CRC_SEPARATE),       # the walk, the gathered lists, one small-record batch
     "sepdirect4": (True, 0, _lib.KARMA_WAL_CRC_SEPARATE),  # the same with the 4-lane kernel only (tools build)
     "inline": (False, 0, _lib.KARMA_WAL_CRC_INLINE),      # the CRCs inside the walk kernel (k_wal_walk_crc)
@@ -55,7 +54,6 @@ WALKS = {
     "listcrc": (True, 0, _lib.KARMA_WAL_CRC_INLINE),      # the walk, then the walkers' lists checksummed by
     "listcrc4k": (True, 4096, _lib.KARMA_WAL_CRC_INLINE), # the LDS-staged kernel (k_wal_list_crc; tools build)
 }
-_DIRECT_VARIANT = {"octet": "1"}  # KARMA_DIRECT_VARIANT of the tools-build plans
 _LIST_CRC = ("listcrc", "listcrc4k")  # KARMA_WAL_LIST_CRC=1
 _NO_STAGED = ("sepdirect4",)  # KARMA_SMALL_STAGED=0
 _WALK = {"name": "split"}
@@ -71,14 +69,11 @@ def _walk_env(monkeypatch, walk):
         monkeypatch.setenv("KARMA_SMALL_STAGED", "0")
     else:
         monkeypatch.delenv("KARMA_SMALL_STAGED", raising=False)
-    if WALKS[walk][0] and walk not in _DIRECT_VARIANT and walk not in _LIST_CRC and walk not in _NO_STAGED:
+    if WALKS[walk][0] and walk not in _LIST_CRC and walk not in _NO_STAGED:
         monkeypatch.setenv("KARMA_WALK_VARIANT", "1")  # read by the tools build only (ab.h)
     else:
         monkeypatch.delenv("KARMA_WALK_VARIANT", raising=False)
-    if walk in _DIRECT_VARIANT:
-        monkeypatch.setenv("KARMA_DIRECT_VARIANT", _DIRECT_VARIANT[walk])
-    else:
-        monkeypatch.delenv("KARMA_DIRECT_VARIANT", raising=False)
+    monkeypatch.delenv("KARMA_DIRECT_VARIANT", raising=False)
 
 
 def _replay(lib, wal, start=0, d_wal=None, seg=SEG, host=True):
@@ -286,7 +281,7 @@ def test_replay_large_records_jumps(lib, seg, walk, monkeypatch):
         assert got == (list(w[0]), w[1], w[2])
 
 
-@pytest.mark.parametrize("walk", ["split", "split4k", "octet", "sep", "inline", "inline4k", "listcrc", "listcrc4k"])
+@pytest.mark.parametrize("walk", ["split", "split4k", "sep", "inline", "inline4k", "listcrc", "listcrc4k"])
 def test_replay_payloads_that_look_like_wal_records(lib, walk, monkeypatch):
     """Payloads that are themselves WAL images (valid header chains inside records): a sub-range
     walker can start on a header inside a payload, and the resolver must then walk the sub-range

@@ -9,11 +9,6 @@ copy for each variant in interleaved rounds (same process, same image):
 
     shipped              the shipped library, default plan
     sub=<bytes>          the shipped library, sub-range walkers of <bytes> (walk_sub_bytes)
-    direct               tools build, KARMA_DIRECT_VARIANT=1 (k_ragged_direct: one record per 8 lanes)
-    direct_v1            tools build, KARMA_DIRECT_VARIANT=2 (the same, un-pipelined rounds)
-    lanes                tools build, KARMA_DIRECT_VARIANT=3 (k_ragged_lanes: one record per lane)
-    direct4              tools build, KARMA_DIRECT_VARIANT=4 (= the shipped k_ragged_direct4<4>)
-    direct2              tools build, KARMA_DIRECT_VARIANT=5 (k_ragged_direct4<2>: pairs of lanes)
     units                the shipped library, ragged plan instead of the direct kernel (crc_batch)
     ab                   tools build, default plan
     nodirect             tools build, KARMA_WALK_DIRECT=0: the walkers read tiles only (no direct header rounds)
@@ -101,16 +96,6 @@ def main():
     for v in a.variants.split(","):
         if v == "shipped":
             variants[v] = (L, 0, 0, None)
-        elif v == "direct":
-            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "1"))
-        elif v == "direct_v1":
-            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "2"))
-        elif v == "lanes":
-            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "3"))
-        elif v == "direct4":
-            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "4"))
-        elif v == "direct2":
-            variants[v] = (AB, 0, 0, ("KARMA_DIRECT_VARIANT", "5"))
         elif v == "listcrc":  # the walk, then the walkers' lists by the LDS-staged kernel (k_wal_list_crc)
             variants[v] = (AB, 0, 4, ("KARMA_WAL_LIST_CRC", "1"))
         elif v == "inline":  # the shipped library, KARMA_WAL_CRC_INLINE (k_wal_walk_crc)
