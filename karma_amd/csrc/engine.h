@@ -103,6 +103,36 @@ struct UnitDesc {
 };
 static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
 
+// ---- ragged batches on the byte grid (DESIGN.md §4 "The byte grid") ----------
+// When a batch's records are sorted by address and do not overlap (every WAL, segment and KFP
+// batch), the bytes they span are cut on the absolute kGridTile grid instead: one tile per
+// group of 8 lanes, every wave-step 8 consecutive tiles, as k_units_fixed cuts 1M x 4 KiB
+// records.  A record's bytes are read in aligned 16-byte windows with the bytes outside the
+// record masked to zero and ~init xored into its first four bytes (a zero prefix leaves the
+// register at zero), so no head or tail byte is stepped on its own; a tile emits one register
+// per record that ends in it (gend) and one for the record that runs past its end (gstate).
+#ifndef KARMA_GRID_TILE
+#define KARMA_GRID_TILE 2048  // a build-time A/B knob
+#endif
+constexpr uint32_t kGridTile = KARMA_GRID_TILE;
+constexpr uint32_t kGridChunks = kGridTile / kChunk;
+static_assert(kGridTile % kChunk == 0 && (kGridTile & (kGridTile - 1)) == 0, "tiles of whole chunks, power of two");
+// Largest gap between consecutive records the grid streams across.  Below a 4 KiB page every
+// byte it reads lies on a page that also holds record bytes, so it reads no unmapped memory.
+constexpr uint64_t kGridMaxGap = kGridTile;
+constexpr uint32_t kGridInterior = 1u << 31;  // tile word: one record covers the tile (no edge, no init)
+struct GridRec {
+    uint64_t p;    // address of the record's first byte
+    uint32_t n;    // length
+    uint32_t inj;  // ~init: xored into the record's first four bytes
+};
+static_assert(sizeof(GridRec) == 16, "one 16-byte load per record");
+// The grid's combine blob: build_combine_blob(kGridTile), then Z_{-16} (the inverse of 16 zero
+// bytes: a record's register is read at its end rounded up to 16 and moved back).
+constexpr int kGridCombInv16 = kCombWords;
+constexpr int kGridCombWords = kCombWords + 1024;
+void build_grid_comb_blob(uint32_t* out /*kGridCombWords*/);
+
 // Ragged batches cut record bodies at absolute unit_bytes boundaries (so full
 // units are unit-aligned and every chunk is a whole cache line) and order the
 // units for balance: all full units first, in record order, then
@@ -156,6 +186,17 @@ struct RaggedArgs {
     // cmp_stored[r] (records of length 0 excepted) and keeps the first mismatch in *cmp_bad.
     const uint32_t* cmp_stored;
     unsigned long long* cmp_bad;
+    // The byte grid (k_ragged_grid_plan; tile_cap == 0: not attempted).  The plan checks the
+    // grid's conditions per block (gflag); the kernels after it read every block's flag and take
+    // the grid path only when all hold, else the unit plan above (k_ragged_plan runs only then).
+    GridRec* grec;             // n_rec
+    uint32_t* gtile;           // tile_cap: first record reaching into the tile | kGridInterior
+    uint32_t* gstate;          // tile_cap: register of the record running past the tile's end
+    uint32_t* gend;            // n_rec: register of the record's last tile, at its end rounded up to 16
+    uint32_t* gflag;           // per plan block: nonzero = a condition fails
+    unsigned long long* gctl;  // [0] tiles, [1] address of tile 0, [2] first byte read, [3] last byte read + 1
+    uint64_t tile_cap;
+    const uint32_t* gcomb_blob;  // kGridCombWords
 };
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
@@ -186,6 +227,8 @@ inline uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock 
 // launch_ragged_scan only counts units (block_sums / block_psums), for callers that must size
 // the unit table first.
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
+// a.tile_cap > 0: the byte grid's plan first (k_ragged_grid_plan); the unit plan then runs only
+// when a grid condition fails, and the units kernel and finalize take the path the flags say.
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // One record per group of 4 lanes, no plan kernels (uses arena, off, len, n_rec, init, out, and
 // blob = build_quad_blob's; the tools build's KARMA_DIRECT_VARIANT=20 runs the LDS-staged

@@ -54,6 +54,34 @@ struct Map {
         for (int i = 0; i < 32; ++i) m.col[i] = a.apply(b.col[i]);
         return m;
     }
+    // The inverse map (Z_d is invertible: the CRC polynomial has a constant term), by
+    // Gauss-Jordan elimination on [M | I]: row r holds bit r of every column.
+    static Map inverse(const Map& m) {
+        uint64_t rows[32];
+        for (int r = 0; r < 32; ++r) {
+            uint64_t row = 1ull << (32 + r);
+            for (int i = 0; i < 32; ++i)
+                if ((m.col[i] >> r) & 1u) row |= 1ull << i;
+            rows[r] = row;
+        }
+        for (int c = 0; c < 32; ++c) {
+            int piv = c;
+            while (piv < 32 && !((rows[piv] >> c) & 1u)) ++piv;
+            if (piv == 32) return identity();  // singular: not a CRC shift (never happens)
+            const uint64_t t = rows[piv];
+            rows[piv] = rows[c];
+            rows[c] = t;
+            for (int r = 0; r < 32; ++r)
+                if (r != c && ((rows[r] >> c) & 1u)) rows[r] ^= rows[c];
+        }
+        Map inv;
+        for (int i = 0; i < 32; ++i) {
+            uint32_t col = 0;
+            for (int r = 0; r < 32; ++r) col |= (uint32_t)((rows[r] >> (32 + i)) & 1u) << r;
+            inv.col[i] = col;
+        }
+        return inv;
+    }
     // Z_d by square-and-multiply over Z_1 (d may be up to 2^63).
     static Map zero_bytes(uint64_t d) {
         Map result = identity();
