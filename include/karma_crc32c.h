@@ -94,8 +94,41 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
                                       uint32_t* d_out, karma_stream_t stream);
 
 /* *d_out = Extend(init, d_data, n): one long buffer split over the whole GPU
- * and folded back with a polynomial combine. */
+ * and folded back with a polynomial combine.
+ * Forward progress: this call (and karma_crc32c_batch_fixed with n_rec == 1 and a record
+ * split over more than 8 units) is ONE kernel whose last workgroup waits on the other
+ * workgroups' tagged wave states and folds them.  It assumes that every workgroup of the grid
+ * is eventually scheduled while the last one waits: the grid has at most one workgroup per
+ * compute unit and the hardware dispatches workgroups in index order, so the ones waited for
+ * were dispatched first.  Concurrent kernels on other streams only delay them (they are
+ * tested concurrently with other segment scans and ragged batches); do not launch it where a
+ * co-resident persistent kernel could hold every compute unit forever. */
 int karma_crc32c_stream(uint32_t init, const void* d_data, size_t n, uint32_t* d_out, karma_stream_t stream);
+
+/* ---- resource lifetime ---------------------------------------------------
+ * crc32c::Extend (karma-util/crc32c.h) allocates nothing.  The device batch entry points keep,
+ * per (device, stream), what their kernels point at: a workspace sized for the largest batch seen
+ * on the stream, the ragged plan's look-back words and the single-record combine's words.  For
+ * hipStreamPerThread the state is per calling thread.  An outgrown buffer is freed once its
+ * stream has drained, unless a hipGraph was ever captured on that stream (a captured call keeps
+ * its address): then it is kept until karma_crc32c_trim.  The host-memory, WAL and KFP entry
+ * points keep per-device streams, device buffers and pinned staging.  Nothing else is kept.
+ *
+ * karma_crc32c_release_stream  waits for `stream` and frees its state (before destroying a
+ *                              stream, or when a thread is done with hipStreamPerThread).  Do
+ *                              not call it while a graph captured on that stream may still be
+ *                              launched, nor while the stream is capturing (KARMA_E_INVALID).
+ * karma_crc32c_trim            waits for the device and frees what no live stream holds: the
+ *                              state of exited threads' hipStreamPerThread, the outgrown buffers
+ *                              (unless a graph hold is active) and the per-device contexts of the
+ *                              host, WAL and KFP entry points (recreated by their next call).
+ * karma_crc32c_graph_hold      counts the captured graphs a caller keeps (delta +1 / -1); while
+ *                              the count is above 0, trim keeps outgrown buffers.  Returns the
+ *                              count (>= 0) or a KARMA_E_* status.
+ * device: the device index, or -1 for the calling thread's current device. */
+int karma_crc32c_release_stream(int device, karma_stream_t stream);
+int karma_crc32c_trim(int device);
+int karma_crc32c_graph_hold(int device, int delta);
 
 /* ---- host-memory batches (synchronous; H2D, kernel, D2H overlapped) ------- */
 int karma_crc32c_batch_fixed_host(const void* h_data, size_t rec_bytes, size_t n_rec, uint32_t init,

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -19,6 +20,7 @@
 #include "bounds.h"
 #include "engine.h"
 #include "karma_crc32c.h"
+#include "stream_state.h"
 
 using namespace karma::engine;
 
@@ -69,38 +71,75 @@ struct DevState {
     std::map<std::pair<uint64_t, uint64_t>, uint32_t*> bcomb;  // (unit bytes, states per thread) -> block blob
 };
 
-struct Workspace {
-    void* ptr = nullptr;
-    size_t bytes = 0;
+// HIP operations of the per-stream state (stream_state.h).
+struct HipStateOps {
+    int alloc(void** p, size_t bytes) {
+        const hipError_t e = hipMalloc(p, bytes);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMalloc (stream state)");
+    }
+    void free(void* p) { (void)hipFree(p); }
+    int zero(void* p, size_t bytes, void* s) {
+        const hipError_t e = hipMemsetAsync(p, 0, bytes, (hipStream_t)s);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync (stream state)");
+    }
+    int sync_stream(void* s) {
+        const hipError_t e = hipStreamSynchronize((hipStream_t)s);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipStreamSynchronize (stream state)");
+    }
+    int sync_device(int dev) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        hipError_t e = hipSetDevice(dev);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        (void)hipSetDevice(cur);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipDeviceSynchronize (trim)");
+    }
+    bool capturing(void* s) {
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing((hipStream_t)s, &st) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return st != hipStreamCaptureStatusNone;
+    }
 };
 
 // One lock for the library state; held across planning and enqueueing so a
 // workspace is never reallocated between another call's lookup and launch.
 std::mutex g_mu;
 std::vector<DevState> g_dev;
-std::map<std::pair<int, void*>, Workspace> g_ws;
+// Per (device, stream): the workspace, the ragged plan's look-back words and the fused record
+// combine's words (stream_state.h: what is freed when, and what a captured graph keeps).
+//   look-back words (RaggedArgs::lb, crc_ragged.hip): [0] counts started plan blocks, [1 + b]
+//     block b's full-unit status and [1 + half + b] its partial-unit status, tagged with the
+//     call's seq; then the control words lb_ctl.  Calls on one stream run in order, so a call
+//     sees only its own tag or older ones.  The counter and the tag live on the device
+//     (k_ragged_plan / k_ragged_finalize), so a captured ragged call replays any number of
+//     times.  Zeroed when allocated; the device clears them when the 22-bit tag wraps.
+//   fused words (FixedArgs::fctl, k_units_fixed FUSE): [0] unused, [1] the last finished call's
+//     tag, then kBlockCombMaxPerThread * 1024 tagged wave states.  Zeroed once and never moved:
+//     the tags only grow, so no state a later call reads carries its tag before that call wrote it.
+StreamStates<HipStateOps> g_states;
+using State = StreamStates<HipStateOps>::State;
 
-// The ragged plan's look-back words per (device, stream) (RaggedArgs::lb, crc_ragged.hip):
-// [0] counts started plan blocks, [1 + b] block b's full-unit status and [1 + half + b] its
-// partial-unit status, tagged with the call's seq; then the two control words lb_ctl.
-// Calls on one stream run in order, so a call sees only its own tag or older ones.  The
-// counter and the tag are kept on the device (k_ragged_plan / k_ragged_finalize), none on the
-// host: a ragged call captured in a hipGraph may be replayed any number of times.  The words
-// are zeroed when allocated; the device clears them when the 22-bit tag wraps.
-// hipStreamPerThread is one handle for many streams: it is keyed per calling thread.
-struct Lookback {
-    unsigned long long* words = nullptr;
-    uint64_t cap = 0;   // words: 1 + 2 * half + 3
-    uint64_t half = 0;  // plan blocks a call may have
+// hipStreamPerThread is one handle for many streams: its state is keyed per calling thread, by a
+// generation number (odd, so never a stream handle), not by an address a later thread may reuse.
+// A thread's exit hands its per-thread state to the next trim (its stream is gone).
+std::atomic<uint64_t> g_thread_gen{0};
+struct ThreadKey {
+    uintptr_t key = 0;
+    ~ThreadKey() {
+        if (!key) return;
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_states.orphan(key);
+    }
 };
-std::map<std::pair<int, void*>, Lookback> g_lb;
-
-// The fused record combine's words per (device, stream) (FixedArgs::fctl, k_units_fixed FUSE):
-// [0] workgroups finished, [1] the last finished call's tag, then kBlockCombMaxPerThread * 1024
-// tagged wave states.  Allocated and zeroed once and never moved: the tags only grow, so no
-// state a later call could read carries its tag before that call wrote it.
-std::map<std::pair<int, void*>, unsigned long long*> g_fused;
-thread_local char t_per_thread_key;  // the look-back key of this thread's hipStreamPerThread
+thread_local ThreadKey t_key;
+uintptr_t stream_key(hipStream_t s) {
+    if (s != hipStreamPerThread) return reinterpret_cast<uintptr_t>(s);
+    if (!t_key.key) t_key.key = (uintptr_t)((++g_thread_gen << 1) | 1u);
+    return t_key.key;
+}
 
 int current_device(int* dev) {
     int n = 0;
@@ -166,66 +205,38 @@ int block_comb_blob(DevState& d, uint64_t unit_bytes, uint64_t per_thread, const
     return 0;
 }
 
-// A per-(device, stream) scratch buffer, grown on demand (*reallocated: it was).
-// Per-stream state is keyed by the stream handle; hipStreamPerThread is one handle for many
-// streams, so it is keyed by the calling thread.
-void* stream_key(hipStream_t s) { return s == hipStreamPerThread ? (void*)&t_per_thread_key : (void*)s; }
-
-// Buffers a stream's workspace or look-back words outgrew.  They are kept, not freed: a ragged
-// call captured in a hipGraph keeps their addresses in its kernel arguments, and a later,
-// larger call on the same stream must not free memory such a graph still uses.  (Growth is
-// by at least 1.25x, so the retired buffers add up to a few times the largest one.)
-std::vector<void*> g_retired;
-
-int workspace(int dev, hipStream_t s, size_t bytes, void** out, bool* reallocated = nullptr) {
-    Workspace& w = g_ws[{dev, stream_key(s)}];
-    if (reallocated) *reallocated = w.bytes < bytes;
-    if (w.bytes < bytes) {
-        if (w.ptr) {
-            g_retired.push_back(w.ptr);
-            w.ptr = nullptr;
-            w.bytes = 0;
-        }
-        const size_t want = align256(bytes + bytes / 4);
-        KARMA_HIP(hipMalloc(&w.ptr, want));
-        w.bytes = want;
-    }
-    *out = w.ptr;
+// Caller holds g_mu.  The stream's scratch buffer, grown on demand (by a quarter more than asked).
+int workspace(int dev, hipStream_t s, size_t bytes, void** out) {
+    State& st = g_states.get(dev, stream_key(s), s);
+    KARMA_RC(g_states.grow(st, st.ws, bytes, align256(bytes + bytes / 4), false));
+    *out = st.ws.p;
     return 0;
 }
 
 // Caller holds g_mu.
 int fused_words(int dev, hipStream_t s, unsigned long long** out) {
-    unsigned long long*& w = g_fused[{dev, stream_key(s)}];
-    if (!w) {
-        const size_t bytes = (2 + kBlockCombMaxPerThread * 1024) * sizeof(unsigned long long);
-        KARMA_HIP(hipMalloc(&w, bytes));
-        KARMA_HIP(hipMemsetAsync(w, 0, bytes, s));
-    }
-    *out = w;
+    State& st = g_states.get(dev, stream_key(s), s);
+    const size_t bytes = (2 + kBlockCombMaxPerThread * 1024) * sizeof(unsigned long long);
+    KARMA_RC(g_states.grow(st, st.fused, bytes, bytes, true));
+    *out = static_cast<unsigned long long*>(st.fused.p);
     return 0;
 }
 
 // Caller holds g_mu.  Binds the stream's look-back words for nb plan blocks.
 int bind_lookback(int dev, hipStream_t s, uint64_t nb, RaggedArgs& a) {
-    Lookback& L = g_lb[{dev, stream_key(s)}];
-    if (L.half < nb) {
-        if (L.words) {
-            g_retired.push_back(L.words);
-            L.words = nullptr;
-            L.cap = L.half = 0;
-        }
-        const uint64_t half = std::max<uint64_t>(2 * nb, 2048);
-        const uint64_t cap = 1 + 2 * half + 3;
-        KARMA_HIP(hipMalloc(&L.words, cap * sizeof(unsigned long long)));
-        KARMA_HIP(hipMemsetAsync(L.words, 0, cap * sizeof(unsigned long long), s));
-        L.half = half;
-        L.cap = cap;
+    State& st = g_states.get(dev, stream_key(s), s);
+    const uint64_t want_half = std::max<uint64_t>(2 * nb, 2048);
+    const uint64_t have_half = st.lb.p ? (st.lb.bytes / sizeof(unsigned long long) - 4) / 2 : 0;
+    if (have_half < nb) {
+        const size_t bytes = (1 + 2 * want_half + 3) * sizeof(unsigned long long);
+        KARMA_RC(g_states.grow(st, st.lb, bytes, bytes, true));
     }
-    a.lb = L.words;
-    a.lbp = L.words + 1 + L.half;
-    a.lb_ctl = L.words + 1 + 2 * L.half;
-    a.lb_words = 2 * L.half;
+    unsigned long long* w = static_cast<unsigned long long*>(st.lb.p);
+    const uint64_t half = (st.lb.bytes / sizeof(unsigned long long) - 4) / 2;
+    a.lb = w;
+    a.lbp = w + 1 + half;
+    a.lb_ctl = w + 1 + 2 * half;
+    a.lb_words = 2 * half;
     // (the tools build can lower the wrap point to test it: KARMA_LB_SEQ_MAX, ab.h)
     a.lb_seq_max = (uint32_t)std::min<long>(KARMA_AB_KNOB("KARMA_LB_SEQ_MAX", 1l << 22), 1l << 22);
     return 0;
@@ -715,6 +726,43 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
 
 int karma_crc32c_stream(uint32_t init, const void* d_data, size_t n, uint32_t* d_out, karma_stream_t stream) {
     return karma_crc32c_batch_fixed(d_data, n, 1, nullptr, init, d_out, stream);
+}
+
+// ---- resource lifetime (include/karma_crc32c.h, stream_state.h) -----------------------------
+namespace {
+int select_device(int device, int* dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(KARMA_E_NO_DEVICE, "no HIP device visible");
+    if (device >= n) return fail(KARMA_E_INVALID, "device index out of range");
+    if (device >= 0) KARMA_HIP(hipSetDevice(device));
+    KARMA_HIP(hipGetDevice(dev));
+    return 0;
+}
+}  // namespace
+
+int karma_crc32c_release_stream(int device, karma_stream_t stream) {
+    int dev = 0;
+    KARMA_RC(select_device(device, &dev));
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (HipStateOps().capturing(stream)) return fail(KARMA_E_INVALID, "release_stream: the stream is capturing");
+    return g_states.release(dev, stream_key((hipStream_t)stream));
+}
+
+int karma_crc32c_trim(int device) {
+    int dev = 0;
+    KARMA_RC(select_device(device, &dev));
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        KARMA_RC(g_states.trim(dev));
+    }
+    return karma::engine::trim_host_contexts(dev);
+}
+
+int karma_crc32c_graph_hold(int device, int delta) {
+    int dev = 0;
+    KARMA_RC(select_device(device, &dev));
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_states.hold(dev, delta);
 }
 
 }  // extern "C"

@@ -359,6 +359,16 @@ struct KfpWalk {
 // The structural part of connection::read_frame's parse loop over buf; returns KARMA_KFP_*.
 int kfp_walk(const uint8_t* buf, size_t buf_bytes, size_t max_frames, KfpWalk* out);
 
+// karma_crc32c_trim: the per-device contexts of the host-memory, WAL and KFP entry points (their
+// streams, events, device buffers and pinned staging) released after their in-flight call, if
+// any, has finished; recreated by the next call.  0 or the first error.
+int trim_host_contexts(int dev);
+int trim_replay_ctx(int dev);      // wal.cc
+int trim_host_batch_ctx(int dev);  // host_batch.cc
+int trim_append_ctx(int dev);      // wal_append.cc
+int trim_kfp_ctx(int dev);         // kfp.cc
+int trim_stage(int dev);           // host_stage.cc
+
 // Synthetic data: bytes of the counter-based splitmix64 stream.
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n_bytes, uint64_t seed, uint64_t first_byte, hipStream_t s);
 // Read-only streaming probe (achievable-HBM reference): xor-reduces n_bytes.

@@ -100,6 +100,17 @@ struct HostCtx {
         ready = true;
         return 0;
     }
+    void reset() {  // karma_crc32c_trim (the caller holds mu)
+        if (!ready) return;
+        for (Slot& s : slot) {
+            (void)hipStreamSynchronize(s.st);
+            for (Buf* b : {&s.d_data, &s.d_off, &s.d_len, &s.d_out, &s.h_off, &s.h_len, &s.h_out}) b->release();
+            (void)hipEventDestroy(s.done);
+            (void)hipStreamDestroy(s.st);
+            s = Slot{};
+        }
+        ready = false;
+    }
 };
 
 std::mutex g_ctx_mu;
@@ -171,6 +182,13 @@ int fixed_pinned(HostCtx& c, const char* src, size_t rec_bytes, size_t n_rec, ui
 }
 
 }  // namespace
+
+int karma::engine::trim_host_batch_ctx(int dev) {
+    HostCtx& c = ctx_for(dev);
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.reset();
+    return 0;
+}
 
 extern "C" {
 

@@ -43,6 +43,21 @@ struct Stage {
         ready = true;
         return 0;
     }
+    void reset() {  // karma_crc32c_trim (the caller holds mu)
+        if (!ready) return;
+        for (int t = 0; t < kWorkers; ++t) {
+            (void)hipStreamSynchronize(st[t]);
+            (void)hipStreamDestroy(st[t]);
+            st[t] = nullptr;
+            for (int k = 0; k < 2; ++k) {
+                (void)hipEventDestroy(ev[t][k]);
+                (void)hipHostFree(buf[t][k]);
+                ev[t][k] = nullptr;
+                buf[t][k] = nullptr;
+            }
+        }
+        ready = false;
+    }
 };
 
 std::mutex g_mu;
@@ -187,6 +202,21 @@ int staged_upload(int dev, void* d_dst, const HostFill& fill, uint64_t src_off, 
     for (int rc : rcs)
         if (rc) return rc == KARMA_E_IO ? rc : set_last_error(rc, "staged upload");
     return 0;
+}
+
+int trim_stage(int dev) {
+    Stage& S = stage_for(dev);
+    std::lock_guard<std::mutex> lk(S.mu);
+    S.reset();
+    return 0;
+}
+
+int trim_host_contexts(int dev) {
+    // the staging last: the other contexts' calls may be using it
+    int rc = trim_replay_ctx(dev);
+    for (int r : {trim_host_batch_ctx(dev), trim_append_ctx(dev), trim_kfp_ctx(dev), trim_stage(dev)})
+        if (!rc) rc = r;
+    return rc;
 }
 
 int staged_copy(int dev, void* d_dst, const void* h_src, size_t bytes) {

@@ -35,6 +35,14 @@ bool host_is_pinned(const void* h);
 // True when [h, h + bytes) lies inside one page-locked host allocation.
 bool host_range_pinned(const void* h, size_t bytes);
 
+// karma_crc32c_trim's per-module releases (engine.h); trim_host_contexts calls them all.
+int trim_replay_ctx(int dev);
+int trim_host_batch_ctx(int dev);
+int trim_append_ctx(int dev);
+int trim_kfp_ctx(int dev);
+int trim_stage(int dev);
+int trim_host_contexts(int dev);
+
 // body(t) for t in [0, n) on n std::threads (n small: the host stages of a call).
 void run_threads(int n, const std::function<void(int)>& body);
 

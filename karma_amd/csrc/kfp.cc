@@ -33,6 +33,30 @@
 namespace karma::engine {
 int set_last_error(int code, const std::string& what);  // capi.cc
 
+namespace {
+// crc_spans' grow-only device copies of the span lists, per device.
+struct SpanBufs {
+    std::mutex mu;
+    void *off = nullptr, *len = nullptr, *out = nullptr;
+    size_t cap = 0;  // records
+    void release() {  // the caller holds mu
+        (void)hipFree(off);
+        (void)hipFree(len);
+        (void)hipFree(out);
+        off = len = out = nullptr;
+        cap = 0;
+    }
+};
+std::mutex g_span_mu;
+std::vector<std::unique_ptr<SpanBufs>> g_span_bufs;
+SpanBufs* span_bufs(int dev) {
+    std::lock_guard<std::mutex> g(g_span_mu);
+    if ((int)g_span_bufs.size() <= dev) g_span_bufs.resize(dev + 1);
+    if (!g_span_bufs[dev]) g_span_bufs[dev] = std::make_unique<SpanBufs>();
+    return g_span_bufs[dev].get();
+}
+}  // namespace
+
 // CRCs of the spans (off[i], len[i]) of a buffer in one ragged GPU batch: from host
 // memory (batch_ragged_host), or over the caller's device copy d_buf.
 int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std::vector<uint64_t>& off,
@@ -52,27 +76,10 @@ int crc_spans(const void* h_buf, const void* d_buf, size_t buf_bytes, const std:
     int dev = 0;
     if (device >= 0 && hipSetDevice(device) != hipSuccess) return set_last_error(KARMA_E_HIP, "hipSetDevice");
     if (hipGetDevice(&dev) != hipSuccess) return set_last_error(KARMA_E_HIP, "hipGetDevice");
-    struct SpanBufs {
-        std::mutex mu;
-        void *off = nullptr, *len = nullptr, *out = nullptr;
-        size_t cap = 0;  // records
-    };
-    static std::mutex g_mu;
-    static std::vector<std::unique_ptr<SpanBufs>> g_bufs;
-    SpanBufs* B;
-    {
-        std::lock_guard<std::mutex> g(g_mu);
-        if ((int)g_bufs.size() <= dev) g_bufs.resize(dev + 1);
-        if (!g_bufs[dev]) g_bufs[dev] = std::make_unique<SpanBufs>();
-        B = g_bufs[dev].get();
-    }
+    SpanBufs* B = span_bufs(dev);
     std::lock_guard<std::mutex> lk(B->mu);
     if (B->cap < off.size()) {
-        (void)hipFree(B->off);
-        (void)hipFree(B->len);
-        (void)hipFree(B->out);
-        B->off = B->len = B->out = nullptr;
-        B->cap = 0;
+        B->release();
         const size_t cap = off.size() + off.size() / 8;
         if (hipMalloc(&B->off, cap * 8) != hipSuccess || hipMalloc(&B->len, cap * 4) != hipSuccess ||
             hipMalloc(&B->out, cap * 4) != hipSuccess)
@@ -175,6 +182,11 @@ struct EncBuf {
         host = pinned_host;
         return 0;
     }
+    void release() {
+        if (p) (void)(host ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        bytes = 0;
+    }
     template <typename T>
     T* as() const {
         return static_cast<T*>(p);
@@ -206,6 +218,19 @@ struct EncCtx {
             ev.push_back(e);
         }
         return 0;
+    }
+    void reset() {  // karma_crc32c_trim (the caller holds mu)
+        if (!ready) return;
+        for (auto& x : st) {
+            (void)hipStreamSynchronize(x);
+            (void)hipStreamDestroy(x);
+            x = nullptr;
+        }
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        ev.clear();
+        for (EncBuf* b : {&h_span, &h_off, &h_len, &h_crc, &d_span, &d_off, &d_len, &d_crc}) b->release();
+        std::vector<size_t>().swap(bstart);
+        ready = false;
     }
 };
 
@@ -371,6 +396,19 @@ int encode_pass(EncCtx& C, int dev, const EncFrames& F, size_t f0, size_t m, uin
 }
 
 }  // namespace
+
+int karma::engine::trim_kfp_ctx(int dev) {
+    {
+        EncCtx& c = enc_ctx(dev);
+        std::lock_guard<std::mutex> lk(c.mu);
+        c.reset();
+    }
+    SpanBufs* B = span_bufs(dev);
+    std::lock_guard<std::mutex> lk(B->mu);
+    B->release();
+    return 0;
+}
+
 
 extern "C" {
 

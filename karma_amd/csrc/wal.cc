@@ -137,6 +137,11 @@ struct DevBuf {
         host = pinned_host;
         return 0;
     }
+    void release() {
+        if (p) (void)(host ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        bytes = 0;
+    }
     template <typename T>
     T* as() const {
         return static_cast<T*>(p);
@@ -163,6 +168,16 @@ struct ReplayCtx {
         ready = true;
         return 0;
     }
+    // karma_crc32c_trim (the caller holds mu): everything freed, recreated by the next replay.
+    void reset() {
+        if (!ready) return;
+        (void)hipStreamSynchronize(st);
+        for (DevBuf* b : {&img, &crec, &clen, &ccrc, &meta, &sub, &span, &cbase, &off, &len, &stored, &crc, &sum, &h_small})
+            b->release();
+        (void)hipStreamDestroy(st);
+        st = nullptr;
+        ready = false;
+    }
 };
 std::mutex g_rctx_mu;
 std::vector<std::unique_ptr<ReplayCtx>> g_rctx;
@@ -173,6 +188,17 @@ ReplayCtx& replay_ctx(int dev) {
     if (!g_rctx[dev]) g_rctx[dev] = std::make_unique<ReplayCtx>();
     return *g_rctx[dev];
 }
+
+}  // namespace
+
+int karma::engine::trim_replay_ctx(int dev) {
+    ReplayCtx& c = replay_ctx(dev);
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.reset();
+    return 0;
+}
+
+namespace {
 
 // Fills dst with image bytes [off, off + n) (offsets relative to the image start); the
 // image is streamed into HBM through the library's pinned staging (host_stage.h).

@@ -92,6 +92,11 @@ struct Buf {
         host = pinned_host;
         return 0;
     }
+    void release() {
+        if (p) (void)(host ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        bytes = 0;
+    }
     template <typename T>
     T* as() const {
         return static_cast<T*>(p);
@@ -126,6 +131,20 @@ struct AppendCtx {
             ev.push_back(e);
         }
         return 0;
+    }
+    void reset() {  // karma_crc32c_trim (the caller holds mu)
+        if (!ready) return;
+        for (auto& s : st) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+            s = nullptr;
+        }
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        ev.clear();
+        for (Buf* b : {&h_pay, &h_off, &h_len, &h_crc, &d_pay, &d_off, &d_len, &d_crc}) b->release();
+        std::vector<uint64_t>().swap(at);
+        std::vector<size_t>().swap(bstart);
+        ready = false;
     }
 };
 
@@ -382,6 +401,13 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
 }
 
 }  // namespace
+
+int karma::engine::trim_append_ctx(int dev) {
+    AppendCtx& c = ctx_for(dev);
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.reset();
+    return 0;
+}
 
 extern "C" int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const uint32_t* h_len, size_t n,
                                       void* h_wal, size_t wal_bytes, size_t seg_bytes, uint64_t* h_cursor,

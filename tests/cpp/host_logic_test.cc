@@ -13,7 +13,12 @@
 //      (validation, placement, directory scan, structural walks) and refuses cleanly;
 //   6. the grouped point-to-point gather (gather_p2p.h, karma_crc32c_gather_u32 without
 //      ncclGather) through a recording stub of the RCCL calls: every rank's shard lands at
-//      recv + p * count on the root, the root's own by its copy, each slot written once.
+//      recv + p * count on the root, the root's own by its copy, each slot written once;
+//   7. the per-stream state's lifetime (stream_state.h, karma_crc32c_release_stream / _trim /
+//      _graph_hold) through a recording allocator: 1,000 streams created, used with every kind
+//      of growth, released; captured streams keep outgrown buffers until a trim with no graph
+//      hold; exited threads' state is freed by the next trim; nothing leaks or is freed twice
+//      (ASan would also report either).
 #include <hip/hip_runtime_api.h>
 #include <unistd.h>
 
@@ -21,12 +26,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <random>
 #include <string>
 #include <vector>
 
 #include "engine.h"
 #include "gather_p2p.h"
+#include "stream_state.h"
 #include "karma-util/crc32c.h"
 #include "karma_crc32c.h"
 #include "wal_place.h"
@@ -383,6 +390,103 @@ void test_gather_p2p() {
     std::printf("gather_p2p: slots checked for 1..8 ranks, every root\n");
 }
 
+// ---- 7. stream state lifetime ------------------------------------------------------------
+struct FakeOps {
+    struct World {
+        std::map<void*, size_t> live;  // allocation -> bytes
+        std::map<void*, int> pending;  // stream -> work not yet drained
+        std::map<void*, bool> capturing;
+        std::vector<void*> freed_while_pending;  // buffers freed while their stream had work
+        std::map<void*, void*> owner;            // allocation -> stream that used it last
+        size_t allocs = 0, frees = 0, syncs = 0, device_syncs = 0;
+    };
+    World* w;
+    int alloc(void** p, size_t bytes) {
+        *p = std::malloc(bytes ? bytes : 1);
+        w->live[*p] = bytes;
+        ++w->allocs;
+        return 0;
+    }
+    void free(void* p) {
+        CHECK(w->live.count(p) == 1);  // never freed twice, never a foreign pointer
+        auto o = w->owner.find(p);
+        if (o != w->owner.end() && w->pending[o->second] > 0) w->freed_while_pending.push_back(p);
+        w->live.erase(p);
+        ++w->frees;
+        std::free(p);
+    }
+    int zero(void* p, size_t bytes, void* s) {
+        std::memset(p, 0, bytes);
+        w->owner[p] = s;
+        ++w->pending[s];
+        return 0;
+    }
+    int sync_stream(void* s) {
+        w->pending[s] = 0;
+        ++w->syncs;
+        return 0;
+    }
+    int sync_device(int) {
+        for (auto& kv : w->pending) kv.second = 0;
+        ++w->device_syncs;
+        return 0;
+    }
+    bool capturing(void* s) { return w->capturing.count(s) && w->capturing[s]; }
+};
+
+void test_stream_state_lifetime(std::mt19937_64& rng) {
+    using namespace karma::engine;
+    FakeOps::World world;
+    StreamStates<FakeOps> S(FakeOps{&world});
+    auto use = [&](int dev, uintptr_t key, void* s, size_t ws, size_t lb, bool fused) {
+        auto& st = S.get(dev, key, s);
+        CHECK(S.grow(st, st.ws, ws, ws + ws / 4, false) == 0);
+        world.owner[st.ws.p] = s;
+        ++world.pending[s];  // a kernel on s uses the workspace
+        if (lb) CHECK(S.grow(st, st.lb, lb, lb, true) == 0);
+        if (fused) CHECK(S.grow(st, st.fused, 4096, 4096, true) == 0);
+    };
+    // 1,000 streams, each used with growing batches, then released: everything is freed, and no
+    // buffer is freed while its stream still had work queued
+    for (int i = 0; i < 1000; ++i) {
+        void* s = reinterpret_cast<void*>(uintptr_t(0x10000 + 16 * i));
+        for (int k = 0; k < 4; ++k) use(0, (uintptr_t)s, s, 1000 + (rng() % 100000), (k + 1) * 2048, k == 2);
+        CHECK(S.release(0, (uintptr_t)s) == 0);
+    }
+    CHECK(S.states() == 0 && world.live.empty());
+    CHECK(world.freed_while_pending.empty());
+    CHECK(world.allocs == world.frees);
+    // a captured stream keeps what it outgrows until a trim without a graph hold
+    void* cs = reinterpret_cast<void*>(uintptr_t(0x900000));
+    use(1, (uintptr_t)cs, cs, 1000, 0, false);
+    world.capturing[cs] = true;
+    use(1, (uintptr_t)cs, cs, 1000, 0, false);  // (the capture is noticed)
+    world.capturing[cs] = false;
+    const size_t before = world.live.size();
+    use(1, (uintptr_t)cs, cs, 50000, 0, false);  // outgrown: kept
+    CHECK(world.live.size() == before + 1);
+    CHECK(S.hold(1, +1) == 1);
+    CHECK(S.trim(1) == 0);
+    CHECK(world.live.size() == before + 1);  // held
+    CHECK(S.hold(1, -1) == 0);
+    CHECK(S.trim(1) == 0);
+    CHECK(world.live.size() == before);  // freed
+    CHECK(S.hold(1, -5) == 0);            // never below zero
+    // a per-thread key orphaned at thread exit: freed by the next trim on its device only
+    const uintptr_t tkey = 0x13;
+    use(2, tkey, nullptr, 777, 4096, true);
+    use(3, tkey, nullptr, 999, 0, false);
+    S.orphan(tkey);
+    CHECK(S.zombies() == 2);
+    CHECK(S.trim(2) == 0);
+    CHECK(S.zombies() == 1);
+    CHECK(S.trim(3) == 0);
+    CHECK(S.zombies() == 0);
+    CHECK(S.release(1, (uintptr_t)cs) == 0);
+    CHECK(S.release(1, 12345) == 0);  // unknown: nothing to do
+    CHECK(world.live.empty() && world.allocs == world.frees);
+}
+
 int main() {
     std::mt19937_64 rng(20260131);
     test_host_crc(rng);
@@ -391,6 +495,7 @@ int main() {
     test_walk_plan();
     test_abi_without_device();
     test_gather_p2p();
+    test_stream_state_lifetime(rng);
     if (g_fail) {
         std::printf("host_logic_test: %d failures\n", g_fail);
         return 1;

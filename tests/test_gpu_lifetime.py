@@ -1,0 +1,244 @@
+"""Resource lifetime of the C ABI (karma_crc32c_release_stream / _trim / _graph_hold,
+include/karma_crc32c.h; the bookkeeping is karma_amd/csrc/stream_state.h, also driven under ASan
+by tests/cpp/host_logic_test.cc), and the fused segment fold's forward-progress contract under
+concurrency (include/karma_crc32c.h, karma_crc32c_stream).  The reference's crc32c::Extend
+allocates nothing (karma-util/crc32c.h:16); Karma's callers are long-lived io and connection
+threads (sivir.cc:137-153, connection.cc:14-79), so per-stream state must be releasable."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_lib
+import synth
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import karma_amd as K  # noqa: E402
+from karma_amd import _lib  # noqa: E402
+
+MIB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _eq(got, want):
+    got = np.asarray(got, dtype=np.uint32)
+    want = np.asarray(want, dtype=np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first {[(int(i), hex(int(got[i])), hex(int(want[i]))) for i in bad[:4]]}"
+
+
+def _hip():
+    h = ctypes.CDLL("libamdhip64.so")
+    h.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    h.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    return h
+
+
+def _free():
+    torch.cuda.synchronize()
+    return torch.cuda.mem_get_info()[0]
+
+
+def test_thousand_streams_released(dev):
+    """1,000 streams (created with hipStreamCreate, so every handle is new), each used by a
+    sorted and an unsorted ragged batch (byte grid, unit plan: workspace and look-back words), a
+    64 MiB segment scan (the fused combine's words) and a fixed batch, then released and
+    destroyed; WAL replays and appends in between (per-device contexts), then one trim: device
+    free memory returns to within 16 MiB of where it started."""
+    L = _lib.lib()
+    hip = _hip()
+    rng = np.random.default_rng(2)
+    n = 20000
+    lens = rng.integers(0, 3000, n).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 8)]).astype(np.uint64)
+    arena_bytes = int(offs[-1]) + int(lens[-1]) + 64
+    arena = torch.empty(max(arena_bytes, 64 * MIB), dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(arena, 17)
+    host = arena.cpu().numpy()
+    perm = rng.permutation(n)
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    d_off_p = torch.from_numpy(offs[perm].astype(np.int64)).to(dev)
+    d_len_p = torch.from_numpy(lens[perm].astype(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    out_p = torch.empty(n, dtype=torch.int32, device=dev)
+    seg_out = torch.empty(1, dtype=torch.int32, device=dev)
+    fix_out = torch.empty(4096, dtype=torch.int32, device=dev)
+    want = oracle_lib.ragged_crcs(host, offs, lens)
+    want_seg = oracle_lib.extend(0, host[: 64 * MIB].tobytes())
+    want_fix = oracle_lib.fixed_crcs(host[: 4096 * 4096], 4096)
+    total = int(lens.sum())
+    # a small WAL image for the per-device contexts (replay from host memory, then append)
+    seg = 1 << 16
+    plens = rng.integers(1, 500, 3000).astype(np.uint32)
+    poffs = np.concatenate([[0], np.cumsum(plens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    src = rng.integers(0, 256, int(plens.sum()) + 16, dtype=np.uint8)
+    wal = np.zeros(64 * seg, np.uint8)
+    cur, nf = ctypes.c_uint64(0), ctypes.c_size_t()
+    nrec, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+
+    def one_stream(sh):
+        _lib.check("ragged", L.karma_crc32c_batch_ragged(arena.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, total,
+                                                         None, 0, out.data_ptr(), sh))
+        _lib.check("ragged", L.karma_crc32c_batch_ragged(arena.data_ptr(), d_off_p.data_ptr(), d_len_p.data_ptr(), n,
+                                                         total, None, 0, out_p.data_ptr(), sh))
+        _lib.check("stream", L.karma_crc32c_stream(0, arena.data_ptr(), 64 * MIB, seg_out.data_ptr(), sh))
+        _lib.check("fixed", L.karma_crc32c_batch_fixed(arena.data_ptr(), 4096, 4096, None, 0, fix_out.data_ptr(), sh))
+
+    # warm-up: the per-device tables (kept for the process) exist before the baseline
+    s0 = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(s0)) == 0
+    one_stream(s0)
+    assert L.karma_crc32c_release_stream(-1, s0) == 0
+    assert hip.hipStreamDestroy(s0) == 0
+    assert L.karma_crc32c_trim(-1) == 0
+    base = _free()
+    worst = 0
+    for i in range(1000):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        one_stream(s)
+        if i % 250 == 0:
+            assert hip.hipStreamSynchronize(s) == 0
+            _eq(out.cpu().numpy().view(np.uint32), want)
+            _eq(out_p.cpu().numpy().view(np.uint32), want[perm])
+            assert int(seg_out.cpu().numpy().view(np.uint32)[0]) == want_seg
+            _eq(fix_out.cpu().numpy().view(np.uint32), want_fix)
+            cur.value = 0
+            _lib.check("wal_append", L.karma_wal_append_batch(src.ctypes.data, poffs.ctypes.data, plens.ctypes.data,
+                                                              plens.size, wal.ctypes.data, wal.nbytes, seg,
+                                                              ctypes.byref(cur), None, ctypes.byref(nf), 0))
+            _lib.check("wal_replay", L.karma_wal_replay(wal.ctypes.data, None, wal.nbytes, seg, 0, ctypes.byref(nrec),
+                                                        ctypes.byref(stop), ctypes.byref(status), None, 0, 0))
+            assert nrec.value == plens.size
+            worst = max(worst, base - _free())
+        assert L.karma_crc32c_release_stream(-1, s) == 0
+        assert hip.hipStreamDestroy(s) == 0
+    assert L.karma_crc32c_trim(-1) == 0
+    after = _free()
+    assert base - after < 16 * MIB, f"{(base - after) / MIB:.1f} MiB not returned (peak {(worst) / MIB:.1f} MiB)"
+
+
+def test_per_thread_stream_state_is_freed_after_thread_exit(dev):
+    """hipStreamPerThread state is per calling thread; a thread that exits hands it to the next
+    trim (its stream is gone)."""
+    L = _lib.lib()
+    ptds = ctypes.c_void_p(2)  # hipStreamPerThread
+    arena = torch.empty(64 * MIB, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(arena, 5)
+    want = oracle_lib.extend(0, arena.cpu().numpy().tobytes())
+    outs = [torch.empty(1, dtype=torch.int32, device=dev) for _ in range(8)]
+    assert L.karma_crc32c_trim(-1) == 0
+    base = _free()
+    errs = []
+
+    def work(k):
+        try:
+            for _ in range(3):
+                _lib.check("stream", L.karma_crc32c_stream(0, arena.data_ptr(), arena.numel(), outs[k].data_ptr(), ptds))
+            torch.cuda.synchronize()
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for o in outs:
+        assert int(o.cpu().numpy().view(np.uint32)[0]) == want
+    assert L.karma_crc32c_trim(-1) == 0
+    assert base - _free() < 16 * MIB
+
+
+def test_graph_hold_keeps_outgrown_buffers(dev):
+    """A ragged call captured on a stream, then a larger uncaptured call on it (the workspace
+    grows): the graph still replays exactly, also across a trim under a graph hold; after the hold
+    is dropped a trim frees the outgrown buffer."""
+    L = _lib.lib()
+    rng = np.random.default_rng(4)
+    n = 30000
+    arena_bytes = 48 * MIB
+    arena = torch.empty(arena_bytes, dtype=torch.uint8, device=dev)
+    lens = rng.integers(0, 600, n).astype(np.uint32)
+    offs = rng.integers(0, arena_bytes - 600, n).astype(np.uint64)
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.uint32, device=dev)
+    s = torch.cuda.Stream()
+    K.fill_splitmix64(arena, 1)
+    with torch.cuda.stream(s):
+        K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=int(lens.sum()), stream=s)
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=int(lens.sum()), stream=s)
+    assert L.karma_crc32c_graph_hold(-1, 1) == 1
+    big_l = rng.integers(0, 20000, 4 * n).astype(np.uint32)
+    big_o = rng.integers(0, arena_bytes - 20000, big_l.size).astype(np.uint64)
+    with torch.cuda.stream(s):  # grows the stream's workspace: the old one is retired, not freed
+        K.extend_batch_ragged(arena, torch.from_numpy(big_o.astype(np.int64)).to(dev),
+                              torch.from_numpy(big_l.astype(np.int32)).to(dev), total_len=int(big_l.sum()), stream=s)
+    s.synchronize()
+    assert L.karma_crc32c_trim(-1) == 0  # held: the graph's buffers stay
+    for seed in (2, 3):
+        K.fill_splitmix64(arena, seed)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        _eq(out.cpu().numpy(), oracle_lib.ragged_crcs(arena.cpu().numpy(), offs, lens))
+    del g
+    torch.cuda.synchronize()
+    assert L.karma_crc32c_graph_hold(-1, -1) == 0
+    before = _free()
+    assert L.karma_crc32c_trim(-1) == 0
+    assert _free() >= before  # the outgrown workspace went back
+    assert L.karma_crc32c_release_stream(-1, s.cuda_stream) == 0
+
+
+def test_segment_scans_on_four_streams_concurrently(dev):
+    """The fused segment fold (one kernel whose last workgroup waits on the others' tagged states)
+    launched on 4 streams at once, 16 times each with no synchronisation between launches, beside
+    a ragged batch on a fifth stream: every CRC exact (include/karma_crc32c.h's forward-progress
+    contract: other kernels only delay the workgroups waited for)."""
+    seg, nseg = 64 << 20, 16
+    buf = torch.empty(seg * nseg, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 31)
+    want = oracle_lib.splitmix_fixed_crcs(31, seg, 0, nseg, threads=16)
+    streams = [torch.cuda.Stream() for _ in range(5)]
+    outs = [torch.full((nseg,), -1, dtype=torch.int32, device=dev) for _ in range(4)]
+    rng = np.random.default_rng(9)
+    lens = synth.loguniform_lengths(3, 40000, 64, 65536).astype(np.uint32)
+    offs, arena_bytes = synth.ragged_layout(lens, header=8)
+    assert arena_bytes <= buf.numel()
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    rout = torch.empty(lens.size, dtype=torch.uint32, device=dev)
+    host = buf[:arena_bytes + 16].cpu().numpy()
+    want_r = oracle_lib.ragged_crcs(host, offs, lens)
+    torch.cuda.synchronize()
+    for i in range(nseg):
+        for k, st in enumerate(streams[:4]):
+            j = (i + 5 * k) % nseg
+            _lib.check("stream", _lib.lib().karma_crc32c_stream(0, buf.data_ptr() + j * seg, seg,
+                                                                 outs[k].data_ptr() + 4 * j, st.cuda_stream))
+        if i % 4 == 0:
+            with torch.cuda.stream(streams[4]):
+                K.extend_batch_ragged(buf, d_off, d_len, out=rout, total_len=int(lens.sum()), stream=streams[4])
+    torch.cuda.synchronize()
+    for k in range(4):
+        _eq(outs[k].cpu().numpy().view(np.uint32), want)
+    _eq(rout.cpu().numpy(), want_r)
+    for st in streams:
+        assert _lib.lib().karma_crc32c_release_stream(-1, st.cuda_stream) == 0
