@@ -603,6 +603,40 @@ class GatherPipeline:
         self.sync.record(self.gathered[slot], self.sync.gather_stream)
 
 
+def shard_self_check(arena, out, rec: int, n_rec: int, value, seed: int = 1, first: int = 64, rand: int = 64):
+    """A sampled set of this rank's records checked after timing: the device CRCs of the first
+    `first` records and `rand` random ones against value(bytes) (the host crc32c::Value of the
+    product library: include/karma-util/crc32c.h).  arena / out are tensors (the rank's shard and
+    its CRCs, on the device on the box; CPU tensors in tests/test_bench_pipeline.py).  Returns the
+    record indices, their device CRCs (so rank 0 can check the gathered copy) and the mismatches."""
+    import torch
+    idx = np.unique(np.concatenate([np.arange(min(first, n_rec)),
+                                    np.random.default_rng(seed).integers(0, n_rec, rand)])).astype(np.int64)
+    o = out.view(torch.int32) if out.dtype == torch.uint32 else out  # (uint32 tensors index poorly)
+    got = o[torch.from_numpy(idx).to(out.device)].cpu().numpy().astype(np.int64).astype(np.uint32)
+    bad = 0
+    for j, r in enumerate(idx):
+        b = arena[int(r) * rec:(int(r) + 1) * rec].cpu().numpy()
+        bad += int(int(value(b)) != int(got[j]))
+    return {"idx": idx.tolist(), "crc": [int(x) for x in got], "mismatches": bad}
+
+
+def aggregate_self_checks(checks, gathered=None, n_rec: int = 0):
+    """Rank 0's view of every rank's shard_self_check (all-gathered): per rank the records
+    sampled and mismatches, the totals, and -- with the CRCs rank 0 gathered over RCCL
+    (`gathered`, n_rec per rank in rank order) -- how many sampled CRCs differ in the gathered
+    copy (a gather that misplaces or corrupts a shard shows here)."""
+    per_rank = [{"sampled_records": len(c["idx"]), "mismatches": int(c["mismatches"])} for c in checks]
+    total = {"sampled_records": sum(p["sampled_records"] for p in per_rank),
+             "mismatches": sum(p["mismatches"] for p in per_rank), "ranks": len(checks),
+             "check": "per rank: the first 64 and 64 random records of its shard, device CRC vs host crc32c::Value"}
+    if gathered is not None:
+        g = np.asarray(gathered)
+        total["gather_mismatches"] = int(sum(int(g[r * n_rec + i]) != int(v) for r, c in enumerate(checks)
+                                             for i, v in zip(c["idx"], c["crc"])))
+    return per_rank, total
+
+
 def main():
     args = parse()
     import torch
@@ -886,14 +920,21 @@ def main():
         got = cur["out"].cpu().numpy()
         bad = sum(int(K.Value(arena[i * rec:(i + 1) * rec].cpu().numpy()) != int(got[i])) for i in range(4))
         check = {"sampled_records": 4, "mismatches": bad}
-    if out is not None and rank == 0 and wl in ("fixed", "stream"):
-        idx = np.unique(np.concatenate([np.arange(min(64, n_rec)), np.random.default_rng(1).integers(0, n_rec, 64)]))
-        got = cur["out"].cpu().numpy()
-        bad = 0
-        for r in idx[: 16 if wl == "stream" else len(idx)]:
-            b = arena[int(r) * rec:(int(r) + 1) * rec].cpu().numpy()
-            bad += int(K.Value(b) != int(got[r]))
-        check = {"sampled_records": int(len(idx[: 16 if wl == "stream" else len(idx)])), "mismatches": bad}
+    rank_checks = None
+    if out is not None and wl in ("fixed", "stream"):
+        # every rank checks a sample of its own shard; rank 0 also checks those records in the
+        # CRCs it gathered (N > 1), so the line proves every shard, not only rank 0's
+        mine = shard_self_check(arena, cur["out"], rec, n_rec, K.Value, seed=1 + rank,
+                                rand=64 if wl == "fixed" else 0, first=64 if wl == "fixed" else 16)
+        if world > 1:
+            rank_checks = [None] * world
+            dist.all_gather_object(rank_checks, mine)
+            if rank == 0:
+                g = gather_buf.cpu().numpy() if gather_buf is not None else None
+                per, check = aggregate_self_checks(rank_checks, g, n_rec)
+                per_rank["self_check"] = per
+        else:
+            check = {"sampled_records": len(mine["idx"]), "mismatches": mine["mismatches"]}
 
     if rank == 0:
         total_bytes = payload * world * args.steps

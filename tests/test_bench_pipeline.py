@@ -132,3 +132,61 @@ def test_bench_defaults_to_config5_shard_on_8_gpus():
     assert bench.records_per_gpu(0, 1, "fixed") == (1 << 20, False)
     assert bench.records_per_gpu(0, 4, "fixed") == (1 << 20, False)
     assert bench.records_per_gpu(12345, 8, "fixed") == (12345, False)
+
+
+def _check_worker(rank, world, port, q):
+    """Each rank: its shard's bytes and CRCs (oracle CRCs standing in for the device batch; rank 1
+    corrupts one sampled CRC), shard_self_check with the oracle standing in for the host Value,
+    all_gather_object, and rank 0 aggregates against a gathered copy (as RCCL's gather leaves it)
+    -- once intact, once with a shard misplaced."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    try:
+        import synth
+        n_local = 700
+        lo = rank * n_local
+        arena = torch.from_numpy(synth.splitmix_np(42, lo * REC, n_local * REC).copy())
+        crcs = oracle_lib.splitmix_fixed_crcs(42, REC, lo, n_local).astype(np.int64)
+        out = torch.from_numpy(crcs.copy())
+        if rank == 1:
+            out[3] ^= 1  # a wrong device CRC in a sampled record (the first 64 are always sampled)
+        mine = bench.shard_self_check(arena, out, REC, n_local, lambda b: oracle_lib.extend(0, b.tobytes()),
+                                      seed=1 + rank)
+        checks = [None] * world
+        dist.all_gather_object(checks, mine)
+        full = [torch.zeros(n_local, dtype=torch.int64) for _ in range(world)] if rank == 0 else None
+        dist.gather(out, full, dst=0)
+        res = None
+        if rank == 0:
+            gathered = torch.cat(full).numpy()
+            per, tot = bench.aggregate_self_checks(checks, gathered, n_local)
+            swapped = np.concatenate([gathered[n_local:], gathered[:n_local]])  # shards in the wrong order
+            _, tot_bad = bench.aggregate_self_checks(checks, swapped, n_local)
+            res = (per, tot["mismatches"], tot["gather_mismatches"], tot_bad["gather_mismatches"] > 100,
+                   tot["sampled_records"])
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_self_check_every_shard_world2():
+    """bench.py's N > 1 self-check: every rank samples its own shard after timing, rank 0 reports
+    each rank's result (per_rank.self_check) and checks the sampled records in the CRCs it
+    gathered, so one wrong shard or a misplaced gather shows in the line."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_check_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict(q.get(timeout=10) for _ in range(world))
+    per, mism, gmism, swapped_seen, sampled = got[0]
+    assert [p["mismatches"] for p in per] == [0, 1]
+    assert all(p["sampled_records"] >= 64 for p in per) and sampled == sum(p["sampled_records"] for p in per)
+    assert mism == 1 and gmism == 0 and swapped_seen
+    assert got[1] is None
