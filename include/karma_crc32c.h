@@ -181,7 +181,8 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
  * page-locking of the caller's buffer).  seg_bytes < 2^31.
  * Outputs: *h_n_records type-0 records accepted, their header offsets in h_rec_off
  * (optional, up to rec_cap), *h_stop the WAL offset where replay stops (the writer's
- * resume point), *h_status KARMA_WAL_*.  Keeps the reference's size-0 quirk (the CRC
+ * resume point; up to 4 bytes past wal_bytes when an accepted size-0 record ends the image,
+ * and such a stop is accepted back as `start`: it replays nothing), *h_status KARMA_WAL_*.  Keeps the reference's size-0 quirk (the CRC
  * of an empty type-0 record is taken over the stale 4-byte len/type word). */
 int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,

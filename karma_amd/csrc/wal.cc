@@ -159,6 +159,7 @@ struct ReplayCtx {
     hipStream_t st = nullptr;
     DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, sum;
     DevBuf h_small;                             // pinned readback of the summary
+    uint64_t img_gen = 0;                       // uploads of a host image into img so far
     int init(int dev) {
         if (ready) return 0;
         hipDeviceProp_t prop;
@@ -176,6 +177,7 @@ struct ReplayCtx {
             b->release();
         (void)hipStreamDestroy(st);
         st = nullptr;
+        ++img_gen;  // a replay between passes must not take the freed image for its own
         ready = false;
     }
 };
@@ -204,9 +206,14 @@ namespace {
 // image is streamed into HBM through the library's pinned staging (host_stage.h).
 using ImageFill = karma::engine::HostFill;
 
+// A host image already in the replay context's device buffer (replay_core's later passes reuse it):
+// its first segment and the context's upload count when it was uploaded (gen 0: none).
+struct Uploaded {
+    uint64_t seg = 0, gen = 0;
+};
 int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
-                int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned);
+                int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned, Uploaded* up);
 
 // sivir::open's loop (sivir.cc:31-41) as device passes.  One pass replays from `start` until
 // scan_record would return false, or until an accepted size-0 record carries the chain past a
@@ -214,17 +221,20 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
 // (it advances record.size() = 12, wal.cc:66 / sivir.cc:38), so the next pass starts there.
 // The records of all passes are concatenated.  A chain carried past the image's last segment
 // ends replay (scan_record finds no segment, wal.cc:86) with the stop offset past wal_bytes,
-// where sivir::open's start_wal_offset is left.
+// where sivir::open's start_wal_offset is left.  A host image is streamed into HBM once: the later
+// passes start at or past the first one's segment and walk the copy already there.
 int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                 int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned = nullptr) {
     uint64_t total = 0;
+    Uploaded up;
     while (true) {
         uint64_t n = 0, stop = 0;
         int status = 0;
         const uint64_t got = std::min<uint64_t>(total, rec_cap);
         if (const int rc = replay_pass(d_wal, fill, wal_bytes, seg_bytes, start, &n, &stop, &status,
-                                       h_rec_off ? h_rec_off + got : nullptr, rec_cap - got, device, tuning, h_pinned))
+                                       h_rec_off ? h_rec_off + got : nullptr, rec_cap - got, device, tuning, h_pinned,
+                                       &up))
             return rc;
         total += n;
         if (status != (int)karma::engine::kWalSpill) {
@@ -257,8 +267,10 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
 int karma_wal_replay_tuned(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                            uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                            int device, const karma_wal_tuning* tuning) {
+    // (start may lie up to 4 bytes past the image: where replay stops after an accepted size-0
+    // record at the image end, wal.cc:66 / sivir.cc:38; such a stop is a valid start, replaying nothing)
     if ((!h_wal && !d_wal) || !h_n_records || !h_stop || !h_status || seg_bytes < 1 || wal_bytes % seg_bytes ||
-        start > wal_bytes || seg_bytes >= (uint64_t(1) << 31) ||
+        start > wal_bytes + 4 || seg_bytes >= (uint64_t(1) << 31) ||
         (tuning && (tuning->crc_batch < 0 || tuning->crc_batch > KARMA_WAL_CRC_INLINE)))
         return fail(KARMA_E_INVALID, "wal_replay");
     const uint8_t* src = static_cast<const uint8_t*>(h_wal);
@@ -281,7 +293,7 @@ namespace {
 // out are relative to the image start.
 int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                 uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
-                int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned) {
+                int device, const karma_wal_tuning* tuning, const uint8_t* h_pinned, Uploaded* up) {
     using namespace karma::engine;
     const uint64_t nseg = wal_bytes / seg_bytes;
     const uint64_t s0 = std::min<uint64_t>(start / seg_bytes, nseg);
@@ -306,8 +318,14 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     // 0. the image in HBM: the caller's copy, or the host image streamed in
     if (d_wal) {
         A.wal = static_cast<const uint8_t*>(d_wal) + base0;
+    } else if (up && up->gen && up->gen == c.img_gen && s0 >= up->seg) {
+        // a later pass of the same replay: the image is still in the context's buffer (no other
+        // upload since, the context's lock held by each pass)
+        A.wal = c.img.as<const uint8_t>() + (s0 - up->seg) * seg_bytes;
     } else {
         if (const int rc = c.img.ensure(img_bytes)) return rc;
+        ++c.img_gen;
+        if (up) *up = Uploaded{s0, c.img_gen};
         if (h_pinned) {
             if (hipMemcpyAsync(c.img.p, h_pinned + base0, img_bytes, hipMemcpyHostToDevice, c.st) != hipSuccess ||
                 hipStreamSynchronize(c.st) != hipSuccess)
@@ -330,8 +348,10 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     // build's other walk / small-record kernels, and KARMA_WAL_CRC_SEPARATE, walk first and
     // then run one small-record batch over the gathered lists (the round-2 path).
     const bool dev_plan = img_bytes <= kDevicePlanMax && batch != KARMA_WAL_CRC_UNITS;
-    const bool inline_crc =
-        dev_plan && batch == KARMA_WAL_CRC_INLINE && KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 0;
+    // (k_wal_plan packs the inline path's first mismatch as ordinal << 24 | segment: fewer than
+    // 2^24 segments, else the gathered batch)
+    const bool inline_crc = dev_plan && batch == KARMA_WAL_CRC_INLINE && nwork < (uint64_t(1) << 24) &&
+                            KARMA_AB_KNOB("KARMA_WALK_VARIANT", 0) == 0;
     // the walkers' lists checksummed after the walk by the LDS-staged kernel (k_wal_list_crc)
     // instead of by the walkers themselves (k_wal_walk_crc)
     const bool list_crc = inline_crc && KARMA_AB_KNOB("KARMA_WAL_LIST_CRC", 0) != 0;

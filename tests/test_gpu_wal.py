@@ -515,4 +515,8 @@ def test_replay_accepted_size0_records_advance_12(lib, seg, walk, monkeypatch):
         for start in (zs[len(zs) // 2], zs[-1], zs[-1] + 12 if zs[-1] + 12 <= wal.size else zs[-1]):
             ws = wal_model.replay(wal.tobytes(), seg, start)
             assert _replay(lib, wal, start=start, seg=seg) == (list(ws[0]), ws[1], ws[2]), start
+        # a stop past the image end (a size-0 record in the last 11 bytes) is a valid start:
+        # replaying from it finds nothing (sivir::open's next scan_record returns false)
+        for past in range(1, 5):
+            assert _replay(lib, wal, start=wal.size + past, seg=seg) == ([], wal.size + past, 0)
     assert spills > 0, "some size-0 record must carry the chain into the next segment"
