@@ -402,10 +402,11 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap, uint64_t tile_cap = 0) 
     return L;
 }
 
-// Tiles the byte grid may need for a batch of total_len bytes: the records' bytes plus an
-// eighth for the headers and gaps between them (a batch whose span needs more takes the unit
-// plan: k_ragged_grid_plan checks it), and the partial tiles at both ends.
-uint64_t grid_tile_cap(uint64_t total_len) { return ceil_div(total_len + total_len / 8, kGridTile) + 2; }
+// Tiles the byte grid may stream for a batch of n records, total_len bytes: a span of up to twice
+// the records' bytes plus 64 bytes per record for the headers and gaps between them, and the
+// partial tiles at both ends.  A batch spread wider takes the unit plan (k_ragged_grid_plan
+// checks it): the grid reads every byte of the span, the unit plan costs per record.
+uint64_t grid_tile_cap(uint64_t total_len, uint64_t n_rec) { return ceil_div(2 * total_len + 64 * n_rec, kGridTile) + 2; }
 
 void bind_grid(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t tile_cap, const uint32_t* gcomb) {
     char* b = static_cast<char*>(ws);
@@ -471,7 +472,7 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         cap = cap_full + 2 * n_rec;
         // the byte grid is tried first when the batch may be sorted (the tools build's
         // KARMA_RAGGED_GRID=0 turns it off for A/B)
-        const uint64_t tile_cap = n_rec < (1ull << 31) && KARMA_AB_KNOB("KARMA_RAGGED_GRID", 1) ? grid_tile_cap(total_len) : 0;
+        const uint64_t tile_cap = n_rec < (1ull << 31) && KARMA_AB_KNOB("KARMA_RAGGED_GRID", 1) ? grid_tile_cap(total_len, n_rec) : 0;
         const RaggedLayout L = ragged_layout(n_rec, cap, tile_cap);
         KARMA_RC(workspace(dev, s, L.total, &ws));
         bind_ragged(a, ws, L, cap);

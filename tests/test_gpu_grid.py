@@ -137,7 +137,7 @@ def test_batches_outside_the_grid_take_the_unit_plan(raw, case):
     elif case == "gap":
         offs[4000:] += np.uint64(2049)
     elif case == "low_total":
-        total = int(lens.sum()) // 2  # the grid's tiles do not fit its tile table
+        total = int(lens.sum()) // 4  # the grid's tiles do not fit its tile table
     else:  # the same record twice
         offs[2000] = offs[1999]
         lens[2000] = lens[1999]
