@@ -16,6 +16,8 @@
  *   karma_crc32c_*_sharded / gather the same, records sharded over GPUs, CRCs gathered over RCCL
  *   karma_wal_append_batch          sivir::build_sqe + segment_file::append_record   sivir.cc:276-317
  *   karma_wal_replay                sivir::open's wal::scan_record loop              sivir.cc:31-41, wal.cc:34-87
+ *   karma_wal_replay_multi          the same over several devices of one process
+ *   karma_crc32c_*_host_multi       sivir::build_sqe's batch over several devices    sivir.cc:276-317
  *   karma_wal_replay_dir            wal::load_from_path + the same loop              wal.cc:9-27
  *   karma_kfp_encode_batch          transport::frame::encode                         frame.cc:41-60
  *   karma_kfp_parse_batch           connection::read_frame's frame::parse loop       connection.cc:20-27, frame.cc:62-130
@@ -136,6 +138,17 @@ int karma_crc32c_batch_fixed_host(const void* h_data, size_t rec_bytes, size_t n
 int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, const uint64_t* h_off,
                                    const uint32_t* h_len, size_t n_rec, uint32_t init, uint32_t* h_out, int device);
 
+/* The same over several devices of this process (one host thread per device, each device's
+ * PCIe link, staging and streams at once): the records are cut into contiguous ranges -- equal
+ * counts (fixed) or equal bytes (ragged) -- one per listed device, and the CRCs written into
+ * h_out in record order.  A device may be listed more than once (its shares then run one
+ * after the other).  Synchronous; any share's failure fails the call. */
+int karma_crc32c_batch_fixed_host_multi(const void* h_data, size_t rec_bytes, size_t n_rec, uint32_t init,
+                                        uint32_t* h_out, const int* devices, int n_dev);
+int karma_crc32c_batch_ragged_host_multi(const void* h_arena, size_t arena_bytes, const uint64_t* h_off,
+                                         const uint32_t* h_len, size_t n_rec, uint32_t init, uint32_t* h_out,
+                                         const int* devices, int n_dev);
+
 /* ---- multi-GPU: one process per GPU, RCCL over xGMI ---------------------- */
 int karma_crc32c_get_unique_id(void* uid, size_t uid_bytes);
 int karma_crc32c_comm_init(karma_comm_t* comm, int nranks, const void* uid, int rank);
@@ -187,6 +200,16 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
 int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
                      int device);
+
+/* karma_wal_replay of a host image over several devices: the segments from start's segment on
+ * are cut into contiguous ranges, one per listed device, replayed at once (each range streamed
+ * over its own device's link), and merged in WAL order: a range's records count while every
+ * range before it ended cleanly at its last segment's end, as the one-device replay would have
+ * walked on.  When an accepted size-0 record carries the chain 1-4 bytes past a range's end the
+ * rest is replayed from there on devices[0].  Same outputs as karma_wal_replay. */
+int karma_wal_replay_multi(const void* h_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start, uint64_t* h_n_records,
+                           uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap, const int* devices,
+                           int n_dev);
 
 /* Plan overrides of karma_wal_replay_tuned.  Every setting gives the same result (the
  * replay is exact whatever the plan); they exist for tests and tuning.  Zero = the

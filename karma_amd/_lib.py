@@ -57,6 +57,10 @@ SIGNATURES = {
     "karma_crc32c_graph_hold": (_i, [_i, _i]),
     "karma_crc32c_batch_fixed_host": (_i, [_vp, _sz, _sz, _u32, _vp, _i]),
     "karma_crc32c_batch_ragged_host": (_i, [_vp, _sz, _vp, _vp, _sz, _u32, _vp, _i]),
+    "karma_crc32c_batch_fixed_host_multi": (_i, [_vp, _sz, _sz, _u32, _vp, _vp, _i]),
+    "karma_crc32c_batch_ragged_host_multi": (_i, [_vp, _sz, _vp, _vp, _sz, _u32, _vp, _vp, _i]),
+    "karma_wal_replay_multi": (_i, [_vp, _sz, _sz, _u64, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_i), _vp, _sz,
+                                    _vp, _i]),
     "karma_crc32c_get_unique_id": (_i, [_vp, _sz]),
     "karma_crc32c_comm_init": (_i, [_c.POINTER(_vp), _i, _vp, _i]),
     "karma_crc32c_comm_destroy": (_i, [_vp]),

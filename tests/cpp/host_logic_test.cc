@@ -18,7 +18,12 @@
 //      _graph_hold) through a recording allocator: 1,000 streams created, used with every kind
 //      of growth, released; captured streams keep outgrown buffers until a trim with no graph
 //      hold; exited threads' state is freed by the next trim; nothing leaks or is freed twice
-//      (ASan would also report either).
+//      (ASan would also report either);
+//   8. the multi-device host batches' split and merge (multi_dev.h) through stubs of the
+//      one-device calls: ranges cover the batch once in order, byte-balanced cuts, the shares'
+//      CRCs land in record order, a failing share fails the call with its detail, and replay
+//      shares merge as one sequential replay would (clean ends, a stop inside a range, a spill
+//      past a range's end handed back).
 #include <hip/hip_runtime_api.h>
 #include <unistd.h>
 
@@ -27,6 +32,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
+#include <thread>
 #include <random>
 #include <string>
 #include <vector>
@@ -34,6 +41,7 @@
 #include "engine.h"
 #include "gather_p2p.h"
 #include "stream_state.h"
+#include "multi_dev.h"
 #include "karma-util/crc32c.h"
 #include "karma_crc32c.h"
 #include "wal_place.h"
@@ -264,6 +272,11 @@ void test_abi_without_device() {
     std::fclose(f);
     CHECK(karma_wal_replay_dir(dir, 0, 8192, &base, &nrec, &stop, &status, recoff, 100, 0) == KARMA_E_NO_DEVICE);
     CHECK(karma_wal_replay_dir(dir, 0, 0, &base, &nrec, &stop, &status, recoff, 100, 0) == KARMA_E_INVALID);
+    const int devs[2] = {0, 1};
+    CHECK(karma_crc32c_batch_fixed_host_multi(src.data(), 300, 100, 0, out.data(), devs, 2) == KARMA_E_NO_DEVICE);
+    CHECK(karma_crc32c_batch_fixed_host_multi(src.data(), 300, 100, 0, out.data(), devs, 0) == KARMA_E_INVALID);
+    CHECK(karma_wal_replay_multi(wal.data(), wal.size(), 4096, 0, &nrec, &stop, &status, recoff, 100, devs, 2) ==
+          KARMA_E_NO_DEVICE);
     for (int i = 0; i < 3; ++i) unlink((std::string(dir) + "/" + std::to_string(8192 + i * 4096)).c_str());
     unlink((std::string(dir) + "/LOCK").c_str());
     rmdir(dir);
@@ -487,6 +500,107 @@ void test_stream_state_lifetime(std::mt19937_64& rng) {
     CHECK(world.live.empty() && world.allocs == world.frees);
 }
 
+// ---- 8. multi-device split and merge -------------------------------------------------------
+void test_multi_device_split(std::mt19937_64& rng) {
+    using namespace karma::engine;
+    // contiguous equal-count ranges
+    for (size_t n : {0ul, 1ul, 7ul, 8ul, 1000ul, 1000003ul})
+        for (int parts = 1; parts <= 9; ++parts) {
+            size_t prev = 0;
+            for (int k = 0; k < parts; ++k) {
+                const size_t lo = share_lo(n, parts, k), hi = share_lo(n, parts, k + 1);
+                CHECK(lo == prev && hi >= lo && hi - lo <= n / parts + 1);
+                prev = hi;
+            }
+            CHECK(prev == n);
+        }
+    // byte-balanced cuts: non-decreasing, cover [0, n), each share within one record of total/parts
+    for (int trial = 0; trial < 200; ++trial) {
+        const size_t n = rng() % 3000;
+        std::vector<uint32_t> len(n);
+        uint64_t total = 0;
+        for (auto& l : len) total += (l = (uint32_t)(rng() % 2 ? rng() % 100 : rng() % 70000));
+        uint32_t mx = 0;
+        for (uint32_t l : len) mx = std::max(mx, l);
+        const int parts = 1 + (int)(rng() % 8);
+        const auto cuts = byte_balanced_cuts(len.data(), n, parts);
+        CHECK(cuts.size() == (size_t)parts + 1 && cuts[0] == 0 && cuts[parts] == n);
+        for (int k = 0; k < parts; ++k) {
+            CHECK(cuts[k] <= cuts[k + 1]);
+            uint64_t b = 0;
+            for (size_t r = cuts[k]; r < cuts[k + 1]; ++r) b += len[r];
+            CHECK(b <= total / parts + mx + 1);
+        }
+    }
+    // the shares' results land in record order; a failing share fails with its own detail
+    std::vector<uint32_t> out(10007, 0);
+    const int parts = 5;
+    std::string what;
+    int rc = run_shares(
+        parts,
+        [&](int k) {
+            for (size_t r = share_lo(out.size(), parts, k); r < share_lo(out.size(), parts, k + 1); ++r) out[r] = (uint32_t)r * 3u;
+            return 0;
+        },
+        [] { return std::string("none"); }, &what);
+    CHECK(rc == 0);
+    for (size_t r = 0; r < out.size(); ++r) CHECK(out[r] == r * 3u);
+    // (the detail is read on the failing share's own thread, right after its call)
+    std::vector<std::thread::id> ids(parts);
+    std::vector<std::string> tag(parts);
+    std::mutex mu;
+    rc = run_shares(
+        parts,
+        [&](int k) {
+            std::lock_guard<std::mutex> g(mu);
+            ids[k] = std::this_thread::get_id();
+            tag[k] = "share-" + std::to_string(k);
+            return k == 3 || k == 4 ? -3 - k : 0;
+        },
+        [&] {
+            std::lock_guard<std::mutex> g(mu);
+            for (int k = 0; k < parts; ++k)
+                if (ids[k] == std::this_thread::get_id()) return tag[k];
+            return std::string("?");
+        },
+        &what);
+    CHECK(rc == -6 && what == "device share 3: share-3");
+    // replay shares: whole segments from start's segment, contiguous, start kept in share 0
+    const uint64_t seg = 4096;
+    for (uint64_t nseg : {1ull, 2ull, 5ull, 64ull})
+        for (uint64_t start : {0ull, 100ull, 4096ull * 1 + 17})
+            for (int p : {1, 2, 3, 8}) {
+                if (start >= nseg * seg) continue;
+                auto sh = replay_shares(nseg * seg, seg, start, p);
+                CHECK(!sh.empty() && sh[0].start == start && sh[0].lo == start / seg * seg && sh.back().hi == nseg * seg);
+                for (size_t k = 0; k < sh.size(); ++k) {
+                    CHECK(sh[k].hi > sh[k].lo && sh[k].lo % seg == 0 && sh[k].hi % seg == 0);
+                    if (k) CHECK(sh[k].lo == sh[k - 1].hi && sh[k].start == sh[k].lo);
+                }
+            }
+    // merge: clean ends chain the shares; a stop inside a range ends replay there; a stop past a
+    // range's end is handed back (-1)
+    auto mk = [](uint64_t lo, uint64_t hi, uint64_t n, uint64_t stop, int st) {
+        ReplayShare s;
+        s.lo = lo;
+        s.hi = hi;
+        s.n = n;
+        s.stop = stop;
+        s.status = st;
+        for (uint64_t i = 0; i < n; ++i) s.rec.push_back(lo + 16 * i);
+        return s;
+    };
+    uint64_t n = 0, stop = 0, rec[64];
+    int st = 0;
+    std::vector<ReplayShare> sh = {mk(0, 100, 3, 100, 0), mk(100, 200, 2, 200, 0), mk(200, 300, 4, 300, 0)};
+    CHECK(merge_replays(sh, 300, &n, &stop, &st, rec, 64, 0) == 2 && n == 9 && stop == 300 && st == 0);
+    CHECK(rec[0] == 0 && rec[3] == 100 && rec[5] == 200 && rec[8] == 248);
+    sh = {mk(0, 100, 3, 100, 0), mk(100, 200, 2, 150, 1), mk(200, 300, 4, 300, 0)};
+    CHECK(merge_replays(sh, 300, &n, &stop, &st, rec, 4, 0) == 1 && n == 5 && stop == 150 && st == 1);
+    sh = {mk(0, 100, 3, 102, 0), mk(100, 200, 2, 200, 0)};
+    CHECK(merge_replays(sh, 200, &n, &stop, &st, nullptr, 0, 0) == -1 && n == 3 && stop == 102);
+}
+
 int main() {
     std::mt19937_64 rng(20260131);
     test_host_crc(rng);
@@ -496,6 +610,7 @@ int main() {
     test_abi_without_device();
     test_gather_p2p();
     test_stream_state_lifetime(rng);
+    test_multi_device_split(rng);
     if (g_fail) {
         std::printf("host_logic_test: %d failures\n", g_fail);
         return 1;
