@@ -603,22 +603,29 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
         };
         pick(0);
         uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        // this lane's window of chunk c as the current record sees it (windows past its end or
+        // wholly before its start are not stepped; masks only at its edges)
+        auto step_cur = [&](int32_t w, const u32x4& v) {
+            if (w < ((ce + 15) & ~15) && w + 16 > cp) {
+                u32x4 x = v;
+                if (w < cp + 4 || w + 16 > ce) x = grid_mask(v, w, cp, ce, cinj);
+                step4(lds, X, a0, a1, a2, a3, x);
+            }
+        };
         auto process = [&](uint32_t c, const u32x4& v) {
+            if (!active) return;
             const int32_t w = (int32_t)(c * kChunk + l * 16), cnext = (int32_t)((c + 1) * kChunk);
-            bool go = active;
-            while (go) {
-                const int32_t cend = (ce + 15) & ~15;
-                if (w < cend && w + 16 > cp) {
-                    u32x4 x = v;
-                    if (w < cp + 4 || w + 16 > ce) x = grid_mask(v, w, cp, ce, cinj);
-                    step4(lds, X, a0, a1, a2, a3, x);
-                }
-                if (cend > cnext) break;  // the record runs past this chunk
-                const uint32_t R = grid_fold(lds, l, ((uint32_t)(cend - 16) >> 4) & (kGroupLanes - 1), a0, a1, a2, a3);
+            step_cur(w, v);
+            // the record's last window is in this chunk: its register, then the records starting
+            // in the same chunk (the rare path: most chunks hold no record end)
+            while (((ce + 15) & ~15) <= cnext) {
+                const uint32_t R = grid_fold(lds, l, ((uint32_t)(((ce + 15) & ~15) - 16) >> 4) & (kGroupLanes - 1),
+                                             a0, a1, a2, a3);
                 if (l == 0) KB_WRITE(A.gend, cr, A.n_rec, kKbGrid, R);
                 a0 = a1 = a2 = a3 = 0;
                 pick(j + 1);
-                go = active && cp < cnext;  // the next record starts in this chunk
+                if (!active || cp >= cnext) break;  // no record, or the next starts in a later chunk
+                step_cur(w, v);
             }
         };
         uint64_t sc = nws;
