@@ -101,14 +101,17 @@ def test_grid_edges_on_tile_and_chunk_boundaries(raw):
     host, dbuf = raw
     rng = np.random.default_rng(3)
     recs, pos = [], 0
-    for k in range(1, 400):
-        edge = k * 2048 + int(rng.choice([-3, -2, -1, 0, 1, 128 - 3, 128, 1024 - 1]))
+    for k in range(1, 600):
+        edge = (pos // 2048 + 1) * 2048 + int(rng.choice([-3, -2, -1, 0, 1, 128 - 3, 128, 1024 - 1]))
         if edge < pos:
-            continue
+            edge += 2048
+        if edge - pos > 64:  # a filler record up to a few bytes before the edge (gaps stay small)
+            recs.append((pos + 1, edge - pos - int(rng.integers(2, 8))))
+            pos = recs[-1][0] + recs[-1][1]
         n = int(rng.choice([0, 1, 2, 3, 4, 5, 15, 16, 17, 127, 128, 129, int(rng.integers(200, 1500))]))
         recs.append((edge, n))
         pos = edge + n
-        if k % 50 == 0:  # a long record over many tiles
+        if k % 100 == 0:  # a long record over many tiles
             big = int(rng.choice([64 * 2048 - 5, 65 * 2048 + 9, 200 * 2048 + 1, 3 << 20]))
             recs.append((pos + 7, big))
             pos += 7 + big
