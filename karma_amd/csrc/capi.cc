@@ -53,6 +53,8 @@ int hip_fail(hipError_t e, const char* what) {
 constexpr uint64_t kMinSplitUnit = 2048;  // smallest unit when records are split
 constexpr uint32_t kDirectMaxLen = 1024;  // ragged records up to this: one record per group
 constexpr uint64_t kOverdecompose = 4;    // units per group before splitting records
+constexpr uint64_t kSegOnceUnits = 128;      // units per workgroup of k_segment_once (8 x 16 waves)
+constexpr uint64_t kSegOnceMin = 256 << 10;  // single records from this size take it
 constexpr uint64_t kSplitOverdecompose = 64;  // units per group once split (2 KiB units up to 4 GiB
                                               // batches; 4: config 4 0.653 ms, 64: 0.609)
 
@@ -326,6 +328,24 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
         return 0;
     }
     KARMA_RC(comb_blob(ds, unit, &a.comb_maps));  // Z_U, Z_2U, Z_4U lead the unit's combine blob
+    if (n_rec == 1 && rec_bytes >= kSegOnceMin &&
+        rec_bytes <= (uint64_t)ds.cu * kSegOnceUnits * segment_once_max_unit(a.arena, rec_bytes) &&
+        KARMA_AB_KNOB("KARMA_SEGMENT_ONCE", 1)) {
+        // one segment (up to 64 MiB on 256 CUs): every wave streams one wave-step of 8 units with all
+        // of its loads in flight at once, workgroups fold their waves (k_segment_once)
+        const uint64_t G = std::min<uint64_t>(ds.cu, std::max<uint64_t>(1, ceil_div(rec_bytes, kSegOnceUnits * 512)));
+        a.unit_bytes = round_up(ceil_div(rec_bytes, kSegOnceUnits * G), kChunk);
+        a.units_per_rec = kSegOnceUnits * G;
+        a.fold_k = 0;
+        KARMA_RC(comb_blob(ds, a.unit_bytes, &a.comb_maps));
+        KARMA_RC(comb_blob(ds, a.unit_bytes * kSegOnceUnits, &a.block_blob));
+        unsigned long long* w = nullptr;
+        KARMA_RC(fused_words(dev, s, &w));
+        a.fctl = w;
+        a.partial = reinterpret_cast<uint32_t*>(w + 2);
+        KARMA_HIP(launch_segment_once(a, (int)G, s));
+        return 0;
+    }
     if (n_rec == 1 && k / kGroupsPerWave <= kBlockCombMaxPerThread * 1024) {
         // one record (a segment scan): the units kernel's last workgroup folds the wave states
         // itself (k_units_fixed FUSE), one launch instead of two

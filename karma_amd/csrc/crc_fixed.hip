@@ -243,6 +243,162 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     }
 }
 
+// ---- one segment, one wave-step per wave (karma_crc32c_stream up to grid x 16 x 8 units) ------
+// DESIGN.md §4 "The single segment": a 64 MiB scan is 4,096 wave-steps of 8 x 2 KiB units, one per
+// wave of a 256-workgroup grid, so the looping kernel above spends its time in latency: the LDS
+// table fill behind the first chunk loads (~4.7 us), four batches of chunk loads one round trip
+// each, and a last-workgroup fold of 4,096 wave states (~4.8 us).  Here every lane issues the
+// table words it fills first and then all of its unit's chunk loads (<= 16, 64 VGPRs), so the
+// fill overlaps the stream and the stream is one round trip; the 16-copy stride image (64 KiB,
+// read conflict-free by stride_step16s) leaves LDS for the fold maps.  Each workgroup folds its
+// 16 wave states in LDS and publishes one tagged state; the grid's last workgroup folds those
+// (at most 1024: a 64-lane tree per wave, then a Horner step per wave) and writes the CRC.
+// Forward progress: as the FUSE kernel (include/karma_crc32c.h: grid <= CUs, in-order dispatch).
+constexpr int kSegZ4 = kRep16Words;                        // Z4, Z16, Z32, Z64, byte table (the blob's)
+constexpr int kSegComb = kSegZ4 + kSmallWords;             // comb_maps: Z_{U 2^k}, k = 0..6
+constexpr int kSegGrid = kSegComb + kCombMaps * 1024;      // block_blob: Z_{128 U 2^k}, k = 0..6
+constexpr int kSegLdsWords = kSegGrid + kCombMaps * 1024;  // 140,288 bytes
+static_assert(kSegLdsWords * 4 <= 160 * 1024, "LDS of one workgroup");
+constexpr int kSegMaxChunks = 16;                          // units of at most 2 KiB
+
+template <int WORDS, int THREADS>
+struct LdsCopy {  // a global -> LDS copy split in two: the loads, then (after other loads) the stores
+    static constexpr int N4 = WORDS / 4, IT = (N4 + THREADS - 1) / THREADS;
+    u32x4 v[IT];
+    __device__ __forceinline__ void load(const uint32_t* __restrict__ g) {
+#pragma unroll
+        for (int q = 0; q < IT; ++q) {
+            const int i = (int)threadIdx.x + q * THREADS;
+            if (i < N4) v[q] = *(const gu32x4*)(reinterpret_cast<const u32x4*>(g) + i);
+        }
+    }
+    __device__ __forceinline__ void store(uint32_t* lds) const {
+#pragma unroll
+        for (int q = 0; q < IT; ++q) {
+            const int i = (int)threadIdx.x + q * THREADS;
+            if (i < N4) reinterpret_cast<u32x4*>(lds)[i] = v[q];
+        }
+    }
+};
+
+template <bool NT>
+__global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
+    KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
+                 (reinterpret_cast<uintptr_t>(A.arena + A.rec_bytes) + 15) & ~uintptr_t(15));
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kSegLdsWords];
+    __shared__ uint32_t s_tag, wst[kWavesPerBlock];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t l = lane & (kGroupLanes - 1), grp = lane / kGroupLanes;
+    const bool last_wg = blockIdx.x + 1 == gridDim.x;
+    if (threadIdx.x == 0) {
+        const uint32_t t = (uint32_t)__hip_atomic_load(A.fctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        s_tag = t ? t : 1u;
+    }
+    // 1. the table words this thread fills (issued first: waited for before the chunk loads)
+    constexpr int NV16 = kRep16Words / 4, IT16 = NV16 / kBlockThreads;
+    uint32_t e16[IT16];
+#pragma unroll
+    for (int q = 0; q < IT16; ++q) {
+        const int v = (int)threadIdx.x + q * kBlockThreads, row = v >> 4, k = (v >> 2) & 3;
+        e16[q] = *(const __attribute__((address_space(1))) uint32_t*)(A.blob + kBlobStride + k * 256 + row);
+    }
+    LdsCopy<kSmallWords, kBlockThreads> small;
+    small.load(A.blob + 1024);
+    LdsCopy<kCombMaps * 1024, kBlockThreads> comb, grid;
+    comb.load(A.comb_maps);
+    if (last_wg) grid.load(A.block_blob);
+    // 2. this lane's unit: every chunk load, the head block and the init word
+    const uint64_t U = A.units_per_rec;
+    const uint64_t u = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kGroupsPerWave + grp;
+    const FixedPlan P = fixed_plan(A, u, U, l);
+    const LaneUnit& L = P.L;
+    const bool ok0 = L.nch > 0 && L.w >= L.us && L.w < L.ue;
+    u32x4 v[kSegMaxChunks];
+    v[0] = ldg<NT>(ok0 ? L.w : L.lclamp);
+#pragma unroll
+    for (int q = 1; q < kSegMaxChunks; ++q) v[q] = ldg<NT>(pmin(L.w + q * kChunk, L.lclamp));
+    const u32x4 hv = ld16(P.hblk);
+    const Geom g0 = geom(A.arena, A.rec_bytes);  // the record's tail block: the last thread's
+    const u32x4 tv = ld16(last_wg && threadIdx.x == 0 && g0.e > g0.b ? g0.b : g0.a);
+    // 3. the tables into LDS (their loads were issued before the chunks': vmcnt counts in order)
+    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
+#pragma unroll
+    for (int q = 0; q < IT16; ++q) l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e16[q], e16[q], e16[q], e16[q]};
+    small.store(lds + kSegZ4);
+    comb.store(lds + kSegComb);
+    if (last_wg) grid.store(lds + kSegGrid);
+    __syncthreads();
+    // 4. the unit's windows (stride_step16s: the 16-copy image in swapped lane order), the lane
+    //    fold and the 8-lane tree
+    const uint32_t X = lane_const16();
+    uint32_t inj = 0;
+    if (P.inj_at) inj = P.hfrom < 16 ? steps_in_vec(lds, kSegZ4, kSegZ4 + 4096, ~A.init_scalar, hv, P.hfrom, 16u)
+                                     : ~A.init_scalar;
+    u32x4 x0 = ok0 ? v[0] : u32x4{0u, 0u, 0u, 0u};
+    if (ok0 && L.w == P.inj_at) x0.x ^= inj;
+    uint32_t a0 = x0.x, a1 = x0.y, a2 = x0.z, a3 = x0.w;
+#pragma unroll
+    for (int q = 1; q < kSegMaxChunks; ++q)
+        if (q < L.nch - 1 || (q == L.nch - 1 && L.lok)) step4<24>(lds, X, a0, a1, a2, a3, v[q]);
+    uint32_t c = lane_fold_at(lds, kSegZ4, a0, a1, a2, a3);
+    c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + L.m + 1) & (kGroupLanes - 1))), 64);
+    uint32_t t = __shfl_down(c, 1, kGroupLanes);
+    c = zmap(lds, kSegZ4 + 1024, c) ^ t;
+    t = __shfl_down(c, 2, kGroupLanes);
+    c = zmap(lds, kSegZ4 + 2048, c) ^ t;
+    t = __shfl_down(c, 4, kGroupLanes);
+    c = zmap(lds, kSegZ4 + 3072, c) ^ t;
+    // 5. the wave's 8 units (Z_U, Z_2U, Z_4U), the workgroup's 16 waves (Z_8U .. Z_64U)
+    t = __shfl_down(c, 8, 64);
+    c = zmap(lds, kSegComb, c) ^ t;
+    t = __shfl_down(c, 16, 64);
+    c = zmap(lds, kSegComb + 1024, c) ^ t;
+    t = __shfl_down(c, 32, 64);
+    c = zmap(lds, kSegComb + 2048, c) ^ t;
+    if (lane == 0) wst[wave] = c;
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t s = lane < kWavesPerBlock ? wst[lane] : 0u;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t o = __shfl_down(s, 1u << d, kWavesPerBlock);
+            s = zmap(lds, kSegComb + (3 + d) * 1024, s) ^ o;
+        }
+        if (lane == 0)  // tagged: visible to the last workgroup without a fence
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(A.partial) + blockIdx.x,
+                               ((unsigned long long)s_tag << 32) | s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!last_wg) return;
+    // 6. the grid's last workgroup: its states, end-aligned (leading zeros pad them to whole waves),
+    //    a 64-lane tree per wave (Z_{128U 2^d}), the wave results by Horner (Z_{64 128U}), the tail
+    const uint32_t G = gridDim.x, nw = (G + 63) / 64, pad = nw * 64 - G;
+    uint32_t s = 0;
+    if (threadIdx.x < nw * 64 && threadIdx.x >= pad) {
+        unsigned long long* st = reinterpret_cast<unsigned long long*>(A.partial) + (threadIdx.x - pad);
+        unsigned long long w = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((uint32_t)(w >> 32) != s_tag) {  // a workgroup whose state is not visible yet
+            __builtin_amdgcn_s_sleep(1);
+            w = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s = (uint32_t)w;
+    }
+    if (wave < nw) {
+#pragma unroll
+        for (int d = 0; d < 6; ++d) {
+            const uint32_t o = __shfl_down(s, 1u << d, 64);
+            s = zmap(lds, kSegGrid + d * 1024, s) ^ o;
+        }
+        if (lane == 0) wst[wave] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t r = wst[0];
+        for (uint32_t w = 1; w < nw; ++w) r = zmap(lds, kSegGrid + 6 * 1024, r) ^ wst[w];
+        A.out[0] = ~steps_in_vec(lds, kSegZ4, kSegZ4 + 4096, r, tv, 0u, g0.e > g0.b ? (uint32_t)(g0.e - g0.b) : 0u);
+        __hip_atomic_store(A.fctl + 1, (unsigned long long)s_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Records of fewer than 31 bytes may hold no aligned 16-byte block (and tiny
 // batches need no streaming): the general kernel, one unit per group, each
 // unit's loads issued when the unit starts.  Also the A/B baseline (variant 1).
@@ -464,6 +620,19 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
         if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false>), grid, blk, 0, s, a);
         else hipLaunchKernelGGL((k_units_fixed<4, true, false, false>), grid, blk, 0, s, a);
     }
+    units_timer_end(s);
+    return hipGetLastError();
+}
+
+hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t s) {
+    // one record; units_per_rec = 8 units x 16 waves x grid_blocks of at most 2 KiB; fctl, partial,
+    // comb_maps (comb blob of the unit) and block_blob (comb blob of 128 units) bound
+    if (a.n_rec != 1 || !a.fctl || !a.partial || !a.comb_maps || !a.block_blob || a.rec_bytes < 31 ||
+        a.units_per_rec != (uint64_t)grid_blocks * kWavesPerBlock * kGroupsPerWave ||
+        a.unit_bytes > segment_once_max_unit(a.arena, a.rec_bytes) || a.unit_bytes % kChunk || grid_blocks > 1024)
+        return hipErrorInvalidValue;
+    units_timer_begin(s);
+    hipLaunchKernelGGL(k_segment_once<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     return hipGetLastError();
 }

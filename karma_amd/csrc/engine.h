@@ -210,6 +210,16 @@ void units_timer_end(hipStream_t s);
 
 // Launchers (stream-ordered, no allocation, no synchronisation).
 hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s);
+// One record streamed one wave-step per wave (k_segment_once: a segment scan up to grid x 128
+// units of <= 2 KiB): units_per_rec = 128 x grid_blocks, comb_maps = the unit's combine blob,
+// block_blob = the combine blob of 128 units, fctl / partial = the fused words.
+hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t s);
+// Its largest unit: 16 chunk loads per lane, so 2 KiB when the body's end (16-aligned) sits on the
+// 128-byte grid, else 1,920 bytes (units are end-aligned: one then spans a chunk more).
+inline uint64_t segment_once_max_unit(const uint8_t* rec, uint64_t rec_bytes) {
+    const uintptr_t b = (reinterpret_cast<uintptr_t>(rec) + rec_bytes) & ~uintptr_t(15);
+    return b % 128 == 0 ? 16 * 128 : 15 * 128;
+}
 // One combine level for the fixed layout: k_in states per record -> k_out = ceil(k_in / 64).
 hipError_t launch_combine_fixed(const FixedArgs& a, const uint32_t* in_states, uint64_t k_in, uint32_t* out_states,
                                 uint64_t k_out, const uint32_t* comb_blob, hipStream_t s);

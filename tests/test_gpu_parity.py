@@ -238,6 +238,25 @@ def test_stream_fused_combine_segments_and_graph_replay(dev):
         assert int(o1.item()) == int(oracle_lib.splitmix_fixed_crcs(seed, seg, 0, 1, threads=16)[0])
 
 
+def test_segment_once_sizes_and_alignments(dev):
+    """One record of 256 KiB .. 64 MiB takes k_segment_once (every wave one wave-step of 8 units,
+    its loads in flight at once; workgroup folds, then the last workgroup's).  Sizes at its
+    thresholds, units from 128 B to 2 KiB, starts and ends off the 16- and 128-byte grids (an end
+    off the 128-byte grid caps the unit at 1,920 B: the largest such records fall back to the
+    looping kernel), repeated calls (tags), against the oracle."""
+    n = (64 << 20) + 256
+    buf = torch.empty(n, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 31)
+    host = buf.cpu().numpy()
+    cases = [(0, (256 << 10) - 1), (0, 256 << 10), (5, (256 << 10) + 1), (3, (1 << 20) + 17), (64, 3 << 20),
+             (9, (48 << 20) + 5), (0, 64 << 20), (128, 64 << 20), (16, 64 << 20), (1, (64 << 20) - 1),
+             (5, 60 << 20), (0, (60 << 20) + 7), (77, (32 << 20) - 77), (0, 16 << 20)]
+    for init in (0, 0x9E3779B9):
+        for off, m in cases:
+            got = int(K.extend_stream(init, buf[off: off + m]).item())
+            assert got == oracle_lib.extend(init, host[off: off + m].tobytes()), (hex(init), off, m)
+
+
 def test_config2_full_1m_x_4k(dev):
     n, rec = 1 << 20, 4096
     buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""One segment, isolated calls: k_segment_once (the tools build's KARMA_SEGMENT_ONCE=1, shipped)
+against the looping fused kernel it replaced (=0), at 64 MiB (configs[3]) and smaller sizes.
+Per size and variant: the isolated call (events around it, each call waited for) and the kernel
+alone (events inside the library), medians over interleaved rounds after a 500 ms pre-warm, 64
+distinct segments in rotation; CRCs equal across variants.  Run on the GPU box from the repo root:
+
+    python tools/segment_once_ab.py [--sizes 64,16,4,1] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import karma_amd as K  # noqa: E402
+from karma_amd import _lib  # noqa: E402
+
+L = _lib.load(_lib.AB_LIB_PATH)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--sizes", default="64,16,4,1")
+    p.add_argument("--rounds", type=int, default=6)
+    p.add_argument("--json", default="")
+    a = p.parse_args()
+    dev = torch.device("cuda:0")
+    nseg, top = 64, 64 << 20
+    arena = torch.empty(nseg * top, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(arena, 42)
+    sh = torch.cuda.current_stream().cuda_stream
+    V = ["1", "0"]
+    report = {}
+    for mib in [int(x) for x in a.sizes.split(",")]:
+        seg = mib << 20
+        outs = {v: torch.zeros(nseg, dtype=torch.uint32, device=dev) for v in V}
+        state = {"i": 0}
+
+        def call(v):
+            os.environ["KARMA_SEGMENT_ONCE"] = v
+            i = state["i"] % nseg
+            state["i"] += 1
+            _lib.check("stream", L.karma_crc32c_stream(0, arena.data_ptr() + i * top, seg,
+                                                       outs[v].data_ptr() + 4 * i, sh))
+
+        t_end = time.perf_counter() + 0.5
+        while time.perf_counter() < t_end:
+            call("1")
+            torch.cuda.synchronize()
+        lat = {v: [] for v in V}
+        kern = {v: [] for v in V}
+        for rnd in range(a.rounds):
+            for v in V if rnd % 2 == 0 else V[::-1]:
+                for _ in range(16):
+                    u0, u1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    u0.record()
+                    u1.record()
+                    torch.cuda.synchronize()
+                    L.karma_crc32c_time_next_units(u0.cuda_event, u1.cuda_event)
+                    e0.record()
+                    call(v)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    lat[v].append(e0.elapsed_time(e1) * 1e3)
+                    kern[v].append(u0.elapsed_time(u1) * 1e3)
+        for v in V:  # every segment once per variant: the CRCs to compare
+            state["i"] = 0
+            for _ in range(nseg):
+                call(v)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(outs["0"], outs["1"]))
+        ent = {v: {"call_us_p50": round(float(np.median(lat[v])), 2),
+                   "kernel_us_p50": round(float(np.median(kern[v])), 2),
+                   "call_us_p10_p90": [round(float(np.percentile(lat[v], q)), 2) for q in (10, 90)]} for v in V}
+        ent["crcs_equal"] = same
+        report[f"{mib}MiB"] = ent
+        print(f"{mib} MiB", json.dumps(ent), flush=True)
+        assert same, "variants differ"
+    os.environ.pop("KARMA_SEGMENT_ONCE", None)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(report, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
