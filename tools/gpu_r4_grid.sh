@@ -9,8 +9,10 @@ mkdir -p $O
 T="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
 NEW="tests/test_gpu_grid.py tests/test_gpu_lifetime.py tests/test_gpu_multi_host.py"
 timeout -k 10 300 $T tests/test_gpu_parity.py -k "segment_once or stream_" --karma-lib abbounds > $O/seg_abbounds.log 2>&1
-timeout -k 10 400 $T $NEW --karma-lib abbounds > $O/new_tests_abbounds.log 2>&1
-timeout -k 10 400 $T $NEW tests/test_gpu_parity.py -k "segment_once or stream_ or grid or lifetime or multi" > $O/new_tests.log 2>&1
+timeout -k 10 120 python3 -u tools/lifetime_probe.py 300 > $O/lifetime_probe.log 2>&1
+cat $O/lifetime_probe.log
+timeout -k 10 400 $T $NEW --karma-lib abbounds -k "not thousand" > $O/new_tests_abbounds.log 2>&1
+timeout -k 10 400 $T $NEW tests/test_gpu_parity.py -k "(segment_once or stream_ or grid or lifetime or multi) and not thousand" > $O/new_tests.log 2>&1
 timeout -k 10 300 python3 -u bench.py --workload ragged --steps 100 --warmup 10 --no-cpu-baseline > $O/bench_ragged.json 2> $O/bench_ragged.err
 cat $O/bench_ragged.json
 timeout -k 10 300 python3 -u bench.py --workload segment --steps 200 --warmup 20 --no-cpu-baseline > $O/bench_segment.json 2> $O/bench_segment.err
