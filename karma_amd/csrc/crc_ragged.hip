@@ -516,7 +516,10 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
     const uint32_t lane = threadIdx.x & 63u, l = lane & (kGroupLanes - 1), grp = lane / kGroupLanes;
     const uint32_t gbase = lane & ~(kGroupLanes - 1u), wave = threadIdx.x >> 6;
     const uint32_t X = lane_const();
-    const uint64_t NT = A.gctl[0], base = A.gctl[1], lo = A.gctl[2], hi = A.gctl[3];
+    // (uniform: scalar registers -- every VGPR counts at 1024 threads, and a spill's reload waits
+    // for every load in flight)
+    const uint64_t NT = uniform64(A.gctl[0]), base = uniform64(A.gctl[1]), lo = uniform64(A.gctl[2]),
+                   hi = uniform64(A.gctl[3]);
     if (NT == 0 || hi < lo + 16) return;  // no byte to read (only empty records)
     const uint64_t hi16 = hi - 16;
     const uint64_t nws = (NT + kGroupsPerWave - 1) / kGroupsPerWave;
@@ -531,11 +534,26 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
         if (lane == 0) i = atomicAdd(blk_next, 1u);
         return step_of(__builtin_amdgcn_readfirstlane(__shfl(i, 0)));
     };
-    auto chunk = [&](uint64_t t, uint32_t c) {
-        uint64_t a = base + t * kGridTile + c * kChunk + l * 16;
-        a = a < lo ? lo : a;
-        a = a > hi16 ? hi16 : a;
-        return reinterpret_cast<const uint8_t*>((uintptr_t)a);
+    // A wave-step's 8 tiles: a scalar base and this lane's 32-bit offset, clamped to the bytes the
+    // records span [lo, hi) (steps past the last tile read hi - 16).
+    struct Step {
+        const uint8_t* b;
+        uint32_t lo, hi;
+    };
+    constexpr uint32_t kStepBytes = kGroupsPerWave * kGridTile;
+    auto step_win = [&](uint64_t s) -> Step {
+        const uint64_t wb = base + s * kStepBytes;
+        const uint64_t b = wb <= hi16 ? wb : hi16;
+        const uint64_t rh = hi16 - b;
+        return Step{reinterpret_cast<const uint8_t*>((uintptr_t)b), lo > b ? (uint32_t)(lo - b) : 0u,
+                    rh < kStepBytes ? (uint32_t)rh : kStepBytes};
+    };
+    const uint32_t loff = grp * kGridTile + l * 16;
+    auto chunk = [&](const Step& W, uint32_t c) {
+        uint32_t o = loff + c * kChunk;
+        o = o < W.lo ? W.lo : o;
+        o = o > W.hi ? W.hi : o;
+        return W.b + o;
     };
     auto tword = [&](uint64_t s) -> uint32_t {
         const uint64_t t = s * kGroupsPerWave + grp;
@@ -549,13 +567,23 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
     uint32_t twa = tword(sa);
     u32x4 mva = rec_meta(twa & ~kGridInterior);
     u32x4 nb[PF];
+    {
+        const Step W = step_win(sa);
 #pragma unroll
-    for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(sa * kGroupsPerWave + grp, q));
-    uint32_t twb = tword(sb);
+        for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(W, q));
+    }
     load_stream_tables(lds, A.blob);
     __syncthreads();
+    WLOG_DECL;
+    WLOG_START();
     while (sa < nws) {
         const uint64_t t = sa * kGroupsPerWave + grp;
+        const Step Wa = step_win(sa);
+        // tile b's word, used at this tile's last batch (issued here, not one tile earlier: a
+        // loop-carried copy of a register still being loaded would wait for every load in flight)
+        const uint32_t twb = tword(sb);
+        WLOG_STEP();
+        WLOG_UNIT(l == 0 && t < NT, kGridTile);
         const bool tvalid = t < NT;
         const uint64_t ta = base + t * kGridTile;
         // the tile's record list: lane l holds record r0 + l
@@ -629,7 +657,6 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
             }
         };
         uint64_t sc = nws;
-        uint32_t twc = twb;
         u32x4 mvb = mva;
 #pragma unroll 1
         for (uint32_t k = 0; k < kGridChunks / PF; ++k) {
@@ -638,13 +665,15 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
             for (int q = 0; q < PF; ++q) cur[q] = nb[q];
             if (k + 1 < kGridChunks / PF) {
 #pragma unroll
-                for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(t, (k + 1) * PF + q));
+                for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(Wa, (k + 1) * PF + q));
             } else {  // tile b's metadata and first loads, tile c's word
                 sc = take();
-                mvb = rec_meta(twb & ~kGridInterior);
+                uint32_t tw = twb;
+                asm volatile("" : "+v"(tw));  // its use stays here (hoisted, it waits for the chunk loads)
+                mvb = rec_meta(tw & ~kGridInterior);
+                const Step Wb = step_win(sb);
 #pragma unroll
-                for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(sb * kGroupsPerWave + grp, q));
-                twc = tword(sc);
+                for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(Wb, q));
             }
 #pragma unroll
             for (int q = 0; q < PF; ++q) process(k * PF + q, cur[q]);
@@ -656,9 +685,9 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
         sa = sb;
         sb = sc;
         twa = twb;
-        twb = twc;
         mva = mvb;
     }
+    WLOG_END(bw0 + wave);
 }
 
 // The finalize kernel's grid branch (lds: the grid's combine blob), one lane per record: Horner

@@ -50,6 +50,31 @@ def main():
         "fixed": lambda sh: L.karma_crc32c_batch_fixed(arena.data_ptr(), 4096, 4096, None, 0, out.data_ptr(), sh),
     }
 
+    # the per-device host-path contexts (replay / append from host memory), as the lifetime test
+    seg = 1 << 16
+    plens = rng.integers(1, 500, 3000).astype(np.uint32)
+    poffs = np.concatenate([[0], np.cumsum(plens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    src = rng.integers(0, 256, int(plens.sum()) + 16, dtype=np.uint8)
+    wal = np.zeros(64 * seg, np.uint8)
+    cur, nf = ctypes.c_uint64(0), ctypes.c_size_t()
+    nrec, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+    hbuf = rng.integers(0, 256, 4096 * 64, dtype=np.uint8)
+    hout = np.zeros(4096, np.uint32)
+
+    def wal_host(sh):
+        cur.value = 0
+        st = L.karma_wal_append_batch(src.ctypes.data, poffs.ctypes.data, plens.ctypes.data, plens.size, wal.ctypes.data,
+                                      wal.nbytes, seg, ctypes.byref(cur), None, ctypes.byref(nf), 0)
+        st = st or L.karma_wal_replay(wal.ctypes.data, None, wal.nbytes, seg, 0, ctypes.byref(nrec), ctypes.byref(stop),
+                                      ctypes.byref(status), None, 0, 0)
+        return st
+
+    def host_batch(sh):
+        return L.karma_crc32c_batch_fixed_host(hbuf.ctypes.data, 64, 4096, 0, hout.ctypes.data, 0)
+
+    calls["wal_host"] = wal_host
+    calls["host_batch"] = host_batch
+
     def free():
         torch.cuda.synchronize()
         return torch.cuda.mem_get_info()[0]

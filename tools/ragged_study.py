@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Where does the ragged path lose against the fixed one?  Times the units kernel alone
-(karma_crc32c_time_next_units) and the whole call for several 4 GiB layouts, one process,
-interleaved rounds.  Run on the GPU box from the repo root:  python tools/ragged_study.py
+(karma_crc32c_time_next_units) and the whole call for several 4 GiB layouts, the byte grid and the
+unit plan (the tools build's KARMA_RAGGED_GRID=1 / 0) side by side, one process, interleaved
+rounds.  Run on the GPU box from the repo root:  python tools/ragged_study.py
 """
 import os
 import sys
@@ -40,7 +41,7 @@ def fixed_case(rec, variant="0"):
     return run, n * rec
 
 
-def ragged_case(lens, offs, variant="0"):
+def ragged_case(lens, offs, grid="1"):
     d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
     d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
     n = lens.size
@@ -50,37 +51,29 @@ def ragged_case(lens, offs, variant="0"):
     out = torch.empty(n, dtype=torch.uint32, device=dev)
 
     def run():
-        os.environ["KARMA_RAGGED_VARIANT"] = variant
+        os.environ["KARMA_RAGGED_GRID"] = grid
         _lib.check("ragged", L.karma_crc32c_batch_ragged(raw.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, total,
                                                          None, 0, out.data_ptr(), sh))
     return run, total
 
 
 cases = {}
-FV = os.environ.get("FIXED_VARIANTS", "1").split()
-RV = os.environ.get("RAGGED_VARIANTS", "1").split()
-for rec in (4096, 2048, 1024):
+FV = os.environ.get("FIXED_VARIANTS", "").split()
+for rec in (4096,):
     cases[f"fixed {rec}"] = fixed_case(rec)
     for v in FV:
         cases[f"fixed {rec} v{v}"] = fixed_case(rec, v)
-for rec in (4096, 2048):
-    n = GB // rec
-    cases[f"ragged aligned {rec}"] = ragged_case(np.full(n, rec, np.uint32), np.arange(n, dtype=np.uint64) * rec)
-    for v in RV:
-        cases[f"ragged aligned {rec} v{v}"] = ragged_case(np.full(n, rec, np.uint32), np.arange(n, dtype=np.uint64) * rec, v)
 count = int(GB / (((65536 - 64) / np.log(1024)) + 8))
 lens = synth.loguniform_lengths(7, count, 64, 65536)
 offs, _ = synth.ragged_layout(lens, header=8)
-cases["ragged config3"] = ragged_case(lens, offs)
-for v in RV:
-    cases[f"ragged config3 v{v}"] = ragged_case(lens, offs, v)
 srt = np.sort(lens)[::-1].copy()
 o2, _ = synth.ragged_layout(srt, header=8)
-cases["ragged config3 sorted desc"] = ragged_case(srt, o2)
-# config-3 sizes, but every record starts on a 4 KiB boundary (no partial first units)
-o3 = np.concatenate([[0], np.cumsum((lens.astype(np.uint64) + 4095) // 4096 * 4096)[:-1]]).astype(np.uint64)
-keep = int(np.searchsorted(o3 + lens, np.uint64(GB)))
-cases["ragged config3 4K-aligned starts"] = ragged_case(lens[:keep].copy(), o3[:keep].copy())
+layouts = {"aligned 4096": (np.full(GB // 4096, 4096, np.uint32), np.arange(GB // 4096, dtype=np.uint64) * 4096),
+           "aligned 2048": (np.full(GB // 2048, 2048, np.uint32), np.arange(GB // 2048, dtype=np.uint64) * 2048),
+           "config3": (lens, offs), "config3 sorted desc": (srt, o2)}
+for name, (ln, of) in layouts.items():
+    for g in ("1", "0"):
+        cases[f"ragged {name} {'grid' if g == '1' else 'units'}"] = ragged_case(ln, of, g)
 
 for name, (run, nbytes) in cases.items():
     print("first call:", name, flush=True)
