@@ -44,7 +44,10 @@ constexpr int kCombZ4 = kCombMaps * 1024;
 constexpr int kCombT8 = kCombZ4 + 1024;
 constexpr int kCombCoreWords = kCombT8 + 256;  // what the fixed combine and the head steps need
 constexpr int kCombSmall = kCombT8 + 1024;
-constexpr int kCombSmallMaps = 9;
+#ifndef KARMA_GRID_TILE
+#define KARMA_GRID_TILE 2048  // a build-time A/B knob
+#endif
+constexpr int kCombSmallMaps = KARMA_GRID_TILE > 4096 ? 10 : 9;  // Z_16n, n < 2^maps (>= a grid tile / 16)
 constexpr int kCombWords = kCombSmall + kCombSmallMaps * 1024;
 
 // ---- table blob of the one-block combine (k_combine_block) -----------------
@@ -111,12 +114,11 @@ static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
 // record masked to zero and ~init xored into its first four bytes (a zero prefix leaves the
 // register at zero), so no head or tail byte is stepped on its own; a tile emits one register
 // per record that ends in it (gend) and one for the record that runs past its end (gstate).
-#ifndef KARMA_GRID_TILE
-#define KARMA_GRID_TILE 2048  // a build-time A/B knob
-#endif
+
 constexpr uint32_t kGridTile = KARMA_GRID_TILE;
 constexpr uint32_t kGridChunks = kGridTile / kChunk;
 static_assert(kGridTile % kChunk == 0 && (kGridTile & (kGridTile - 1)) == 0, "tiles of whole chunks, power of two");
+static_assert(kGridTile / 16 < (1u << kCombSmallMaps), "zshift16 spans a tile");
 // Largest gap between consecutive records the grid streams across.  Below a 4 KiB page every
 // byte it reads lies on a page that also holds record bytes, so it reads no unmapped memory.
 constexpr uint64_t kGridMaxGap = kGridTile;

@@ -102,6 +102,23 @@ def main():
         after = free()
         report[name] = {"before_trim_mib": round((base - mid) / MIB, 2), "after_trim_mib": round((base - after) / MIB, 2)}
         print(name, json.dumps(report[name]), flush=True)
+    # tests/test_gpu_lifetime.py's loop as it is (every call on each stream, the host paths every
+    # 250 streams), free memory every 100 streams
+    base = free()
+    for i in range(1000):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        for name in ("ragged_sorted", "ragged_unsorted", "segment", "fixed"):
+            assert not calls[name](s), name
+        if i % 250 == 0:
+            assert hip.hipStreamSynchronize(s) == 0
+            assert not wal_host(s)
+        assert L.karma_crc32c_release_stream(-1, s) == 0
+        assert hip.hipStreamDestroy(s) == 0
+        if i % 100 == 99:
+            print("replica", i + 1, "streams:", round((base - free()) / MIB, 2), "MiB", flush=True)
+    assert L.karma_crc32c_trim(-1) == 0
+    print("replica after trim:", round((base - free()) / MIB, 2), "MiB", flush=True)
     # the same with streams kept (not destroyed) until the end: does the HIP runtime hold memory per stream?
     base = free()
     keep = []

@@ -33,7 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import karma_amd as K  # noqa: E402
 from karma_amd import _lib  # noqa: E402
 
-_lib._LIB = _lib.load(_lib.AB_LIB_PATH)
+_lib._LIB = _lib.load(os.environ.get("KARMA_STUDY_LIB", _lib.AB_LIB_PATH))  # (or another tools build)
 import synth  # noqa: E402
 
 REC = np.dtype([("t0", "<u8"), ("t1", "<u8"), ("hw", "<u4"), ("xcc", "<u4"), ("units", "<u4"), ("kib", "<u4"),

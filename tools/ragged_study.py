@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import karma_amd as K  # noqa: E402
 from karma_amd import _lib  # noqa: E402
 
-_lib._LIB = _lib.load(_lib.AB_LIB_PATH)  # the tools build: the KARMA_* A/B variants (karma_amd/csrc/ab.h)
+# the tools build (the KARMA_* A/B variants, karma_amd/csrc/ab.h), or another build of it named by KARMA_STUDY_LIB
+_lib._LIB = _lib.load(os.environ.get("KARMA_STUDY_LIB", _lib.AB_LIB_PATH))
 import synth  # noqa: E402
 
 L = _lib.lib()
