@@ -497,6 +497,9 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         KARMA_RC(workspace(dev, s, L.total, &ws));
         bind_ragged(a, ws, L, cap);
         if (tile_cap) bind_grid(a, ws, L, tile_cap, ds.gcomb);
+#ifdef KARMA_AB
+        a.ab_grid_mode = (uint32_t)KARMA_AB_KNOB("KARMA_GRID_MODE", 0);
+#endif
     } else {
         // Unknown total: count the units (k_ragged_scan), read the block totals back and size
         // the unit table.

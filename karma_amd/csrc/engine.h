@@ -199,6 +199,10 @@ struct RaggedArgs {
     unsigned long long* gctl;  // [0] tiles, [1] address of tile 0, [2] first byte read, [3] last byte read + 1
     uint64_t tile_cap;
     const uint32_t* gcomb_blob;  // kGridCombWords
+#ifdef KARMA_AB
+    uint32_t ab_grid_mode;  // tools build, KARMA_GRID_MODE (timing only, wrong CRCs): 1 = chunks xored
+                            // (the load pipeline alone), 2 = every window stepped unmasked (+ the LDS work)
+#endif
 };
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are

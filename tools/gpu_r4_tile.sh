@@ -5,6 +5,8 @@
 set -euo pipefail
 O=gpurun_out/r4tile
 mkdir -p $O
+GRID_MODES="1 2" timeout -k 10 400 python3 -u tools/ragged_study.py > $O/study_t2048_modes.log 2>&1
+cat $O/study_t2048_modes.log
 for T in 4096 8192; do
   KARMA_STUDY_LIB=tools/lib/libkarma_crc32c_ab_t$T.so timeout -k 10 300 python3 -u tools/ragged_gap.py --case config3,ragged4k --no-log --calls 10 > $O/gap_t$T.log 2>&1
   cat $O/gap_t$T.log

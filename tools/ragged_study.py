@@ -42,7 +42,7 @@ def fixed_case(rec, variant="0"):
     return run, n * rec
 
 
-def ragged_case(lens, offs, grid="1"):
+def ragged_case(lens, offs, grid="1", mode="0"):
     d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
     d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
     n = lens.size
@@ -53,6 +53,7 @@ def ragged_case(lens, offs, grid="1"):
 
     def run():
         os.environ["KARMA_RAGGED_GRID"] = grid
+        os.environ["KARMA_GRID_MODE"] = mode  # timing-only grid modes (1: loads xored, 2: unmasked steps)
         _lib.check("ragged", L.karma_crc32c_batch_ragged(raw.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, total,
                                                          None, 0, out.data_ptr(), sh))
     return run, total
@@ -75,6 +76,8 @@ layouts = {"aligned 4096": (np.full(GB // 4096, 4096, np.uint32), np.arange(GB /
 for name, (ln, of) in layouts.items():
     for g in ("1", "0"):
         cases[f"ragged {name} {'grid' if g == '1' else 'units'}"] = ragged_case(ln, of, g)
+    for m in os.environ.get("GRID_MODES", "").split():
+        cases[f"ragged {name} grid mode {m}"] = ragged_case(ln, of, "1", m)
 
 for name, (run, nbytes) in cases.items():
     print("first call:", name, flush=True)
