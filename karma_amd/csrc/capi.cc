@@ -396,6 +396,10 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 thread_local RaggedArgs t_last_ragged{};  // karma_ab_ragged_took_grid (tools build)
 #endif
 
+#ifndef KARMA_RAGGED_GRID_DEFAULT
+#define KARMA_RAGGED_GRID_DEFAULT 1  // (a build-time A/B knob: 0 builds a library without the byte grid)
+#endif
+
 struct RaggedLayout {
     size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off;
     size_t grec_off, gtile_off, gstate_off, gend_off, gflag_off, gctl_off, total;
@@ -492,14 +496,11 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         cap = cap_full + 2 * n_rec;
         // the byte grid is tried first when the batch may be sorted (the tools build's
         // KARMA_RAGGED_GRID=0 turns it off for A/B)
-        const uint64_t tile_cap = n_rec < (1ull << 31) && KARMA_AB_KNOB("KARMA_RAGGED_GRID", 1) ? grid_tile_cap(total_len, n_rec) : 0;
+        const uint64_t tile_cap = n_rec < (1ull << 31) && KARMA_AB_KNOB("KARMA_RAGGED_GRID", KARMA_RAGGED_GRID_DEFAULT) ? grid_tile_cap(total_len, n_rec) : 0;
         const RaggedLayout L = ragged_layout(n_rec, cap, tile_cap);
         KARMA_RC(workspace(dev, s, L.total, &ws));
         bind_ragged(a, ws, L, cap);
         if (tile_cap) bind_grid(a, ws, L, tile_cap, ds.gcomb);
-#ifdef KARMA_AB
-        a.ab_grid_mode = (uint32_t)KARMA_AB_KNOB("KARMA_GRID_MODE", 0);
-#endif
     } else {
         // Unknown total: count the units (k_ragged_scan), read the block totals back and size
         // the unit table.
@@ -628,6 +629,12 @@ thread_local hipEvent_t t_units_start = nullptr, t_units_stop = nullptr;
 }  // namespace karma::engine
 // Tools build only (wavelog.h): the units kernels log one WaveLogRec per wave into d_buf
 // (cap records); d_buf = NULL stops the log.
+// Tools build only: k_segment_once writes 8 wall-clock stamps per workgroup into d_buf (NULL: off):
+// entry, tables and loads landed, waves folded, state published; the last workgroup also after
+// its wait and at its end.
+extern "C" int karma_ab_seg_log(void* d_buf) {
+    return karma::engine::set_seg_log(d_buf) == hipSuccess ? 0 : KARMA_E_HIP;
+}
 extern "C" int karma_ab_wave_log(void* d_buf, uint64_t cap) {
     using namespace karma::engine;
     if (set_wave_log_ragged(d_buf, d_buf ? cap : 0) != hipSuccess || set_wave_log_fixed(d_buf, d_buf ? cap : 0) != hipSuccess)

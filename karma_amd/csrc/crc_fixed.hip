@@ -261,6 +261,16 @@ constexpr int kSegLdsWords = kSegGrid + kCombMaps * 1024;  // 140,288 bytes
 static_assert(kSegLdsWords * 4 <= 160 * 1024, "LDS of one workgroup");
 constexpr int kSegMaxChunks = 16;                          // units of at most 2 KiB
 
+#ifdef KARMA_AB  // tools build: per-workgroup phase stamps of k_segment_once (karma_ab_seg_log)
+__device__ uint64_t* g_seg_log;
+#define SEG_STAMP(i)                                                                  \
+    do {                                                                              \
+        if (g_seg_log && threadIdx.x == 0) g_seg_log[blockIdx.x * 8 + (i)] = wall_clock64(); \
+    } while (0)
+#else
+#define SEG_STAMP(i) ((void)0)
+#endif
+
 template <int WORDS, int THREADS>
 struct LdsCopy {  // a global -> LDS copy split in two: the loads, then (after other loads) the stores
     static constexpr int N4 = WORDS / 4, IT = (N4 + THREADS - 1) / THREADS;
@@ -290,6 +300,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t l = lane & (kGroupLanes - 1), grp = lane / kGroupLanes;
     const bool last_wg = blockIdx.x + 1 == gridDim.x;
+    SEG_STAMP(0);
     if (threadIdx.x == 0) {
         const uint32_t t = (uint32_t)__hip_atomic_load(A.fctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
         s_tag = t ? t : 1u;
@@ -328,6 +339,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     comb.store(lds + kSegComb);
     if (last_wg) grid.store(lds + kSegGrid);
     __syncthreads();
+    SEG_STAMP(1);
     // 4. the unit's windows (stride_step16s: the 16-copy image in swapped lane order), the lane
     //    fold and the 8-lane tree
     const uint32_t X = lane_const16();
@@ -356,6 +368,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     t = __shfl_down(c, 32, 64);
     c = zmap(lds, kSegComb + 2048, c) ^ t;
     if (lane == 0) wst[wave] = c;
+    SEG_STAMP(2);
     __syncthreads();
     if (wave == 0) {
         uint32_t s = lane < kWavesPerBlock ? wst[lane] : 0u;
@@ -368,6 +381,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
             __hip_atomic_store(reinterpret_cast<unsigned long long*>(A.partial) + blockIdx.x,
                                ((unsigned long long)s_tag << 32) | s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    SEG_STAMP(3);
     if (!last_wg) return;
     // 6. the grid's last workgroup: its states, end-aligned (leading zeros pad them to whole waves),
     //    a 64-lane tree per wave (Z_{128U 2^d}), the wave results by Horner (Z_{64 128U}), the tail
@@ -391,12 +405,14 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
         if (lane == 0) wst[wave] = s;
     }
     __syncthreads();
+    SEG_STAMP(4);
     if (threadIdx.x == 0) {
         uint32_t r = wst[0];
         for (uint32_t w = 1; w < nw; ++w) r = zmap(lds, kSegGrid + 6 * 1024, r) ^ wst[w];
         A.out[0] = ~steps_in_vec(lds, kSegZ4, kSegZ4 + 4096, r, tv, 0u, g0.e > g0.b ? (uint32_t)(g0.e - g0.b) : 0u);
         __hip_atomic_store(A.fctl + 1, (unsigned long long)s_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    SEG_STAMP(5);
 }
 
 // Records of fewer than 31 bytes may hold no aligned 16-byte block (and tiny
@@ -658,6 +674,10 @@ hipError_t launch_combine_block(const FixedArgs& a, const uint32_t* in_states, u
 KB_DEFINE_COLLECT(fixed)
 #ifdef KARMA_AB
 WLOG_SETTER(fixed)
+hipError_t set_seg_log(void* p) {
+    uint64_t* q = static_cast<uint64_t*>(p);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_seg_log), &q, sizeof(q));
+}
 #endif
 
 }  // namespace engine

@@ -574,16 +574,12 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
     }
     load_stream_tables(lds, A.blob);
     __syncthreads();
-    WLOG_DECL;
-    WLOG_START();
     while (sa < nws) {
         const uint64_t t = sa * kGroupsPerWave + grp;
         const Step Wa = step_win(sa);
         // tile b's word, used at this tile's last batch (issued here, not one tile earlier: a
         // loop-carried copy of a register still being loaded would wait for every load in flight)
         const uint32_t twb = tword(sb);
-        WLOG_STEP();
-        WLOG_UNIT(l == 0 && t < NT, kGridTile);
         const bool tvalid = t < NT;
         const uint64_t ta = base + t * kGridTile;
         // the tile's record list: lane l holds record r0 + l
@@ -675,37 +671,9 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
 #pragma unroll
                 for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(Wb, q));
             }
-#ifdef KARMA_AB
-            if (A.ab_grid_mode == 1) {
-#pragma unroll
-                for (int q = 0; q < PF; ++q) {
-                    a0 ^= cur[q].x;
-                    a1 ^= cur[q].y;
-                    a2 ^= cur[q].z;
-                    a3 ^= cur[q].w;
-                }
-                continue;
-            }
-            if (A.ab_grid_mode == 2) {
-#pragma unroll
-                for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
-                continue;
-            }
-#endif
 #pragma unroll
             for (int q = 0; q < PF; ++q) process(k * PF + q, cur[q]);
         }
-#ifdef KARMA_AB
-        if (A.ab_grid_mode) {  // keep the work: one word per tile
-            if (l == 0 && t < NT) A.gstate[t] = a0 ^ a1 ^ a2 ^ a3;
-            a0 = a1 = a2 = a3 = 0;
-            sa = sb;
-            sb = sc;
-            twa = twb;
-            mva = mvb;
-            continue;
-        }
-#endif
         if (active && ce > (int32_t)kGridTile) {  // the record running past the tile's end
             const uint32_t R = grid_fold(lds, l, kGroupLanes - 1, a0, a1, a2, a3);
             if (l == 0) KB_WRITE(A.gstate, t, A.tile_cap, kKbGrid, R);
@@ -715,7 +683,6 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
         twa = twb;
         mva = mvb;
     }
-    WLOG_END(bw0 + wave);
 }
 
 // The finalize kernel's grid branch (lds: the grid's combine blob), one lane per record: Horner

@@ -199,10 +199,6 @@ struct RaggedArgs {
     unsigned long long* gctl;  // [0] tiles, [1] address of tile 0, [2] first byte read, [3] last byte read + 1
     uint64_t tile_cap;
     const uint32_t* gcomb_blob;  // kGridCombWords
-#ifdef KARMA_AB
-    uint32_t ab_grid_mode;  // tools build, KARMA_GRID_MODE (timing only, wrong CRCs): 1 = chunks xored
-                            // (the load pipeline alone), 2 = every window stepped unmasked (+ the LDS work)
-#endif
 };
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
@@ -210,6 +206,7 @@ struct RaggedArgs {
 #ifdef KARMA_AB
 hipError_t set_wave_log_ragged(void* p, uint64_t cap);  // wavelog.h (tools build)
 hipError_t set_wave_log_fixed(void* p, uint64_t cap);
+hipError_t set_seg_log(void* p);  // k_segment_once's per-workgroup stamps (8 words each)
 #endif
 void units_timer_begin(hipStream_t s);
 void units_timer_end(hipStream_t s);

@@ -8,6 +8,7 @@ distinct segments in rotation; CRCs equal across variants.  Run on the GPU box f
     python tools/segment_once_ab.py [--sizes 64,16,4,1] [--json out.json]
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -81,6 +82,26 @@ def main():
                    "call_us_p10_p90": [round(float(np.percentile(lat[v], q)), 2) for q in (10, 90)]} for v in V}
         ent["crcs_equal"] = same
         report[f"{mib}MiB"] = ent
+        # one logged call of k_segment_once: per-workgroup stamps (us from the earliest entry)
+        if hasattr(L, "karma_ab_seg_log"):
+            os.environ["KARMA_SEGMENT_ONCE"] = "1"
+            log = torch.zeros(256 * 8, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            L.karma_ab_seg_log(ctypes.c_void_p(log.data_ptr()))
+            call("1")
+            torch.cuda.synchronize()
+            L.karma_ab_seg_log(None)
+            st = log.cpu().numpy().reshape(256, 8)
+            st = st[st[:, 0] > 0]
+            t0 = st[:, 0].min()
+            us = (st - t0) / 100.0
+            ent["stamps_us"] = {nm: [round(float(np.percentile(us[:, i], q)), 2) for q in (0, 50, 100)]
+                                for i, nm in enumerate(["entry", "loaded", "waves_folded", "published"])}
+            last = us[-1]
+            ent["last_wg_us"] = {"entry": round(float(last[0]), 2), "loaded": round(float(last[1]), 2),
+                                 "published": round(float(last[3]), 2), "waited": round(float(last[4]), 2),
+                                 "end": round(float(last[5]), 2)}
+            ent["workgroups"] = int(st.shape[0])
         print(f"{mib} MiB", json.dumps(ent), flush=True)
         assert same, "variants differ"
     os.environ.pop("KARMA_SEGMENT_ONCE", None)
