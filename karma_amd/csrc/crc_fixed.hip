@@ -34,12 +34,14 @@ struct FixedPlan {
     bool valid;
 };
 
+// ONE: a single record (no 64-bit division: r = 0).
+template <bool ONE = false>
 __device__ __forceinline__ FixedPlan fixed_plan(const FixedArgs& A, uint64_t u, uint64_t U, uint32_t l) {
     FixedPlan P;
     const uint64_t k = A.units_per_rec;
     P.valid = u < U;
     const uint64_t uu = P.valid ? u : 0;
-    P.r = k == 1 ? uu : uu / k;
+    P.r = ONE ? 0 : k == 1 ? uu : uu / k;
     const uint64_t j = uu - P.r * k;
     const uint8_t* p = A.arena + P.r * A.rec_bytes;
     const Geom g = geom(p, A.rec_bytes);
@@ -277,9 +279,9 @@ struct LdsCopy {  // a global -> LDS copy split in two: the loads, then (after o
     u32x4 v[IT];
     __device__ __forceinline__ void load(const uint32_t* __restrict__ g) {
 #pragma unroll
-        for (int q = 0; q < IT; ++q) {
+        for (int q = 0; q < IT; ++q) {  // (clamped, not branched: a load under a branch is waited for at the join)
             const int i = (int)threadIdx.x + q * THREADS;
-            if (i < N4) v[q] = *(const gu32x4*)(reinterpret_cast<const u32x4*>(g) + i);
+            v[q] = *(const gu32x4*)(reinterpret_cast<const u32x4*>(g) + (i < N4 ? i : N4 - 1));
         }
     }
     __device__ __forceinline__ void store(uint32_t* lds) const {
@@ -296,15 +298,17 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
                  (reinterpret_cast<uintptr_t>(A.arena + A.rec_bytes) + 15) & ~uintptr_t(15));
     __shared__ __attribute__((aligned(16))) uint32_t lds[kSegLdsWords];
-    __shared__ uint32_t s_tag, wst[kWavesPerBlock];
+    __shared__ uint32_t wst[kWavesPerBlock];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t l = lane & (kGroupLanes - 1), grp = lane / kGroupLanes;
     const bool last_wg = blockIdx.x + 1 == gridDim.x;
     SEG_STAMP(0);
-    if (threadIdx.x == 0) {
-        const uint32_t t = (uint32_t)__hip_atomic_load(A.fctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-        s_tag = t ? t : 1u;
-    }
+    // (every load is issued before any is waited for: the call's tag (used before the barrier),
+    // the tables, then the chunks; the grid's fold maps and the tail block come after the steps)
+    // (every thread reads it: a load under a branch would be waited for at the join)
+    // (its low word only: the high one's register would be reused, and waited for, at once)
+    const uint32_t tag =
+        __hip_atomic_load(reinterpret_cast<const uint32_t*>(A.fctl + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     // 1. the table words this thread fills (issued first: waited for before the chunk loads)
     constexpr int NV16 = kRep16Words / 4, IT16 = NV16 / kBlockThreads;
     uint32_t e16[IT16];
@@ -315,30 +319,33 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     }
     LdsCopy<kSmallWords, kBlockThreads> small;
     small.load(A.blob + 1024);
-    LdsCopy<kCombMaps * 1024, kBlockThreads> comb, grid;
+    LdsCopy<kCombMaps * 1024, kBlockThreads> comb;
     comb.load(A.comb_maps);
-    if (last_wg) grid.load(A.block_blob);
     // 2. this lane's unit: every chunk load, the head block and the init word
     const uint64_t U = A.units_per_rec;
     const uint64_t u = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kGroupsPerWave + grp;
-    const FixedPlan P = fixed_plan(A, u, U, l);
+    const FixedPlan P = fixed_plan<true>(A, u, U, l);
     const LaneUnit& L = P.L;
     const bool ok0 = L.nch > 0 && L.w >= L.us && L.w < L.ue;
+    const u32x4 hv = ld16(P.hblk);
     u32x4 v[kSegMaxChunks];
     v[0] = ldg<NT>(ok0 ? L.w : L.lclamp);
 #pragma unroll
     for (int q = 1; q < kSegMaxChunks; ++q) v[q] = ldg<NT>(pmin(L.w + q * kChunk, L.lclamp));
-    const u32x4 hv = ld16(P.hblk);
-    const Geom g0 = geom(A.arena, A.rec_bytes);  // the record's tail block: the last thread's
-    const u32x4 tv = ld16(last_wg && threadIdx.x == 0 && g0.e > g0.b ? g0.b : g0.a);
-    // 3. the tables into LDS (their loads were issued before the chunks': vmcnt counts in order)
+    // 3. the tables into LDS (their loads were issued before the chunks': vmcnt counts in order,
+    //    so waiting for them leaves the chunks in flight; the asm keeps the copies from being
+    //    built, and waited for, between the chunk loads)
     u32x4* l4 = reinterpret_cast<u32x4*>(lds);
 #pragma unroll
-    for (int q = 0; q < IT16; ++q) l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e16[q], e16[q], e16[q], e16[q]};
+    for (int q = 0; q < IT16; ++q) {
+        uint32_t e = e16[q];
+        asm volatile("" : "+v"(e));
+        l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e, e, e, e};
+    }
     small.store(lds + kSegZ4);
     comb.store(lds + kSegComb);
-    if (last_wg) grid.store(lds + kSegGrid);
     __syncthreads();
+    const uint32_t my_tag = tag ? tag : 1u;
     SEG_STAMP(1);
     // 4. the unit's windows (stride_step16s: the 16-copy image in swapped lane order), the lane
     //    fold and the 8-lane tree
@@ -352,6 +359,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
 #pragma unroll
     for (int q = 1; q < kSegMaxChunks; ++q)
         if (q < L.nch - 1 || (q == L.nch - 1 && L.lok)) step4<24>(lds, X, a0, a1, a2, a3, v[q]);
+    LdsCopy<kCombMaps * 1024, kBlockThreads> grid;  // the last workgroup's fold maps, in flight meanwhile
+    if (last_wg) grid.load(A.block_blob);
     uint32_t c = lane_fold_at(lds, kSegZ4, a0, a1, a2, a3);
     c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + L.m + 1) & (kGroupLanes - 1))), 64);
     uint32_t t = __shfl_down(c, 1, kGroupLanes);
@@ -368,6 +377,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     t = __shfl_down(c, 32, 64);
     c = zmap(lds, kSegComb + 2048, c) ^ t;
     if (lane == 0) wst[wave] = c;
+    if (last_wg) grid.store(lds + kSegGrid);
     SEG_STAMP(2);
     __syncthreads();
     if (wave == 0) {
@@ -379,18 +389,20 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
         }
         if (lane == 0)  // tagged: visible to the last workgroup without a fence
             __hip_atomic_store(reinterpret_cast<unsigned long long*>(A.partial) + blockIdx.x,
-                               ((unsigned long long)s_tag << 32) | s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                               ((unsigned long long)my_tag << 32) | s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     SEG_STAMP(3);
     if (!last_wg) return;
     // 6. the grid's last workgroup: its states, end-aligned (leading zeros pad them to whole waves),
     //    a 64-lane tree per wave (Z_{128U 2^d}), the wave results by Horner (Z_{64 128U}), the tail
     const uint32_t G = gridDim.x, nw = (G + 63) / 64, pad = nw * 64 - G;
+    const Geom g0 = geom(A.arena, A.rec_bytes);  // the record's tail block (thread 0), in flight during the wait
+    const u32x4 tv = ld16(threadIdx.x == 0 && g0.e > g0.b ? g0.b : g0.a);
     uint32_t s = 0;
     if (threadIdx.x < nw * 64 && threadIdx.x >= pad) {
         unsigned long long* st = reinterpret_cast<unsigned long long*>(A.partial) + (threadIdx.x - pad);
         unsigned long long w = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while ((uint32_t)(w >> 32) != s_tag) {  // a workgroup whose state is not visible yet
+        while ((uint32_t)(w >> 32) != my_tag) {  // a workgroup whose state is not visible yet
             __builtin_amdgcn_s_sleep(1);
             w = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -410,7 +422,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
         uint32_t r = wst[0];
         for (uint32_t w = 1; w < nw; ++w) r = zmap(lds, kSegGrid + 6 * 1024, r) ^ wst[w];
         A.out[0] = ~steps_in_vec(lds, kSegZ4, kSegZ4 + 4096, r, tv, 0u, g0.e > g0.b ? (uint32_t)(g0.e - g0.b) : 0u);
-        __hip_atomic_store(A.fctl + 1, (unsigned long long)s_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(A.fctl + 1, (unsigned long long)my_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     SEG_STAMP(5);
 }
