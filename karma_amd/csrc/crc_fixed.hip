@@ -321,6 +321,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     small.load(A.blob + 1024);
     LdsCopy<kCombMaps * 1024, kBlockThreads> comb;
     comb.load(A.comb_maps);
+    // every wave's table loads ahead of any wave's chunk loads: the CU returns load data in order
+    // (measured: with the chunk loads issued right behind each wave's own table loads the tables
+    // landed only with the chunks, ~10 us into a 64 MiB call, and no step overlapped the stream)
+    __builtin_amdgcn_s_barrier();
     // 2. this lane's unit: every chunk load, the head block and the init word
     const uint64_t U = A.units_per_rec;
     const uint64_t u = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kGroupsPerWave + grp;

@@ -33,6 +33,9 @@ using namespace dev;
 constexpr int kRaggedPF = 4;       // chunk loads in flight per lane: the small-record kernel
 constexpr int kRaggedUnitsPF = 6;  // ... and the units kernel (k_units_ragged)
 constexpr bool kRaggedNT = true;
+#ifndef KARMA_GRID_TIMING
+#define KARMA_GRID_TIMING 0  // timing builds of the byte grid (Makefile `timing`): wrong CRCs
+#endif
 // A ragged record's unaligned head bytes are stepped by the plan (the entering register goes
 // into the first unit's descriptor), its tail bytes by finalize.  Stepping both edges in the
 // units kernel from the lines it loads anyway saved the plan and finalize 15 us of scattered
@@ -671,13 +674,32 @@ __device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_nex
 #pragma unroll
                 for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(Wb, q));
             }
+#if KARMA_GRID_TIMING == 1  // timing builds only (wrong CRCs): the loads alone
+#pragma unroll
+            for (int q = 0; q < PF; ++q) {
+                a0 ^= cur[q].x;
+                a1 ^= cur[q].y;
+                a2 ^= cur[q].z;
+                a3 ^= cur[q].w;
+            }
+#elif KARMA_GRID_TIMING == 2  // ... every window stepped, no record logic
+#pragma unroll
+            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+#else
 #pragma unroll
             for (int q = 0; q < PF; ++q) process(k * PF + q, cur[q]);
+#endif
         }
+#if KARMA_GRID_TIMING
+        if (l == 0 && t < NT) A.gstate[t] = a0 ^ a1 ^ a2 ^ a3;  // (keeps the work)
+        a0 = a1 = a2 = a3 = 0;
+        (void)active;
+#else
         if (active && ce > (int32_t)kGridTile) {  // the record running past the tile's end
             const uint32_t R = grid_fold(lds, l, kGroupLanes - 1, a0, a1, a2, a3);
             if (l == 0) KB_WRITE(A.gstate, t, A.tile_cap, kKbGrid, R);
         }
+#endif
         sa = sb;
         sb = sc;
         twa = twb;
