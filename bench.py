@@ -243,7 +243,7 @@ def cpu_baseline(workload: str, rec_bytes: int, threads: int, sample=None, orig_
 
 def units_kernel_name(wl: str) -> str:
     """The dominant kernel a batch runs (capi.cc planning, crc_fixed.hip / crc_ragged.hip launchers)."""
-    return "k_units_ragged" if wl == "ragged" else "k_units_fixed"
+    return {"ragged": "k_units_ragged", "segment": "k_segment_once"}.get(wl, "k_units_fixed")
 
 
 def pmc_traffic(path: str, workload: str, n_bytes_per_launch: int):
@@ -356,6 +356,17 @@ def wal_bench(args, L, rank):
                 dev_rate = r
             else:
                 dev_single = r
+        # the replay's CRC kernel alone (HIP events the library records on its replay stream
+        # around that launch: karma_crc32c_time_next_units), rotated images, after the timed loop
+        rot["k"] = len(d_wals)
+        crc_ms = []
+        for _ in range(max(8, min(args.steps, 32))):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            L.karma_crc32c_time_next_units(e0.cuda_event, e1.cuda_event)
+            replay_dev()
+            e1.synchronize()
+            crc_ms.append(e0.elapsed_time(e1))
+        crc_kernel_ms = float(np.median(crc_ms))
         del d_wals
         # the same replay from segment files named by their WAL offsets (karma_wal_replay_dir),
         # page-cached: the files are read straight into the pinned staging buffers
@@ -420,6 +431,24 @@ def wal_bench(args, L, rank):
                                   f"(BASELINE {'configs[0]' if size else 'configs[2]'} records)", "records": n,
                       "record_bytes": size},
            "roofline": None}
+    if args.workload == "wal_replay" and dev_rate is not None:
+        # the dominant kernel of a device-resident replay: the payload CRC batch over the gathered
+        # lists (payload bytes + offset 8 B, length 4 B, stored CRC 4 B, result 4 B per record);
+        # the whole call's image rate beside it
+        algo = payload + 20 * n
+        achieved = algo / (crc_kernel_ms * 1e-3) / 1e9
+        call_s = payload / (dev_rate * GIB)
+        pm = pmc_traffic(os.path.join(ROOT, "profiles", "r04_wal_replay_pmc.json"), "wal_replay", wal_bytes)
+        res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+                           "frac": round(achieved / 8000.0, 4), "traffic": pm,
+                           "traffic_source": "profiles/r04_wal_replay_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, "
+                                             "every kernel of one rotated call)" if pm is not None else None,
+                           "kernel": "the replay's payload CRC batch (k_ragged_staged_pipe)",
+                           "kernel_ms_avg": round(crc_kernel_ms, 4), "algorithmic_bytes_per_launch": algo,
+                           "achieved_source": "algorithmic bytes / the CRC kernel's HIP-event time inside "
+                                              "karma_wal_replay (rotated device-resident images)",
+                           "call_image_bytes": wal_bytes, "call_ms": round(call_s * 1e3, 4),
+                           "call_image_frac": round(wal_bytes / call_s / 8e12, 4)}
     if not args.no_cpu_baseline and size:
         import oracle_lib
         ref = oracle_lib.ref()

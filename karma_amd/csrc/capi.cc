@@ -614,7 +614,9 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
         b.blob = L.ds->lane_blob;
         b.gate_max = stg_max;
         const uint64_t sblocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_cap, 64 * kStgWaves));
+        units_timer_begin(s);  // (karma_crc32c_time_next_units: the replay's CRC kernel)
         KARMA_HIP(launch_ragged_staged_dev(b, (int)sblocks, s));
+        units_timer_end(s);
         if (gate_max <= stg_max) return 0;
         a.gate_min = stg_max + 1;
     }

@@ -16,4 +16,7 @@ find $O/prof -name "*kernel_stats.csv" -exec head -3 {} \;
 LIBS="t2048=karma_amd/lib/libkarma_crc32c.so,gtime1=tools/lib/libkarma_crc32c_gtime1.so,gtime2=tools/lib/libkarma_crc32c_gtime2.so,units=tools/lib/libkarma_crc32c_nogrid.so" \
   timeout -k 10 600 python3 -u tools/ragged_study.py > $O/ragged_timing.log 2>&1
 grep -v "first call" $O/ragged_timing.log
+
+timeout -k 10 300 python3 -u bench.py --workload wal_replay --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_wal_replay.json 2> $O/bench_wal_replay.err
+cat $O/bench_wal_replay.json
 echo done
