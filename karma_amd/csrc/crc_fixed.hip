@@ -303,12 +303,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     const uint32_t l = lane & (kGroupLanes - 1), grp = lane / kGroupLanes;
     const bool last_wg = blockIdx.x + 1 == gridDim.x;
     SEG_STAMP(0);
-    // (every load is issued before any is waited for: the call's tag (used before the barrier),
-    // the tables, then the chunks; the grid's fold maps and the tail block come after the steps)
-    // (every thread reads it: a load under a branch would be waited for at the join)
-    // (its low word only: the high one's register would be reused, and waited for, at once)
-    const uint32_t tag =
-        __hip_atomic_load(reinterpret_cast<const uint32_t*>(A.fctl + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    // (every load is issued before any is waited for: the tables, then the chunks; the call's
+    // tag, the grid's fold maps and the tail block come after the steps -- the tag read is an
+    // agent-scope load of one word that every workgroup makes: issued at entry it held the tables
+    // and chunks behind it for ~8 us on a 64 MiB call)
     // 1. the table words this thread fills (issued first: waited for before the chunk loads)
     constexpr int NV16 = kRep16Words / 4, IT16 = NV16 / kBlockThreads;
     uint32_t e16[IT16];
@@ -349,7 +347,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     small.store(lds + kSegZ4);
     comb.store(lds + kSegComb);
     __syncthreads();
-    const uint32_t my_tag = tag ? tag : 1u;
     SEG_STAMP(1);
     // 4. the unit's windows (stride_step16s: the 16-copy image in swapped lane order), the lane
     //    fold and the 8-lane tree
@@ -365,6 +362,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
         if (q < L.nch - 1 || (q == L.nch - 1 && L.lok)) step4<24>(lds, X, a0, a1, a2, a3, v[q]);
     LdsCopy<kCombMaps * 1024, kBlockThreads> grid;  // the last workgroup's fold maps, in flight meanwhile
     if (last_wg) grid.load(A.block_blob);
+    uint32_t tag = 0;  // wave 0 publishes the workgroup's state, tagged with the call's tag
+    if (wave == 0)
+        tag = __hip_atomic_load(reinterpret_cast<const uint32_t*>(A.fctl + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     uint32_t c = lane_fold_at(lds, kSegZ4, a0, a1, a2, a3);
     c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + L.m + 1) & (kGroupLanes - 1))), 64);
     uint32_t t = __shfl_down(c, 1, kGroupLanes);
@@ -384,7 +384,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     if (last_wg) grid.store(lds + kSegGrid);
     SEG_STAMP(2);
     __syncthreads();
+    __shared__ uint32_t s_tag;
     if (wave == 0) {
+        const uint32_t my_tag = tag ? tag : 1u;
         uint32_t s = lane < kWavesPerBlock ? wst[lane] : 0u;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -394,9 +396,12 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
         if (lane == 0)  // tagged: visible to the last workgroup without a fence
             __hip_atomic_store(reinterpret_cast<unsigned long long*>(A.partial) + blockIdx.x,
                                ((unsigned long long)my_tag << 32) | s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) s_tag = my_tag;
     }
     SEG_STAMP(3);
     if (!last_wg) return;
+    __syncthreads();  // s_tag
+    const uint32_t my_tag = s_tag;
     // 6. the grid's last workgroup: its states, end-aligned (leading zeros pad them to whole waves),
     //    a 64-lane tree per wave (Z_{128U 2^d}), the wave results by Horner (Z_{64 128U}), the tail
     const uint32_t G = gridDim.x, nw = (G + 63) / 64, pad = nw * 64 - G;
