@@ -168,10 +168,12 @@ int dev_state(int dev, DevState** out) {
         build_lane_blob(host.data());
         KARMA_HIP(hipMalloc(&d.lane_blob, kBlobWords * sizeof(uint32_t)));
         KARMA_HIP(hipMemcpy(d.lane_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
-        std::vector<uint32_t> g(kGridCombWords);
-        build_grid_comb_blob(g.data());
-        KARMA_HIP(hipMalloc(&d.gcomb, kGridCombWords * sizeof(uint32_t)));
-        KARMA_HIP(hipMemcpy(d.gcomb, g.data(), kGridCombWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+        if (KARMA_GRID) {
+            std::vector<uint32_t> g(kGridCombWords);
+            build_grid_comb_blob(g.data());
+            KARMA_HIP(hipMalloc(&d.gcomb, kGridCombWords * sizeof(uint32_t)));
+            KARMA_HIP(hipMemcpy(d.gcomb, g.data(), kGridCombWords * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
         d.ready = true;
     }
     *out = &d;
@@ -396,10 +398,6 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 thread_local RaggedArgs t_last_ragged{};  // karma_ab_ragged_took_grid (tools build)
 #endif
 
-#ifndef KARMA_RAGGED_GRID_DEFAULT
-#define KARMA_RAGGED_GRID_DEFAULT 1  // (a build-time A/B knob: 0 builds a library without the byte grid)
-#endif
-
 struct RaggedLayout {
     size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off;
     size_t grec_off, gtile_off, gstate_off, gend_off, gflag_off, gctl_off, total;
@@ -496,7 +494,8 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
         cap = cap_full + 2 * n_rec;
         // the byte grid is tried first when the batch may be sorted (the tools build's
         // KARMA_RAGGED_GRID=0 turns it off for A/B)
-        const uint64_t tile_cap = n_rec < (1ull << 31) && KARMA_AB_KNOB("KARMA_RAGGED_GRID", KARMA_RAGGED_GRID_DEFAULT) ? grid_tile_cap(total_len, n_rec) : 0;
+        const uint64_t tile_cap =
+            KARMA_GRID && n_rec < (1ull << 31) && KARMA_AB_KNOB("KARMA_RAGGED_GRID", 1) ? grid_tile_cap(total_len, n_rec) : 0;
         const RaggedLayout L = ragged_layout(n_rec, cap, tile_cap);
         KARMA_RC(workspace(dev, s, L.total, &ws));
         bind_ragged(a, ws, L, cap);

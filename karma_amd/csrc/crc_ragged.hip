@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
 // its records sorted, non-overlapping, with gaps <= kGridMaxGap and the tiles within tile_cap.
 // Every thread of the block calls this (a block-wide OR).
 __device__ __forceinline__ bool grid_on(const RaggedArgs& A) {
-    if (!A.tile_cap) return false;
+    if (!KARMA_GRID || !A.tile_cap) return false;
     const uint64_t nb = (A.n_rec + kScanBlock - 1) / kScanBlock;
     int bad = 0;
     for (uint64_t i = threadIdx.x; i < nb; i += blockDim.x) bad |= (int)A.gflag[i];
@@ -400,6 +400,7 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
     return UnitDesc{v.x | ((uint64_t)v.y << 32), v.z, v.w};
 }
 
+#if KARMA_GRID  // the byte grid: an experimental build (Makefile `variants`), DESIGN.md §4
 // ---- the byte grid (engine.h; DESIGN.md §4 "The byte grid") ----------------------------------
 // Sorted, non-overlapping records: the bytes they span are cut on the absolute kGridTile grid, one
 // tile per group of 8 lanes, each wave-step 8 consecutive tiles (k_units_fixed's layout).  The
@@ -772,6 +773,8 @@ __device__ void grid_finalize(const RaggedArgs& A, const uint32_t* lds) {
     }
 }
 
+#endif  // KARMA_GRID
+
 // The units kernel: each unit's loads are issued when the unit starts (group_unit), the
 // next descriptor is in flight meanwhile.  (A software-pipelined form, stream_unit's, measured
 // 0.3-0.8 % slower on config 3 in round 2, unlike the fixed layout, where it wins 2.7 %:
@@ -786,10 +789,12 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     __shared__ uint32_t blk_next;  // the block's next wave-step (an LDS counter)
     if (threadIdx.x == 0) blk_next = kWavesPerBlock;
+#if KARMA_GRID
     if (grid_on(A)) {  // (its barrier also publishes blk_next)
         grid_units<kRaggedPF>(A, lds, &blk_next);
         return;
     }
+#endif
     load_stream_tables(lds, A.blob);
     __syncthreads();
     WLOG_DECL;
@@ -851,6 +856,7 @@ __device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, 
 // than 64 units: the whole wave folds all but the last unit with the 64-lane tree.
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
+#if KARMA_GRID
     __shared__ __attribute__((aligned(16))) uint32_t lds[kGridCombWords];
     if (grid_on(A)) {  // (the unit plan did not run: nothing to retire)
         load_comb_tables<kGridCombWords, 1024>(lds, A.gcomb_blob);
@@ -858,6 +864,9 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
         grid_finalize(A, lds);
         return;
     }
+#else
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kCombWords];
+#endif
     if (A.lb) lookback_retire(A);
     load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
     __syncthreads();
@@ -1170,9 +1179,13 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     if (!a.lb || !a.lb_ctl || a.lb_seq_max < 2 || a.lb_seq_max > (1u << 22)) return hipErrorInvalidValue;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
     if (a.tile_cap) {
+#if KARMA_GRID
         if (!a.grec || !a.gtile || !a.gstate || !a.gend || !a.gflag || !a.gctl || !a.gcomb_blob || a.n_rec >= (1ull << 31))
             return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_ragged_grid_plan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+#else
+        return hipErrorInvalidValue;  // a library built without the byte grid
+#endif
     }
     hipLaunchKernelGGL(k_ragged_plan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     units_timer_begin(s);

@@ -44,6 +44,16 @@ constexpr int kCombZ4 = kCombMaps * 1024;
 constexpr int kCombT8 = kCombZ4 + 1024;
 constexpr int kCombCoreWords = kCombT8 + 256;  // what the fixed combine and the head steps need
 constexpr int kCombSmall = kCombT8 + 1024;
+// The ragged byte grid (DESIGN.md §4 "The byte grid"): measured slower than the unit plan on every
+// layout (configs[2] units 0.70-0.73 vs 0.80 of 8 TB/s), so the shipped library leaves it out; the
+// tools build and the `variants` builds carry it.
+#ifndef KARMA_GRID
+#ifdef KARMA_AB
+#define KARMA_GRID 1
+#else
+#define KARMA_GRID 0
+#endif
+#endif
 #ifndef KARMA_GRID_TILE
 #define KARMA_GRID_TILE 2048  // a build-time A/B knob
 #endif

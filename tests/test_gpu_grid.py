@@ -3,7 +3,9 @@ k_ragged_finalize, crc_ragged.hip): sorted, non-overlapping batches of every sha
 oracle, bit for bit; batches that break a grid condition take the unit plan and stay exact; the
 tools build says which path ran (karma_ab_ragged_took_grid), so each case also checks that the
 path it is meant to exercise is the one that ran.  The algebra itself is pinned on the CPU by
-tests/test_grid_math.py."""
+tests/test_grid_math.py.  The grid measured slower than the unit plan, so the
+shipped library is built without it (KARMA_GRID=0, engine.h): these tests run it in the tools
+build, and the same batches through the shipped library's unit plan."""
 import ctypes
 
 import numpy as np
@@ -165,7 +167,7 @@ def test_grid_and_unit_plan_alternate_on_one_stream(raw, dev):
         cases.append((offs, lens, oracle_lib.ragged_crcs(host, offs, lens)))
     s = torch.cuda.Stream()
     torch.cuda.synchronize()
-    with torch.cuda.stream(s):
+    with _lib.using(_lib.AB_LIB_PATH), torch.cuda.stream(s):
         for rnd in range(3):
             for offs, lens, want in cases:
                 _eq(_run(dbuf, offs, lens)[0], want)
@@ -193,18 +195,19 @@ def test_grid_graph_capture_replays(dev):
 
     s = torch.cuda.Stream()
     want = load(1)
-    with torch.cuda.stream(s):
-        K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=cap_total, stream=s)
-    s.synchronize()
-    _eq(out.cpu().numpy(), want)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
-        K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=cap_total, stream=s)
-    for seed in (2, 3):
-        torch.cuda.synchronize()
-        want = load(seed)
-        torch.cuda.synchronize()
-        out.view(torch.int32).fill_(-0x5A5A5A5B)
-        g.replay()
-        torch.cuda.synchronize()
+    with _lib.using(_lib.AB_LIB_PATH):
+        with torch.cuda.stream(s):
+            K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=cap_total, stream=s)
+        s.synchronize()
         _eq(out.cpu().numpy(), want)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=cap_total, stream=s)
+        for seed in (2, 3):
+            torch.cuda.synchronize()
+            want = load(seed)
+            torch.cuda.synchronize()
+            out.view(torch.int32).fill_(-0x5A5A5A5B)
+            g.replay()
+            torch.cuda.synchronize()
+            _eq(out.cpu().numpy(), want)

@@ -12,4 +12,8 @@ cat $O/segment_once_ab.log
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o seg -- python3 -u bench.py --workload segment --steps 200 --warmup 20 --no-cpu-baseline > $O/bench_segment_prof.json 2> $O/bench_segment_prof.err
 cat $O/bench_segment_prof.json
 find $O/prof -name "*kernel_stats.csv" -exec head -3 {} \;
+timeout -k 10 300 $T tests/test_gpu_grid.py --karma-lib abbounds > $O/grid_abbounds.log 2>&1
+tail -1 $O/grid_abbounds.log
+timeout -k 10 300 python3 -u bench.py --workload ragged --steps 100 --warmup 10 --no-cpu-baseline > $O/bench_ragged.json 2> $O/bench_ragged.err
+cat $O/bench_ragged.json
 echo done
