@@ -362,6 +362,9 @@ def wal_bench(args, L, rank):
         crc_ms = []
         for _ in range(max(8, min(args.steps, 32))):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()  # (torch only times events it has recorded once; the library re-records them)
+            e1.record()
+            torch.cuda.synchronize()
             L.karma_crc32c_time_next_units(e0.cuda_event, e1.cuda_event)
             replay_dev()
             e1.synchronize()

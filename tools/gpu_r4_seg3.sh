@@ -16,4 +16,6 @@ timeout -k 10 300 $T tests/test_gpu_grid.py --karma-lib abbounds > $O/grid_abbou
 tail -1 $O/grid_abbounds.log
 timeout -k 10 300 python3 -u bench.py --workload ragged --steps 100 --warmup 10 --no-cpu-baseline > $O/bench_ragged.json 2> $O/bench_ragged.err
 cat $O/bench_ragged.json
+timeout -k 10 300 python3 -u bench.py --workload wal_replay --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_wal_replay.json 2> $O/bench_wal_replay.err
+cat $O/bench_wal_replay.json
 echo done
