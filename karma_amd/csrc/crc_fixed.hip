@@ -319,6 +319,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     small.load(A.blob + 1024);
     LdsCopy<kCombMaps * 1024, kBlockThreads> comb;
     comb.load(A.comb_maps);
+    SEG_STAMP(6);
     // every wave's table loads ahead of any wave's chunk loads: the CU returns load data in order
     // (measured: with the chunk loads issued right behind each wave's own table loads the tables
     // landed only with the chunks, ~10 us into a 64 MiB call, and no step overlapped the stream)
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     v[0] = ldg<NT>(ok0 ? L.w : L.lclamp);
 #pragma unroll
     for (int q = 1; q < kSegMaxChunks; ++q) v[q] = ldg<NT>(pmin(L.w + q * kChunk, L.lclamp));
+    SEG_STAMP(7);
     // 3. the tables into LDS (their loads were issued before the chunks': vmcnt counts in order,
     //    so waiting for them leaves the chunks in flight; the asm keeps the copies from being
     //    built, and waited for, between the chunk loads)

@@ -96,12 +96,31 @@ def main():
             t0 = st[:, 0].min()
             us = (st - t0) / 100.0
             ent["stamps_us"] = {nm: [round(float(np.percentile(us[:, i], q)), 2) for q in (0, 50, 100)]
-                                for i, nm in enumerate(["entry", "loaded", "waves_folded", "published"])}
+                                for i, nm in [(0, "entry"), (6, "tables_issued"), (7, "chunks_issued"), (1, "loaded"),
+                                              (2, "waves_folded"), (3, "published")]}
             last = us[-1]
             ent["last_wg_us"] = {"entry": round(float(last[0]), 2), "loaded": round(float(last[1]), 2),
                                  "published": round(float(last[3]), 2), "waited": round(float(last[4]), 2),
                                  "end": round(float(last[5]), 2)}
             ent["workgroups"] = int(st.shape[0])
+            # the same segment twice back to back, the second logged: data in the MALL and L2,
+            # TLB warm, GPU busy (what is left is the kernel's own latency chain)
+            log.zero_()
+            torch.cuda.synchronize()
+            L.karma_ab_seg_log(ctypes.c_void_p(log.data_ptr()))
+            state["i"] = 0
+            call("1")
+            state["i"] = 0
+            call("1")
+            torch.cuda.synchronize()
+            L.karma_ab_seg_log(None)
+            st = log.cpu().numpy().reshape(256, 8)
+            st = st[st[:, 0] > 0]
+            us = (st - st[:, 0].min()) / 100.0
+            ent["warm_stamps_us"] = {nm: [round(float(np.percentile(us[:, i], q)), 2) for q in (0, 50, 100)]
+                                     for i, nm in [(0, "entry"), (6, "tables_issued"), (7, "chunks_issued"),
+                                                   (1, "loaded"), (2, "waves_folded"), (3, "published")]}
+            ent["warm_last_wg_end_us"] = round(float(us[-1, 5]), 2)
         print(f"{mib} MiB", json.dumps(ent), flush=True)
         assert same, "variants differ"
     os.environ.pop("KARMA_SEGMENT_ONCE", None)
