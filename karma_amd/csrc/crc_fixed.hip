@@ -303,11 +303,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     const uint32_t l = lane & (kGroupLanes - 1), grp = lane / kGroupLanes;
     const bool last_wg = blockIdx.x + 1 == gridDim.x;
     SEG_STAMP(0);
-    // (every load is issued before any is waited for: the tables, then the chunks; the call's
-    // tag, the grid's fold maps and the tail block come after the steps -- the tag read is an
-    // agent-scope load of one word that every workgroup makes: issued at entry it held the tables
-    // and chunks behind it for ~8 us on a 64 MiB call)
-    // 1. the table words this thread fills (issued first: waited for before the chunk loads)
+    // The tables first, into LDS, and only then the chunk loads: issued together, the table loads
+    // (L2 misses after the previous call's stream) queued at the memory channels behind the whole
+    // grid's 64 MiB of chunk requests and landed ~10 us in, after the data, so no step overlapped
+    // the stream.  The call's tag, the grid's fold maps and the tail block are read after the steps.
+    // 1. the table words this thread fills
     constexpr int NV16 = kRep16Words / 4, IT16 = NV16 / kBlockThreads;
     uint32_t e16[IT16];
 #pragma unroll
@@ -320,37 +320,29 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     LdsCopy<kCombMaps * 1024, kBlockThreads> comb;
     comb.load(A.comb_maps);
     SEG_STAMP(6);
-    // every wave's table loads ahead of any wave's chunk loads: the CU returns load data in order
-    // (measured: with the chunk loads issued right behind each wave's own table loads the tables
-    // landed only with the chunks, ~10 us into a 64 MiB call, and no step overlapped the stream)
-    __builtin_amdgcn_s_barrier();
-    // 2. this lane's unit: every chunk load, the head block and the init word
+    // 2. this lane's unit (arithmetic only: it runs while the table loads are in flight)
     const uint64_t U = A.units_per_rec;
     const uint64_t u = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kGroupsPerWave + grp;
     const FixedPlan P = fixed_plan<true>(A, u, U, l);
     const LaneUnit& L = P.L;
     const bool ok0 = L.nch > 0 && L.w >= L.us && L.w < L.ue;
+    // 3. the tables into LDS
+    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
+#pragma unroll
+    for (int q = 0; q < IT16; ++q) l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e16[q], e16[q], e16[q], e16[q]};
+    small.store(lds + kSegZ4);
+    comb.store(lds + kSegComb);
+    __syncthreads();
+    SEG_STAMP(1);
+    // 4. every chunk load of the unit and its head block, consumed in issue order (vmcnt counts)
     const u32x4 hv = ld16(P.hblk);
+    asm volatile("" ::: "memory");  // (issued before the chunks: the first step needs it)
     u32x4 v[kSegMaxChunks];
     v[0] = ldg<NT>(ok0 ? L.w : L.lclamp);
 #pragma unroll
     for (int q = 1; q < kSegMaxChunks; ++q) v[q] = ldg<NT>(pmin(L.w + q * kChunk, L.lclamp));
     SEG_STAMP(7);
-    // 3. the tables into LDS (their loads were issued before the chunks': vmcnt counts in order,
-    //    so waiting for them leaves the chunks in flight; the asm keeps the copies from being
-    //    built, and waited for, between the chunk loads)
-    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
-#pragma unroll
-    for (int q = 0; q < IT16; ++q) {
-        uint32_t e = e16[q];
-        asm volatile("" : "+v"(e));
-        l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e, e, e, e};
-    }
-    small.store(lds + kSegZ4);
-    comb.store(lds + kSegComb);
-    __syncthreads();
-    SEG_STAMP(1);
-    // 4. the unit's windows (stride_step16s: the 16-copy image in swapped lane order), the lane
+    // 5. the unit's windows (stride_step16s: the 16-copy image in swapped lane order), the lane
     //    fold and the 8-lane tree
     const uint32_t X = lane_const16();
     uint32_t inj = 0;
@@ -375,7 +367,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     c = zmap(lds, kSegZ4 + 2048, c) ^ t;
     t = __shfl_down(c, 4, kGroupLanes);
     c = zmap(lds, kSegZ4 + 3072, c) ^ t;
-    // 5. the wave's 8 units (Z_U, Z_2U, Z_4U), the workgroup's 16 waves (Z_8U .. Z_64U)
+    // 6. the wave's 8 units (Z_U, Z_2U, Z_4U), the workgroup's 16 waves (Z_8U .. Z_64U)
     t = __shfl_down(c, 8, 64);
     c = zmap(lds, kSegComb, c) ^ t;
     t = __shfl_down(c, 16, 64);
@@ -404,7 +396,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     if (!last_wg) return;
     __syncthreads();  // s_tag
     const uint32_t my_tag = s_tag;
-    // 6. the grid's last workgroup: its states, end-aligned (leading zeros pad them to whole waves),
+    // 7. the grid's last workgroup: its states, end-aligned (leading zeros pad them to whole waves),
     //    a 64-lane tree per wave (Z_{128U 2^d}), the wave results by Horner (Z_{64 128U}), the tail
     const uint32_t G = gridDim.x, nw = (G + 63) / 64, pad = nw * 64 - G;
     const Geom g0 = geom(A.arena, A.rec_bytes);  // the record's tail block (thread 0), in flight during the wait

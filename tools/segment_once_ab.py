@@ -96,7 +96,7 @@ def main():
             t0 = st[:, 0].min()
             us = (st - t0) / 100.0
             ent["stamps_us"] = {nm: [round(float(np.percentile(us[:, i], q)), 2) for q in (0, 50, 100)]
-                                for i, nm in [(0, "entry"), (6, "tables_issued"), (7, "chunks_issued"), (1, "loaded"),
+                                for i, nm in [(0, "entry"), (6, "tables_issued"), (1, "tables_in_lds"), (7, "chunks_issued"),
                                               (2, "waves_folded"), (3, "published")]}
             last = us[-1]
             ent["last_wg_us"] = {"entry": round(float(last[0]), 2), "loaded": round(float(last[1]), 2),
@@ -118,8 +118,8 @@ def main():
             st = st[st[:, 0] > 0]
             us = (st - st[:, 0].min()) / 100.0
             ent["warm_stamps_us"] = {nm: [round(float(np.percentile(us[:, i], q)), 2) for q in (0, 50, 100)]
-                                     for i, nm in [(0, "entry"), (6, "tables_issued"), (7, "chunks_issued"),
-                                                   (1, "loaded"), (2, "waves_folded"), (3, "published")]}
+                                     for i, nm in [(0, "entry"), (6, "tables_issued"), (1, "tables_in_lds"),
+                                                   (7, "chunks_issued"), (2, "waves_folded"), (3, "published")]}
             ent["warm_last_wg_end_us"] = round(float(us[-1, 5]), 2)
         print(f"{mib} MiB", json.dumps(ent), flush=True)
         assert same, "variants differ"
