@@ -1,0 +1,9 @@
+#!/usr/bin/env bash
+# Round 4 final, part B: rocprofv3 kernel traces and FETCH/WRITE passes (each its own run) for
+# the fixed, ragged and segment bench lines; the replay's trace, SQ and FETCH/WRITE passes.
+set -euo pipefail
+for W in fixed ragged segment; do
+  timeout -k 10 900 bash tools/profile_round.sh r04 $W > gpurun_out/profile_r04_$W.log 2>&1
+done
+timeout -k 10 900 bash tools/pmc_replay.sh r04 > gpurun_out/pmc_replay_r04.log 2>&1
+echo done
