@@ -586,7 +586,7 @@ int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_
 }
 int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
                            uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
-                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s) {
+                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s, int which) {
     if (!n_cap) return 0;
     Locked L;
     if (L.rc) return L.rc;
@@ -606,9 +606,11 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
     // Two gated launches split the range of the batch's largest payload (known on the device
     // only): up to kStgGateLen the LDS-staged kernel (64 consecutive WAL payloads per wave's
     // stage, windows aligned to the record ends: k_ragged_staged_pipe), above it the 4-lane
-    // groups (k_ragged_direct4); the other one returns at once.
+    // groups (k_ragged_direct4); the other one returns at once (~5 us for the 4-lane kernel's
+    // 4,096 waves to read the gate).  kSmallStaged / kSmallDirect launch one of them only.
     const uint32_t stg_max = std::min<uint32_t>(gate_max, kStgGateLen);
-    if (KARMA_AB_KNOB("KARMA_SMALL_STAGED", 1)) {
+    if (which == kSmallDirect) a.gate_min = stg_max + 1;
+    if (which != kSmallDirect && KARMA_AB_KNOB("KARMA_SMALL_STAGED", 1)) {
         RaggedArgs b = a;
         b.blob = L.ds->lane_blob;
         b.gate_max = stg_max;
@@ -616,7 +618,7 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
         units_timer_begin(s);  // (karma_crc32c_time_next_units: the replay's CRC kernel)
         KARMA_HIP(launch_ragged_staged_dev(b, (int)sblocks, s));
         units_timer_end(s);
-        if (gate_max <= stg_max) return 0;
+        if (gate_max <= stg_max || which == kSmallStaged) return 0;
         a.gate_min = stg_max + 1;
     }
     const uint64_t blocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_cap, 64 * kWavesPerBlock));

@@ -265,17 +265,25 @@ hipError_t launch_ragged_direct_dev(const RaggedArgs& a, int grid_blocks, hipStr
 // (WAL replay): CRCs of arena[off[r], off[r] + len[r]) with Value's init.
 int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, size_t n_rec,
                        uint32_t* d_out, hipStream_t s);
-// The same with the record count in device memory (*d_n, at most n_cap records), run only when
-// *d_gate_len <= gate_max (else the kernel does nothing).
-// With d_stored set it is also the CRC check: the first record whose CRC differs from
-// d_stored[r] (length 0 excepted) goes to *d_first_bad (atomicMin).
 // The 4-lane small-record kernel's table blob on the current device (k_wal_walk_crc's tables).
 int device_quad_blob(int dev, const uint32_t** out);
 // The staged kernels' blob (Z_16 stride tables: k_ragged_staged, k_wal_list_crc).
 int device_lane_blob(int dev, const uint32_t** out);
+// The same as ragged_small_batch with the record count in device memory (*d_n, at most n_cap
+// records), run only when *d_gate_len <= gate_max (else the kernels do nothing).  `which` picks
+// the launches: kSmallBoth = the LDS-staged kernel up to kStgGateLen and the 4-lane kernel above
+// it (one of the two returns at once); kSmallStaged / kSmallDirect = only that one (the caller
+// checks the batch's largest payload afterwards and runs the batch again when it was not
+// covered: small_batch_covers).  With d_stored set it is also the CRC check: the first record
+// whose CRC differs from d_stored[r] (length 0 excepted) goes to *d_first_bad (atomicMin).
+enum SmallWhich : int { kSmallBoth = 0, kSmallStaged = 1, kSmallDirect = 2 };
+inline bool small_batch_covers(int which, uint32_t max_len, uint32_t gate_max) {
+    if (max_len > gate_max) return false;
+    return which == kSmallBoth || (which == kSmallStaged ? max_len <= kStgGateLen : max_len > kStgGateLen);
+}
 int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
                            uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
-                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s);
+                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s, int which = kSmallBoth);
 
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {

@@ -160,6 +160,10 @@ struct ReplayCtx {
     DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, sum;
     DevBuf h_small;                             // pinned readback of the summary
     uint64_t img_gen = 0;                       // uploads of a host image into img so far
+    // the largest payload of the last device-planned pass on this context: the next pass
+    // launches only the small-record kernel that covered it (karma::engine::SmallWhich)
+    bool have_len_hint = false;
+    uint32_t len_hint = 0;
     int init(int dev) {
         if (ready) return 0;
         hipDeviceProp_t prop;
@@ -398,6 +402,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     A.first_bad = &A.sum->first_bad;
     A.wal_end = wal_bytes;
     const uint32_t direct_max = batch == KARMA_WAL_CRC_DIRECT ? ~0u : kSmallRecordMax;  // the device-side gate
+    int small_which = kSmallBoth;
     auto bind_lists = [&](uint64_t cap) {  // the contiguous lists for up to cap candidates
         if (const int rc = c.off.ensure(cap * 8)) return rc;
         if (const int rc = c.len.ensure(cap * 4)) return rc;
@@ -428,9 +433,14 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         if (const int rc = bind_lists(cap_all)) return rc;
         if (launch_wal_gather(A, nwork, fused_plan, c.st) != hipSuccess)
             return fail(KARMA_E_HIP, "wal_replay: gather");
-        // the CRC batch is also the check (first mismatch into the summary): no compare launch
+        // the CRC batch is also the check (first mismatch into the summary): no compare launch.
+        // Which kernel covers the largest payload is known on the device only; the last pass's
+        // largest payload picks one launch (the other one, gated off, cost ~5 us), and a pass
+        // whose records it did not cover runs the batch again below (one more round trip).
+        small_which = !c.have_len_hint ? kSmallBoth : c.len_hint <= kStgGateLen ? kSmallStaged : kSmallDirect;
         if (const int rc = ragged_small_batch_dev(A.wal + 8, A.off, A.len, &A.sum->n_all, cap_all, &A.sum->max_len,
-                                                  direct_max, c.crc.as<uint32_t>(), A.stored, A.first_bad, c.st))
+                                                  direct_max, c.crc.as<uint32_t>(), A.stored, A.first_bad, c.st,
+                                                  small_which))
             return rc;
     }
     WalSummary* S = c.h_small.as<WalSummary>();
@@ -450,15 +460,22 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     // inline CRCs complete: the first mismatch is known (no gathered lists exist yet)
     const bool inline_done = inline_crc && !S->crc_unknown;
     const bool lists = dev_plan && !inline_crc;  // the device-planned gather wrote them
+    // the device-sized batch ran and covered every payload
+    const bool batch_done = lists && small && small_batch_covers(small_which, max_len, direct_max);
+    if (lists && n_all) {
+        c.have_len_hint = true;
+        c.len_hint = max_len;
+    }
     uint64_t accepted = n_all;
     if (inline_done && S->first_bad < n_all) {
         accepted = S->first_bad;
         status = KARMA_WAL_CORRUPT;
         end = base0 + S->bad_off;
     }
-    if (n_all && !inline_done && !(lists && small)) {
+    if (n_all && !inline_done && !batch_done) {
         // 3. the host-sized CRC batch: large payloads (the ragged plan), an image too large for
-        //    the device-planned lists, or runs the inline walk could not checksum
+        //    the device-planned lists, runs the inline walk could not checksum, or payloads the
+        //    one small-record kernel launched above did not cover
         if (!lists) {
             if (const int rc = bind_lists(n_all)) return rc;
             if (launch_wal_gather(A, nwork, false, c.st) != hipSuccess)

@@ -520,3 +520,36 @@ def test_replay_accepted_size0_records_advance_12(lib, seg, walk, monkeypatch):
         for past in range(1, 5):
             assert _replay(lib, wal, start=wal.size + past, seg=seg) == ([], wal.size + past, 0)
     assert spills > 0, "some size-0 record must carry the chain into the next segment"
+
+
+@pytest.mark.parametrize("walk", ["split", "sep", "split4k"])
+def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
+    """The device-planned replay launches one small-record kernel, chosen by the largest payload of
+    the previous call on the same device (the staged kernel up to 183 B, the 4-lane kernel up to
+    1 KiB); a call whose payloads that kernel does not cover runs the batch again.  Every
+    transition between the classes (<= 183 B, 184 B-1 KiB, larger, and a WAL with no record), with
+    and without a corrupt payload, must give scan_record's result."""
+    _walk_env(monkeypatch, walk)
+    seg = 64 << 10
+    wals = {}
+    for name, lo, hi, seed in (("small", 1, 183, 81), ("edge", 170, 200, 82), ("mid", 184, 1024, 83),
+                               ("large", 100, 6000, 84)):
+        src, offs, lens = _payloads(seed, 1500, lo, hi)
+        nseg = int((lens.astype(np.int64) + 8).sum() // (seg - 6100)) + 2
+        wal = np.zeros(nseg * seg, np.uint8)
+        cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+        assert len(rec) == lens.size
+        bad = wal.copy()
+        k = 1000
+        bad[int(rec[k]) + 8 + int(lens[k]) // 2] ^= 0x40
+        wals[name] = wal
+        wals[name + "_bad"] = bad
+    wals["empty"] = np.zeros(4 * seg, np.uint8)
+    want = {k: wal_model.replay(w.tobytes(), seg) for k, w in wals.items()}
+    order = ["small", "small_bad", "mid", "mid_bad", "small", "mid", "large", "small_bad", "edge", "edge_bad",
+             "mid", "large_bad", "mid_bad", "empty", "small", "edge", "small", "mid", "small"]
+    dev = {k: torch.from_numpy(w).cuda() for k, w in wals.items()}
+    for i, name in enumerate(order):
+        w = want[name]
+        got = _replay(lib, wals[name], d_wal=dev[name], seg=seg, host=bool(i % 2))
+        assert got == (list(w[0]), w[1], w[2]), (i, name, walk)

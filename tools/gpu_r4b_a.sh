@@ -1,0 +1,20 @@
+#!/usr/bin/env bash
+# Round 4, session 2, part A: the new replay test on the bounds build, then the GPU suite on the
+# shipped and bounds builds, smoke(), the default and driver-style bench lines.
+set -euo pipefail
+O=gpurun_out/r4b
+mkdir -p $O
+T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+timeout -k 10 300 $T tests/test_gpu_wal.py -k size_class --karma-lib bounds > $O/size_class_bounds.log 2>&1
+tail -1 $O/size_class_bounds.log
+timeout -k 10 600 $T tests -m gpu > $O/r04_gpu_tests.log 2>&1
+tail -1 $O/r04_gpu_tests.log
+timeout -k 10 600 $T tests -m gpu --karma-lib bounds > $O/r04_gpu_tests_bounds.log 2>&1
+tail -1 $O/r04_gpu_tests_bounds.log
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/r04_smoke.log 2>&1
+tail -1 $O/r04_smoke.log
+timeout -k 10 300 python3 -u bench.py > $O/r04_bench_default.json 2> $O/r04_bench_default.err
+cat $O/r04_bench_default.json
+timeout -k 10 200 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/r04_bench_driver_style.json 2> $O/r04_bench_driver_style.err
+cat $O/r04_bench_driver_style.json
+echo done
