@@ -106,14 +106,20 @@ def test_thousand_streams_released(dev):
         assert nrec.value == plens.size
 
     # warm-up: what a process keeps once it has used a device (the per-device tables, the code
-    # objects of every kernel launched) exists before the baseline
-    s0 = ctypes.c_void_p()
-    assert hip.hipStreamCreate(ctypes.byref(s0)) == 0
-    one_stream(s0)
-    wal_round()
-    assert L.karma_crc32c_release_stream(-1, s0) == 0
-    assert hip.hipStreamDestroy(s0) == 0
-    assert L.karma_crc32c_trim(-1) == 0
+    # objects of every kernel launched) exists before the baseline.  Streams share the runtime's
+    # hardware queues (GPU_MAX_HW_QUEUES, 4 here) round robin, and each queue keeps the scratch
+    # memory its kernels once needed (the bounds-checked build's WAL kernels use 280-360 B of
+    # scratch per lane: ~150 MiB a queue), so every queue runs the calls once before the baseline
+    # (a trim destroys the WAL contexts' streams: the next replay's stream takes the next queue).
+    for _ in range(8):
+        s0 = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s0)) == 0
+        one_stream(s0)
+        assert hip.hipStreamSynchronize(s0) == 0
+        assert L.karma_crc32c_release_stream(-1, s0) == 0
+        assert hip.hipStreamDestroy(s0) == 0
+        wal_round()
+        assert L.karma_crc32c_trim(-1) == 0
     base = _free()
     worst = 0
     for i in range(1000):

@@ -5,8 +5,8 @@ set -euo pipefail
 O=gpurun_out/r4b
 mkdir -p $O
 T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-timeout -k 10 300 $T tests/test_gpu_wal.py -k size_class --karma-lib bounds > $O/size_class_bounds.log 2>&1
-tail -1 $O/size_class_bounds.log
+timeout -k 10 300 $T tests/test_gpu_lifetime.py --karma-lib bounds > $O/lifetime_bounds.log 2>&1
+tail -1 $O/lifetime_bounds.log
 timeout -k 10 600 $T tests -m gpu > $O/r04_gpu_tests.log 2>&1
 tail -1 $O/r04_gpu_tests.log
 timeout -k 10 600 $T tests -m gpu --karma-lib bounds > $O/r04_gpu_tests_bounds.log 2>&1
