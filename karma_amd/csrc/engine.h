@@ -377,7 +377,7 @@ hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& p
 hipError_t launch_wal_plan(const WalArgs& a, uint64_t nseg, hipStream_t s);
 // Gather: one block per segment of the nseg walked; segments from sum->w1 on do nothing.
 // fused_plan (nseg <= 1024): the gather computes the plan itself (no launch_wal_plan before it).
-hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, hipStream_t s);
+hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, int cu, hipStream_t s);
 // The first of n candidates whose payload CRC differs from the stored one (atomicMin into *first_bad).
 hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);
 

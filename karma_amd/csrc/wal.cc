@@ -431,7 +431,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         return fail(KARMA_E_HIP, "wal_replay: header walk");
     if (dev_plan && !inline_crc) {
         if (const int rc = bind_lists(cap_all)) return rc;
-        if (launch_wal_gather(A, nwork, fused_plan, c.st) != hipSuccess)
+        if (launch_wal_gather(A, nwork, fused_plan, c.cu, c.st) != hipSuccess)
             return fail(KARMA_E_HIP, "wal_replay: gather");
         // the CRC batch is also the check (first mismatch into the summary): no compare launch.
         // Which kernel covers the largest payload is known on the device only; the last pass's
@@ -478,7 +478,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         //    one small-record kernel launched above did not cover
         if (!lists) {
             if (const int rc = bind_lists(n_all)) return rc;
-            if (launch_wal_gather(A, nwork, false, c.st) != hipSuccess)
+            if (launch_wal_gather(A, nwork, false, c.cu, c.st) != hipSuccess)
                 return fail(KARMA_E_HIP, "wal_replay: gather");
         }
         // payload = header + 8: the arena is the image shifted by the header
@@ -504,7 +504,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         }
         if (h_rec_off && rec_cap && accepted && inline_done) {  // the offsets: the lists are gathered now
             if (const int rc = bind_lists(n_all)) return rc;
-            if (launch_wal_gather(A, nwork, false, c.st) != hipSuccess)
+            if (launch_wal_gather(A, nwork, false, c.cu, c.st) != hipSuccess)
                 return fail(KARMA_E_HIP, "wal_replay: gather");
         }
         if (h_rec_off && rec_cap && accepted) {

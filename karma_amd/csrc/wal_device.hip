@@ -1121,7 +1121,7 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
             g0 += s_pre[v];
             n_all += s_all[v];
         }
-        if (blockIdx.x == 0 && tid == 0) {
+        if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
             WalSummary S{n_all, A.wal_end, w1, KARMA_WAL_END, s_max, 1u, ~0ull, 0ull};
             if (A.meta[w1 - 1].kind != KARMA_WAL_END) {
                 S.status = A.meta[w1 - 1].kind;
@@ -1140,12 +1140,14 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
     const uint32_t* clen = A.cand_len + blockIdx.x * A.cand_cap;
     const uint32_t* ccrc = A.cand_crc + blockIdx.x * A.cand_cap;
     __syncthreads();
-    const uint32_t count = s_count;
+    // gridDim.y blocks per segment (few segments would leave CUs idle), each a contiguous part
+    const uint32_t per = (s_count + gridDim.y - 1) / gridDim.y, i_lo = blockIdx.y * per;
+    const uint32_t count = min(s_count, i_lo + per);
     // kGatherU candidates per thread per trip, every load issued before the first store: one
     // memory latency per trip instead of one per candidate (a segment of 1 MiB holds ~5600
     // candidates of 180 B: one trip of 1024 threads)
     constexpr int kGatherU = 8;
-    for (uint32_t i0 = threadIdx.x; i0 < count; i0 += kGatherU * blockDim.x) {
+    for (uint32_t i0 = i_lo + threadIdx.x; i0 < count; i0 += kGatherU * blockDim.x) {
         uint32_t vr[kGatherU], vn[kGatherU], vc[kGatherU];
 #pragma unroll
         for (int u = 0; u < kGatherU; ++u) {
@@ -1224,13 +1226,17 @@ hipError_t launch_wal_plan(const WalArgs& a, uint64_t nseg, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, hipStream_t s) {
+hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, int cu, hipStream_t s) {
     if (!nseg) return hipSuccess;
+    // blocks per segment: about 2 blocks per CU in all (1 MiB segments of 180-B records: 188
+    // segments, 3 blocks of ~1,900 candidates each)
+    const uint64_t parts = std::min<uint64_t>(8, std::max<uint64_t>(1, (2 * (uint64_t)cu + nseg - 1) / nseg));
+    const dim3 grid((unsigned)nseg, (unsigned)parts);
     if (fused_plan) {
         if (nseg > 1024) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_wal_gather<true>, dim3((unsigned)nseg), dim3(1024), 0, s, a);
+        hipLaunchKernelGGL(k_wal_gather<true>, grid, dim3(1024), 0, s, a);
     } else {
-        hipLaunchKernelGGL(k_wal_gather<false>, dim3((unsigned)nseg), dim3(1024), 0, s, a);
+        hipLaunchKernelGGL(k_wal_gather<false>, grid, dim3(1024), 0, s, a);
     }
     return hipGetLastError();
 }

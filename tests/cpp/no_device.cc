@@ -27,7 +27,7 @@ hipError_t launch_wal_walk(const WalArgs&, uint64_t, const WalWalkPlan&, hipStre
 hipError_t launch_ragged_direct_dev(const RaggedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_ragged_staged_dev(const RaggedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_wal_plan(const WalArgs&, uint64_t, hipStream_t) { return hipErrorNoDevice; }
-hipError_t launch_wal_gather(const WalArgs&, uint64_t, bool, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_wal_gather(const WalArgs&, uint64_t, bool, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_wal_compare(const WalArgs&, uint64_t, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_fill_splitmix(uint8_t*, uint64_t, uint64_t, uint64_t, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_stream_probe(const uint8_t*, uint64_t, uint32_t*, int, hipStream_t) { return hipErrorNoDevice; }

@@ -17,6 +17,7 @@ copy for each variant in interleaved rounds (same process, same image):
     listcrc              tools build, KARMA_WAL_CRC_INLINE + KARMA_WAL_LIST_CRC=1: the walk, then the walkers' lists checksummed by
                          the LDS-staged one-record-per-lane kernel (k_wal_list_crc)
     sepdirect4           tools build, KARMA_WAL_CRC_SEPARATE with KARMA_SMALL_STAGED=0 (the 4-lane batch)
+    lib=<path>           another build of the library (e.g. the previous commit's), default plan
     sep                  the shipped library, KARMA_WAL_CRC_SEPARATE: walk, gather, one batch (round 2's path;
                          the default now checksums inside the walk kernel, k_wal_walk_crc)
 
@@ -114,6 +115,9 @@ def main():
             variants[v] = (L, 0, 3, None)
         elif v.startswith("sub="):
             variants[v] = (L, int(v[4:]), 0, None)
+        elif v.startswith("lib="):  # another build's default plan, loaded beside the shipped one
+            path = v[4:]
+            variants[v] = (_lib.load(path if os.path.isabs(path) else os.path.join(ROOT, path)), 0, 0, None)
     res = {v: [] for v in variants}
     res1 = {v: [] for v in variants}
 
