@@ -243,6 +243,7 @@ int bind_lookback(int dev, hipStream_t s, uint64_t nb, RaggedArgs& a) {
     a.lb_words = 2 * half;
     // (the tools build can lower the wrap point to test it: KARMA_LB_SEQ_MAX, ab.h)
     a.lb_seq_max = (uint32_t)std::min<long>(KARMA_AB_KNOB("KARMA_LB_SEQ_MAX", 1l << 22), 1l << 22);
+    a.dyn_shift = (uint32_t)std::min<long>(std::max<long>(KARMA_AB_KNOB("KARMA_RAGGED_DYN", KARMA_RAGGED_DYN_SHIFT), 0), 16);
     return 0;
 }
 

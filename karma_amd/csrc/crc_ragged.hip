@@ -307,6 +307,7 @@ __device__ void lookback_retire(const RaggedArgs& A) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         lb_store(A.lb, 0ull);
         lb_store(A.lb_ctl, wrap ? 0ull : (unsigned long long)seq);
+        lb_store(A.lb_ctl + 2, 0ull);  // k_units_ragged's dynamic wave-step counter
     }
 }
 
@@ -807,9 +808,17 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     const uint64_t U = M.U;
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     // As k_units_fixed, the block's wave-steps b*16 + j + r*nwaves are taken in order from an
-    // LDS counter, one step ahead (the next descriptor is loaded while a unit streams).
+    // LDS counter, one step ahead (the next descriptor is loaded while a unit streams).  With
+    // dyn_shift, the static shares end at S (whole rounds) and the last steps [S, nws) go to
+    // whichever wave asks first, from a global counter: a unit here streams for tens of us, so
+    // static shares of the last steps leave CUs idle while others finish.
     const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
-    const uint32_t nidx = (uint32_t)((nws + nwaves - 1) / nwaves) * kWavesPerBlock;
+    uint64_t S = nws;
+    if (A.dyn_shift) {
+        const uint64_t s = (nws - (nws >> A.dyn_shift)) / nwaves * nwaves;
+        S = s >= nwaves ? s : nws;
+    }
+    const uint32_t nidx = (uint32_t)((S + nwaves - 1) / nwaves) * kWavesPerBlock;
     const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
     uint64_t wb = bw0 + (threadIdx.x >> 6);
     uint64_t u = wb * kGroupsPerWave + grp;
@@ -823,6 +832,12 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
             if (lane == 0) i = atomicAdd(&blk_next, 1u);
             i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
             wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
+            if (i >= nidx && S < nws) {  // the static share is done: a dynamic step (one round trip)
+                unsigned long long j = 0;
+                if (lane == 0) j = atomicAdd(A.lb_ctl + 2, 1ull);
+                j = (unsigned long long)__builtin_amdgcn_readfirstlane((int)__shfl((int)j, 0));
+                wb_next = S + j < nws ? S + j : nws;
+            }
         }
         const uint64_t un = wb_next * kGroupsPerWave + grp;
         d = un < U ? load_desc(&KB_READ(A.desc, M.slot(un), A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};

@@ -54,6 +54,9 @@ constexpr int kCombSmall = kCombT8 + 1024;
 #define KARMA_GRID 0
 #endif
 #endif
+#ifndef KARMA_RAGGED_DYN_SHIFT
+#define KARMA_RAGGED_DYN_SHIFT 0  // RaggedArgs::dyn_shift (a build-time A/B knob; the tools build's KARMA_RAGGED_DYN)
+#endif
 #ifndef KARMA_GRID_TILE
 #define KARMA_GRID_TILE 2048  // a build-time A/B knob
 #endif
@@ -176,9 +179,12 @@ struct RaggedArgs {
     // to seq, or, at lb_seq_max, clears the lb_words status words and restarts the tags at 1.
     unsigned long long* lb;
     unsigned long long* lbp;   // the same for the blocks' partial unit counts
-    unsigned long long* lb_ctl;  // [0] the last finished call's tag, [1] the running call's
+    unsigned long long* lb_ctl;  // [0] the last finished call's tag, [1] the running call's, [2] dyn steps taken
     uint64_t lb_words;         // status words after lb[0] (both arrays)
     uint32_t lb_seq_max;       // 2^22 (the tools build lowers it to test the wrap)
+    // k_units_ragged: the last nws >> dyn_shift wave-steps (0: none) are taken from a global
+    // counter (lb_ctl[2], reset by k_ragged_finalize) instead of each workgroup's static share
+    uint32_t dyn_shift;
     UnitDesc* desc;            // unit_cap entries
     uint64_t unit_cap;         // capacity of desc / partial
     uint64_t part_base;        // first slot of the partial units (full units take [0, part_base))

@@ -623,3 +623,41 @@ def test_ragged_bounded_consecutive_records(raw, dev, shape, variant, monkeypatc
                                              torch.cuda.current_stream().cuda_stream)
     assert st == 0, L.karma_crc32c_last_error()
     _eq(out.cpu().numpy().view(np.uint32), oracle_lib.ragged_crcs(host[start:], offs, lens, init))
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3, 16])
+def test_ragged_dynamic_tail_steps(dev, shift, monkeypatch):
+    """k_units_ragged with the last nws >> shift wave-steps taken from a global counter
+    (RaggedArgs::dyn_shift; the tools build's KARMA_RAGGED_DYN): configs[2]'s length mix, short
+    records (many wave-steps), a batch too small for any dynamic step, back to back on one stream
+    (k_ragged_finalize resets the counter) and replayed from a captured graph, exact against the
+    oracle.  Unit plan only (KARMA_RAGGED_GRID=0)."""
+    monkeypatch.setenv("KARMA_RAGGED_DYN", str(shift))
+    monkeypatch.setenv("KARMA_RAGGED_GRID", "0")
+    rng = np.random.default_rng(60 + shift)
+    arena_bytes = 256 << 20
+    host = rng.integers(0, 256, arena_bytes, dtype=np.uint8)
+    arena = torch.from_numpy(host).to(dev)
+    shapes = []
+    for n, lo, hi in ((20000, 64, 65536), (300000, 1, 700), (50, 1, 20000)):
+        lens = (synth.loguniform_lengths(shift + n, n, lo, hi) if hi == 65536 else rng.integers(lo, hi, n)).astype(np.uint32)
+        offs = rng.integers(0, arena_bytes - hi, n).astype(np.uint64)
+        shapes.append((torch.from_numpy(offs.astype(np.int64)).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev),
+                       int(lens.sum()), oracle_lib.ragged_crcs(host, offs, lens)))
+    s = torch.cuda.Stream()
+    with _lib.using(_lib.AB_LIB_PATH), torch.cuda.stream(s):
+        for i in range(7):
+            d_off, d_len, total, want = shapes[i % 3]
+            _eq(K.extend_batch_ragged(arena, d_off, d_len, total_len=total, stream=s).cpu().numpy(), want)
+        d_off, d_len, total, want = shapes[0]
+        out = torch.empty(d_off.numel(), dtype=torch.uint32, device=dev)
+        K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=total, stream=s)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            K.extend_batch_ragged(arena, d_off, d_len, out=out, total_len=total, stream=s)
+        for _ in range(3):
+            out.view(torch.int32).fill_(-0x5A5A5A5B)
+            g.replay()
+            torch.cuda.synchronize()
+            _eq(out.cpu().numpy(), want)
