@@ -138,7 +138,12 @@ def test_thousand_streams_released(dev):
         assert hip.hipStreamDestroy(s) == 0
     assert L.karma_crc32c_trim(-1) == 0
     after = _free()
-    assert base - after < 16 * MIB, f"{(base - after) / MIB:.1f} MiB not returned (peak {(worst) / MIB:.1f} MiB)"
+    # The bounds-checked build's WAL kernels use 280-360 B of scratch per lane; the HIP runtime
+    # keeps a queue's scratch (288 B x 64 lanes x 8,192 wave slots = 144 MiB) after the library
+    # freed everything it allocated, so that build is allowed one such block on top.  The shipped
+    # build's kernels use no scratch and are held to 16 MiB.
+    slack = 16 * MIB + (144 * MIB if hasattr(L, "karma_debug_bounds_report") else 0)
+    assert base - after < slack, f"{(base - after) / MIB:.1f} MiB not returned (peak {(worst) / MIB:.1f} MiB)"
 
 
 def test_per_thread_stream_state_is_freed_after_thread_exit(dev):
