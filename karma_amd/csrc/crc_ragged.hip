@@ -789,7 +789,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
     __shared__ uint32_t blk_next;  // the block's next wave-step (an LDS counter)
+    __shared__ uint32_t blk_dyn[kDynChunks];  // dynamic tail: base of the block's c-th chunk of 16 steps
     if (threadIdx.x == 0) blk_next = kWavesPerBlock;
+    for (uint32_t c = threadIdx.x; c < kDynChunks; c += blockDim.x) blk_dyn[c] = ~0u;
 #if KARMA_GRID
     if (grid_on(A)) {  // (its barrier also publishes blk_next)
         grid_units<kRaggedPF>(A, lds, &blk_next);
@@ -810,12 +812,15 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     // As k_units_fixed, the block's wave-steps b*16 + j + r*nwaves are taken in order from an
     // LDS counter, one step ahead (the next descriptor is loaded while a unit streams).  With
     // dyn_shift, the static shares end at S (whole rounds) and the last steps [S, nws) go to
-    // whichever wave asks first, from a global counter: a unit here streams for tens of us, so
-    // static shares of the last steps leave CUs idle while others finish.
+    // whichever workgroup asks first: a unit here streams for tens of us, so static shares of the
+    // last steps leave CUs idle while others finish.  A workgroup takes 16 steps
+    // per global atomic (one wave grabs, its 15 siblings read the chunk's base from LDS): one
+    // atomic per step on one address serialised at the memory side (~18 ns each, measured).
     const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
     uint64_t S = nws;
     if (A.dyn_shift) {
-        const uint64_t s = (nws - (nws >> A.dyn_shift)) / nwaves * nwaves;
+        const uint64_t d = min(nws >> A.dyn_shift, (uint64_t)kDynMaxSteps);
+        const uint64_t s = (nws - d) / nwaves * nwaves;
         S = s >= nwaves ? s : nws;
     }
     const uint32_t nidx = (uint32_t)((S + nwaves - 1) / nwaves) * kWavesPerBlock;
@@ -832,11 +837,22 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
             if (lane == 0) i = atomicAdd(&blk_next, 1u);
             i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
             wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
-            if (i >= nidx && S < nws) {  // the static share is done: a dynamic step (one round trip)
-                unsigned long long j = 0;
-                if (lane == 0) j = atomicAdd(A.lb_ctl + 2, 1ull);
-                j = (unsigned long long)__builtin_amdgcn_readfirstlane((int)__shfl((int)j, 0));
-                wb_next = S + j < nws ? S + j : nws;
+            if (i >= nidx && S < nws) {  // the static share is done: the dynamic tail
+                const uint32_t k = i - nidx, c = k / kWavesPerBlock, j = k % kWavesPerBlock;
+                uint32_t base = ~0u;
+                if (c < kDynChunks) {
+                    if (j == 0) {  // this wave grabs the chunk (one round trip) and publishes its base
+                        if (lane == 0) {
+                            base = (uint32_t)atomicAdd(A.lb_ctl + 2, (unsigned long long)kWavesPerBlock);
+                            __hip_atomic_store(&blk_dyn[c], base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    } else if (lane == 0) {  // the chunk's grabber holds an earlier index: it is running
+                        while ((base = __hip_atomic_load(&blk_dyn[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == ~0u)
+                            __builtin_amdgcn_s_sleep(2);
+                    }
+                    base = __builtin_amdgcn_readfirstlane(__shfl((int)base, 0));
+                }
+                wb_next = base != ~0u && S + base + j < nws ? S + base + j : nws;
             }
         }
         const uint64_t un = wb_next * kGroupsPerWave + grp;

@@ -57,6 +57,11 @@ constexpr int kCombSmall = kCombT8 + 1024;
 #ifndef KARMA_RAGGED_DYN_SHIFT
 #define KARMA_RAGGED_DYN_SHIFT 0  // RaggedArgs::dyn_shift (a build-time A/B knob; the tools build's KARMA_RAGGED_DYN)
 #endif
+// The dynamic tail's size (RaggedArgs::dyn_shift): at most kDynMaxSteps steps (~70 us of the whole
+// GPU streaming), taken in chunks of 16 (one per workgroup grab); a workgroup's chunk bases live in
+// kDynChunks LDS words, enough for every chunk (the static part ends on a whole round, up to
+// nwaves steps earlier than nws - kDynMaxSteps).
+constexpr uint32_t kDynMaxSteps = 8192, kDynChunks = 1024;
 #ifndef KARMA_GRID_TILE
 #define KARMA_GRID_TILE 2048  // a build-time A/B knob
 #endif

@@ -438,6 +438,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         // largest payload picks one launch (the other one, gated off, cost ~5 us), and a pass
         // whose records it did not cover runs the batch again below (one more round trip).
         small_which = !c.have_len_hint ? kSmallBoth : c.len_hint <= kStgGateLen ? kSmallStaged : kSmallDirect;
+        if (const long w = KARMA_AB_KNOB("KARMA_SMALL_WHICH", -1); w >= 0 && w <= 2) small_which = (int)w;  // (A/B)
         if (const int rc = ragged_small_batch_dev(A.wal + 8, A.off, A.len, &A.sum->n_all, cap_all, &A.sum->max_len,
                                                   direct_max, c.crc.as<uint32_t>(), A.stored, A.first_bad, c.st,
                                                   small_which))

@@ -1230,7 +1230,8 @@ hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, i
     if (!nseg) return hipSuccess;
     // blocks per segment: about 2 blocks per CU in all (1 MiB segments of 180-B records: 188
     // segments, 3 blocks of ~1,900 candidates each)
-    const uint64_t parts = std::min<uint64_t>(8, std::max<uint64_t>(1, (2 * (uint64_t)cu + nseg - 1) / nseg));
+    uint64_t parts = std::min<uint64_t>(8, std::max<uint64_t>(1, (2 * (uint64_t)cu + nseg - 1) / nseg));
+    if (const long p = KARMA_AB_KNOB("KARMA_GATHER_PARTS", 0); p > 0) parts = (uint64_t)std::min(p, 64l);  // (A/B)
     const dim3 grid((unsigned)nseg, (unsigned)parts);
     if (fused_plan) {
         if (nseg > 1024) return hipErrorInvalidValue;

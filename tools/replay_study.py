@@ -17,6 +17,8 @@ copy for each variant in interleaved rounds (same process, same image):
     listcrc              tools build, KARMA_WAL_CRC_INLINE + KARMA_WAL_LIST_CRC=1: the walk, then the walkers' lists checksummed by
                          the LDS-staged one-record-per-lane kernel (k_wal_list_crc)
     sepdirect4           tools build, KARMA_WAL_CRC_SEPARATE with KARMA_SMALL_STAGED=0 (the 4-lane batch)
+    ab:NAME=VALUE        tools build, default plan, with one KARMA_* knob set (e.g. KARMA_GATHER_PARTS=1,
+                         KARMA_SMALL_WHICH=0: both small-record launches)
     lib=<path>           another build of the library (e.g. the previous commit's), default plan
     sep                  the shipped library, KARMA_WAL_CRC_SEPARATE: walk, gather, one batch (round 2's path;
                          the default now checksums inside the walk kernel, k_wal_walk_crc)
@@ -115,6 +117,9 @@ def main():
             variants[v] = (L, 0, 3, None)
         elif v.startswith("sub="):
             variants[v] = (L, int(v[4:]), 0, None)
+        elif v.startswith("ab:"):  # tools build, default plan, one knob: ab:NAME=VALUE
+            name, _, val = v[3:].partition("=")
+            variants[v] = (AB, 0, 0, (name, val))
         elif v.startswith("lib="):  # another build's default plan, loaded beside the shipped one
             path = v[4:]
             variants[v] = (_lib.load(path if os.path.isabs(path) else os.path.join(ROOT, path)), 0, 0, None)
@@ -133,7 +138,8 @@ def main():
 
     for r in range(a.rounds):
         for v, (lib, sub, batch, env) in variants.items():
-            for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC", "KARMA_SMALL_STAGED", "KARMA_WALK_DIRECT"):
+            for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC", "KARMA_SMALL_STAGED", "KARMA_WALK_DIRECT",
+                      "KARMA_GATHER_PARTS", "KARMA_SMALL_WHICH"):
                 os.environ.pop(k, None)
             if env:
                 os.environ[env[0]] = env[1]
