@@ -30,6 +30,8 @@ def main():
     p.add_argument("--sizes", default="64,16,4,1")
     p.add_argument("--rounds", type=int, default=6)
     p.add_argument("--json", default="")
+    p.add_argument("--libs", default="", help="name=path,... : builds compared at their defaults "
+                   "(instead of the tools build's KARMA_SEGMENT_ONCE=1 / 0)")
     a = p.parse_args()
     dev = torch.device("cuda:0")
     nseg, top = 64, 64 << 20
@@ -37,6 +39,12 @@ def main():
     K.fill_splitmix64(arena, 42)
     sh = torch.cuda.current_stream().cuda_stream
     V = ["1", "0"]
+    libs = {}
+    for item in filter(None, a.libs.split(",")):
+        name, _, path = item.partition("=")
+        libs[name] = _lib.load(path if os.path.isabs(path) else os.path.join(ROOT, path))
+    if libs:
+        V = list(libs)
     report = {}
     for mib in [int(x) for x in a.sizes.split(",")]:
         seg = mib << 20
@@ -44,15 +52,17 @@ def main():
         state = {"i": 0}
 
         def call(v):
-            os.environ["KARMA_SEGMENT_ONCE"] = v
+            lib = libs.get(v, L)
+            if not libs:
+                os.environ["KARMA_SEGMENT_ONCE"] = v
             i = state["i"] % nseg
             state["i"] += 1
-            _lib.check("stream", L.karma_crc32c_stream(0, arena.data_ptr() + i * top, seg,
-                                                       outs[v].data_ptr() + 4 * i, sh))
+            _lib.check("stream", lib.karma_crc32c_stream(0, arena.data_ptr() + i * top, seg,
+                                                         outs[v].data_ptr() + 4 * i, sh))
 
         t_end = time.perf_counter() + 0.5
         while time.perf_counter() < t_end:
-            call("1")
+            call(V[0])
             torch.cuda.synchronize()
         lat = {v: [] for v in V}
         kern = {v: [] for v in V}
@@ -64,7 +74,7 @@ def main():
                     u0.record()
                     u1.record()
                     torch.cuda.synchronize()
-                    L.karma_crc32c_time_next_units(u0.cuda_event, u1.cuda_event)
+                    libs.get(v, L).karma_crc32c_time_next_units(u0.cuda_event, u1.cuda_event)
                     e0.record()
                     call(v)
                     e1.record()
@@ -76,14 +86,14 @@ def main():
             for _ in range(nseg):
                 call(v)
         torch.cuda.synchronize()
-        same = bool(torch.equal(outs["0"], outs["1"]))
+        same = all(bool(torch.equal(outs[V[0]], outs[v])) for v in V)
         ent = {v: {"call_us_p50": round(float(np.median(lat[v])), 2),
                    "kernel_us_p50": round(float(np.median(kern[v])), 2),
                    "call_us_p10_p90": [round(float(np.percentile(lat[v], q)), 2) for q in (10, 90)]} for v in V}
         ent["crcs_equal"] = same
         report[f"{mib}MiB"] = ent
         # one logged call of k_segment_once: per-workgroup stamps (us from the earliest entry)
-        if hasattr(L, "karma_ab_seg_log"):
+        if hasattr(L, "karma_ab_seg_log") and not libs:
             os.environ["KARMA_SEGMENT_ONCE"] = "1"
             log = torch.zeros(256 * 8, dtype=torch.int64, device=dev)
             torch.cuda.synchronize()
