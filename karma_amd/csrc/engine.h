@@ -55,7 +55,7 @@ constexpr int kCombSmall = kCombT8 + 1024;
 #endif
 #endif
 #ifndef KARMA_RAGGED_DYN_SHIFT
-#define KARMA_RAGGED_DYN_SHIFT 0  // RaggedArgs::dyn_shift (a build-time A/B knob; the tools build's KARMA_RAGGED_DYN)
+#define KARMA_RAGGED_DYN_SHIFT 3  // RaggedArgs::dyn_shift (a build-time A/B knob; the tools build's KARMA_RAGGED_DYN)
 #endif
 // The dynamic tail's size (RaggedArgs::dyn_shift): at most kDynMaxSteps steps (~70 us of the whole
 // GPU streaming), taken in chunks of 16 (one per workgroup grab); a workgroup's chunk bases live in

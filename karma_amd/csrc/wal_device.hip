@@ -1228,10 +1228,13 @@ hipError_t launch_wal_plan(const WalArgs& a, uint64_t nseg, hipStream_t s) {
 
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, int cu, hipStream_t s) {
     if (!nseg) return hipSuccess;
-    // blocks per segment: about 2 blocks per CU in all (1 MiB segments of 180-B records: 188
-    // segments, 3 blocks of ~1,900 candidates each)
-    uint64_t parts = std::min<uint64_t>(8, std::max<uint64_t>(1, (2 * (uint64_t)cu + nseg - 1) / nseg));
-    if (const long p = KARMA_AB_KNOB("KARMA_GATHER_PARTS", 0); p > 0) parts = (uint64_t)std::min(p, 64l);  // (A/B)
+    // One block per segment.  (Splitting a segment's candidates over ~2 blocks per CU in all --
+    // 3 blocks per segment for the bench image's 188 segments -- made the gather 16.3 us instead
+    // of 12 and the rotated replay call 4 us slower, profiles/r04_replay_ab.txt: every block reads
+    // all the metas and the segment's spans.  The tools build keeps KARMA_GATHER_PARTS for A/B.)
+    (void)cu;
+    uint64_t parts = 1;
+    if (const long p = KARMA_AB_KNOB("KARMA_GATHER_PARTS", 0); p > 0) parts = (uint64_t)std::min(p, 64l);
     const dim3 grid((unsigned)nseg, (unsigned)parts);
     if (fused_plan) {
         if (nseg > 1024) return hipErrorInvalidValue;
