@@ -320,18 +320,29 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A, Str
     const uint32_t l = lane & (kGroupLanes - 1), grp = lane / kGroupLanes;
     const bool last_wg = blockIdx.x + 1 == gridDim.x;
     SEG_STAMP(0);
-    // The stride image is computed, not loaded: any table load issued ahead of the chunk loads is
-    // a memory round trip in front of the whole stream (round 4: tables_in_lds ~2.9 us after entry),
-    // and issued with them it queues behind the grid's 64 MiB of chunk requests.  Slicing table k
-    // of Z_128 is linear in the byte: entry e = xor of the basis words B.w[8k + i] over e's set bits.
-    // 1. this thread's entries (rows (t >> 4) + 64 q of table k = (t >> 2) & 3, 16 copies as
-    //    stride_step16s reads them: the layout load_stg_tables-style copies would write)
+    // The stride image is computed, not loaded (slicing table k of Z_128 is linear in the byte:
+    // entry e = xor of the basis words B.w[8k + i] over e's set bits), so the chunk loads are issued
+    // without waiting for any table.  The fold tables are loaded first and stored into LDS while
+    // the chunks are in flight: issued behind the chunks they landed as the stream ended (the
+    // folds then waited, +1.3 us per call), and waited for ahead of the chunks they delay the
+    // whole stream by a round trip (round 4).
+    LdsCopy<kSmallWords, kBlockThreads> small;
+    small.load(A.blob + 1024);
+    LdsCopy<kCombMaps * 1024, kBlockThreads> comb;
+    comb.load(A.comb_maps);
+    SEG_STAMP(6);
+    // 1. this thread's stride-image entries (rows (t >> 4) + 64 q of table k = (t >> 2) & 3, in the
+    //    16 copies stride_step16s reads)
     {
         const uint32_t k = (threadIdx.x >> 2) & 3u, r0 = threadIdx.x >> 4;
+        // (the basis words as scalars first: selected by address, the compiler reads them with
+        // per-lane vector loads from the kernarg segment, one more memory round trip)
+        uint32_t w[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) w[i] = __builtin_amdgcn_readfirstlane(B.w[i]);
         uint32_t b[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            b[i] = k == 0 ? B.w[i] : k == 1 ? B.w[8 + i] : k == 2 ? B.w[16 + i] : B.w[24 + i];
+        for (int i = 0; i < 8; ++i) b[i] = k == 0 ? w[i] : k == 1 ? w[8 + i] : k == 2 ? w[16 + i] : w[24 + i];
         uint32_t elo = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) elo ^= (r0 >> i) & 1u ? b[i] : 0u;
@@ -357,12 +368,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A, Str
     v[0] = ldg<NT>(ok0 ? L.w : L.lclamp);
 #pragma unroll
     for (int q = 1; q < kSegMaxChunks; ++q) v[q] = ldg<NT>(pmin(L.w + q * kChunk, L.lclamp));
-    // 4. the fold tables behind the chunks (they land as the stream ends; only the folds need them)
-    LdsCopy<kSmallWords, kBlockThreads> small;
-    small.load(A.blob + 1024);
-    LdsCopy<kCombMaps * 1024, kBlockThreads> comb;
-    comb.load(A.comb_maps);
+    asm volatile("" ::: "memory");  // (every chunk load issued before the table stores wait on vmcnt)
     SEG_STAMP(7);
+    // 4. the fold tables into LDS (their loads were issued before the chunks': waiting for them
+    //    leaves the chunks in flight)
+    small.store(lds + kSegZ4);
+    comb.store(lds + kSegComb);
+    __syncthreads();
     // 5. the unit's windows (stride_step16s: the 16-copy image in swapped lane order), the lane
     //    fold and the 8-lane tree
     const uint32_t X = lane_const16();
@@ -379,9 +391,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A, Str
     uint32_t tag = 0;  // wave 0 publishes the workgroup's state, tagged with the call's tag
     if (wave == 0)
         tag = __hip_atomic_load(reinterpret_cast<const uint32_t*>(A.fctl + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    small.store(lds + kSegZ4);
-    comb.store(lds + kSegComb);
-    __syncthreads();  // the fold tables
     uint32_t c = lane_fold_at(lds, kSegZ4, a0, a1, a2, a3);
     c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + L.m + 1) & (kGroupLanes - 1))), 64);
     uint32_t t = __shfl_down(c, 1, kGroupLanes);
