@@ -9,8 +9,6 @@
 // k_combine_fixed, one level per factor of 64, with maps Z_{D*2^d}.
 #include <hip/hip_runtime.h>
 
-#include <vector>
-
 #include "ab.h"
 #include "crc_device.h"
 #include "engine.h"
@@ -258,9 +256,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
 // 16 wave states in LDS and publishes one tagged state; the grid's last workgroup folds those
 // (at most 1024: a 64-lane tree per wave, then a Horner step per wave) and writes the CRC.
 // Forward progress: as the FUSE kernel (include/karma_crc32c.h: grid <= CUs, in-order dispatch).
-struct StrideBasis {  // k_segment_once's stride image, as basis words: entry 1 << i of table k at w[8 k + i]
-    uint32_t w[32];
-};
 constexpr int kSegZ4 = kRep16Words;                        // Z4, Z16, Z32, Z64, byte table (the blob's)
 constexpr int kSegComb = kSegZ4 + kSmallWords;             // comb_maps: Z_{U 2^k}, k = 0..6
 constexpr int kSegGrid = kSegComb + kCombMaps * 1024;      // block_blob: Z_{128 U 2^k}, k = 0..6
@@ -298,20 +293,8 @@ struct LdsCopy {  // a global -> LDS copy split in two: the loads, then (after o
     }
 };
 
-// Bytes [from, to) of the 16-byte block v stepped through r bit by bit (the reflected polynomial,
-// no tables): the record head's few bytes, before any table is in LDS.
-__device__ __forceinline__ uint32_t steps_in_vec_bitwise(uint32_t r, const u32x4& v, uint32_t from, uint32_t to) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    for (uint32_t i = from; i < to; ++i) {
-        r ^= (w[i >> 2] >> (8u * (i & 3u))) & 255u;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) r = (r >> 1) ^ (0x82F63B78u & (0u - (r & 1u)));
-    }
-    return r;
-}
-
 template <bool NT>
-__global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A, StrideBasis B) {
+__global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
                  (reinterpret_cast<uintptr_t>(A.arena + A.rec_bytes) + 15) & ~uintptr_t(15));
     __shared__ __attribute__((aligned(16))) uint32_t lds[kSegLdsWords];
@@ -320,66 +303,51 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A, Str
     const uint32_t l = lane & (kGroupLanes - 1), grp = lane / kGroupLanes;
     const bool last_wg = blockIdx.x + 1 == gridDim.x;
     SEG_STAMP(0);
-    // The stride image is computed, not loaded (slicing table k of Z_128 is linear in the byte:
-    // entry e = xor of the basis words B.w[8k + i] over e's set bits), so the chunk loads are issued
-    // without waiting for any table.  The fold tables are loaded first and stored into LDS while
-    // the chunks are in flight: issued behind the chunks they landed as the stream ended (the
-    // folds then waited, +1.3 us per call), and waited for ahead of the chunks they delay the
-    // whole stream by a round trip (round 4).
+    // The tables first, into LDS, and only then the chunk loads: issued together, the table loads
+    // (L2 misses after the previous call's stream) queued at the memory channels behind the whole
+    // grid's 64 MiB of chunk requests and landed ~10 us in, after the data, so no step overlapped
+    // the stream.  The call's tag, the grid's fold maps and the tail block are read after the steps.
+    // 1. the table words this thread fills
+    constexpr int NV16 = kRep16Words / 4, IT16 = NV16 / kBlockThreads;
+    uint32_t e16[IT16];
+#pragma unroll
+    for (int q = 0; q < IT16; ++q) {
+        const int v = (int)threadIdx.x + q * kBlockThreads, row = v >> 4, k = (v >> 2) & 3;
+        e16[q] = *(const __attribute__((address_space(1))) uint32_t*)(A.blob + kBlobStride + k * 256 + row);
+    }
     LdsCopy<kSmallWords, kBlockThreads> small;
     small.load(A.blob + 1024);
     LdsCopy<kCombMaps * 1024, kBlockThreads> comb;
     comb.load(A.comb_maps);
     SEG_STAMP(6);
-    // 1. this thread's stride-image entries (rows (t >> 4) + 64 q of table k = (t >> 2) & 3, in the
-    //    16 copies stride_step16s reads)
-    {
-        const uint32_t k = (threadIdx.x >> 2) & 3u, r0 = threadIdx.x >> 4;
-        // (the basis words as scalars first: selected by address, the compiler reads them with
-        // per-lane vector loads from the kernarg segment, one more memory round trip)
-        uint32_t w[32];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) w[i] = __builtin_amdgcn_readfirstlane(B.w[i]);
-        uint32_t b[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) b[i] = k == 0 ? w[i] : k == 1 ? w[8 + i] : k == 2 ? w[16 + i] : w[24 + i];
-        uint32_t elo = 0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) elo ^= (r0 >> i) & 1u ? b[i] : 0u;
-        u32x4* l4 = reinterpret_cast<u32x4*>(lds);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t e = elo ^ (q & 1 ? b[6] : 0u) ^ (q & 2 ? b[7] : 0u);
-            l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e, e, e, e};
-        }
-    }
-    // 2. this lane's unit (arithmetic only)
+    // 2. this lane's unit (arithmetic only: it runs while the table loads are in flight)
     const uint64_t U = A.units_per_rec;
     const uint64_t u = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kGroupsPerWave + grp;
     const FixedPlan P = fixed_plan<true>(A, u, U, l);
     const LaneUnit& L = P.L;
     const bool ok0 = L.nch > 0 && L.w >= L.us && L.w < L.ue;
+    // 3. the tables into LDS
+    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
+#pragma unroll
+    for (int q = 0; q < IT16; ++q) l4[(int)threadIdx.x + q * kBlockThreads] = u32x4{e16[q], e16[q], e16[q], e16[q]};
+    small.store(lds + kSegZ4);
+    comb.store(lds + kSegComb);
     __syncthreads();
     SEG_STAMP(1);
-    // 3. every chunk load of the unit and its head block, consumed in issue order (vmcnt counts)
+    // 4. every chunk load of the unit and its head block, consumed in issue order (vmcnt counts)
     const u32x4 hv = ld16(P.hblk);
     asm volatile("" ::: "memory");  // (issued before the chunks: the first step needs it)
     u32x4 v[kSegMaxChunks];
     v[0] = ldg<NT>(ok0 ? L.w : L.lclamp);
 #pragma unroll
     for (int q = 1; q < kSegMaxChunks; ++q) v[q] = ldg<NT>(pmin(L.w + q * kChunk, L.lclamp));
-    asm volatile("" ::: "memory");  // (every chunk load issued before the table stores wait on vmcnt)
     SEG_STAMP(7);
-    // 4. the fold tables into LDS (their loads were issued before the chunks': waiting for them
-    //    leaves the chunks in flight)
-    small.store(lds + kSegZ4);
-    comb.store(lds + kSegComb);
-    __syncthreads();
     // 5. the unit's windows (stride_step16s: the 16-copy image in swapped lane order), the lane
     //    fold and the 8-lane tree
     const uint32_t X = lane_const16();
     uint32_t inj = 0;
-    if (P.inj_at) inj = P.hfrom < 16 ? steps_in_vec_bitwise(~A.init_scalar, hv, P.hfrom, 16u) : ~A.init_scalar;
+    if (P.inj_at) inj = P.hfrom < 16 ? steps_in_vec(lds, kSegZ4, kSegZ4 + 4096, ~A.init_scalar, hv, P.hfrom, 16u)
+                                     : ~A.init_scalar;
     u32x4 x0 = ok0 ? v[0] : u32x4{0u, 0u, 0u, 0u};
     if (ok0 && L.w == P.inj_at) x0.x ^= inj;
     uint32_t a0 = x0.x, a1 = x0.y, a2 = x0.z, a3 = x0.w;
@@ -687,21 +655,6 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     return hipGetLastError();
 }
 
-namespace {
-// Entry 1 << i of slicing table k of Z_128 (the stream blob's stride tables) at w[8 k + i].
-StrideBasis stride_basis() {
-    static const StrideBasis b = [] {
-        std::vector<uint32_t> blob(kBlobWords);
-        build_stream_blob(blob.data());
-        StrideBasis s{};
-        for (int k = 0; k < 4; ++k)
-            for (int i = 0; i < 8; ++i) s.w[8 * k + i] = blob[kBlobStride + k * 256 + (1u << i)];
-        return s;
-    }();
-    return b;
-}
-}  // namespace
-
 hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     // one record; units_per_rec = 8 units x 16 waves x grid_blocks of at most 2 KiB; fctl, partial,
     // comb_maps (comb blob of the unit) and block_blob (comb blob of 128 units) bound
@@ -710,7 +663,7 @@ hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t 
         a.unit_bytes > segment_once_max_unit(a.arena, a.rec_bytes) || a.unit_bytes % kChunk || grid_blocks > 1024)
         return hipErrorInvalidValue;
     units_timer_begin(s);
-    hipLaunchKernelGGL(k_segment_once<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a, stride_basis());
+    hipLaunchKernelGGL(k_segment_once<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     return hipGetLastError();
 }
