@@ -318,8 +318,18 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
     a.fctl = nullptr;
     a.block_blob = nullptr;
     a.comb_m = 0;
+    a.dyn_ctl = nullptr;
+    a.dyn_shift = 0;
     if (fold_k) {
         KARMA_RC(comb_blob(ds, unit, &a.comb_maps));
+        // the dynamic tail's counter: word 0 of the stream's fused words (the fused fold and the
+        // segment kernel leave it unused)
+        if (const long sh = KARMA_AB_KNOB("KARMA_FIXED_DYN", KARMA_FIXED_DYN_SHIFT); sh > 0) {
+            unsigned long long* w = nullptr;
+            KARMA_RC(fused_words(dev, s, &w));
+            a.dyn_ctl = w;
+            a.dyn_shift = (uint32_t)std::min(sh, 16l);
+        }
         // (the tools build's KARMA_FIXED_GRID_MULT: that many workgroups per CU, dispatched in
         // rounds, so the hardware hands the later ones to the CUs that finish first)
         const long gm = KARMA_AB_KNOB("KARMA_FIXED_GRID_MULT", 1);

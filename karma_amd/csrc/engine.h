@@ -112,7 +112,17 @@ struct FixedArgs {
     unsigned long long* fctl;
     const uint32_t* block_blob; // kBlockCombWords (block_comb_blob for D = 8 units, m states per thread)
     uint64_t comb_m;            // states per thread of the fused fold
+    // Dynamic tail (not with the fused fold): the last min(nws >> dyn_shift, kFixedDynMaxSteps)
+    // wave-steps are taken kFixedDynChunk at a time per workgroup from dyn_ctl[0] (low 32 bits;
+    // the high 32 count the workgroups that finished: the last one zeroes the word for the next
+    // call on the stream).  dyn_shift 0 or dyn_ctl nullptr: static shares only.
+    unsigned long long* dyn_ctl;
+    uint32_t dyn_shift;
 };
+constexpr uint32_t kFixedDynChunk = 64, kFixedDynMaxSteps = 16384, kFixedDynRing = 4;
+#ifndef KARMA_FIXED_DYN_SHIFT
+#define KARMA_FIXED_DYN_SHIFT 0  // FixedArgs::dyn_shift (a build-time A/B knob; the tools build's KARMA_FIXED_DYN)
+#endif
 
 // One unit of a ragged batch: the 16-aligned span [us, us + span) of a record body; inj is
 // xored into the span's first word: for the record's first unit the register entering the
