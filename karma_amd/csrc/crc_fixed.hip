@@ -122,6 +122,15 @@ __device__ void fused_record_fold(const FixedArgs& A, uint32_t* lds, uint32_t* w
     }
 }
 
+// The fixed kernel's dynamic tail measured no gain (1M x 4 KiB 0.6041 vs 0.6023 ms, 256K x 16 KiB
+// 0.6224 vs 0.6144: profiles/r04_fixed_dyn_tail_ab.txt), so only the tools build and the fdyn
+// builds compile it.
+#if defined(KARMA_AB) || KARMA_FIXED_DYN_SHIFT > 0
+constexpr bool kFixedDynBuilt = true;
+#else
+constexpr bool kFixedDynBuilt = false;
+#endif
+
 // The dynamic tail's k-th step of this workgroup (k_units_fixed): chunks of kFixedDynChunk steps,
 // one global atomic each, taken by the wave that draws a chunk's first index; the chunk's other
 // waves read its base from an LDS ring slot tagged with the chunk.  A slot is reused for chunk
@@ -193,7 +202,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     // workgroups that ask first, kFixedDynChunk per global atomic (one wave grabs, its siblings read
     // the base from LDS): per-CU speed differences otherwise leave the last static steps on a few
     // CUs (DESIGN.md §4 "The dynamic tail").
-    constexpr bool kDyn = BAL && !FUSE;
+    constexpr bool kDyn = kFixedDynBuilt && BAL && !FUSE;
     uint64_t S = nws;
     if (kDyn && A.dyn_ctl && A.dyn_shift) {  // (whole rounds: a block's static share ends at nidx)
         const uint64_t d = min(nws >> A.dyn_shift, (uint64_t)kFixedDynMaxSteps);
