@@ -168,7 +168,7 @@ void build_grid_comb_blob(uint32_t* out /*kGridCombWords*/);
 // units for balance: all full units first, in record order, then
 // each block's partial first/last units bucketed by chunk count, longest first,
 // so the 8 units a wave streams together have (nearly) equal length.
-constexpr int kBuckets = 65;  // chunk counts 1..64 of a partial unit (index = chunks)
+constexpr int kBuckets = (int)(kDefaultUnit / kChunk) + 1;  // chunk counts of a partial unit (index = chunks; 65 for 8 KiB units)
 static_assert(kDefaultUnit / kChunk < kBuckets, "a partial unit has at most unit/kChunk chunks");
 
 struct RaggedArgs {
