@@ -22,7 +22,7 @@ constexpr int kStgWaves = 7;  // k_ragged_staged: one 448-thread workgroup per C
 // in one wave's 12 KiB stage (crc_device.h kStgBytes: (12288 - 64) / 64 - 8).
 constexpr uint32_t kStgGateLen = 183;
 #ifndef KARMA_RAGGED_UNIT
-#define KARMA_RAGGED_UNIT 8192  // a build-time A/B knob (tools/ragged_unit_ab.sh)
+#define KARMA_RAGGED_UNIT 8192  // a build-time A/B knob (tools/ragged_study.py over builds with -DKARMA_RAGGED_UNIT=...)
 #endif
 constexpr uint64_t kDefaultUnit = KARMA_RAGGED_UNIT;  // unit size for ragged batches
 
@@ -65,7 +65,7 @@ constexpr uint32_t kDynMaxSteps = 8192, kDynChunks = 1024;
 #ifndef KARMA_GRID_TILE
 #define KARMA_GRID_TILE 2048  // a build-time A/B knob
 #endif
-constexpr int kCombSmallMaps = KARMA_GRID_TILE > 4096 ? 10 : 9;  // Z_16n, n < 2^maps (>= a grid tile / 16)
+constexpr int kCombSmallMaps = (KARMA_GRID_TILE > 4096 || KARMA_RAGGED_UNIT > 8192) ? 10 : 9;  // Z_16n, n < 2^maps (>= a grid tile / 16, a ragged unit / 16)
 constexpr int kCombWords = kCombSmall + kCombSmallMaps * 1024;
 
 // ---- table blob of the one-block combine (k_combine_block) -----------------
