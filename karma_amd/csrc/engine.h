@@ -66,8 +66,9 @@ constexpr uint32_t kDynMaxSteps = 8192, kDynChunks = 1024;
 #define KARMA_GRID_TILE 2048  // a build-time A/B knob
 #endif
 constexpr int kCombSmallMaps = (KARMA_GRID_TILE > 4096 || KARMA_RAGGED_UNIT > 8192) ? 10 : 9;  // Z_16n, n < 2^maps (>= a grid tile / 16, a ragged unit / 16)
-static_assert((16ull << kCombSmallMaps) > (unsigned long long)KARMA_RAGGED_UNIT &&
-                  (16ull << kCombSmallMaps) > (unsigned long long)KARMA_GRID_TILE,
+// (a partial last unit is shorter than the unit: n = its length / 16 < unit / 16)
+static_assert((16ull << kCombSmallMaps) >= (unsigned long long)KARMA_RAGGED_UNIT &&
+                  (16ull << kCombSmallMaps) >= (unsigned long long)KARMA_GRID_TILE,
               "finalize's last-unit maps Z_16n must reach a whole unit / tile");
 constexpr int kCombWords = kCombSmall + kCombSmallMaps * 1024;
 
