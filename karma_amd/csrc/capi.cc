@@ -597,7 +597,8 @@ int ragged_small_batch(const void* d_arena, const uint64_t* d_off, const uint32_
 }
 int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
                            uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
-                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s, int which) {
+                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s, int which,
+                           bool stage_skew, uint32_t* d_skew_seen) {
     if (!n_cap) return 0;
     Locked L;
     if (L.rc) return L.rc;
@@ -625,9 +626,10 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
         RaggedArgs b = a;
         b.blob = L.ds->lane_blob;
         b.gate_max = stg_max;
+        b.stage_skew_seen = d_skew_seen;
         const uint64_t sblocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_cap, 64 * kStgWaves));
         units_timer_begin(s);  // (karma_crc32c_time_next_units: the replay's CRC kernel)
-        KARMA_HIP(launch_ragged_staged_dev(b, (int)sblocks, s));
+        KARMA_HIP(launch_ragged_staged_dev(b, (int)sblocks, s, stage_skew));
         units_timer_end(s);
         if (gate_max <= stg_max || which == kSmallStaged) return 0;
         a.gate_min = stg_max + 1;

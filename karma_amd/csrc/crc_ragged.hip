@@ -1032,8 +1032,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // 8-B headers put every lane on one bank) read their windows without conflicts; stores then go
 // out as dwords.  The 16-copy stride image is read with lanes 16-31 taking the tables in swapped
 // order (stride_step16s: no bank conflicts; the plain order measured 2-way conflicts).
+// SK: the kernel carries the skewed stage beside the plain one (a second code path: 172 VGPRs,
+// 3-5 us on 188-B strides); without it a bank-poor batch is staged plainly (correct, with bank
+// conflicts).  Either form reports bank-poor batches in *stage_skew_seen, so the WAL replay picks
+// the next call's form from this one's records.
+template <bool SK>
 __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArgs A) {
-    constexpr bool END = true, SK = true;
+    constexpr bool END = true;
     constexpr int NW = kStgWaves, SMODE = 24;
     constexpr int TW = kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
     constexpr uint32_t kLead = 16u, kFit = kStgBytes - 32u;
@@ -1091,13 +1096,16 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
     extent(o, n, lo, hi);
     bool fits = hi != 0 && hi - lo <= kFit;
     // does the batch at (o, n, lo) need the skewed stage?  (banks of the records' first dwords)
+    bool poor_seen = false;
     auto skewed = [&](uint64_t o, uint32_t n, uintptr_t lo) {
-        if constexpr (!SK) return false;
+        if (!SK && !A.stage_skew_seen) return false;
         const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
         uint32_t bits = n ? 1u << (((uint32_t)(p - lo) >> 2) & 31u) : 0u;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) bits |= (uint32_t)__shfl_xor((int)bits, d);
-        return __builtin_popcount(__builtin_amdgcn_readfirstlane(bits)) < 12;
+        const bool poor = __builtin_popcount(__builtin_amdgcn_readfirstlane(bits)) < 12;
+        poor_seen |= poor;
+        return SK && poor;
     };
     bool sk = fits && skewed(o, n, lo);
     if (fits) issue(lo, hi);
@@ -1167,6 +1175,7 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
         o2 = o3; n2 = n3; ini2 = ini3;
         lo = lo2; hi = hi2; fits = fits2; sk = sk2;
     }
+    if (poor_seen && A.stage_skew_seen && lane == 0) *A.stage_skew_seen = 1u;  // (benign races: all store 1)
 }
 
 
@@ -1178,16 +1187,19 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
     // (the tools build's KARMA_DIRECT_VARIANT=20: the LDS-staged kernel over the bounded ABI, so
     // the tests hold it to parity on batches of every shape; the caller passes the lane blob)
     if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 20)
-        hipLaunchKernelGGL(k_ragged_staged_pipe, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        hipLaunchKernelGGL(k_ragged_staged_pipe<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 21)  // (the plain stage only)
+        hipLaunchKernelGGL(k_ragged_staged_pipe<false>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else
         hipLaunchKernelGGL(k_ragged_direct4, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     return hipGetLastError();
 }
 
-hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
+hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew) {
     if (a.n_rec == 0 || !a.n_dev || !a.gate_len) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ragged_staged_pipe, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    if (skew) hipLaunchKernelGGL(k_ragged_staged_pipe<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else hipLaunchKernelGGL(k_ragged_staged_pipe<false>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -223,6 +223,9 @@ struct RaggedArgs {
     // cmp_stored[r] (records of length 0 excepted) and keeps the first mismatch in *cmp_bad.
     const uint32_t* cmp_stored;
     unsigned long long* cmp_bad;
+    // k_ragged_staged_pipe: set to 1 when a batch's records start on few LDS banks (the skewed
+    // stage's case), whichever stage the kernel has; nullptr: not reported
+    uint32_t* stage_skew_seen;
     // The byte grid (k_ragged_grid_plan; tile_cap == 0: not attempted).  The plan checks the
     // grid's conditions per block (gflag); the kernels after it read every block's flag and take
     // the grid path only when all hold, else the unit plan above (k_ragged_plan runs only then).
@@ -284,7 +287,7 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
 hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // k_ragged_direct4 with a device-sized batch (a.n_dev / a.gate_len set): WAL replay's
 // device-planned path, whatever the tools build's variant.
-hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s);
+hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew = true);
 hipError_t launch_ragged_direct_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // Library-internal entry (capi.cc) for callers that know every record is small
 // (WAL replay): CRCs of arena[off[r], off[r] + len[r]) with Value's init.
@@ -308,7 +311,8 @@ inline bool small_batch_covers(int which, uint32_t max_len, uint32_t gate_max) {
 }
 int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uint32_t* d_len, const uint64_t* d_n,
                            uint64_t n_cap, const uint32_t* d_gate_len, uint32_t gate_max, uint32_t* d_out,
-                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s, int which = kSmallBoth);
+                           const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s, int which = kSmallBoth,
+                           bool stage_skew = true, uint32_t* d_skew_seen = nullptr);
 
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {
@@ -341,8 +345,10 @@ struct WalSummary {
     uint32_t crc_unknown;  // inline CRCs (k_wal_walk_crc): 1 = some candidate of [0, w1) was not checksummed
     uint64_t first_bad;  // the first candidate whose payload CRC differs (~0: none), set by the CRC check
     uint64_t bad_off;    // inline CRCs: that candidate's header offset relative to wal (k_wal_plan)
+    uint32_t stage_skew; // the staged small-record batch met records on few LDS banks (RaggedArgs::stage_skew_seen)
+    uint32_t pad;
 };
-static_assert(sizeof(WalSummary) == 48, "one 48-byte summary, read back in one copy");
+static_assert(sizeof(WalSummary) == 56, "one 56-byte summary, read back in one copy");
 
 // One sub-range walker's result: where it started (a header it found, or the
 // sub-range end: none), its list length, its stop kind / offset and where it left

@@ -164,6 +164,9 @@ struct ReplayCtx {
     // launches only the small-record kernel that covered it (karma::engine::SmallWhich)
     bool have_len_hint = false;
     uint32_t len_hint = 0;
+    // whether the last pass's staged batch met records on few LDS banks: this pass then launches
+    // the staged kernel with the skewed stage (else the plain-stage form, 3-5 us faster)
+    bool skew_hint = true;
     int init(int dev) {
         if (ready) return 0;
         hipDeviceProp_t prop;
@@ -439,9 +442,11 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         // whose records it did not cover runs the batch again below (one more round trip).
         small_which = !c.have_len_hint ? kSmallBoth : c.len_hint <= kStgGateLen ? kSmallStaged : kSmallDirect;
         if (const long w = KARMA_AB_KNOB("KARMA_SMALL_WHICH", -1); w >= 0 && w <= 2) small_which = (int)w;  // (A/B)
+        const long skew_knob = KARMA_AB_KNOB("KARMA_STAGE_SKEW", -1);  // (A/B: 0 plain, 1 skewed stage)
         if (const int rc = ragged_small_batch_dev(A.wal + 8, A.off, A.len, &A.sum->n_all, cap_all, &A.sum->max_len,
                                                   direct_max, c.crc.as<uint32_t>(), A.stored, A.first_bad, c.st,
-                                                  small_which))
+                                                  small_which, skew_knob >= 0 ? skew_knob != 0 : c.skew_hint,
+                                                  &A.sum->stage_skew))
             return rc;
     }
     WalSummary* S = c.h_small.as<WalSummary>();
@@ -466,6 +471,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     if (lists && n_all) {
         c.have_len_hint = true;
         c.len_hint = max_len;
+        if (small_which != kSmallDirect && max_len <= kStgGateLen) c.skew_hint = S->stage_skew != 0;
     }
     uint64_t accepted = n_all;
     if (inline_done && S->first_bad < n_all) {

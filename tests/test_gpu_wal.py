@@ -553,3 +553,34 @@ def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
         w = want[name]
         got = _replay(lib, wals[name], d_wal=dev[name], seg=seg, host=bool(i % 2))
         assert got == (list(w[0]), w[1], w[2]), (i, name, walk)
+
+
+@pytest.mark.parametrize("walk", ["split", "sep"])
+def test_replay_stage_skew_hint_between_calls(lib, walk, monkeypatch):
+    """The staged small-record kernel comes in two forms, with the bank-skewed stage (records on
+    few LDS banks: strides that are multiples of 32 bytes) and without it; a call takes the form
+    the previous call's records asked for, and a plain stage over bank-poor records is slower but
+    exact.  Uniform 120-B payloads (128-B stride: every record on one bank), 180-B (188-B stride)
+    and 56-B (64-B stride) WALs in every order, with a corrupt payload, against the model."""
+    _walk_env(monkeypatch, walk)
+    seg = 64 << 10
+    wals, want = {}, {}
+    for size in (120, 180, 56):
+        n = 4000
+        lens = np.full(n, size, np.uint32)
+        offs = (np.arange(n, dtype=np.uint64) * size).astype(np.uint64)
+        src = synth.splitmix_np(size, 0, n * size + 16).copy()
+        nseg = n * (size + 8) // (seg - 256) + 2
+        wal = np.zeros(nseg * seg, np.uint8)
+        cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+        assert len(rec) == n
+        bad = wal.copy()
+        bad[int(rec[2345]) + 8 + size // 3] ^= 0x08
+        for name, img in ((f"{size}", wal), (f"{size}_bad", bad)):
+            wals[name] = img
+            want[name] = wal_model.replay(img.tobytes(), seg)
+    dev = {k: torch.from_numpy(w).cuda() for k, w in wals.items()}
+    order = ["180", "120", "120", "180", "120_bad", "56", "180_bad", "120", "56_bad", "180", "180", "120"]
+    for i, name in enumerate(order):
+        w = want[name]
+        assert _replay(lib, wals[name], d_wal=dev[name], seg=seg, host=False) == (list(w[0]), w[1], w[2]), (i, name)
