@@ -876,7 +876,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // 16 bytes through the aligned body (Z_16 stride tables in the 16-copy image: stride_step16),
 // the STEP4W lane fold and the unaligned tail; records with no aligned 16-byte block inside
 // are stepped word by word.  n must be > 0 (an empty record's CRC is init).
-template <typename Src>
+template <int MODE = 8, typename Src>
 __device__ __forceinline__ uint32_t lane_record(const uint32_t* lds, uint32_t X, int z4, int t8, uintptr_t p,
                                                 uint32_t n, uint32_t init, Src&& src) {
     uint32_t r = ~init;
@@ -893,7 +893,7 @@ __device__ __forceinline__ uint32_t lane_record(const uint32_t* lds, uint32_t X,
     if (p < a) r = steps_in_vec(lds, z4, t8, r, src(a - 16), (uint32_t)(p - (a - 16)), 16u);
     const u32x4 v0 = src(a);
     uint32_t a0 = v0.x ^ r, a1 = v0.y, a2 = v0.z, a3 = v0.w;
-    for (uintptr_t w = a + 16; w < b; w += 16) step4<8>(lds, X, a0, a1, a2, a3, src(w));
+    for (uintptr_t w = a + 16; w < b; w += 16) step4<MODE>(lds, X, a0, a1, a2, a3, src(w));
     r = lane_fold_at(lds, z4, a0, a1, a2, a3);
     if (e > b) r = steps_in_vec(lds, z4, t8, r, src(b), 0u, (uint32_t)(e - b));
     return ~r;

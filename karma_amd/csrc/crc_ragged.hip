@@ -1036,13 +1036,16 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // 3-5 us on 188-B strides); without it a bank-poor batch is staged plainly (correct, with bank
 // conflicts).  Either form reports bank-poor batches in *stage_skew_seen, so the WAL replay picks
 // the next call's form from this one's records.
-template <bool SK>
-__global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArgs A) {
+// R8 (plain stage only): the 8-copy stride image (32 KiB, stride_step8) instead of the 16-copy
+// one, so kStgWaves8 waves' stages fit the LDS (the plain form's 146 VGPRs allow 3 waves per SIMD).
+template <bool SK, bool R8 = false>
+__global__ __launch_bounds__((R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
+    static_assert(!(SK && R8), "the 8-copy form has the plain stage only");
     constexpr bool END = true;
-    constexpr int NW = kStgWaves, SMODE = 24;
-    constexpr int TW = kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
+    constexpr int NW = R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : 24;
+    constexpr int TW = R8 ? kRep8Words : kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
     constexpr uint32_t kLead = 16u, kFit = kStgBytes - 32u;
-    constexpr uint32_t kStride = kStgBytes + kStgBytes / 32;  // bytes per wave's stage
+    constexpr uint32_t kStride = SK ? kStgBytes + kStgBytes / 32 : kStgBytes;  // bytes per wave's stage
     uint64_t n_rec = A.n_rec;
     if (A.n_dev) {
         if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
@@ -1050,7 +1053,14 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
     }
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[BUF + NW * (int)(kStride / 4)];
-    load_stg_tables<NW * 64>(lds, A.blob);
+    static_assert((BUF + NW * (int)(kStride / 4)) * 4 <= 160 * 1024, "LDS of one workgroup");
+    if constexpr (R8) {
+        load_rep8_stride<NW * 64>(lds, A.blob);
+        copy_to_lds<1024, NW * 64>(lds + Z4, A.blob + kBlobZ4);
+        copy_to_lds<256, NW * 64>(lds + T8, A.blob + kBlobT8);
+    } else {
+        load_stg_tables<NW * 64>(lds, A.blob);
+    }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t X = lane_const16();
@@ -1153,7 +1163,7 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
                         return *reinterpret_cast<const uint32_t*>(stage + 4u * q);
                     });
                 else if (fits)
-                    res = lane_record(lds, X, Z4, T8, p, n, ini, [&](uintptr_t a) {
+                    res = lane_record<R8 ? 32 : 8>(lds, X, Z4, T8, p, n, ini, [&](uintptr_t a) {
                         const uint32_t at = kLead + (uint32_t)(a - lo);
                         if (sk) {
                             const uint32_t d = at / 4 + at / 128;
@@ -1162,7 +1172,7 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe(RaggedArg
                         return *reinterpret_cast<const u32x4*>(stage + at);
                     });
                 else
-                    res = lane_record(lds, X, Z4, T8, p, n, ini,
+                    res = lane_record<R8 ? 32 : 8>(lds, X, Z4, T8, p, n, ini,
                                       [&](uintptr_t a) { return ld16(reinterpret_cast<const uint8_t*>(a)); });
             }
             A.out[ri] = res;
@@ -1187,9 +1197,11 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
     // (the tools build's KARMA_DIRECT_VARIANT=20: the LDS-staged kernel over the bounded ABI, so
     // the tests hold it to parity on batches of every shape; the caller passes the lane blob)
     if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 20)
-        hipLaunchKernelGGL(k_ragged_staged_pipe<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 21)  // (the plain stage only)
-        hipLaunchKernelGGL(k_ragged_staged_pipe<false>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 22)  // (the 8-copy image, kStgWaves8 waves)
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false, true>), dim3(grid_blocks), dim3(kStgWaves8 * 64), 0, s, a);
     else
         hipLaunchKernelGGL(k_ragged_direct4, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
@@ -1198,8 +1210,14 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
 
 hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew) {
     if (a.n_rec == 0 || !a.n_dev || !a.gate_len) return hipErrorInvalidValue;
-    if (skew) hipLaunchKernelGGL(k_ragged_staged_pipe<true>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
-    else hipLaunchKernelGGL(k_ragged_staged_pipe<false>, dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    if (skew) {
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    } else if (KARMA_AB_KNOB("KARMA_STAGE_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves)
+        const uint64_t g = std::min<uint64_t>((uint64_t)grid_blocks, (a.n_rec + 64 * kStgWaves8 - 1) / (64 * kStgWaves8));
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false, true>), dim3((unsigned)g), dim3(kStgWaves8 * 64), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    }
     return hipGetLastError();
 }
 

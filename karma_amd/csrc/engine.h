@@ -18,6 +18,7 @@ constexpr int kBlockThreads = 1024;            // one workgroup per CU
 constexpr int kWavesPerBlock = kBlockThreads / 64;
 constexpr int kGroupsPerWave = 64 / kGroupLanes;
 constexpr int kStgWaves = 7;  // k_ragged_staged: one 448-thread workgroup per CU (LDS-bound)
+constexpr int kStgWaves8 = 10;  // ... its plain-stage form on the 8-copy stride image (tools build A/B)
 // Consecutive payloads up to this length (with 8-byte WAL headers between them) put 64 records
 // in one wave's 12 KiB stage (crc_device.h kStgBytes: (12288 - 64) / 64 - 8).
 constexpr uint32_t kStgGateLen = 183;

@@ -548,13 +548,14 @@ def test_ragged_low_total_len_is_still_exact(raw, dev):
         _eq(got, want)
 
 
-@pytest.mark.parametrize("variant", ["shipped", "20"])
+@pytest.mark.parametrize("variant", ["shipped", "20", "21", "22"])
 @pytest.mark.parametrize("bound", [0, 64, 1024, 1 << 20])
 def test_ragged_bounded_direct_path(raw, dev, bound, variant, monkeypatch):
     """karma_crc32c_batch_ragged_bounded: with max_len <= 1 KiB one record per group (no plan
     kernels); any bound -- too low included -- gives the exact CRCs, with per-record inits.
-    Variant 20 is the tools build's LDS-staged kernel (KARMA_DIRECT_VARIANT: here every batch is
-    too spread out to stage: its global path)."""
+    Variants 20 / 21 / 22 are the tools build's LDS-staged kernel with the skewed stage, the plain
+    stage only, and the plain stage on the 8-copy image with 10 waves (KARMA_DIRECT_VARIANT: here
+    every batch is too spread out to stage: their global path)."""
     host, dbuf = raw
     if variant == "shipped":
         L = _lib.lib()
@@ -578,7 +579,7 @@ def test_ragged_bounded_direct_path(raw, dev, bound, variant, monkeypatch):
 
 
 
-@pytest.mark.parametrize("variant", ["shipped", "20"])
+@pytest.mark.parametrize("variant", ["shipped", "20", "21", "22"])
 @pytest.mark.parametrize("shape", ["wal180", "mixed", "tiny", "unaligned_arena"])
 def test_ragged_bounded_consecutive_records(raw, dev, shape, variant, monkeypatch):
     """Consecutive small records (a WAL image's payloads, a writer's block) through the bounded

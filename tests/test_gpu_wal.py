@@ -53,9 +53,12 @@ WALKS = {
     "inline4k": (False, 4096, _lib.KARMA_WAL_CRC_INLINE),
     "listcrc": (True, 0, _lib.KARMA_WAL_CRC_INLINE),      # the walk, then the walkers' lists checksummed by
     "listcrc4k": (True, 4096, _lib.KARMA_WAL_CRC_INLINE), # the LDS-staged kernel (k_wal_list_crc; tools build)
+    "r8": (True, 0, _lib.KARMA_WAL_CRC_PLAN),             # the plan, the plain-stage small-record kernel on the
+                                                          # 8-copy image with 10 waves (KARMA_STAGE_R8; tools build)
 }
 _LIST_CRC = ("listcrc", "listcrc4k")  # KARMA_WAL_LIST_CRC=1
 _NO_STAGED = ("sepdirect4",)  # KARMA_SMALL_STAGED=0
+_R8 = ("r8",)  # KARMA_STAGE_R8=1
 _WALK = {"name": "split"}
 
 
@@ -69,7 +72,11 @@ def _walk_env(monkeypatch, walk):
         monkeypatch.setenv("KARMA_SMALL_STAGED", "0")
     else:
         monkeypatch.delenv("KARMA_SMALL_STAGED", raising=False)
-    if WALKS[walk][0] and walk not in _LIST_CRC and walk not in _NO_STAGED:
+    if walk in _R8:
+        monkeypatch.setenv("KARMA_STAGE_R8", "1")
+    else:
+        monkeypatch.delenv("KARMA_STAGE_R8", raising=False)
+    if WALKS[walk][0] and walk not in _LIST_CRC and walk not in _NO_STAGED and walk not in _R8:
         monkeypatch.setenv("KARMA_WALK_VARIANT", "1")  # read by the tools build only (ab.h)
     else:
         monkeypatch.delenv("KARMA_WALK_VARIANT", raising=False)
@@ -428,7 +435,7 @@ def test_replay_randomized_against_model(lib, monkeypatch):
             assert got == (list(want[0]), want[1], want[2]), (case, walk, seg, mix)
 
 
-@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc"])
+@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc", "r8"])
 @pytest.mark.parametrize("seg", [4096 + 4, 65536, 1 << 20])
 def test_replay_uniform_runs_speculative_walk(lib, seg, walk, monkeypatch):
     """Runs of one record size (the walker reads a round of headers at the last stride, lane j at
@@ -522,7 +529,7 @@ def test_replay_accepted_size0_records_advance_12(lib, seg, walk, monkeypatch):
     assert spills > 0, "some size-0 record must carry the chain into the next segment"
 
 
-@pytest.mark.parametrize("walk", ["split", "sep", "split4k"])
+@pytest.mark.parametrize("walk", ["split", "sep", "split4k", "r8"])
 def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
     """The device-planned replay launches one small-record kernel, chosen by the largest payload of
     the previous call on the same device (the staged kernel up to 183 B, the 4-lane kernel up to
@@ -555,7 +562,7 @@ def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
         assert got == (list(w[0]), w[1], w[2]), (i, name, walk)
 
 
-@pytest.mark.parametrize("walk", ["split", "sep"])
+@pytest.mark.parametrize("walk", ["split", "sep", "r8"])
 def test_replay_stage_skew_hint_between_calls(lib, walk, monkeypatch):
     """The staged small-record kernel comes in two forms, with the bank-skewed stage (records on
     few LDS banks: strides that are multiples of 32 bytes) and without it; a call takes the form
