@@ -757,7 +757,8 @@ int karma_crc32c_batch_ragged_bounded(const void* d_arena, const uint64_t* d_off
         a.init = d_init;
         a.init_scalar = init;
         a.out = d_out;
-        const bool staged = KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 20;  // tools build: the LDS-staged kernel
+        const long dv = KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0);
+        const bool staged = dv >= 20 && dv <= 22;  // tools build: the LDS-staged kernel (its three forms)
         a.blob = staged ? L.ds->lane_blob : L.ds->quad_blob;
         bind_arena_bounds(a);
         // a wave takes 64 records: no more workgroups than the batch fills (each one loads its

@@ -1200,8 +1200,10 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL((k_ragged_staged_pipe<true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 21)  // (the plain stage only)
         hipLaunchKernelGGL((k_ragged_staged_pipe<false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+#ifdef KARMA_AB
     else if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 22)  // (the 8-copy image, kStgWaves8 waves)
         hipLaunchKernelGGL((k_ragged_staged_pipe<false, true>), dim3(grid_blocks), dim3(kStgWaves8 * 64), 0, s, a);
+#endif
     else
         hipLaunchKernelGGL(k_ragged_direct4, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
@@ -1212,9 +1214,12 @@ hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStr
     if (a.n_rec == 0 || !a.n_dev || !a.gate_len) return hipErrorInvalidValue;
     if (skew) {
         hipLaunchKernelGGL((k_ragged_staged_pipe<true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
-    } else if (KARMA_AB_KNOB("KARMA_STAGE_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves)
+#ifdef KARMA_AB
+    } else if (KARMA_AB_KNOB("KARMA_STAGE_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves; not
+        // shipped: 1M x 180 B 0.1219 vs 0.1215 ms per replay call, 100-B payloads 0.0978 vs 0.1007)
         const uint64_t g = std::min<uint64_t>((uint64_t)grid_blocks, (a.n_rec + 64 * kStgWaves8 - 1) / (64 * kStgWaves8));
         hipLaunchKernelGGL((k_ragged_staged_pipe<false, true>), dim3((unsigned)g), dim3(kStgWaves8 * 64), 0, s, a);
+#endif
     } else {
         hipLaunchKernelGGL((k_ragged_staged_pipe<false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     }
