@@ -711,3 +711,31 @@ def test_fixed_dynamic_tail_steps(dev, shift, monkeypatch):
             g.replay()
             torch.cuda.synchronize()
             _eq(o1.cpu().numpy(), want4)
+
+
+def test_ragged_dynamic_tail_streams_concurrently(dev):
+    """The shipped ragged path (dynamic tail on, k = 3) on three streams at once, 4 calls each with
+    no synchronisation between launches: each stream has its own look-back words and tail counter
+    (lb_ctl[2]), so the calls never share a step; every CRC against the oracle."""
+    rng = np.random.default_rng(303)
+    arena_bytes = 512 << 20
+    host = rng.integers(0, 256, arena_bytes, dtype=np.uint8)
+    arena = torch.from_numpy(host).to(dev)
+    cases = []
+    for k in range(3):
+        n = (30000, 200000, 60000)[k]
+        lens = (synth.loguniform_lengths(k + 11, n, 64, 65536) if k != 1 else rng.integers(1, 2000, n)).astype(np.uint32)
+        offs = rng.integers(0, arena_bytes - 65536, n).astype(np.uint64)
+        cases.append((torch.from_numpy(offs.astype(np.int64)).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev),
+                      int(lens.sum()), oracle_lib.ragged_crcs(host, offs, lens)))
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = [[torch.full((c[0].numel(),), -1, dtype=torch.int32, device=dev) for _ in range(4)] for c in cases]
+    torch.cuda.synchronize()
+    for i in range(4):
+        for k, (d_off, d_len, total, _) in enumerate(cases):
+            with torch.cuda.stream(streams[k]):
+                K.extend_batch_ragged(arena, d_off, d_len, out=outs[k][i], total_len=total, stream=streams[k])
+    torch.cuda.synchronize()
+    for k, c in enumerate(cases):
+        for i in range(4):
+            _eq(outs[k][i].cpu().numpy().view(np.uint32), c[3])
