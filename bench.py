@@ -441,10 +441,10 @@ def wal_bench(args, L, rank):
         algo = payload + 20 * n
         achieved = algo / (crc_kernel_ms * 1e-3) / 1e9
         call_s = payload / (dev_rate * GIB)
-        pm = pmc_traffic(os.path.join(ROOT, "profiles", "r04f_wal_replay_pmc.json"), "wal_replay", wal_bytes)
+        pm = pmc_traffic(os.path.join(ROOT, "profiles", "r04g_wal_replay_pmc.json"), "wal_replay", wal_bytes)
         res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                            "frac": round(achieved / 8000.0, 4), "traffic": pm,
-                           "traffic_source": "profiles/r04f_wal_replay_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, "
+                           "traffic_source": "profiles/r04g_wal_replay_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, "
                                              "every kernel of one rotated call)" if pm is not None else None,
                            "kernel": "the replay's payload CRC batch (k_ragged_staged_pipe)",
                            "kernel_ms_avg": round(crc_kernel_ms, 4), "algorithmic_bytes_per_launch": algo,
