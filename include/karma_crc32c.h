@@ -125,12 +125,17 @@ int karma_crc32c_stream(uint32_t init, const void* d_data, size_t n, uint32_t* d
  *                              (unless a graph hold is active) and the per-device contexts of the
  *                              host, WAL and KFP entry points (recreated by their next call).
  * karma_crc32c_graph_hold      counts the captured graphs a caller keeps (delta +1 / -1); while
- *                              the count is above 0, trim keeps outgrown buffers.  Returns the
+ *                              the count is above 0, trim keeps outgrown buffers and the state of
+ *                              exited threads whose hipStreamPerThread saw a capture.  Returns the
  *                              count (>= 0) or a KARMA_E_* status.
  * device: the device index, or -1 for the calling thread's current device. */
 int karma_crc32c_release_stream(int device, karma_stream_t stream);
 int karma_crc32c_trim(int device);
 int karma_crc32c_graph_hold(int device, int delta);
+/* The per-(device, stream) states the library holds, over all devices (live streams' states;
+ * not the exited threads' states a trim has yet to free).  For leak checks: after trim the
+ * library's own streams hold none. */
+int karma_crc32c_stream_states(void);
 
 /* ---- host-memory batches (synchronous; H2D, kernel, D2H overlapped) ------- */
 int karma_crc32c_batch_fixed_host(const void* h_data, size_t rec_bytes, size_t n_rec, uint32_t init,

@@ -55,6 +55,7 @@ SIGNATURES = {
     "karma_crc32c_release_stream": (_i, [_i, _vp]),
     "karma_crc32c_trim": (_i, [_i]),
     "karma_crc32c_graph_hold": (_i, [_i, _i]),
+    "karma_crc32c_stream_states": (_i, []),
     "karma_crc32c_batch_fixed_host": (_i, [_vp, _sz, _sz, _u32, _vp, _i]),
     "karma_crc32c_batch_ragged_host": (_i, [_vp, _sz, _vp, _vp, _sz, _u32, _vp, _i]),
     "karma_crc32c_batch_fixed_host_multi": (_i, [_vp, _sz, _sz, _u32, _vp, _vp, _i]),

@@ -622,6 +622,8 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
     // 4,096 waves to read the gate).  kSmallStaged / kSmallDirect launch one of them only.
     const uint32_t stg_max = std::min<uint32_t>(gate_max, kStgGateLen);
     if (which == kSmallDirect) a.gate_min = stg_max + 1;
+    // (tools build, KARMA_SMALL_STAGED=0: the 4-lane launch below then takes the whole range,
+    // gate_min 0, whatever `which` says, so the caller's small_batch_covers never overstates)
     if (which != kSmallDirect && KARMA_AB_KNOB("KARMA_SMALL_STAGED", 1)) {
         RaggedArgs b = a;
         b.blob = L.ds->lane_blob;
@@ -669,6 +671,18 @@ void units_timer_end(hipStream_t s) {
 }
 // shared with rccl_comm.cc so RCCL failures land in karma_crc32c_last_error()
 int set_last_error(int code, const std::string& what) { return fail(code, what); }
+// The library's own streams (host, WAL, KFP contexts): their per-stream state freed before the
+// context destroys the stream, so no state outlives its handle (which hipStreamCreate may hand
+// out again).
+int release_internal_stream(int dev, hipStream_t s) {
+    if (!s) return 0;
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_states.release(dev, stream_key(s));
+}
+size_t stream_state_count() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_states.states();
+}
 }  // namespace karma::engine
 
 extern "C" {
@@ -812,6 +826,8 @@ int karma_crc32c_graph_hold(int device, int delta) {
     std::lock_guard<std::mutex> lk(g_mu);
     return g_states.hold(dev, delta);
 }
+
+int karma_crc32c_stream_states(void) { return (int)karma::engine::stream_state_count(); }
 
 }  // extern "C"
 

@@ -418,8 +418,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     //    fold and the 8-lane tree
     const uint32_t X = lane_const16();
     uint32_t inj = 0;
-    if (P.inj_at) inj = P.hfrom < 16 ? steps_in_vec(lds, kSegZ4, kSegZ4 + 4096, ~A.init_scalar, hv, P.hfrom, 16u)
-                                     : ~A.init_scalar;
+    if (P.inj_at) {  // (a per-record init array holds one value: the record's)
+        const uint32_t init = A.init ? *(const __attribute__((address_space(1))) uint32_t*)A.init : A.init_scalar;
+        inj = P.hfrom < 16 ? steps_in_vec(lds, kSegZ4, kSegZ4 + 4096, ~init, hv, P.hfrom, 16u) : ~init;
+    }
     u32x4 x0 = ok0 ? v[0] : u32x4{0u, 0u, 0u, 0u};
     if (ok0 && L.w == P.inj_at) x0.x ^= inj;
     uint32_t a0 = x0.x, a1 = x0.y, a2 = x0.z, a3 = x0.w;

@@ -431,6 +431,10 @@ int trim_host_batch_ctx(int dev);  // host_batch.cc
 int trim_append_ctx(int dev);      // wal_append.cc
 int trim_kfp_ctx(int dev);         // kfp.cc
 int trim_stage(int dev);           // host_stage.cc
+// A context's own stream: its per-stream batch state (workspace, look-back and fused words) freed
+// before the context destroys the handle (capi.cc).
+int release_internal_stream(int dev, hipStream_t s);
+size_t stream_state_count();
 
 // Synthetic data: bytes of the counter-based splitmix64 stream.
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n_bytes, uint64_t seed, uint64_t first_byte, hipStream_t s);

@@ -100,10 +100,11 @@ struct HostCtx {
         ready = true;
         return 0;
     }
-    void reset() {  // karma_crc32c_trim (the caller holds mu)
+    void reset(int dev) {  // karma_crc32c_trim (the caller holds mu)
         if (!ready) return;
         for (Slot& s : slot) {
             (void)hipStreamSynchronize(s.st);
+            (void)karma::engine::release_internal_stream(dev, s.st);
             for (Buf* b : {&s.d_data, &s.d_off, &s.d_len, &s.d_out, &s.h_off, &s.h_len, &s.h_out}) b->release();
             (void)hipEventDestroy(s.done);
             (void)hipStreamDestroy(s.st);
@@ -186,7 +187,7 @@ int fixed_pinned(HostCtx& c, const char* src, size_t rec_bytes, size_t n_rec, ui
 int karma::engine::trim_host_batch_ctx(int dev) {
     HostCtx& c = ctx_for(dev);
     std::lock_guard<std::mutex> lk(c.mu);
-    c.reset();
+    c.reset(dev);
     return 0;
 }
 

@@ -219,10 +219,11 @@ struct EncCtx {
         }
         return 0;
     }
-    void reset() {  // karma_crc32c_trim (the caller holds mu)
+    void reset(int dev) {  // karma_crc32c_trim (the caller holds mu)
         if (!ready) return;
         for (auto& x : st) {
             (void)hipStreamSynchronize(x);
+            (void)karma::engine::release_internal_stream(dev, x);
             (void)hipStreamDestroy(x);
             x = nullptr;
         }
@@ -401,7 +402,7 @@ int karma::engine::trim_kfp_ctx(int dev) {
     {
         EncCtx& c = enc_ctx(dev);
         std::lock_guard<std::mutex> lk(c.mu);
-        c.reset();
+        c.reset(dev);
     }
     SpanBufs* B = span_bufs(dev);
     std::lock_guard<std::mutex> lk(B->mu);

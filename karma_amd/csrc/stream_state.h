@@ -98,18 +98,21 @@ class StreamStates {
     }
 
     // Waits for the device, then frees what no live stream holds: the orphaned states, and --
-    // unless a graph hold is active -- every retired buffer.
+    // unless a graph hold is active -- every retired buffer.  An orphaned state that saw a capture
+    // is kept while a hold is active too (a graph captured on hipStreamPerThread by a thread that
+    // has exited still points into it).
     int trim(int dev) {
         if (const int rc = ops_.sync_device(dev)) return rc;
+        const bool held = holds(dev) > 0;
         for (auto it = zombies_.begin(); it != zombies_.end();) {
-            if (it->first == dev) {
+            if (it->first == dev && !(held && it->second.captured)) {
                 free_state(it->second);
                 it = zombies_.erase(it);
             } else {
                 ++it;
             }
         }
-        if (holds(dev) > 0) return 0;
+        if (held) return 0;
         for (auto& kv : states_) {
             if (kv.first.first != dev) continue;
             for (void* p : kv.second.retired) ops_.free(p);

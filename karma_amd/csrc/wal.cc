@@ -177,9 +177,10 @@ struct ReplayCtx {
         return 0;
     }
     // karma_crc32c_trim (the caller holds mu): everything freed, recreated by the next replay.
-    void reset() {
+    void reset(int dev) {
         if (!ready) return;
         (void)hipStreamSynchronize(st);
+        (void)karma::engine::release_internal_stream(dev, st);
         for (DevBuf* b : {&img, &crec, &clen, &ccrc, &meta, &sub, &span, &cbase, &off, &len, &stored, &crc, &sum, &h_small})
             b->release();
         (void)hipStreamDestroy(st);
@@ -203,7 +204,7 @@ ReplayCtx& replay_ctx(int dev) {
 int karma::engine::trim_replay_ctx(int dev) {
     ReplayCtx& c = replay_ctx(dev);
     std::lock_guard<std::mutex> lk(c.mu);
-    c.reset();
+    c.reset(dev);
     return 0;
 }
 

@@ -132,10 +132,11 @@ struct AppendCtx {
         }
         return 0;
     }
-    void reset() {  // karma_crc32c_trim (the caller holds mu)
+    void reset(int dev) {  // karma_crc32c_trim (the caller holds mu)
         if (!ready) return;
         for (auto& s : st) {
             (void)hipStreamSynchronize(s);
+            (void)karma::engine::release_internal_stream(dev, s);
             (void)hipStreamDestroy(s);
             s = nullptr;
         }
@@ -405,7 +406,7 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
 int karma::engine::trim_append_ctx(int dev) {
     AppendCtx& c = ctx_for(dev);
     std::lock_guard<std::mutex> lk(c.mu);
-    c.reset();
+    c.reset(dev);
     return 0;
 }
 

@@ -495,6 +495,22 @@ void test_stream_state_lifetime(std::mt19937_64& rng) {
     CHECK(S.zombies() == 1);
     CHECK(S.trim(3) == 0);
     CHECK(S.zombies() == 0);
+    // ... unless it saw a capture and a graph hold is active: a graph captured on the exited
+    // thread's hipStreamPerThread may still be replayed
+    const uintptr_t gkey = 0x15;
+    void* ps = reinterpret_cast<void*>(uintptr_t(2));  // hipStreamPerThread
+    use(2, gkey, ps, 555, 2048, false);
+    world.capturing[ps] = true;
+    use(2, gkey, ps, 555, 2048, false);
+    world.capturing[ps] = false;
+    S.orphan(gkey);
+    CHECK(S.hold(2, +1) == 1);
+    const size_t live_held = world.live.size();
+    CHECK(S.trim(2) == 0);
+    CHECK(S.zombies() == 1 && world.live.size() == live_held);  // kept under the hold
+    CHECK(S.hold(2, -1) == 0);
+    CHECK(S.trim(2) == 0);
+    CHECK(S.zombies() == 0 && world.live.size() < live_held);  // freed once the hold is gone
     CHECK(S.release(1, (uintptr_t)cs) == 0);
     CHECK(S.release(1, 12345) == 0);  // unknown: nothing to do
     CHECK(world.live.empty() && world.allocs == world.frees);

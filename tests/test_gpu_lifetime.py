@@ -259,3 +259,46 @@ def test_segment_scans_on_four_streams_concurrently(dev):
     _eq(rout.cpu().numpy(), want_r)
     for st in streams:
         assert _lib.lib().karma_crc32c_release_stream(-1, st.cuda_stream) == 0
+
+
+def test_trim_releases_internal_stream_states(dev):
+    """The host-memory, WAL and KFP contexts run their batches on the library's own streams, which
+    trim destroys: the per-stream state those batches left (workspace, look-back words) goes with
+    each stream.  Host batches whose records exceed 1 KiB (the ragged unit plan), a
+    fixed host batch, a replay whose payloads exceed 1 KiB (its host-sized ragged batch) and an
+    append, then trim: the library holds no more states than before, over three cycles."""
+    L = _lib.lib()
+    rng = np.random.default_rng(12)
+    assert L.karma_crc32c_trim(-1) == 0
+    base = L.karma_crc32c_stream_states()
+    n = 3000
+    lens = rng.integers(1500, 9000, n).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 8)]).astype(np.uint64)
+    arena = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]) + 16, dtype=np.uint8)
+    want = oracle_lib.ragged_crcs(arena, offs, lens)
+    out = np.zeros(n, np.uint32)
+    fx = arena[: 512 * 4096]
+    fout = np.zeros(512, np.uint32)
+    seg = 1 << 20
+    plens = rng.integers(1100, 4000, 600).astype(np.uint32)
+    poffs = np.concatenate([[0], np.cumsum(plens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    src = rng.integers(0, 256, int(plens.sum()) + 16, dtype=np.uint8)
+    wal = np.zeros(4 * seg, np.uint8)
+    cur, nf = ctypes.c_uint64(0), ctypes.c_size_t()
+    nrec, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+    for cycle in range(3):
+        _lib.check("ragged_host", L.karma_crc32c_batch_ragged_host(arena.ctypes.data, arena.nbytes, offs.ctypes.data,
+                                                                   lens.ctypes.data, n, 0, out.ctypes.data, -1))
+        _eq(out, want)
+        _lib.check("fixed_host", L.karma_crc32c_batch_fixed_host(fx.ctypes.data, 4096, 512, 0, fout.ctypes.data, -1))
+        _eq(fout, oracle_lib.fixed_crcs(fx, 4096))
+        cur.value = 0
+        _lib.check("wal_append", L.karma_wal_append_batch(src.ctypes.data, poffs.ctypes.data, plens.ctypes.data,
+                                                          plens.size, wal.ctypes.data, wal.nbytes, seg,
+                                                          ctypes.byref(cur), None, ctypes.byref(nf), -1))
+        _lib.check("wal_replay", L.karma_wal_replay(wal.ctypes.data, None, wal.nbytes, seg, 0, ctypes.byref(nrec),
+                                                    ctypes.byref(stop), ctypes.byref(status), None, 0, -1))
+        assert nrec.value == nf.value == plens.size
+        assert L.karma_crc32c_stream_states() > base, "the host batches used per-stream state"
+        assert L.karma_crc32c_trim(-1) == 0
+        assert L.karma_crc32c_stream_states() == base, f"cycle {cycle}: states left behind by the contexts' streams"

@@ -255,6 +255,12 @@ def test_segment_once_sizes_and_alignments(dev):
         for off, m in cases:
             got = int(K.extend_stream(init, buf[off: off + m]).item())
             assert got == oracle_lib.extend(init, host[off: off + m].tobytes()), (hex(init), off, m)
+    # one record with a one-element per-record init array (batch_fixed's d_init) takes the same
+    # kernel: the array's value seeds it, not the scalar
+    for off, m in [(0, 1 << 20), (3, (16 << 20) + 5), (0, 64 << 20)]:
+        ini = torch.from_numpy(np.array([0x7A5C31E9], dtype=np.uint32)).to(dev)
+        got = int(K.value_batch_fixed(buf[off: off + m], m, init=ini).cpu().numpy().astype(np.uint32)[0])
+        assert got == oracle_lib.extend(0x7A5C31E9, host[off: off + m].tobytes()), ("init array", off, m)
 
 
 def test_config2_full_1m_x_4k(dev):
