@@ -210,8 +210,9 @@ int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, siz
  * are cut into contiguous ranges, one per listed device, replayed at once (each range streamed
  * over its own device's link), and merged in WAL order: a range's records count while every
  * range before it ended cleanly at its last segment's end, as the one-device replay would have
- * walked on.  When an accepted size-0 record carries the chain 1-4 bytes past a range's end the
- * rest is replayed from there on devices[0].  Same outputs as karma_wal_replay. */
+ * walked on.  When an accepted size-0 record carries the chain 1-4 bytes past a range's end, the
+ * next range alone is replayed again from there, on its own device (one extra range replay per
+ * such spill).  Same outputs as karma_wal_replay. */
 int karma_wal_replay_multi(const void* h_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start, uint64_t* h_n_records,
                            uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap, const int* devices,
                            int n_dev);

@@ -241,8 +241,14 @@ int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, cons
     T.mark("validate");
     const char* src = static_cast<const char*>(h_arena);
     const bool pinned = karma::engine::host_is_pinned(h_arena);
-    Slot& s = c.slot[0];
-    for (size_t r0 = 0; r0 < n_rec;) {
+    // Two slots on two streams, as the fixed path: slice i + 1's upload (a DMA from pinned caller
+    // memory, or the staging threads' copy from pageable memory) runs while slice i's kernel and
+    // CRC download are in flight on the other stream; a slot is collected before it is reused.
+    int rc = 0;
+    size_t i = 0;
+    for (size_t r0 = 0; r0 < n_rec && !rc; ++i) {
+        Slot& s = c.slot[i & 1];
+        if ((rc = collect(s, h_out))) break;
         // slice = records [r0, r1) whose bytes span [lo, hi) <= kSlice (at least one record);
         // offsets out of order: one slice over every record
         uint64_t lo = h_off[r0], hi = h_off[r0] + h_len[r0];
@@ -256,12 +262,11 @@ int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, cons
             max_len = std::max(max_len, h_len[r1]);
         }
         const size_t nr = r1 - r0;
-        if (const int rc = s.d_data.ensure(std::max<uint64_t>(hi - lo, 16), false)) return rc;
-        if (const int rc = s.d_off.ensure(nr * sizeof(uint64_t), false)) return rc;
-        if (const int rc = s.d_len.ensure(nr * sizeof(uint32_t), false)) return rc;
-        if (const int rc = s.d_out.ensure(nr * sizeof(uint32_t), false)) return rc;
-        if (const int rc = s.h_off.ensure(nr * sizeof(uint64_t), true)) return rc;
-        if (const int rc = s.h_len.ensure(nr * sizeof(uint32_t), true)) return rc;
+        if ((rc = s.d_data.ensure(std::max<uint64_t>(hi - lo, 16), false)) ||
+            (rc = s.d_off.ensure(nr * sizeof(uint64_t), false)) || (rc = s.d_len.ensure(nr * sizeof(uint32_t), false)) ||
+            (rc = s.d_out.ensure(nr * sizeof(uint32_t), false)) || (rc = s.h_off.ensure(nr * sizeof(uint64_t), true)) ||
+            (rc = s.h_len.ensure(nr * sizeof(uint32_t), true)) || (rc = s.h_out.ensure(nr * sizeof(uint32_t), true)))
+            break;
         uint64_t* ho = s.h_off.as<uint64_t>();
         uint64_t total = 0;
         for (size_t k = 0; k < nr; ++k) {
@@ -269,24 +274,32 @@ int karma_crc32c_batch_ragged_host(const void* h_arena, size_t arena_bytes, cons
             total += h_len[r0 + k];
         }
         std::memcpy(s.h_len.p, h_len + r0, nr * sizeof(uint32_t));
-        HB_HIP(hipMemcpyAsync(s.d_off.p, s.h_off.p, nr * sizeof(uint64_t), hipMemcpyHostToDevice, s.st));
-        HB_HIP(hipMemcpyAsync(s.d_len.p, s.h_len.p, nr * sizeof(uint32_t), hipMemcpyHostToDevice, s.st));
-        if (pinned) {
-            HB_HIP(hipMemcpyAsync(s.d_data.p, src + lo, hi - lo, hipMemcpyHostToDevice, s.st));
-        } else if (const int rc = karma::engine::staged_copy(dev, s.d_data.p, src + lo, hi - lo)) {
-            return rc;
+        hipError_t e = hipMemcpyAsync(s.d_off.p, s.h_off.p, nr * sizeof(uint64_t), hipMemcpyHostToDevice, s.st);
+        if (e == hipSuccess) e = hipMemcpyAsync(s.d_len.p, s.h_len.p, nr * sizeof(uint32_t), hipMemcpyHostToDevice, s.st);
+        if (e == hipSuccess && pinned) e = hipMemcpyAsync(s.d_data.p, src + lo, hi - lo, hipMemcpyHostToDevice, s.st);
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "ragged_host: H2D");
+            break;
         }
+        if (!pinned && (rc = karma::engine::staged_copy(dev, s.d_data.p, src + lo, hi - lo))) break;
         T.mark("upload");
-        if (const int rc = karma_crc32c_batch_ragged_bounded(s.d_data.p, s.d_off.as<uint64_t>(), s.d_len.as<uint32_t>(),
-                                                             nr, total, max_len, nullptr, init, s.d_out.as<uint32_t>(),
-                                                             s.st))
-            return rc;
-        HB_HIP(hipMemcpyAsync(h_out + r0, s.d_out.p, nr * sizeof(uint32_t), hipMemcpyDeviceToHost, s.st));
-        HB_HIP(hipStreamSynchronize(s.st));
-        T.mark("batch + D2H");
+        if ((rc = karma_crc32c_batch_ragged_bounded(s.d_data.p, s.d_off.as<uint64_t>(), s.d_len.as<uint32_t>(), nr, total,
+                                                    max_len, nullptr, init, s.d_out.as<uint32_t>(), s.st)))
+            break;
+        e = hipMemcpyAsync(s.h_out.p, s.d_out.p, nr * sizeof(uint32_t), hipMemcpyDeviceToHost, s.st);
+        if (e == hipSuccess) e = hipEventRecord(s.done, s.st);
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "ragged_host: D2H");
+            break;
+        }
+        s.busy = true;
+        s.r0 = r0;
+        s.nr = nr;
         r0 = r1;
     }
-    return KARMA_OK;
+    rc = drain(c, h_out, rc);
+    T.mark("batches + D2H");
+    return rc;
 }
 
 }  // extern "C"

@@ -90,39 +90,30 @@ int karma_wal_replay_multi(const void* h_wal, size_t wal_bytes, size_t seg_bytes
     if (sh.size() <= 1 || start >= wal_bytes)
         return karma_wal_replay(h_wal, nullptr, wal_bytes, seg_bytes, start, h_n_records, h_stop, h_status, h_rec_off,
                                 rec_cap, devices[0]);
+    // share k replayed from the absolute offset `from` (its lo, or a stop a spill carried 1-4 bytes
+    // into its first segment), on its own device
+    auto replay_share = [&](int k, uint64_t from) {
+        karma::engine::ReplayShare& s = sh[k];
+        const uint64_t bytes = s.hi - s.lo;
+        s.start = from;
+        s.rec.assign(h_rec_off ? std::min<uint64_t>(rec_cap, bytes / 8 + 2) : 0, 0);
+        const int r = karma_wal_replay(img + s.lo, nullptr, bytes, seg_bytes, s.start - s.lo, &s.n, &s.stop, &s.status,
+                                       s.rec.empty() ? nullptr : s.rec.data(), s.rec.size(), devices[k]);
+        if (r) return r;
+        s.stop += s.lo;
+        if (s.rec.size() > s.n) s.rec.resize(s.n);
+        for (uint64_t& o : s.rec) o += s.lo;
+        return 0;
+    };
     std::string what;
     const int parts = (int)sh.size();
-    int rc = karma::engine::run_shares(
-        parts,
-        [&](int k) {
-            karma::engine::ReplayShare& s = sh[k];
-            const uint64_t bytes = s.hi - s.lo;
-            s.rec.assign(h_rec_off ? std::min<uint64_t>(rec_cap, bytes / 8 + 2) : 0, 0);
-            const int r = karma_wal_replay(img + s.lo, nullptr, bytes, seg_bytes, s.start - s.lo, &s.n, &s.stop,
-                                           &s.status, s.rec.empty() ? nullptr : s.rec.data(), s.rec.size(), devices[k]);
-            if (r) return r;
-            s.stop += s.lo;
-            if (s.rec.size() > s.n) s.rec.resize(s.n);
-            for (uint64_t& o : s.rec) o += s.lo;
-            return 0;
-        },
-        detail, &what);
+    int rc = karma::engine::run_shares(parts, [&](int k) { return replay_share(k, sh[k].start); }, detail, &what);
     if (rc) return set_last_error(rc, what);
-    const int end =
-        karma::engine::merge_replays(sh, wal_bytes, h_n_records, h_stop, h_status, h_rec_off, rec_cap, KARMA_WAL_END);
-    if (end >= 0) return KARMA_OK;
-    // an accepted size-0 record carried the chain past a share's last segment: replay on from
-    // there on one device (the shares after it assumed a segment start)
-    uint64_t n2 = 0, stop2 = 0;
-    int st2 = 0;
-    const uint64_t got = *h_n_records;
-    rc = karma_wal_replay(h_wal, nullptr, wal_bytes, seg_bytes, *h_stop, &n2, &stop2, &st2,
-                          h_rec_off && got < rec_cap ? h_rec_off + got : nullptr, got < rec_cap ? rec_cap - got : 0,
-                          devices[0]);
-    if (rc) return rc;
-    *h_n_records = got + n2;
-    *h_stop = stop2;
-    *h_status = st2;
+    int redo_rc = 0;
+    const int end = karma::engine::merge_replays(
+        sh, h_n_records, h_stop, h_status, h_rec_off, rec_cap, KARMA_WAL_END,
+        [&](int k, uint64_t from) { return replay_share(k, from); }, &redo_rc);
+    if (end < 0) return set_last_error(redo_rc, "wal_replay_multi: share replayed after a size-0 spill: " + detail());
     return KARMA_OK;
 }
 

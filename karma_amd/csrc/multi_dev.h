@@ -88,14 +88,20 @@ inline std::vector<ReplayShare> replay_shares(uint64_t wal_bytes, uint64_t seg_b
 }
 
 // sivir::open's loop (sivir.cc:31-41) over the shares in order: a share's records count only when
-// every share before it walked to its range's end and stopped there cleanly (END at exactly its
-// hi: the chain entered the next range at a segment start, as the shares assumed).  Returns the
-// index of the share whose stop ends replay, or -1 when one stopped PAST its range (an accepted
-// size-0 record carried the chain 1-4 bytes into the next segment, wal.cc:66): the caller then
-// replays on from that share's stop.  *n, *stop, *status: the merged result so far.
-inline int merge_replays(const std::vector<ReplayShare>& sh, uint64_t wal_bytes, uint64_t* n, uint64_t* stop,
-                         int* status, uint64_t* rec_off, size_t rec_cap, int end_status) {
+// every share before it walked to its range's end and stopped there cleanly (END at its hi: the
+// chain entered the next range at a segment start, as the shares assumed).  When a share stops
+// cleanly PAST its range (an accepted size-0 record carried the chain 1-4 bytes into the next
+// segment, wal.cc:66), only the next share is replayed again, from that stop: redo(k, start)
+// re-runs share k from the absolute offset `start` (inside its first segment) and updates sh[k],
+// returning a KARMA status.  The shares after it stay valid as long as the redone share ends at
+// its own hi again, so each spill costs one share replay.  Returns the index of the share whose
+// stop ends replay, or -1 when a redo failed (*redo_rc = its status).  *n, *stop, *status: the
+// merged result.
+template <class Redo>
+inline int merge_replays(std::vector<ReplayShare>& sh, uint64_t* n, uint64_t* stop, int* status, uint64_t* rec_off,
+                         size_t rec_cap, int end_status, Redo&& redo, int* redo_rc) {
     *n = 0;
+    *redo_rc = 0;
     for (size_t k = 0; k < sh.size(); ++k) {
         const ReplayShare& s = sh[k];
         for (uint64_t i = 0; i < s.n; ++i) {
@@ -106,8 +112,12 @@ inline int merge_replays(const std::vector<ReplayShare>& sh, uint64_t wal_bytes,
         *status = s.status;
         const bool last = k + 1 == sh.size();
         if (s.status != end_status || s.stop < s.hi || last) return (int)k;
-        if (s.stop > s.hi) return -1;  // carried into the next share's range past its start
-        (void)wal_bytes;
+        if (s.stop > s.hi) {  // carried into the next share's range past its start: redo that share
+            if (const int rc = redo((int)k + 1, s.stop)) {
+                *redo_rc = rc;
+                return -1;
+            }
+        }
     }
     return (int)sh.size() - 1;
 }

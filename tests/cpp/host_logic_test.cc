@@ -607,14 +607,50 @@ void test_multi_device_split(std::mt19937_64& rng) {
         return s;
     };
     uint64_t n = 0, stop = 0, rec[64];
-    int st = 0;
+    int st = 0, redo_rc = 0;
+    int redos = 0;
+    auto no_redo = [&](int, uint64_t) {
+        ++redos;
+        return 0;
+    };
     std::vector<ReplayShare> sh = {mk(0, 100, 3, 100, 0), mk(100, 200, 2, 200, 0), mk(200, 300, 4, 300, 0)};
-    CHECK(merge_replays(sh, 300, &n, &stop, &st, rec, 64, 0) == 2 && n == 9 && stop == 300 && st == 0);
-    CHECK(rec[0] == 0 && rec[3] == 100 && rec[5] == 200 && rec[8] == 248);
+    CHECK(merge_replays(sh, &n, &stop, &st, rec, 64, 0, no_redo, &redo_rc) == 2 && n == 9 && stop == 300 && st == 0);
+    CHECK(rec[0] == 0 && rec[3] == 100 && rec[5] == 200 && rec[8] == 248 && redos == 0);
     sh = {mk(0, 100, 3, 100, 0), mk(100, 200, 2, 150, 1), mk(200, 300, 4, 300, 0)};
-    CHECK(merge_replays(sh, 300, &n, &stop, &st, rec, 4, 0) == 1 && n == 5 && stop == 150 && st == 1);
+    CHECK(merge_replays(sh, &n, &stop, &st, rec, 4, 0, no_redo, &redo_rc) == 1 && n == 5 && stop == 150 && st == 1);
+    CHECK(redos == 0);
+    // a spill past every share boundary: each costs one replay of the next share alone (a stub
+    // counting the one-device calls), never the rest of the image on one device
+    for (int parts : {2, 3, 8}) {
+        sh.clear();
+        for (int k = 0; k < parts; ++k) sh.push_back(mk(100 * k, 100 * (k + 1), 2, 100 * (k + 1) + 2, 0));
+        std::vector<int> calls(parts, 0);
+        auto redo = [&](int k, uint64_t from) {
+            ++calls[k];
+            CHECK(from == sh[k].lo + 2);
+            sh[k] = mk(sh[k].lo, sh[k].hi, 3, k + 1 == parts ? sh[k].hi : sh[k].hi + 2, 0);  // spills on
+            sh[k].rec.assign({from, from + 40, from + 80});
+            return 0;
+        };
+        CHECK(merge_replays(sh, &n, &stop, &st, rec, 64, 0, redo, &redo_rc) == parts - 1);
+        CHECK(n == 2 + 3 * (uint64_t)(parts - 1) && stop == 100ull * parts && st == 0 && redo_rc == 0);
+        for (int k = 0; k < parts; ++k) CHECK(calls[k] == (k ? 1 : 0));
+        CHECK(rec[2] == 102 && rec[3] == 142);
+    }
+    // a redone share that ends cleanly at its own hi: the later shares' first results stand
+    sh = {mk(0, 100, 3, 102, 0), mk(100, 200, 2, 200, 0), mk(200, 300, 4, 300, 0)};
+    int later = 0;
+    auto redo1 = [&](int k, uint64_t from) {
+        if (k != 1) ++later;
+        sh[k] = mk(sh[k].lo, sh[k].hi, 1, 200, 0);
+        sh[k].rec.assign({from});
+        return 0;
+    };
+    CHECK(merge_replays(sh, &n, &stop, &st, rec, 64, 0, redo1, &redo_rc) == 2 && n == 8 && stop == 300 && later == 0);
+    // a failing redo is reported
     sh = {mk(0, 100, 3, 102, 0), mk(100, 200, 2, 200, 0)};
-    CHECK(merge_replays(sh, 200, &n, &stop, &st, nullptr, 0, 0) == -1 && n == 3 && stop == 102);
+    CHECK(merge_replays(sh, &n, &stop, &st, nullptr, 0, 0, [](int, uint64_t) { return -3; }, &redo_rc) == -1);
+    CHECK(redo_rc == -3 && n == 3 && stop == 102);
 }
 
 int main() {
