@@ -55,6 +55,7 @@ constexpr uint32_t kDirectMaxLen = 1024;  // ragged records up to this: one reco
 constexpr uint64_t kOverdecompose = 4;    // units per group before splitting records
 constexpr uint64_t kSegOnceUnits = 128;      // units per workgroup of k_segment_once (8 x 16 waves)
 constexpr uint64_t kSegOnceMin = 256 << 10;  // single records from this size take it
+constexpr long kSegOnceDefault = 1;          // 1: the grid's last workgroup folds; 2: the last-arriving one
 constexpr uint64_t kSplitOverdecompose = 64;  // units per group once split (2 KiB units up to 4 GiB
                                               // batches; 4: config 4 0.653 ms, 64: 0.609)
 
@@ -118,7 +119,8 @@ std::vector<DevState> g_dev;
 //     sees only its own tag or older ones.  The counter and the tag live on the device
 //     (k_ragged_plan / k_ragged_finalize), so a captured ragged call replays any number of
 //     times.  Zeroed when allocated; the device clears them when the 22-bit tag wraps.
-//   fused words (FixedArgs::fctl, k_units_fixed FUSE): [0] unused, [1] the last finished call's
+//   fused words (FixedArgs::fctl, k_units_fixed FUSE, k_segment_once): [0] arrival tickets (zero
+//     between calls), [1] the last finished call's
 //     tag, then kBlockCombMaxPerThread * 1024 tagged wave states.  Zeroed once and never moved:
 //     the tags only grow, so no state a later call reads carries its tag before that call wrote it.
 StreamStates<HipStateOps> g_states;
@@ -341,9 +343,11 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
         return 0;
     }
     KARMA_RC(comb_blob(ds, unit, &a.comb_maps));  // Z_U, Z_2U, Z_4U lead the unit's combine blob
+    // (the tools build's KARMA_SEGMENT_ONCE: 0 = the looping fused kernel, 2 = the last-arriving
+    // workgroup folds)
+    const long seg_once = KARMA_AB_KNOB("KARMA_SEGMENT_ONCE", kSegOnceDefault);
     if (n_rec == 1 && rec_bytes >= kSegOnceMin &&
-        rec_bytes <= (uint64_t)ds.cu * kSegOnceUnits * segment_once_max_unit(a.arena, rec_bytes) &&
-        KARMA_AB_KNOB("KARMA_SEGMENT_ONCE", 1)) {
+        rec_bytes <= (uint64_t)ds.cu * kSegOnceUnits * segment_once_max_unit(a.arena, rec_bytes) && seg_once) {
         // one segment (up to 64 MiB on 256 CUs): every wave streams one wave-step of 8 units with all
         // of its loads in flight at once, workgroups fold their waves (k_segment_once)
         const uint64_t G = std::min<uint64_t>(ds.cu, std::max<uint64_t>(1, ceil_div(rec_bytes, kSegOnceUnits * 512)));
@@ -356,7 +360,7 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
         KARMA_RC(fused_words(dev, s, &w));
         a.fctl = w;
         a.partial = reinterpret_cast<uint32_t*>(w + 2);
-        KARMA_HIP(launch_segment_once(a, (int)G, s));
+        KARMA_HIP(launch_segment_once(a, (int)G, s, seg_once == 2));
         return 0;
     }
     if (n_rec == 1 && k / kGroupsPerWave <= kBlockCombMaxPerThread * 1024) {

@@ -365,7 +365,12 @@ struct LdsCopy {  // a global -> LDS copy split in two: the loads, then (after o
     }
 };
 
-template <bool NT>
+// ARRIVE: the workgroup that arrives last folds (one ticket per workgroup from fctl[0] after its
+// state is published; the last ticket resets the counter), instead of the grid's highest-index
+// workgroup waiting for the others: no workgroup waits on one that may not have been scheduled, so
+// the forward-progress contract of include/karma_crc32c.h is not needed.  Every workgroup then
+// loads the grid fold maps (any may fold).
+template <bool NT, bool ARRIVE = false>
 __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
                  (reinterpret_cast<uintptr_t>(A.arena + A.rec_bytes) + 15) & ~uintptr_t(15));
@@ -429,7 +434,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     for (int q = 1; q < kSegMaxChunks; ++q)
         if (q < L.nch - 1 || (q == L.nch - 1 && L.lok)) step4<24>(lds, X, a0, a1, a2, a3, v[q]);
     LdsCopy<kCombMaps * 1024, kBlockThreads> grid;  // the last workgroup's fold maps, in flight meanwhile
-    if (last_wg) grid.load(A.block_blob);
+    if (ARRIVE || last_wg) grid.load(A.block_blob);
     uint32_t tag = 0;  // wave 0 publishes the workgroup's state, tagged with the call's tag
     if (wave == 0)
         tag = __hip_atomic_load(reinterpret_cast<const uint32_t*>(A.fctl + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -449,10 +454,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     t = __shfl_down(c, 32, 64);
     c = zmap(lds, kSegComb + 2048, c) ^ t;
     if (lane == 0) wst[wave] = c;
-    if (last_wg) grid.store(lds + kSegGrid);
+    if (ARRIVE || last_wg) grid.store(lds + kSegGrid);
     SEG_STAMP(2);
     __syncthreads();
     __shared__ uint32_t s_tag;
+    __shared__ uint32_t s_last;
     if (wave == 0) {
         const uint32_t my_tag = tag ? tag : 1u;
         uint32_t s = lane < kWavesPerBlock ? wst[lane] : 0u;
@@ -465,10 +471,17 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
             __hip_atomic_store(reinterpret_cast<unsigned long long*>(A.partial) + blockIdx.x,
                                ((unsigned long long)my_tag << 32) | s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (lane == 0) s_tag = my_tag;
+        if (ARRIVE && lane == 0)  // the ticket: taken after the state's store was issued
+            s_last = __hip_atomic_fetch_add(A.fctl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x;
     }
     SEG_STAMP(3);
-    if (!last_wg) return;
-    __syncthreads();  // s_tag
+    if (ARRIVE) {
+        __syncthreads();  // s_last, s_tag
+        if (!s_last) return;
+    } else {
+        if (!last_wg) return;
+        __syncthreads();  // s_tag
+    }
     const uint32_t my_tag = s_tag;
     // 7. the grid's last workgroup: its states, end-aligned (leading zeros pad them to whole waves),
     //    a 64-lane tree per wave (Z_{128U 2^d}), the wave results by Horner (Z_{64 128U}), the tail
@@ -500,6 +513,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
         for (uint32_t w = 1; w < nw; ++w) r = zmap(lds, kSegGrid + 6 * 1024, r) ^ wst[w];
         A.out[0] = ~steps_in_vec(lds, kSegZ4, kSegZ4 + 4096, r, tv, 0u, g0.e > g0.b ? (uint32_t)(g0.e - g0.b) : 0u);
         __hip_atomic_store(A.fctl + 1, (unsigned long long)my_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ARRIVE)  // every ticket of this call is taken: the next call on the stream starts from 0
+            __hip_atomic_store(A.fctl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     SEG_STAMP(5);
 }
@@ -729,7 +744,7 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t s) {
+hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t s, bool arrive) {
     // one record; units_per_rec = 8 units x 16 waves x grid_blocks of at most 2 KiB; fctl, partial,
     // comb_maps (comb blob of the unit) and block_blob (comb blob of 128 units) bound
     if (a.n_rec != 1 || !a.fctl || !a.partial || !a.comb_maps || !a.block_blob || a.rec_bytes < 31 ||
@@ -737,7 +752,10 @@ hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t 
         a.unit_bytes > segment_once_max_unit(a.arena, a.rec_bytes) || a.unit_bytes % kChunk || grid_blocks > 1024)
         return hipErrorInvalidValue;
     units_timer_begin(s);
-    hipLaunchKernelGGL(k_segment_once<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    if (arrive)
+        hipLaunchKernelGGL((k_segment_once<true, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_segment_once<true, false>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     return hipGetLastError();
 }

@@ -113,7 +113,8 @@ struct FixedArgs {
     // tagged, (tag << 32 | state), as agent-scope atomic stores into partial (as uint64); the
     // grid's last workgroup folds them like k_combine_block with block_blob, waiting on each
     // state's tag, and writes the CRC.  fctl[1] = the last finished call's tag (device-resident,
-    // so a captured graph replays correctly; fctl[0] unused).  nullptr: not fused.
+    // so a captured graph replays correctly; fctl[0]: k_segment_once's arrival tickets when the
+    // last-arriving workgroup folds, zero between calls).  nullptr: not fused.
     unsigned long long* fctl;
     const uint32_t* block_blob; // kBlockCombWords (block_comb_blob for D = 8 units, m states per thread)
     uint64_t comb_m;            // states per thread of the fused fold
@@ -255,7 +256,8 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s);
 // One record streamed one wave-step per wave (k_segment_once: a segment scan up to grid x 128
 // units of <= 2 KiB): units_per_rec = 128 x grid_blocks, comb_maps = the unit's combine blob,
 // block_blob = the combine blob of 128 units, fctl / partial = the fused words.
-hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t s);
+// arrive: the last-arriving workgroup folds (a ticket counter in fctl[0]), not the grid's last one.
+hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t s, bool arrive);
 // Its largest unit: 16 chunk loads per lane, so 2 KiB when the body's end (16-aligned) sits on the
 // 128-byte grid, else 1,920 bytes (units are end-aligned: one then spans a chunk more).
 inline uint64_t segment_once_max_unit(const uint8_t* rec, uint64_t rec_bytes) {

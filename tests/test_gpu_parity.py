@@ -263,6 +263,56 @@ def test_segment_once_sizes_and_alignments(dev):
         assert got == oracle_lib.extend(0x7A5C31E9, host[off: off + m].tobytes()), ("init array", off, m)
 
 
+def test_segment_once_arrival_fold(dev, monkeypatch):
+    """k_segment_once with the last-ARRIVING workgroup folding (one ticket per workgroup; the
+    tools build's KARMA_SEGMENT_ONCE=2): sizes at the thresholds and unaligned, repeated calls
+    (the ticket counter is reset by each call's folder), 4 streams launched with no
+    synchronisation, and a graph captured once and replayed with new bytes."""
+    monkeypatch.setenv("KARMA_SEGMENT_ONCE", "2")
+    n = (64 << 20) + 256
+    buf = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    K.fill_splitmix64(buf, 57)
+    host = buf[:n].cpu().numpy()
+    with _lib.using(_lib.AB_LIB_PATH) as L:
+        for init in (0, 0x1F2E3D4C):
+            for off, m in [(0, 256 << 10), (5, (256 << 10) + 1), (3, (1 << 20) + 17), (0, 64 << 20), (1, (64 << 20) - 1),
+                           (77, (32 << 20) - 77)]:
+                for _ in range(2):
+                    got = int(K.extend_stream(init, buf[off: off + m]).item())
+                    assert got == oracle_lib.extend(init, host[off: off + m].tobytes()), (hex(init), off, m)
+        seg = 64 << 20
+        want = oracle_lib.splitmix_fixed_crcs(57, seg, 0, 4, threads=16)
+        streams = [torch.cuda.Stream() for _ in range(4)]
+        outs = [torch.full((4,), -1, dtype=torch.int32, device=dev) for _ in range(4)]
+        torch.cuda.synchronize()
+        for i in range(8):
+            for k, st in enumerate(streams):
+                j = (i + k) % 4
+                _lib.check("stream", L.karma_crc32c_stream(0, buf.data_ptr() + j * seg, seg,
+                                                           outs[k].data_ptr() + 4 * j, st.cuda_stream))
+        torch.cuda.synchronize()
+        for k in range(4):
+            _eq(outs[k].cpu().numpy().view(np.uint32), want)
+        s = torch.cuda.Stream()
+        part = buf[:seg]
+        o1 = torch.empty(1, dtype=torch.uint32, device=dev)
+        with torch.cuda.stream(s):
+            K.extend_stream(0, part, out=o1, stream=s)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            K.extend_stream(0, part, out=o1, stream=s)
+        for seed in (8, 9):
+            torch.cuda.synchronize()
+            K.fill_splitmix64(part, seed)
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            assert int(o1.item()) == int(oracle_lib.splitmix_fixed_crcs(seed, seg, 0, 1, threads=16)[0])
+        for st in streams + [s]:
+            assert L.karma_crc32c_release_stream(-1, st.cuda_stream) == 0
+
+
 def test_config2_full_1m_x_4k(dev):
     n, rec = 1 << 20, 4096
     buf = torch.empty(n * rec, dtype=torch.uint8, device=dev)

@@ -32,13 +32,15 @@ def main():
     p.add_argument("--json", default="")
     p.add_argument("--libs", default="", help="name=path,... : builds compared at their defaults "
                    "(instead of the tools build's KARMA_SEGMENT_ONCE=1 / 0)")
+    p.add_argument("--variants", default="1,0", help="KARMA_SEGMENT_ONCE values of the tools build (1 = the grid's "
+                   "last workgroup folds, 2 = the last-arriving one, 0 = the looping fused kernel)")
     a = p.parse_args()
     dev = torch.device("cuda:0")
     nseg, top = 64, 64 << 20
     arena = torch.empty(nseg * top, dtype=torch.uint8, device=dev)
     K.fill_splitmix64(arena, 42)
     sh = torch.cuda.current_stream().cuda_stream
-    V = ["1", "0"]
+    V = a.variants.split(",")
     libs = {}
     for item in filter(None, a.libs.split(",")):
         name, _, path = item.partition("=")
