@@ -26,7 +26,7 @@ KB_SITES = {1: "WAL image byte outside the image", 2: "WAL image byte outside th
             3: "candidate slot outside the segment's lists", 4: "candidate write dropped by the cap guard",
             5: "sub-range report index", 6: "span index", 7: "segment meta index", 8: "gathered list index",
             9: "gathered slot outside its sub-range", 10: "record byte outside the arena allocation",
-            11: "ragged unit slot >= unit_cap", 12: "byte-grid tile or record index out of range"}
+            11: "ragged unit slot >= unit_cap"}
 
 KARMA_OK = 0
 KARMA_E_INVALID = -1

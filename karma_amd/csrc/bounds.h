@@ -38,7 +38,6 @@ enum KbSite : unsigned {
     kKbRunSlot = 9,      // a gathered slot outside its sub-range's slots
     kKbArena = 10,       // record byte load outside the arena's allocation
     kKbUnit = 11,        // ragged unit descriptor / partial slot >= unit_cap
-    kKbGrid = 12,        // byte-grid tile word / state index >= tile_cap, record index >= n_rec
 };
 
 // Host side: each .hip file's report (KB_DEFINE_COLLECT), read and optionally cleared.

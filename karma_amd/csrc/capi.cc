@@ -69,7 +69,6 @@ struct DevState {
     uint32_t* blob = nullptr;       // the streaming kernels' tables (stride 128)
     uint32_t* lane_blob = nullptr;  // the LDS-staged kernel's tables (stride 16: one record per lane)
     uint32_t* quad_blob = nullptr;  // k_ragged_direct4's tables (stride 64)
-    uint32_t* gcomb = nullptr;      // the ragged byte grid's combine blob (build_grid_comb_blob)
     std::map<uint64_t, uint32_t*> comb;  // unit bytes -> combine blob
     std::map<std::pair<uint64_t, uint64_t>, uint32_t*> bcomb;  // (unit bytes, states per thread) -> block blob
 };
@@ -170,12 +169,6 @@ int dev_state(int dev, DevState** out) {
         build_lane_blob(host.data());
         KARMA_HIP(hipMalloc(&d.lane_blob, kBlobWords * sizeof(uint32_t)));
         KARMA_HIP(hipMemcpy(d.lane_blob, host.data(), kBlobWords * sizeof(uint32_t), hipMemcpyHostToDevice));
-        if (KARMA_GRID) {
-            std::vector<uint32_t> g(kGridCombWords);
-            build_grid_comb_blob(g.data());
-            KARMA_HIP(hipMalloc(&d.gcomb, kGridCombWords * sizeof(uint32_t)));
-            KARMA_HIP(hipMemcpy(d.gcomb, g.data(), kGridCombWords * sizeof(uint32_t), hipMemcpyHostToDevice));
-        }
         d.ready = true;
     }
     *out = &d;
@@ -320,18 +313,8 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
     a.fctl = nullptr;
     a.block_blob = nullptr;
     a.comb_m = 0;
-    a.dyn_ctl = nullptr;
-    a.dyn_shift = 0;
     if (fold_k) {
         KARMA_RC(comb_blob(ds, unit, &a.comb_maps));
-        // the dynamic tail's counter: word 0 of the stream's fused words (the fused fold and the
-        // segment kernel leave it unused)
-        if (const long sh = KARMA_AB_KNOB("KARMA_FIXED_DYN", KARMA_FIXED_DYN_SHIFT); sh > 0) {
-            unsigned long long* w = nullptr;
-            KARMA_RC(fused_words(dev, s, &w));
-            a.dyn_ctl = w;
-            a.dyn_shift = (uint32_t)std::min(sh, 16l);
-        }
         // (the tools build's KARMA_FIXED_GRID_MULT: that many workgroups per CU, dispatched in
         // rounds, so the hardware hands the later ones to the CUs that finish first)
         const long gm = KARMA_AB_KNOB("KARMA_FIXED_GRID_MULT", 1);
@@ -409,17 +392,11 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 }
 
 // ---- ragged records -------------------------------------------------------
-#ifdef KARMA_AB
-thread_local RaggedArgs t_last_ragged{};  // karma_ab_ragged_took_grid (tools build)
-#endif
-
 struct RaggedLayout {
-    size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off;
-    size_t grec_off, gtile_off, gstate_off, gend_off, gflag_off, gctl_off, total;
+    size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off, total;
 };
 
-// tile_cap: tiles of the byte grid (0: no grid arrays).
-RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap, uint64_t tile_cap = 0) {
+RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     RaggedLayout L;
     const uint64_t nb = ragged_scan_blocks(n_rec);
     L.fbase_off = 0;
@@ -428,33 +405,8 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap, uint64_t tile_cap = 0) 
     L.psums_off = L.sums_off + align256(nb * sizeof(uint64_t));
     L.desc_off = L.psums_off + align256(nb * sizeof(uint64_t));
     L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
-    L.grec_off = L.part_off + align256(cap * sizeof(uint32_t));
-    const uint64_t gn = tile_cap ? n_rec : 0;
-    L.gtile_off = L.grec_off + align256(gn * sizeof(GridRec));
-    L.gstate_off = L.gtile_off + align256(tile_cap * sizeof(uint32_t));
-    L.gend_off = L.gstate_off + align256(tile_cap * sizeof(uint32_t));
-    L.gflag_off = L.gend_off + align256(gn * sizeof(uint32_t));
-    L.gctl_off = L.gflag_off + align256((tile_cap ? nb : 0) * sizeof(uint32_t));
-    L.total = L.gctl_off + align256(tile_cap ? 4 * sizeof(unsigned long long) : 0);
+    L.total = L.part_off + align256(cap * sizeof(uint32_t));
     return L;
-}
-
-// Tiles the byte grid may stream for a batch of n records, total_len bytes: a span of up to twice
-// the records' bytes plus 64 bytes per record for the headers and gaps between them, and the
-// partial tiles at both ends.  A batch spread wider takes the unit plan (k_ragged_grid_plan
-// checks it): the grid reads every byte of the span, the unit plan costs per record.
-uint64_t grid_tile_cap(uint64_t total_len, uint64_t n_rec) { return ceil_div(2 * total_len + 64 * n_rec, kGridTile) + 2; }
-
-void bind_grid(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t tile_cap, const uint32_t* gcomb) {
-    char* b = static_cast<char*>(ws);
-    a.tile_cap = tile_cap;
-    a.grec = reinterpret_cast<GridRec*>(b + L.grec_off);
-    a.gtile = reinterpret_cast<uint32_t*>(b + L.gtile_off);
-    a.gstate = reinterpret_cast<uint32_t*>(b + L.gstate_off);
-    a.gend = reinterpret_cast<uint32_t*>(b + L.gend_off);
-    a.gflag = reinterpret_cast<uint32_t*>(b + L.gflag_off);
-    a.gctl = reinterpret_cast<unsigned long long*>(b + L.gctl_off);
-    a.gcomb_blob = gcomb;
 }
 
 void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
@@ -507,14 +459,9 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
     if (total_len > 0) {
         cap_full = std::max<uint64_t>(1, ceil_div(total_len, kDefaultUnit));
         cap = cap_full + 2 * n_rec;
-        // the byte grid is tried first when the batch may be sorted (the tools build's
-        // KARMA_RAGGED_GRID=0 turns it off for A/B)
-        const uint64_t tile_cap =
-            KARMA_GRID && n_rec < (1ull << 31) && KARMA_AB_KNOB("KARMA_RAGGED_GRID", 1) ? grid_tile_cap(total_len, n_rec) : 0;
-        const RaggedLayout L = ragged_layout(n_rec, cap, tile_cap);
+        const RaggedLayout L = ragged_layout(n_rec, cap);
         KARMA_RC(workspace(dev, s, L.total, &ws));
         bind_ragged(a, ws, L, cap);
-        if (tile_cap) bind_grid(a, ws, L, tile_cap, ds.gcomb);
     } else {
         // Unknown total: count the units (k_ragged_scan), read the block totals back and size
         // the unit table.
@@ -542,30 +489,8 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
     a.part_base = cap_full;
     KARMA_RC(bind_lookback(dev, s, ragged_scan_blocks(n_rec), a));
     KARMA_HIP(launch_ragged_main(a, ds.cu, s));
-#ifdef KARMA_AB
-    t_last_ragged = a;
-#endif
     return 0;
 }
-
-#ifdef KARMA_AB
-}  // namespace
-// Tools build only: which path this thread's last ragged call took (the byte grid or the unit
-// plan), read from the grid plan's per-block flags after a device sync.
-extern "C" int karma_ab_ragged_took_grid(int* out) {
-    const RaggedArgs& a = t_last_ragged;
-    *out = 0;
-    if (!a.tile_cap) return 0;
-    KARMA_HIP(hipDeviceSynchronize());
-    std::vector<uint32_t> f(ragged_scan_blocks(a.n_rec));
-    KARMA_HIP(hipMemcpy(f.data(), a.gflag, f.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    *out = 1;
-    for (uint32_t x : f)
-        if (x) *out = 0;
-    return 0;
-}
-namespace {
-#endif
 
 struct Locked {
     std::lock_guard<std::mutex> lk{g_mu};

@@ -122,48 +122,6 @@ __device__ void fused_record_fold(const FixedArgs& A, uint32_t* lds, uint32_t* w
     }
 }
 
-// The fixed kernel's dynamic tail measured no gain (1M x 4 KiB 0.6041 vs 0.6023 ms, 256K x 16 KiB
-// 0.6224 vs 0.6144: profiles/r04_fixed_dyn_tail_ab.txt), so only the tools build and the fdyn
-// builds compile it.
-#if defined(KARMA_AB) || KARMA_FIXED_DYN_SHIFT > 0
-constexpr bool kFixedDynBuilt = true;
-#else
-constexpr bool kFixedDynBuilt = false;
-#endif
-
-// The dynamic tail's k-th step of this workgroup (k_units_fixed): chunks of kFixedDynChunk steps,
-// one global atomic each, taken by the wave that draws a chunk's first index; the chunk's other
-// waves read its base from an LDS ring slot tagged with the chunk.  A slot is reused for chunk
-// c + R only after all kFixedDynChunk - 1 readers of chunk c counted themselves out (every reader
-// holds an index drawn before the reusing grabber's, and chunk c's grabber never waits on a
-// later chunk: progress by induction from the first R chunks).  Lane 0 spins; the wave's result
-// is uniform.
-__device__ __forceinline__ uint64_t fixed_dyn_step(const FixedArgs& A, uint32_t k, uint64_t S, uint64_t nws,
-                                                   uint32_t lane, unsigned long long* slot, uint32_t* ack) {
-    const uint32_t c = k / kFixedDynChunk, j = k % kFixedDynChunk, r = c % kFixedDynRing;
-    uint32_t base = 0;
-    if (lane == 0) {
-        if (j == 0) {
-            if (c >= kFixedDynRing)
-                while (__hip_atomic_load(&ack[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != kFixedDynChunk - 1)
-                    __builtin_amdgcn_s_sleep(1);
-            __hip_atomic_store(&ack[r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            base = (uint32_t)atomicAdd(A.dyn_ctl, (unsigned long long)kFixedDynChunk);
-            __hip_atomic_store(&slot[r], ((unsigned long long)(c + 1) << 32) | base, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-            unsigned long long v;
-            while (((v = __hip_atomic_load(&slot[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 32) != c + 1)
-                __builtin_amdgcn_s_sleep(1);
-            base = (uint32_t)v;
-            __hip_atomic_fetch_add(&ack[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    }
-    base = __builtin_amdgcn_readfirstlane(__shfl((int)base, 0));
-    const uint64_t st = S + base + j;
-    return st < nws ? st : nws;
-}
-
 template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0, bool BAL = true, int KW = 1, bool FUSE = false>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     static_assert(!FUSE || WAVE_COMB, "the fused combine folds wave states");
@@ -173,10 +131,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kMaps ? kLdsWordsComb : kLdsWords];
     __shared__ uint32_t blk_next;  // BAL: the block's next wave-step (an LDS counter, lgkmcnt only)
     __shared__ uint32_t s_tag;  // FUSE: this call's tag
-    // dynamic tail: chunk c's base in ring slot c % R, tagged (c + 1) << 32; the slot's readers count
-    // themselves in dyn_ack, and chunk c + R's grabber waits for all of them before reusing it
-    __shared__ unsigned long long dyn_slot[kFixedDynRing];
-    __shared__ uint32_t dyn_ack[kFixedDynRing];
     if (FUSE && threadIdx.x == 0) {
         const uint32_t t = (uint32_t)__hip_atomic_load(A.fctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
         s_tag = t ? t : 1u;
@@ -198,22 +152,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
     const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
     if (BAL && threadIdx.x == 0) blk_next = kWavesPerBlock;  // steps 0..15 go to waves 0..15
-    // Dynamic tail (BAL, not FUSE): static shares cover steps [0, S); the last D = nws - S go to the
-    // workgroups that ask first, kFixedDynChunk per global atomic (one wave grabs, its siblings read
-    // the base from LDS): per-CU speed differences otherwise leave the last static steps on a few
-    // CUs (DESIGN.md §4 "The dynamic tail").
-    constexpr bool kDyn = kFixedDynBuilt && BAL && !FUSE;
-    uint64_t S = nws;
-    if (kDyn && A.dyn_ctl && A.dyn_shift) {  // (whole rounds: a block's static share ends at nidx)
-        const uint64_t d = min(nws >> A.dyn_shift, (uint64_t)kFixedDynMaxSteps);
-        const uint64_t s = (nws - d) / nwaves * nwaves;
-        S = s >= nwaves ? s : nws;
-    }
-    const bool dyn = kDyn && S < nws;
-    if (kDyn && threadIdx.x < kFixedDynRing) {
-        dyn_slot[threadIdx.x] = 0;
-        dyn_ack[threadIdx.x] = 0;
-    }
+    // (a dynamic tail -- the last steps taken from a global counter -- measured no gain here:
+    // 1M x 4 KiB 0.6041 vs 0.6023 ms, 256K x 16 KiB 0.6224 vs 0.6144, profiles/r04_fixed_dyn_tail_ab.txt)
+    const uint64_t S = nws;
     const uint32_t nidx = (uint32_t)((S + nwaves - 1) / nwaves) * kWavesPerBlock;
     // unit u's head block and init value, then its chunk loads, then the tables
     FixedPlan P = fixed_plan(A, u, U, l);
@@ -243,8 +184,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
                 if (lane == 0) i = atomicAdd(&blk_next, 1u);
                 i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
                 wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
-                if (dyn && i >= nidx)  // the static share is done: the dynamic tail
-                    wb_next = fixed_dyn_step(A, i - nidx, S, nws, lane, dyn_slot, dyn_ack);
             }
             N = fixed_plan(A, wb_next * kGroupsPerWave + grp, U, l);
             hv = ld16(N.hblk);
@@ -295,14 +234,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
         u = wb * kGroupsPerWave + grp;
     }
     WLOG_END(wlog_id);
-    if (dyn) {  // every step of this workgroup taken: count it out; the last one clears the word
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned long long old = atomicAdd(A.dyn_ctl, 1ull << 32);
-            if ((uint32_t)(old >> 32) + 1u == gridDim.x)
-                __hip_atomic_store(A.dyn_ctl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
     if constexpr (FUSE) {  // the grid's last workgroup folds the record's wave states
         // (no completion counter: 256 workgroups' atomics on one word serialise at the memory
         // side; the fold waits on each state's tag instead.  Every workgroup reads the tag at

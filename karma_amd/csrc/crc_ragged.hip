@@ -33,9 +33,6 @@ using namespace dev;
 constexpr int kRaggedPF = 4;       // chunk loads in flight per lane: the small-record kernel
 constexpr int kRaggedUnitsPF = 6;  // ... and the units kernel (k_units_ragged)
 constexpr bool kRaggedNT = true;
-#ifndef KARMA_GRID_TIMING
-#define KARMA_GRID_TIMING 0  // timing builds of the byte grid (Makefile `timing`): wrong CRCs
-#endif
 // A ragged record's unaligned head bytes are stepped by the plan (the entering register goes
 // into the first unit's descriptor), its tail bytes by finalize.  Stepping both edges in the
 // units kernel from the lines it loads anyway saved the plan and finalize 15 us of scattered
@@ -187,17 +184,6 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
     }
 }
 
-// The plan's verdict, read by every kernel after it: true when every block of the grid plan found
-// its records sorted, non-overlapping, with gaps <= kGridMaxGap and the tiles within tile_cap.
-// Every thread of the block calls this (a block-wide OR).
-__device__ __forceinline__ bool grid_on(const RaggedArgs& A) {
-    if (!KARMA_GRID || !A.tile_cap) return false;
-    const uint64_t nb = (A.n_rec + kScanBlock - 1) / kScanBlock;
-    int bad = 0;
-    for (uint64_t i = threadIdx.x; i < nb; i += blockDim.x) bad |= (int)A.gflag[i];
-    return !__syncthreads_or(bad);
-}
-
 // ---- the single-pass plan ----------------------------------------------------
 // Block status words for the decoupled look-back (RaggedArgs::lb): seq << 42 | flag << 40 |
 // value.  The words are read and written with agent-scope atomics (cache-coherent across
@@ -319,7 +305,6 @@ __device__ void lookback_retire(const RaggedArgs& A) {
 // streams 3 % faster on configs[2] than block-interleaved runs).  Replaces round 1's
 // k_ragged_scan + k_ragged_desc: one launch, and no block reads every other block's totals.
 __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
-    if (grid_on(A)) return;  // the batch takes the byte grid (k_ragged_grid_plan planned it)
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4, byte table
     __shared__ unsigned long long cnt[kBuckets];
@@ -401,380 +386,6 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
     return UnitDesc{v.x | ((uint64_t)v.y << 32), v.z, v.w};
 }
 
-#if KARMA_GRID  // the byte grid: an experimental build (Makefile `variants`), DESIGN.md §4
-// ---- the byte grid (engine.h; DESIGN.md §4 "The byte grid") ----------------------------------
-// Sorted, non-overlapping records: the bytes they span are cut on the absolute kGridTile grid, one
-// tile per group of 8 lanes, each wave-step 8 consecutive tiles (k_units_fixed's layout).  The
-// algebra is restated lane by lane in tests/grid_model.py and checked against the oracle on the
-// CPU (tests/test_grid_math.py).
-
-// One thread per record (1024 per block): the record's address, length and ~init (grec), the
-// conditions against the record before it, and the tiles whose first reaching record it is --
-// [ceil(e_{r-1} / tile), ceil(e_r / tile)) relative to the first record's tile -- each with the
-// interior flag when the record covers the tile with no edge and no init byte in it.  A wave's
-// records own consecutive tiles: lane i writes tiles i, i + 64, ... of the wave's run and finds
-// its record by a search over the lanes' inclusive tile counts (coalesced, balanced stores).
-// Writes nothing for a wave that breaks a condition (the batch then takes the unit plan).
-__global__ __launch_bounds__(kScanBlock) void k_ragged_grid_plan(RaggedArgs A) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t r = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x;
-    const bool valid = r < A.n_rec;
-    const uint64_t arena = reinterpret_cast<uintptr_t>(A.arena);
-    const uint64_t p0 = arena + A.off[0];
-    const uint64_t tb0 = p0 / kGridTile;
-    uint64_t p = 0, e = 0;
-    if (valid) {
-        p = arena + A.off[r];
-        e = p + A.len[r];
-        const uint32_t init = A.init ? A.init[r] : A.init_scalar;
-        A.grec[r] = GridRec{p, A.len[r], ~init};
-    }
-    uint64_t ep = (uint64_t)__shfl_up((long long)e, 1);  // the previous record's end
-    if (lane == 0 && valid && r > 0) ep = arena + A.off[r - 1] + A.len[r - 1];
-    bool bad = valid && r > 0 && (p < ep || p - ep > kGridMaxGap);
-    const bool wbad = __ballot(bad) != 0;
-    const uint64_t thi = valid ? (e + kGridTile - 1) / kGridTile - tb0 : 0;
-    const uint64_t tlo = r == 0 ? 0 : (ep + kGridTile - 1) / kGridTile - tb0;
-    const uint64_t cnt = valid && !wbad && thi > tlo ? thi - tlo : 0;
-    const uint64_t incl = wave_incl_scan(cnt);
-    const uint64_t tot = __shfl(incl, 63);
-    const uint64_t tw0 = __shfl(tlo, 0);
-    const uint64_t rbase = r - lane;
-    for (uint64_t k = 0; k < tot; k += 64) {  // uniform trip count: shuffles see every lane
-        const uint64_t i = k + lane;
-        int o = 0;  // owner: the first lane whose inclusive count exceeds i
-#pragma unroll
-        for (int s = 32; s > 0; s >>= 1)
-            if (__shfl(incl, o + s - 1) <= i) o += s;
-        o = o < 63 ? o : 63;
-        const uint64_t po = (uint64_t)__shfl((long long)p, o), eo = (uint64_t)__shfl((long long)e, o);
-        const uint64_t t = tw0 + i;
-        const uint64_t ta = (tb0 + t) * kGridTile;
-        const bool inner = po + 4 <= ta && eo > ta + kGridTile;
-        if (i < tot && t < A.tile_cap) A.gtile[t] = (uint32_t)(rbase + o) | (inner ? kGridInterior : 0u);
-    }
-    if (valid && r + 1 == A.n_rec) {  // the last record: the tile count and the end of the bytes read
-        A.gctl[0] = thi;
-        A.gctl[3] = (e + 15) & ~uint64_t(15);
-        if (thi > A.tile_cap) bad = true;
-    }
-    if (r == 0) {
-        A.gctl[1] = tb0 * kGridTile;
-        A.gctl[2] = p0 & ~uint64_t(15);
-    }
-    const int bbad = __syncthreads_or((int)bad);
-    if (threadIdx.x == 0) A.gflag[blockIdx.x] = (uint32_t)bbad;
-}
-
-// x tile-relative, clamped to [-64, tile + 64] (further out it only matters which side it is on).
-__device__ __forceinline__ int32_t grid_rel(uint64_t x, uint64_t ta) {
-    const int64_t d = (int64_t)(x - ta);
-    return d < -64 ? -64 : d > (int64_t)kGridTile + 64 ? (int32_t)kGridTile + 64 : (int32_t)d;
-}
-
-// The window at tile offset w (16 bytes in v) as record [cp, ce) sees it: bytes outside the record
-// zeroed, inj xored into the record's first four bytes (one or two of the window's words; the
-// rest of a split init word lands in the window before, on another lane or another tile).
-__device__ __forceinline__ u32x4 grid_mask(const u32x4& v, int32_t w, int32_t cp, int32_t ce, uint32_t inj) {
-    uint32_t x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int32_t a = w + 4 * k;
-        const int32_t lo = min(max(cp - a, 0), 4), hi = min(max(ce - a, 0), 4);
-        const uint32_t mhi = hi >= 4 ? ~0u : (1u << (8 * hi)) - 1u, mlo = lo >= 4 ? ~0u : (1u << (8 * lo)) - 1u;
-        x[k] &= hi > lo ? (mhi & ~mlo) : 0u;
-        const int32_t d = cp - a;
-        if (d >= 0 && d < 4) x[k] ^= inj << (8 * d);
-        else if (d < 0 && d > -4) x[k] ^= inj >> (-8 * d);
-    }
-    return u32x4{x[0], x[1], x[2], x[3]};
-}
-
-// The group's register: the lane fold (crc32c.cc STEP4W order), the lanes rotated so lane m (the
-// one holding the last window) comes last, and the 8-lane tree.  Valid in group lane 0; every lane
-// of the group calls this.
-__device__ __forceinline__ uint32_t grid_fold(const uint32_t* lds, uint32_t l, uint32_t m, uint32_t a0, uint32_t a1,
-                                              uint32_t a2, uint32_t a3) {
-    uint32_t c = lane_fold(lds, a0, a1, a2, a3);
-    const uint32_t lane = threadIdx.x & 63u;
-    c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + m + 1) & (kGroupLanes - 1))), 64);
-    uint32_t t = __shfl_down(c, 1, kGroupLanes);
-    c = zmap(lds, kLZ16, c) ^ t;
-    t = __shfl_down(c, 2, kGroupLanes);
-    c = zmap(lds, kLZ32, c) ^ t;
-    t = __shfl_down(c, 4, kGroupLanes);
-    c = zmap(lds, kLZ64, c) ^ t;
-    return c;
-}
-
-// The units kernel's grid branch.  Wave-steps come from the block's LDS counter as in
-// k_units_fixed, two ahead: while tile a streams, tile b's chunk loads and its records' GridRec
-// (lane l: record owner + l) are issued before a's last batch is stepped, and tile c's word is
-// loaded, so neither metadata load is waited for.  Chunk addresses are arithmetic, clamped to the
-// bytes the records span (gctl[2], gctl[3]).  Per chunk the group steps its current record's
-// windows (masked at the record's edges) and, when the record's last window lies in the chunk,
-// folds it into gend[r] and moves on to the next record starting in the chunk; at the tile end the
-// record running past it goes to gstate[t].
-template <int PF>
-__device__ void grid_units(const RaggedArgs& A, uint32_t* lds, uint32_t* blk_next) {
-    static_assert(kGridChunks % PF == 0, "whole batches per tile");
-    const uint32_t lane = threadIdx.x & 63u, l = lane & (kGroupLanes - 1), grp = lane / kGroupLanes;
-    const uint32_t gbase = lane & ~(kGroupLanes - 1u), wave = threadIdx.x >> 6;
-    const uint32_t X = lane_const();
-    // (uniform: scalar registers -- every VGPR counts at 1024 threads, and a spill's reload waits
-    // for every load in flight)
-    const uint64_t NT = uniform64(A.gctl[0]), base = uniform64(A.gctl[1]), lo = uniform64(A.gctl[2]),
-                   hi = uniform64(A.gctl[3]);
-    if (NT == 0 || hi < lo + 16) return;  // no byte to read (only empty records)
-    const uint64_t hi16 = hi - 16;
-    const uint64_t nws = (NT + kGroupsPerWave - 1) / kGroupsPerWave;
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint32_t nidx = (uint32_t)((nws + nwaves - 1) / nwaves) * kWavesPerBlock;
-    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
-    auto step_of = [&](uint32_t i) -> uint64_t {
-        return i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
-    };
-    auto take = [&]() -> uint64_t {
-        uint32_t i = 0;
-        if (lane == 0) i = atomicAdd(blk_next, 1u);
-        return step_of(__builtin_amdgcn_readfirstlane(__shfl(i, 0)));
-    };
-    // A wave-step's 8 tiles: a scalar base and this lane's 32-bit offset, clamped to the bytes the
-    // records span [lo, hi) (steps past the last tile read hi - 16).
-    struct Step {
-        const uint8_t* b;
-        uint32_t lo, hi;
-    };
-    constexpr uint32_t kStepBytes = kGroupsPerWave * kGridTile;
-    auto step_win = [&](uint64_t s) -> Step {
-        const uint64_t wb = base + s * kStepBytes;
-        const uint64_t b = wb <= hi16 ? wb : hi16;
-        const uint64_t rh = hi16 - b;
-        return Step{reinterpret_cast<const uint8_t*>((uintptr_t)b), lo > b ? (uint32_t)(lo - b) : 0u,
-                    rh < kStepBytes ? (uint32_t)rh : kStepBytes};
-    };
-    const uint32_t loff = grp * kGridTile + l * 16;
-    auto chunk = [&](const Step& W, uint32_t c) {
-        uint32_t o = loff + c * kChunk;
-        o = o < W.lo ? W.lo : o;
-        o = o > W.hi ? W.hi : o;
-        return W.b + o;
-    };
-    auto tword = [&](uint64_t s) -> uint32_t {
-        const uint64_t t = s * kGroupsPerWave + grp;
-        return *(const __attribute__((address_space(1))) uint32_t*)(A.gtile + (t < NT ? t : NT - 1));
-    };
-    auto rec_meta = [&](uint32_t r0) -> u32x4 {
-        const uint64_t r = (uint64_t)r0 + l;
-        return ldmeta16(A.grec + (r < A.n_rec ? r : A.n_rec - 1));
-    };
-    uint64_t sa = step_of(wave), sb = take();
-    uint32_t twa = tword(sa);
-    u32x4 mva = rec_meta(twa & ~kGridInterior);
-    u32x4 nb[PF];
-    {
-        const Step W = step_win(sa);
-#pragma unroll
-        for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(W, q));
-    }
-    load_stream_tables(lds, A.blob);
-    __syncthreads();
-    while (sa < nws) {
-        const uint64_t t = sa * kGroupsPerWave + grp;
-        const Step Wa = step_win(sa);
-        // tile b's word, used at this tile's last batch (issued here, not one tile earlier: a
-        // loop-carried copy of a register still being loaded would wait for every load in flight)
-        const uint32_t twb = tword(sb);
-        const bool tvalid = t < NT;
-        const uint64_t ta = base + t * kGridTile;
-        // the tile's record list: lane l holds record r0 + l
-        uint32_t r0 = twa & ~kGridInterior;
-        int32_t lp, le;
-        uint32_t linj, gm;
-        bool more;
-        auto fill = [&](const u32x4& mv) {
-            const uint64_t p = mv.x | ((uint64_t)mv.y << 32);
-            const bool in_tile = tvalid && (uint64_t)r0 + l < A.n_rec && p < ta + kGridTile;
-            lp = grid_rel(p, ta);
-            le = grid_rel(p + mv.z, ta);
-            linj = mv.w;
-            gm = (uint32_t)(__ballot(in_tile && mv.z >= 4) >> gbase) & 0xffu;
-            more = ((__ballot(in_tile) >> (gbase + kGroupLanes - 1)) & 1u) != 0;
-        };
-        if (twa & kGridInterior) {  // one record covers the tile: no edge, no init byte
-            lp = -64;
-            le = (int32_t)kGridTile + 64;
-            linj = 0;
-            gm = tvalid ? 1u : 0u;
-            more = false;
-        } else {
-            fill(mva);
-        }
-        // the group's current record (j in the list; replicated in the group's lanes)
-        uint32_t j = 0, cinj = 0, cr = 0;
-        int32_t cp = 0, ce = 0;
-        bool active = false;
-        auto pick = [&](uint32_t from) {  // the first record of the list at or after `from` with >= 4 bytes
-            uint32_t m = from < kGroupLanes ? gm & ~((1u << from) - 1u) : 0u;
-            while (m == 0 && more) {  // more records start in the tile than the list holds (rare)
-                r0 += kGroupLanes;
-                fill(rec_meta(r0));
-                m = gm;
-            }
-            active = m != 0;
-            if (active) {
-                j = (uint32_t)__builtin_ctz(m);
-                cp = __shfl(lp, (int)(gbase + j));
-                ce = __shfl(le, (int)(gbase + j));
-                cinj = __shfl(linj, (int)(gbase + j));
-                cr = r0 + j;
-            }
-        };
-        pick(0);
-        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-        // this lane's window of chunk c as the current record sees it (windows past its end or
-        // wholly before its start are not stepped; masks only at its edges)
-        auto step_cur = [&](int32_t w, const u32x4& v) {
-            if (w < ((ce + 15) & ~15) && w + 16 > cp) {
-                u32x4 x = v;
-                if (w < cp + 4 || w + 16 > ce) x = grid_mask(v, w, cp, ce, cinj);
-                step4(lds, X, a0, a1, a2, a3, x);
-            }
-        };
-        auto process = [&](uint32_t c, const u32x4& v) {
-            if (!active) return;
-            const int32_t w = (int32_t)(c * kChunk + l * 16), cnext = (int32_t)((c + 1) * kChunk);
-            step_cur(w, v);
-            // the record's last window is in this chunk: its register, then the records starting
-            // in the same chunk (the rare path: most chunks hold no record end)
-            while (((ce + 15) & ~15) <= cnext) {
-                const uint32_t R = grid_fold(lds, l, ((uint32_t)(((ce + 15) & ~15) - 16) >> 4) & (kGroupLanes - 1),
-                                             a0, a1, a2, a3);
-                if (l == 0) KB_WRITE(A.gend, cr, A.n_rec, kKbGrid, R);
-                a0 = a1 = a2 = a3 = 0;
-                pick(j + 1);
-                if (!active || cp >= cnext) break;  // no record, or the next starts in a later chunk
-                step_cur(w, v);
-            }
-        };
-        uint64_t sc = nws;
-        u32x4 mvb = mva;
-#pragma unroll 1
-        for (uint32_t k = 0; k < kGridChunks / PF; ++k) {
-            u32x4 cur[PF];
-#pragma unroll
-            for (int q = 0; q < PF; ++q) cur[q] = nb[q];
-            if (k + 1 < kGridChunks / PF) {
-#pragma unroll
-                for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(Wa, (k + 1) * PF + q));
-            } else {  // tile b's metadata and first loads, tile c's word
-                sc = take();
-                uint32_t tw = twb;
-                asm volatile("" : "+v"(tw));  // its use stays here (hoisted, it waits for the chunk loads)
-                mvb = rec_meta(tw & ~kGridInterior);
-                const Step Wb = step_win(sb);
-#pragma unroll
-                for (int q = 0; q < PF; ++q) nb[q] = ldg<kRaggedNT>(chunk(Wb, q));
-            }
-#if KARMA_GRID_TIMING == 1  // timing builds only (wrong CRCs): the loads alone
-#pragma unroll
-            for (int q = 0; q < PF; ++q) {
-                a0 ^= cur[q].x;
-                a1 ^= cur[q].y;
-                a2 ^= cur[q].z;
-                a3 ^= cur[q].w;
-            }
-#elif KARMA_GRID_TIMING == 2  // ... every window stepped, no record logic
-#pragma unroll
-            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
-#else
-#pragma unroll
-            for (int q = 0; q < PF; ++q) process(k * PF + q, cur[q]);
-#endif
-        }
-#if KARMA_GRID_TIMING
-        if (l == 0 && t < NT) A.gstate[t] = a0 ^ a1 ^ a2 ^ a3;  // (keeps the work)
-        a0 = a1 = a2 = a3 = 0;
-        (void)active;
-#else
-        if (active && ce > (int32_t)kGridTile) {  // the record running past the tile's end
-            const uint32_t R = grid_fold(lds, l, kGroupLanes - 1, a0, a1, a2, a3);
-            if (l == 0) KB_WRITE(A.gstate, t, A.tile_cap, kKbGrid, R);
-        }
-#endif
-        sa = sb;
-        sb = sc;
-        twa = twb;
-        mva = mvb;
-    }
-}
-
-// The finalize kernel's grid branch (lds: the grid's combine blob), one lane per record: Horner
-// over the record's tiles (Z_tile between tile ends, Z_{its last piece} before gend), then
-// Z_{-16} Z_{16 - s} back over the s zero bytes between its end and its end rounded up to 16.
-// Records spanning more than 64 tiles are folded by the whole wave (the 64-lane tree, Z_{64 tile}
-// per block of 64 states).  Records of fewer than 4 bytes are stepped here, byte by byte.
-__device__ void grid_finalize(const RaggedArgs& A, const uint32_t* lds) {
-    const uint64_t base = A.gctl[1];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t r0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; r0 < A.n_rec;
-         r0 += nwaves * 64) {
-        const uint64_t r = r0 + lane;
-        const bool valid = r < A.n_rec;
-        u32x4 g = {0u, 0u, 0u, 0u};
-        if (valid) g = ldmeta16(A.grec + r);
-        const uint64_t p = g.x | ((uint64_t)g.y << 32), e = p + g.z;
-        const bool gridded = valid && g.z >= 4;
-        const uint64_t E = (e + 15) & ~uint64_t(15);
-        const uint64_t t0 = gridded ? ((p & ~uint64_t(15)) - base) / kGridTile : 0;
-        const uint64_t t1 = gridded ? (E - 1 - base) / kGridTile : 0;
-        uint32_t acc = 0;
-        const bool huge = gridded && t1 - t0 > 64;
-        if (gridded && !huge && t1 > t0) {
-            acc = A.gstate[t0];
-            for (uint64_t t = t0 + 1; t < t1; t += 8) {  // Z_tile steps, 8 loads in flight
-                uint32_t s[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) s[q] = t + q < t1 ? A.gstate[t + q] : 0u;
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (t + q < t1) acc = zmap(lds, 0, acc) ^ s[q];
-            }
-        }
-        uint64_t hm = __ballot(huge);
-        while (hm) {
-            const int h = __ffsll((long long)hm) - 1;
-            hm &= hm - 1;
-            const uint64_t ht0 = __shfl(t0, h), hk = __shfl(t1, h) - ht0;  // states t0 .. t1 - 1
-            const uint64_t nb = (hk + 63) / 64;
-            const int64_t pad = (int64_t)(nb * 64 - hk);
-            uint32_t w = 0;
-            for (uint64_t blk = 0; blk < nb; ++blk) {
-                const int64_t idx = (int64_t)(blk * 64 + lane) - pad;
-                uint32_t v = idx >= 0 ? A.gstate[ht0 + idx] : 0u;
-                v = wave_tree(lds, v);
-                w = zmap(lds, 6 * 1024, w) ^ v;
-            }
-            w = __shfl(w, 0);
-            if ((int)lane == h) acc = w;
-        }
-        if (!valid) continue;
-        uint32_t res;
-        if (gridded) {
-            const uint32_t ge = A.gend[r];
-            acc = t1 > t0 ? zshift16(lds, acc, (uint32_t)((E - (base + t1 * kGridTile)) / 16)) ^ ge : ge;
-            const uint32_t s = (uint32_t)(E - e);
-            if (s) acc = zmap(lds, kGridCombInv16, steps_in_vec(lds, kCombZ4, kCombT8, acc, u32x4{0u, 0u, 0u, 0u}, 0u, 16u - s));
-            res = ~acc;
-        } else {
-            res = short_record(lds, kCombZ4, kCombT8, reinterpret_cast<const uint8_t*>((uintptr_t)p), g.z, ~g.w);
-        }
-        A.out[r] = res;
-    }
-}
-
-#endif  // KARMA_GRID
 
 // The units kernel: each unit's loads are issued when the unit starts (group_unit), the
 // next descriptor is in flight meanwhile.  (A software-pipelined form, stream_unit's, measured
@@ -792,12 +403,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     __shared__ uint32_t blk_dyn[kDynChunks];  // dynamic tail: base of the block's c-th chunk of 16 steps
     if (threadIdx.x == 0) blk_next = kWavesPerBlock;
     for (uint32_t c = threadIdx.x; c < kDynChunks; c += blockDim.x) blk_dyn[c] = ~0u;
-#if KARMA_GRID
-    if (grid_on(A)) {  // (its barrier also publishes blk_next)
-        grid_units<kRaggedPF>(A, lds, &blk_next);
-        return;
-    }
-#endif
     load_stream_tables(lds, A.blob);
     __syncthreads();
     WLOG_DECL;
@@ -887,17 +492,7 @@ __device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, 
 // than 64 units: the whole wave folds all but the last unit with the 64-lane tree.
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
-#if KARMA_GRID
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kGridCombWords];
-    if (grid_on(A)) {  // (the unit plan did not run: nothing to retire)
-        load_comb_tables<kGridCombWords, 1024>(lds, A.gcomb_blob);
-        __syncthreads();
-        grid_finalize(A, lds);
-        return;
-    }
-#else
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombWords];
-#endif
     if (A.lb) lookback_retire(A);
     load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
     __syncthreads();
@@ -1244,15 +839,6 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     if (a.n_rec == 0) return hipSuccess;
     if (!a.lb || !a.lb_ctl || a.lb_seq_max < 2 || a.lb_seq_max > (1u << 22)) return hipErrorInvalidValue;
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
-    if (a.tile_cap) {
-#if KARMA_GRID
-        if (!a.grec || !a.gtile || !a.gstate || !a.gend || !a.gflag || !a.gctl || !a.gcomb_blob || a.n_rec >= (1ull << 31))
-            return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_ragged_grid_plan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
-#else
-        return hipErrorInvalidValue;  // a library built without the byte grid
-#endif
-    }
     hipLaunchKernelGGL(k_ragged_plan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     units_timer_begin(s);
     hipLaunchKernelGGL(k_units_ragged<>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);

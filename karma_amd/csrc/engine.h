@@ -45,16 +45,6 @@ constexpr int kCombZ4 = kCombMaps * 1024;
 constexpr int kCombT8 = kCombZ4 + 1024;
 constexpr int kCombCoreWords = kCombT8 + 256;  // what the fixed combine and the head steps need
 constexpr int kCombSmall = kCombT8 + 1024;
-// The ragged byte grid (DESIGN.md §4 "The byte grid"): measured slower than the unit plan on every
-// layout (configs[2] units 0.70-0.73 vs 0.80 of 8 TB/s), so the shipped library leaves it out; the
-// tools build and the `variants` builds carry it.
-#ifndef KARMA_GRID
-#ifdef KARMA_AB
-#define KARMA_GRID 1
-#else
-#define KARMA_GRID 0
-#endif
-#endif
 #ifndef KARMA_RAGGED_DYN_SHIFT
 #define KARMA_RAGGED_DYN_SHIFT 3  // RaggedArgs::dyn_shift (a build-time A/B knob; the tools build's KARMA_RAGGED_DYN)
 #endif
@@ -63,14 +53,10 @@ constexpr int kCombSmall = kCombT8 + 1024;
 // kDynChunks LDS words, enough for every chunk (the static part ends on a whole round, up to
 // nwaves steps earlier than nws - kDynMaxSteps).
 constexpr uint32_t kDynMaxSteps = 8192, kDynChunks = 1024;
-#ifndef KARMA_GRID_TILE
-#define KARMA_GRID_TILE 2048  // a build-time A/B knob
-#endif
-constexpr int kCombSmallMaps = (KARMA_GRID_TILE > 4096 || KARMA_RAGGED_UNIT > 8192) ? 10 : 9;  // Z_16n, n < 2^maps (>= a grid tile / 16, a ragged unit / 16)
+constexpr int kCombSmallMaps = KARMA_RAGGED_UNIT > 8192 ? 10 : 9;  // Z_16n, n < 2^maps (>= a ragged unit / 16)
 // (a partial last unit is shorter than the unit: n = its length / 16 < unit / 16)
-static_assert((16ull << kCombSmallMaps) >= (unsigned long long)KARMA_RAGGED_UNIT &&
-                  (16ull << kCombSmallMaps) >= (unsigned long long)KARMA_GRID_TILE,
-              "finalize's last-unit maps Z_16n must reach a whole unit / tile");
+static_assert((16ull << kCombSmallMaps) >= (unsigned long long)KARMA_RAGGED_UNIT,
+              "finalize's last-unit maps Z_16n must reach a whole unit");
 constexpr int kCombWords = kCombSmall + kCombSmallMaps * 1024;
 
 // ---- table blob of the one-block combine (k_combine_block) -----------------
@@ -118,17 +104,7 @@ struct FixedArgs {
     unsigned long long* fctl;
     const uint32_t* block_blob; // kBlockCombWords (block_comb_blob for D = 8 units, m states per thread)
     uint64_t comb_m;            // states per thread of the fused fold
-    // Dynamic tail (not with the fused fold): the last min(nws >> dyn_shift, kFixedDynMaxSteps)
-    // wave-steps are taken kFixedDynChunk at a time per workgroup from dyn_ctl[0] (low 32 bits;
-    // the high 32 count the workgroups that finished: the last one zeroes the word for the next
-    // call on the stream).  dyn_shift 0 or dyn_ctl nullptr: static shares only.
-    unsigned long long* dyn_ctl;
-    uint32_t dyn_shift;
 };
-constexpr uint32_t kFixedDynChunk = 64, kFixedDynMaxSteps = 16384, kFixedDynRing = 4;
-#ifndef KARMA_FIXED_DYN_SHIFT
-#define KARMA_FIXED_DYN_SHIFT 0  // FixedArgs::dyn_shift (a build-time A/B knob; the tools build's KARMA_FIXED_DYN)
-#endif
 
 // One unit of a ragged batch: the 16-aligned span [us, us + span) of a record body; inj is
 // xored into the span's first word: for the record's first unit the register entering the
@@ -139,35 +115,6 @@ struct UnitDesc {
     uint32_t inj;
 };
 static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
-
-// ---- ragged batches on the byte grid (DESIGN.md §4 "The byte grid") ----------
-// When a batch's records are sorted by address and do not overlap (every WAL, segment and KFP
-// batch), the bytes they span are cut on the absolute kGridTile grid instead: one tile per
-// group of 8 lanes, every wave-step 8 consecutive tiles, as k_units_fixed cuts 1M x 4 KiB
-// records.  A record's bytes are read in aligned 16-byte windows with the bytes outside the
-// record masked to zero and ~init xored into its first four bytes (a zero prefix leaves the
-// register at zero), so no head or tail byte is stepped on its own; a tile emits one register
-// per record that ends in it (gend) and one for the record that runs past its end (gstate).
-
-constexpr uint32_t kGridTile = KARMA_GRID_TILE;
-constexpr uint32_t kGridChunks = kGridTile / kChunk;
-static_assert(kGridTile % kChunk == 0 && (kGridTile & (kGridTile - 1)) == 0, "tiles of whole chunks, power of two");
-static_assert(kGridTile / 16 < (1u << kCombSmallMaps), "zshift16 spans a tile");
-// Largest gap between consecutive records the grid streams across.  Below a 4 KiB page every
-// byte it reads lies on a page that also holds record bytes, so it reads no unmapped memory.
-constexpr uint64_t kGridMaxGap = kGridTile;
-constexpr uint32_t kGridInterior = 1u << 31;  // tile word: one record covers the tile (no edge, no init)
-struct GridRec {
-    uint64_t p;    // address of the record's first byte
-    uint32_t n;    // length
-    uint32_t inj;  // ~init: xored into the record's first four bytes
-};
-static_assert(sizeof(GridRec) == 16, "one 16-byte load per record");
-// The grid's combine blob: build_combine_blob(kGridTile), then Z_{-16} (the inverse of 16 zero
-// bytes: a record's register is read at its end rounded up to 16 and moved back).
-constexpr int kGridCombInv16 = kCombWords;
-constexpr int kGridCombWords = kCombWords + 1024;
-void build_grid_comb_blob(uint32_t* out /*kGridCombWords*/);
 
 // Ragged batches cut record bodies at absolute unit_bytes boundaries (so full
 // units are unit-aligned and every chunk is a whole cache line) and order the
@@ -228,17 +175,6 @@ struct RaggedArgs {
     // k_ragged_staged_pipe: set to 1 when a batch's records start on few LDS banks (the skewed
     // stage's case), whichever stage the kernel has; nullptr: not reported
     uint32_t* stage_skew_seen;
-    // The byte grid (k_ragged_grid_plan; tile_cap == 0: not attempted).  The plan checks the
-    // grid's conditions per block (gflag); the kernels after it read every block's flag and take
-    // the grid path only when all hold, else the unit plan above (k_ragged_plan runs only then).
-    GridRec* grec;             // n_rec
-    uint32_t* gtile;           // tile_cap: first record reaching into the tile | kGridInterior
-    uint32_t* gstate;          // tile_cap: register of the record running past the tile's end
-    uint32_t* gend;            // n_rec: register of the record's last tile, at its end rounded up to 16
-    uint32_t* gflag;           // per plan block: nonzero = a condition fails
-    unsigned long long* gctl;  // [0] tiles, [1] address of tile 0, [2] first byte read, [3] last byte read + 1
-    uint64_t tile_cap;
-    const uint32_t* gcomb_blob;  // kGridCombWords
 };
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
@@ -281,8 +217,6 @@ inline uint64_t ragged_scan_blocks(uint64_t n_rec) { return (n_rec + kScanBlock 
 // launch_ragged_scan only counts units (block_sums / block_psums), for callers that must size
 // the unit table first.
 hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s);
-// a.tile_cap > 0: the byte grid's plan first (k_ragged_grid_plan); the unit plan then runs only
-// when a grid condition fails, and the units kernel and finalize take the path the flags say.
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s);
 // One record per group of 4 lanes, no plan kernels (uses arena, off, len, n_rec, init, out, and
 // blob = build_quad_blob's; the tools build's KARMA_DIRECT_VARIANT=20 runs the LDS-staged

@@ -51,10 +51,5 @@ void build_combine_blob(uint64_t unit_bytes, uint32_t* out) {
     for (int i = 0; i < kCombSmallMaps; ++i) gf2::slicing_tables(Map::zero_bytes(16ull << i), out + kCombSmall + i * 1024);
 }
 
-void build_grid_comb_blob(uint32_t* out) {
-    build_combine_blob(kGridTile, out);
-    gf2::slicing_tables(gf2::Map::inverse(gf2::Map::zero_bytes(16)), out + kGridCombInv16);
-}
-
 }  // namespace engine
 }  // namespace karma

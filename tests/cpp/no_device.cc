@@ -12,7 +12,7 @@
 namespace karma::engine {
 
 hipError_t launch_fixed(const FixedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
-hipError_t launch_segment_once(const FixedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_segment_once(const FixedArgs&, int, hipStream_t, bool) { return hipErrorNoDevice; }
 hipError_t launch_combine_fixed(const FixedArgs&, const uint32_t*, uint64_t, uint32_t*, uint64_t, const uint32_t*,
                                 hipStream_t) {
     return hipErrorNoDevice;

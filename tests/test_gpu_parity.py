@@ -688,9 +688,8 @@ def test_ragged_dynamic_tail_steps(dev, shift, monkeypatch):
     (RaggedArgs::dyn_shift; the tools build's KARMA_RAGGED_DYN): configs[2]'s length mix, short
     records (many wave-steps), a batch too small for any dynamic step, back to back on one stream
     (k_ragged_finalize resets the counter) and replayed from a captured graph, exact against the
-    oracle.  Unit plan only (KARMA_RAGGED_GRID=0)."""
+    oracle."""
     monkeypatch.setenv("KARMA_RAGGED_DYN", str(shift))
-    monkeypatch.setenv("KARMA_RAGGED_GRID", "0")
     rng = np.random.default_rng(60 + shift)
     arena_bytes = 256 << 20
     host = rng.integers(0, 256, arena_bytes, dtype=np.uint8)
@@ -718,55 +717,6 @@ def test_ragged_dynamic_tail_steps(dev, shift, monkeypatch):
             g.replay()
             torch.cuda.synchronize()
             _eq(out.cpu().numpy(), want)
-
-
-@pytest.mark.parametrize("shift", [1, 3, 5])
-def test_fixed_dynamic_tail_steps(dev, shift, monkeypatch):
-    """k_units_fixed with the last wave-steps taken kFixedDynChunk at a time from a per-stream
-    global counter (FixedArgs::dyn_shift; the tools build's KARMA_FIXED_DYN): the bench's 1M x 4 KiB
-    (two 2 KiB units folded per wave), 200K x 16 KiB (eight per wave), 20K x 16 KiB with per-record inits,
-    back to back on one stream (the last workgroup clears the counter), on two streams at once
-    (each its own counter), and replayed from a captured graph, every CRC against the oracle."""
-    monkeypatch.setenv("KARMA_FIXED_DYN", str(shift))
-    buf = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
-    K.fill_splitmix64(buf, 77)
-    want4 = oracle_lib.splitmix_fixed_crcs(77, 4096, 0, 1 << 20, threads=16)
-    n16 = 200_000
-    want16 = oracle_lib.splitmix_fixed_crcs(77, 16384, 0, n16, threads=16)
-    rng = np.random.default_rng(shift)
-    ni = 20_000  # per-record inits: the oracle over a host copy of these records
-    ini = rng.integers(0, 1 << 32, ni, dtype=np.uint64).astype(np.uint32)
-    host = buf[: ni * 16384].cpu().numpy()
-    want16i = oracle_lib.ragged_crcs(host, np.arange(ni, dtype=np.uint64) * 16384, np.full(ni, 16384, np.uint32), ini)
-    del host
-    d_ini = torch.from_numpy(ini.view(np.int32)).to(dev)
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    with _lib.using(_lib.AB_LIB_PATH):
-        with torch.cuda.stream(s1):
-            for i in range(4):
-                _eq(K.value_batch_fixed(buf, 4096, stream=s1).cpu().numpy(), want4)
-                if i % 2:
-                    got = K.value_batch_fixed(buf[: ni * 16384], 16384, init=d_ini, stream=s1)
-                    _eq(got.cpu().numpy(), want16i)
-                else:
-                    _eq(K.value_batch_fixed(buf[: n16 * 16384], 16384, stream=s1).cpu().numpy(), want16)
-        torch.cuda.synchronize()
-        o1 = torch.empty(1 << 20, dtype=torch.uint32, device=dev)
-        o2 = torch.empty(n16, dtype=torch.uint32, device=dev)
-        for _ in range(3):  # two streams at once
-            K.value_batch_fixed(buf, 4096, out=o1, stream=s1)
-            K.value_batch_fixed(buf[: n16 * 16384], 16384, out=o2, stream=s2)
-        torch.cuda.synchronize()
-        _eq(o1.cpu().numpy(), want4)
-        _eq(o2.cpu().numpy(), want16)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s1):
-            K.value_batch_fixed(buf, 4096, out=o1, stream=s1)
-        for _ in range(3):
-            o1.view(torch.int32).fill_(-0x5A5A5A5B)
-            g.replay()
-            torch.cuda.synchronize()
-            _eq(o1.cpu().numpy(), want4)
 
 
 def test_ragged_dynamic_tail_streams_concurrently(dev):

@@ -4,7 +4,7 @@ per round and build, 3 warm calls then 20 calls between two HIP events (ms per c
 interleaved (order reversed every other round), after a 500 ms pre-warm; CRCs compared with the
 first build's.  Run on the GPU box from the repo root:
 
-    LIBS="shipped=karma_amd/lib/libkarma_crc32c.so,fdyn3=tools/lib/libkarma_crc32c_fdyn3.so" \\
+    LIBS="shipped=karma_amd/lib/libkarma_crc32c.so,prev=tools/lib/libkarma_crc32c_prev.so" \\
         python tools/fixed_libs_ab.py
 """
 import os

@@ -4,14 +4,12 @@ VERDICT item 4.)  Run on the GPU box from the repo root:
 
     python tools/ragged_gap.py                    # wave logs + unit-kernel times, every case
     python tools/ragged_gap.py --case config3 --calls 20 --no-log   # one case (rocprofv3 passes)
-    python tools/ragged_gap.py --case config3,config3:nogrid         # byte grid vs unit plan
 
 Cases (4 GiB of payload each, the tools build so the fixed v1 kernel and the wave log exist):
     fixed      1M x 4 KiB through karma_crc32c_batch_fixed (k_units_fixed, 2 KiB units folded in the wave)
     fixed_v1   the same with KARMA_CRC_VARIANT=1 (k_units_fixed_v1: each unit's loads issued when it starts)
-    ragged4k   the same records through karma_crc32c_batch_ragged (k_units_ragged: the byte grid)
-    config3    BASELINE configs[2]: 454,320 log-uniform 64 B-64 KiB records (k_units_ragged: the byte grid)
-    <case>:nogrid  a ragged case through the unit plan (8 KiB units; KARMA_RAGGED_GRID=0)
+    ragged4k   the same records through karma_crc32c_batch_ragged (k_units_ragged)
+    config3    BASELINE configs[2]: 454,320 log-uniform 64 B-64 KiB records (k_units_ragged)
 
 The wave log (wavelog.h, karma_ab_wave_log) gives per wave: stream start / end (100 MHz
 wall clock), its CU / XCC, units and bytes.  Printed per case: kernel span, the spread of the
@@ -76,9 +74,8 @@ def main():
         d_off, d_len, n, total, ref = layouts[key]
         out = torch.empty(n, dtype=torch.uint32, device=dev)
 
-        def run():  # config3:nogrid = the unit plan (KARMA_RAGGED_GRID=0), else the byte grid
+        def run():
             os.environ["KARMA_CRC_VARIANT"] = "0"
-            os.environ["KARMA_RAGGED_GRID"] = "0" if variant == "nogrid" else "1"
             _lib.check("ragged", L.karma_crc32c_batch_ragged(raw.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n,
                                                              total, None, 0, out.data_ptr(), sh))
 
@@ -86,18 +83,11 @@ def main():
             torch.cuda.synchronize()
             got = out.cpu().numpy().copy()
             if "want" not in ref:
-                v = os.environ.get("KARMA_RAGGED_GRID", "1")
-                os.environ["KARMA_RAGGED_GRID"] = "0"
-                _lib.check("ragged", L.karma_crc32c_batch_ragged(raw.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
-                                                                 n, total, None, 0, out.data_ptr(), sh))
-                torch.cuda.synchronize()
-                ref["want"] = out.cpu().numpy().copy()
-                os.environ["KARMA_RAGGED_GRID"] = v
+                ref["want"] = got
             return int((got != ref["want"]).sum())
         run.check = check
         return run, total
 
-    # a case name may carry a ragged variant: config3:nogrid = the unit plan (KARMA_RAGGED_GRID=0)
     want = a.case.split(",") if a.case != "all" else ["fixed", "fixed_v1", "ragged4k", "config3"]
     for w in want:
         base, _, var = w.partition(":")
