@@ -193,14 +193,22 @@ struct Barrier {
 //   d. per block, in order, once its CRCs are back: the CRC fields -- between blocks of c.
 //      (the block's image lines are then still in the caches), and the rest once every
 //      block is enqueued.
+// img: the image [*cursor, wal_bytes) is page-locked (the caller's io_uring-registered or
+// hipHostMalloc'd WAL buffer): no payload is packed.  Each block's framed image span -- headers,
+// payloads and any footer between them, the bytes the reference writes with its one copy
+// (segment_file.cc:25-27) -- is DMAed straight from the image, and the CRC batch reads the
+// payloads in that device copy (d_pay holds [cur0, end_cursor) of the image).
 int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_off, const uint32_t* len, size_t n,
                 uint64_t pay_total, uint32_t max_len, uint8_t* wal, size_t wal_bytes, size_t seg_bytes,
-                uint64_t* cursor, uint64_t* rec_off, size_t* n_framed) {
+                uint64_t* cursor, uint64_t* rec_off, size_t* n_framed, bool img) {
     karma::engine::PhaseTimer T("wal_append");
     // blocks: at most n / kBlockRecords + (payload / smallest block) + the doubling steps
     const size_t max_blocks = n / kBlockRecords + pay_total / kBlockBytesFirst + 32;
-    if (const int rc = C.h_pay.ensure(pay_total + 16, true)) return rc;
-    if (const int rc = C.d_pay.ensure(pay_total + 16, false)) return rc;
+    const uint64_t cur0 = *cursor;
+    if (!img) {
+        if (const int rc = C.h_pay.ensure(pay_total + 16, true)) return rc;
+        if (const int rc = C.d_pay.ensure(pay_total + 16, false)) return rc;
+    }
     if (const int rc = C.h_off.ensure(n * 8, true, true)) return rc;
     if (const int rc = C.d_off.ensure(n * 8, false)) return rc;
     if (const int rc = C.h_len.ensure(n * 4, true, true)) return rc;
@@ -211,7 +219,7 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
     if (C.at.size() < n) C.at.resize(n);
     if (C.bstart.size() < max_blocks + 2) C.bstart.resize(max_blocks + 2);
     T.mark("buffers");
-    uint8_t* hp = C.h_pay.as<uint8_t>();
+    uint8_t* hp = img ? nullptr : C.h_pay.as<uint8_t>();
     uint64_t* ho = C.h_off.as<uint64_t>();
     uint32_t* hl = C.h_len.as<uint32_t>();
     uint32_t* hc = C.h_crc.as<uint32_t>();
@@ -249,8 +257,9 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
         // the block's packed payloads [plo, phi) (V(i) - 8 i: read before this loop turns at[]
         // into WAL offsets; at[hi] belongs to the next block, which may be converting it)
         const uint64_t plo = at[lo] - kHeader * lo, phi = at[hi - 1] - kHeader * (hi - 1) + len[hi - 1];
-        bool contiguous = true;
+        bool contiguous = !img;
         for (size_t i = lo + 1; i < hi && contiguous; ++i) contiguous = src_off[i] == src_off[i - 1] + len[i - 1];
+        uint64_t ibase = 0;  // img: the block's first header (WAL offset)
         for (size_t i = lo; i < hi; ++i) {  // segment_file::append_record: length field + payload
             while (i >= runs[r].i1) ++r;
             const uint64_t v = at[i], pk = v - kHeader * i;  // V(i), packed payload offset
@@ -259,33 +268,40 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
             const uint32_t L = len[i];
             put32(p + 4, L << 8 | 0u);
             copy_payload(p + kHeader, src + src_off[i], L);
-            if (!contiguous) copy_payload(hp + pk, src + src_off[i], L);
-            ho[i] = pk - plo;  // the block's kernel sees its own slice: offsets rebased onto dp + plo
+            if (img) {
+                if (i == lo) ibase = at[i];
+                ho[i] = at[i] + kHeader - ibase;  // the payload in the block's image span
+            } else {
+                if (!contiguous) copy_payload(hp + pk, src + src_off[i], L);
+                ho[i] = pk - plo;  // the block's kernel sees its own slice: offsets rebased onto dp + plo
+            }
             hl[i] = L;
         }
         if (contiguous) std::memcpy(hp + plo, src + src_off[lo], phi - plo);
         hipStream_t s = C.st[k % kStreams];
         const size_t nr = hi - lo;
-        uint8_t* dp = C.d_pay.as<uint8_t>();
         uint64_t* hoff = ho + lo;
         uint64_t* doff = C.d_off.as<uint64_t>() + lo;
         uint32_t* dlen = C.d_len.as<uint32_t>() + lo;
-        if (hipMemcpyAsync(dp + plo, hp + plo, phi - plo, hipMemcpyHostToDevice, s) != hipSuccess)
-            return (int)KARMA_E_HIP;
+        // the bytes the block's kernel reads: its packed payloads, or (img) its image span
+        uint8_t* dp = img ? C.d_pay.as<uint8_t>() + (ibase - cur0) : C.d_pay.as<uint8_t>() + plo;
+        const uint8_t* hsrc = img ? wal + ibase : hp + plo;
+        const uint64_t dma = img ? at[hi - 1] + kHeader + len[hi - 1] - ibase : phi - plo;
+        if (hipMemcpyAsync(dp, hsrc, dma, hipMemcpyHostToDevice, s) != hipSuccess) return (int)KARMA_E_HIP;
         if (max_len <= kZeroCopyMaxLen) {
             // the small-record kernel reads each record's offset and length once and writes its CRC
             // once: it does so over PCIe, from and into the fine-grained host arrays, so the block's
             // only copy is its payload DMA (the small copies each cost the DMA engine ~10 us)
             // (a block of empty payloads has max_len 0, which the ABI reads as "no bound": bound it
             // by 1 so it too takes the small-record kernel and not the unknown-total plan)
-            if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, hoff, hl + lo, nr, phi - plo,
+            if (const int rc = karma_crc32c_batch_ragged_bounded(dp, hoff, hl + lo, nr, phi - plo,
                                                                  std::max<uint32_t>(max_len, 1), nullptr, 0, hc + lo, s))
                 return rc;
         } else {
             if (hipMemcpyAsync(doff, hoff, nr * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
                 hipMemcpyAsync(dlen, hl + lo, nr * 4, hipMemcpyHostToDevice, s) != hipSuccess)
                 return (int)KARMA_E_HIP;
-            if (const int rc = karma_crc32c_batch_ragged_bounded(dp + plo, doff, dlen, nr, phi - plo, max_len, nullptr,
+            if (const int rc = karma_crc32c_batch_ragged_bounded(dp, doff, dlen, nr, phi - plo, max_len, nullptr,
                                                                  0, C.d_crc.as<uint32_t>() + lo, s))
                 return rc;
             if (hipMemcpyAsync(hc + lo, C.d_crc.as<uint32_t>() + lo, nr * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
@@ -370,6 +386,10 @@ int append_pass(AppendCtx& C, int dev, const uint8_t* src, const uint64_t* src_o
                 bstart[++nb] = lo;
                 b = lo;
                 blimit = std::min(2 * blimit, kBlockBytesMax);
+            }
+            // img: the device copy of the image span this pass frames
+            if (img) {
+                if (const int rc = C.d_pay.ensure(end_cursor - cur0 + 16, false)) set_rc(rc);
             }
             T.mark("b. placement + blocks");
         }
@@ -458,8 +478,10 @@ extern "C" int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_o
             max_len = std::max(max_len, h_len[done + m]);
         }
         size_t framed = 0;
+        const bool img = cur < wal_bytes && karma::engine::host_range_pinned(wal + cur, wal_bytes - cur) &&
+                         KARMA_AB_KNOB("KARMA_APPEND_IMAGE_DMA", 1);
         if (const int rc = append_pass(C, dev, src, h_src_off + done, h_len + done, m, bytes, max_len, wal, wal_bytes,
-                                       seg_bytes, &cur, h_rec_off ? h_rec_off + done : nullptr, &framed))
+                                       seg_bytes, &cur, h_rec_off ? h_rec_off + done : nullptr, &framed, img))
             return rc;  // *h_cursor and *h_n_framed keep the passes already complete
         done += framed;
         *h_cursor = cur;

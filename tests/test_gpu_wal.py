@@ -131,6 +131,11 @@ def test_append_in_several_passes_matches_reference_framing(call_bytes, monkeypa
             assert cur == mcur and list(rec) == mrec, (call_bytes, nseg, cursor)
             assert wal.tobytes() == bytes(model), (call_bytes, nseg, cursor)
             assert (len(rec) == lens.size) == (nseg == 200)
+            # the same into a page-locked image: each pass DMAs its framed image spans (no pack copy)
+            pw = torch.zeros(wal.nbytes, dtype=torch.uint8).pin_memory().numpy()
+            cur2, rec2 = _append(ab, src, offs, lens, pw, cursor=cursor)
+            assert cur2 == mcur and list(rec2) == mrec, ("pinned", call_bytes, nseg, cursor)
+            assert pw.tobytes() == bytes(model), ("pinned", call_bytes, nseg, cursor)
 
 
 @pytest.mark.parametrize("mix", ["small", "mixed", "large"])
