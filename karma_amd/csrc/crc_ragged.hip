@@ -376,6 +376,10 @@ __device__ __forceinline__ UnitMap unit_map(const RaggedArgs& A) {
         m.U = m.Fc + (P < pcap ? P : pcap);
         m.shift = A.part_base - m.Fc;
     }
+    // wave-uniform: scalar registers, so no later use waits on the loads of fbase (vmcnt)
+    m.U = uniform64(m.U);
+    m.Fc = uniform64(m.Fc);
+    m.shift = uniform64(m.shift);
     return m;
 }
 
@@ -395,6 +399,113 @@ __device__ __forceinline__ UnitDesc load_desc(const UnitDesc* d) {
 // records 0.6656 vs 0.6525; 8: no better than 4 -- profiles/r02_ragged_pf_ab.txt).  With one
 // 1024-thread workgroup per CU (the 145 KiB LDS image) the chunks in flight per CU are what
 // keeps HBM busy across the unit boundaries this kernel does not pipeline.
+// The next wave-step of this wave (k_units_ragged): the block's static share from its LDS
+// counter, then (dyn_shift) the dynamic tail, 16 steps per workgroup grab from lb_ctl[2], the
+// chunk's base published in LDS by the wave that grabbed it.  Uniform over the wave.
+__device__ __forceinline__ uint64_t ragged_next_step(const RaggedArgs& A, uint32_t* blk_next, uint32_t* blk_dyn,
+                                                     uint32_t nidx, uint64_t S, uint64_t nws, uint64_t bw0,
+                                                     uint64_t nwaves, uint32_t lane) {
+    uint32_t i = 0;
+    if (lane == 0) i = atomicAdd(blk_next, 1u);
+    i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
+    uint64_t wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
+    if (i >= nidx && S < nws) {  // the static share is done: the dynamic tail
+        const uint32_t k = i - nidx, c = k / kWavesPerBlock, j = k % kWavesPerBlock;
+        uint32_t base = ~0u;
+        if (c < kDynChunks) {
+            if (j == 0) {  // this wave grabs the chunk (one round trip) and publishes its base
+                if (lane == 0) {
+                    base = (uint32_t)atomicAdd(A.lb_ctl + 2, (unsigned long long)kWavesPerBlock);
+                    __hip_atomic_store(&blk_dyn[c], base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            } else if (lane == 0) {  // the chunk's grabber holds an earlier index: it is running
+                while ((base = __hip_atomic_load(&blk_dyn[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == ~0u)
+                    __builtin_amdgcn_s_sleep(2);
+            }
+            base = __builtin_amdgcn_readfirstlane(__shfl((int)base, 0));
+        }
+        wb_next = base != ~0u && S + base + j < nws ? S + base + j : nws;
+    }
+    return wb_next;
+}
+
+// The units kernel software-pipelined across units (stream_unit, as k_units_fixed): the next
+// wave-step's descriptor is loaded when a unit starts, and its first chunk loads are issued
+// before the current unit's last PF chunks are stepped, so no wave waits on a fresh chunk load at
+// a unit boundary.  An empty slot (past the table) streams nothing at a safe address (the blob).
+// The tools build's KARMA_RAGGED_VARIANT=1 (DESIGN.md §4 "The ragged gap").
+template <int PF>
+__global__ __launch_bounds__(kBlockThreads) void k_units_ragged_pipe(RaggedArgs A) {
+    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.blob, A.blob + kBlobWords);  // the blob: empty units' address
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    __shared__ uint32_t blk_next;
+    __shared__ uint32_t blk_dyn[kDynChunks];
+    if (threadIdx.x == 0) blk_next = kWavesPerBlock;
+    for (uint32_t c = threadIdx.x; c < kDynChunks; c += blockDim.x) blk_dyn[c] = ~0u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const UnitMap M = unit_map(A);
+    const uint64_t U = M.U;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
+    uint64_t S = nws;
+    if (A.dyn_shift) {
+        const uint64_t d = min(nws >> A.dyn_shift, (uint64_t)kDynMaxSteps);
+        const uint64_t s = (nws - d) / nwaves * nwaves;
+        S = s >= nwaves ? s : nws;
+    }
+    const uint32_t nidx = (uint32_t)((S + nwaves - 1) / nwaves) * kWavesPerBlock;
+    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(A.blob);
+    auto lane_of = [&](const UnitDesc& d) {
+        const uint8_t* us = d.span ? reinterpret_cast<const uint8_t*>(d.us) : safe;
+        return lane_unit(us, us + d.span, l);
+    };
+    uint64_t wb = bw0 + (threadIdx.x >> 6);
+    uint64_t u = wb * kGroupsPerWave + grp;
+    UnitDesc d = u < U ? load_desc(A.desc + M.slot(u)) : UnitDesc{0, 0, 0};
+    // Two load sets, ping-pong: unit k streams from one while unit k + 1's loads go into the other.
+    // (With one set carried around the loop the compiler copied the next unit's load registers into
+    // the loop-carried ones at the back edge, waiting for them there: vmcnt(0) at every unit end.)
+    LaneUnit La = lane_of(d), Lb = La;
+    UnitLoads<PF> Da, Db;
+    issue_unit_loads<PF, kRaggedNT>(La, Da);  // before the table fill (which then costs no round trip)
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t X = lane_const();
+    WLOG_DECL;
+    WLOG_START();
+    // one unit streamed from (L, D); the next one's loads issued into (Ln, Dn)
+    auto step = [&](const LaneUnit& L, UnitLoads<PF>& D, LaneUnit& Ln, UnitLoads<PF>& Dn) {
+        const UnitDesc cur = d;
+        const bool valid = u < U;
+        const uint64_t wb_next = ragged_next_step(A, &blk_next, blk_dyn, nidx, S, nws, bw0, nwaves, lane);
+        const uint64_t un = wb_next * kGroupsPerWave + grp;
+        // unbranched (slot 0 for a step past the table; U > 0 here): a load under a branch is waited
+        // for at the join, which would drain this unit's chunk loads; the descriptor is used only
+        // when the next unit's loads are issued
+        const bool nvalid = un < U;
+        const UnitDesc draw = load_desc(&KB_READ(A.desc, M.slot(nvalid ? un : 0), A.unit_cap, kKbUnit));
+        const uint32_t R = stream_unit<PF, kRaggedNT>(lds, X, l, L, D, L.us, cur.inj, [&](UnitLoads<PF>&) {
+            d = nvalid ? draw : UnitDesc{0, 0, 0};
+            Ln = lane_of(d);
+            issue_unit_loads<PF, kRaggedNT>(Ln, Dn);
+        });
+        if (valid && l == 0) KB_WRITE(A.partial, M.slot(u), A.unit_cap, kKbUnit, R);
+        WLOG_STEP();
+        WLOG_UNIT(valid && l == 0, cur.span);
+        wb = wb_next;
+        u = un;
+    };
+    while (wb < nws) {
+        step(La, Da, Lb, Db);
+        if (wb >= nws) break;
+        step(Lb, Db, La, Da);
+    }
+    WLOG_END(bw0 + (threadIdx.x >> 6));
+}
+
 template <int PF = kRaggedUnitsPF>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
@@ -436,30 +547,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     while (wb < nws) {
         const UnitDesc cur = d;
         const bool valid = u < U;
-        uint64_t wb_next;
-        {
-            uint32_t i = 0;
-            if (lane == 0) i = atomicAdd(&blk_next, 1u);
-            i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
-            wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
-            if (i >= nidx && S < nws) {  // the static share is done: the dynamic tail
-                const uint32_t k = i - nidx, c = k / kWavesPerBlock, j = k % kWavesPerBlock;
-                uint32_t base = ~0u;
-                if (c < kDynChunks) {
-                    if (j == 0) {  // this wave grabs the chunk (one round trip) and publishes its base
-                        if (lane == 0) {
-                            base = (uint32_t)atomicAdd(A.lb_ctl + 2, (unsigned long long)kWavesPerBlock);
-                            __hip_atomic_store(&blk_dyn[c], base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                    } else if (lane == 0) {  // the chunk's grabber holds an earlier index: it is running
-                        while ((base = __hip_atomic_load(&blk_dyn[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == ~0u)
-                            __builtin_amdgcn_s_sleep(2);
-                    }
-                    base = __builtin_amdgcn_readfirstlane(__shfl((int)base, 0));
-                }
-                wb_next = base != ~0u && S + base + j < nws ? S + base + j : nws;
-            }
-        }
+        const uint64_t wb_next = ragged_next_step(A, &blk_next, blk_dyn, nidx, S, nws, bw0, nwaves, lane);
         const uint64_t un = wb_next * kGroupsPerWave + grp;
         d = un < U ? load_desc(&KB_READ(A.desc, M.slot(un), A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
         const uint8_t* us = reinterpret_cast<const uint8_t*>(cur.us);
@@ -841,7 +929,14 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     const uint64_t nb = ragged_scan_blocks(a.n_rec);
     hipLaunchKernelGGL(k_ragged_plan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
     units_timer_begin(s);
-    hipLaunchKernelGGL(k_units_ragged<>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    // (the tools build's KARMA_RAGGED_VARIANT=1: the units kernel pipelined across units, PF 4 or 6)
+    const long rv = KARMA_AB_KNOB("KARMA_RAGGED_VARIANT", KARMA_RAGGED_PIPE);
+    if (rv == 1)
+        hipLaunchKernelGGL(k_units_ragged_pipe<4>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (rv == 2)
+        hipLaunchKernelGGL(k_units_ragged_pipe<6>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_units_ragged<>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
     // at most 2 per CU (each loads the 73 KiB combine image; one or four per CU measured no
