@@ -120,6 +120,8 @@ def load(path: str) -> ctypes.CDLL:
         except OSError as e:  # pragma: no cover - depends on the host
             raise KarmaUnavailable(f"cannot load {path}: {e}") from e
         for name, (res, args) in SIGNATURES.items():
+            if not hasattr(handle, name) and path != LIB_PATH:
+                continue  # an older build compared side by side (tools/): an entry point it predates
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

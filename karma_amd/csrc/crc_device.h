@@ -333,25 +333,24 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
         const uint8_t* wl = base + (nch - 1) * kChunk + 16 * l;  // this lane's window in the last chunk
         const bool lok = wl < ue;
         const uint8_t* lclamp = lok ? wl : ue - 16;               // always a valid address
-        // Chunk 0 and the PF chunks after it go out together, unbranched (chunk 0 clamped to a
-        // valid address, masked after): with chunk 0 under a branch and its injected word xored
-        // before the PF loads, the compiler waited for chunk 0 (s_waitcnt vmcnt(0)) before
-        // issuing them, two memory round trips per unit (DESIGN.md §4 "The ragged gap, found").
-        const bool ok = w >= us && w < ue;
-        u32x4 v = ldg<NT>(ok ? w : lclamp);
-        const bool inj_here = w == inj_at;
+        // (Chunk 0 under a branch, its injected word xored before the PF loads are issued: the
+        // compiler then waits for chunk 0 before issuing them.  Issuing all PF + 1 loads together
+        // (clamped, masked after) measured 0.7-1.2 % SLOWER on every ragged layout, and so did the
+        // kernel pipelined across units: profiles/r05_ragged_group_unit_pipe_ab.txt)
+        {
+            const bool ok = w >= us && w < ue;
+            u32x4 v = ok ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
+            if (w == inj_at) v.x ^= inj;
+            a0 = v.x;
+            a1 = v.y;
+            a2 = v.z;
+            a3 = v.w;
+        }
         int64_t rem = nch - 1;  // chunks after chunk 0; the final one is masked per lane
         w += kChunk;
         u32x4 nb[PF];
 #pragma unroll
         for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
-        __builtin_amdgcn_sched_barrier(0);  // (nothing that waits on chunk 0 moves above the loads)
-        if (!ok) v = u32x4{0u, 0u, 0u, 0u};
-        if (inj_here) v.x ^= inj;
-        a0 = v.x;
-        a1 = v.y;
-        a2 = v.z;
-        a3 = v.w;
         while (rem > PF) {  // PF full chunks (at least one more follows)
             u32x4 cur[PF];
 #pragma unroll

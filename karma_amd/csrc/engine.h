@@ -26,8 +26,8 @@ constexpr uint32_t kStgGateLen = 183;
 #define KARMA_RAGGED_UNIT 8192  // a build-time A/B knob (tools/ragged_study.py over builds with -DKARMA_RAGGED_UNIT=...)
 #endif
 constexpr uint64_t kDefaultUnit = KARMA_RAGGED_UNIT;  // unit size for ragged batches
-#ifndef KARMA_RAGGED_PIPE
-#define KARMA_RAGGED_PIPE 0  // the ragged units kernel: 0 = k_units_ragged, 1 / 2 = k_units_ragged_pipe<4 / 6> (A/B builds)
+#ifndef KARMA_STAGE_DEPTH
+#define KARMA_STAGE_DEPTH 1  // batches in flight per wave of the LDS-staged small-record kernel (A/B builds: 2)
 #endif
 
 // ---- table blob of the streaming kernel (uint32 words) ---------------------

@@ -460,8 +460,7 @@ def test_rejects_bad_arguments(dev):
         K.value_batch_fixed(buf, 7)
 
 
-@pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", v) for v in "127"] + [("KARMA_FOLD_MAX_K", "1")] +
-                         [("KARMA_RAGGED_VARIANT", v) for v in "12"])
+@pytest.mark.parametrize("env,val", [("KARMA_CRC_VARIANT", v) for v in "127"] + [("KARMA_FOLD_MAX_K", "1")])
 def test_kernel_variants_match_oracle(raw, dev, env, val, monkeypatch):
     """The A/B kernels of the tools build (karma_amd/csrc/ab.h, tools/variant_bench.py) are held to
     the same parity as the shipped ones."""
