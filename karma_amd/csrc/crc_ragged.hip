@@ -797,167 +797,6 @@ __global__ __launch_bounds__((R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_s
 }
 
 
-// The staged kernel with TWO batches' loads in flight per wave (k_ragged_staged_pipe has one):
-// batch k is stepped from the stage while batches k + 1 and k + 2 are in flight in two register
-// sets, so each batch's loads have two batches' steps to land (the one-ahead kernel waited ~2.4 us
-// per batch at 7 waves per CU: r04g_wal_replay_pmc.json, SQ_WAIT_ANY 0.47 of wave cycles).  The
-// loop is unrolled by two so the register sets alternate without copies.  Plain and skewed stage,
-// 16-copy image, as k_ragged_staged_pipe (the tools build's KARMA_STAGE_DEPTH=2).
-template <bool SK>
-__global__ __launch_bounds__(kStgWaves * 64) void k_ragged_staged_pipe2(RaggedArgs A) {
-    constexpr int NW = kStgWaves, SMODE = 24;
-    constexpr int TW = kRep16Words, Z4 = TW, BUF = TW + 1280;
-    constexpr uint32_t kLead = 16u, kFit = kStgBytes - 32u;
-    constexpr uint32_t kStride = SK ? kStgBytes + kStgBytes / 32 : kStgBytes;
-    uint64_t n_rec = A.n_rec;
-    if (A.n_dev) {
-        if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
-        n_rec = *A.n_dev;
-    }
-    KB_SET_ARENA(A.kb_lo, A.kb_hi);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[BUF + NW * (int)(kStride / 4)];
-    static_assert((BUF + NW * (int)(kStride / 4)) * 4 <= 160 * 1024, "LDS of one workgroup");
-    load_stg_tables<NW * 64>(lds, A.blob);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: scalar loop control)
-    const uint32_t X = lane_const16();
-    uint8_t* stage = reinterpret_cast<uint8_t*>(lds + BUF) + wave * kStride;
-    uint32_t* stage32 = reinterpret_cast<uint32_t*>(stage);
-    const uint64_t step = (uint64_t)gridDim.x * NW * 64;
-    uint64_t base = ((uint64_t)blockIdx.x * NW + wave) * 64;
-    if (base >= n_rec) return;
-    struct Meta {
-        uint64_t o;
-        uint32_t n, ini;
-    };
-    struct Ext {
-        uintptr_t lo, hi;
-        bool fits, sk;
-    };
-    auto ld_meta = [&](uint64_t b) {
-        const uint64_t ri = b + lane;
-        const bool v = ri < n_rec;
-        return Meta{v ? A.off[ri] : 0, v ? A.len[ri] : 0u, v ? (A.init ? A.init[ri] : A.init_scalar) : 0u};
-    };
-    bool poor_seen = false;
-    auto extent = [&](const Meta& m) {
-        const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + m.o;
-        uint64_t l = m.n ? (p & ~uintptr_t(15)) : ~0ull, h = m.n ? ((p + m.n + 15) & ~uintptr_t(15)) : 0ull;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t ol = (uint64_t)__shfl_xor((long long)l, d), oh = (uint64_t)__shfl_xor((long long)h, d);
-            l = ol < l ? ol : l;
-            h = oh > h ? oh : h;
-        }
-        Ext E;
-        E.lo = uniform64(l);
-        E.hi = uniform64(h);
-        E.fits = E.hi != 0 && E.hi - E.lo <= kFit;
-        E.sk = false;
-        if (E.fits && (SK || A.stage_skew_seen)) {  // the records' first dwords on few LDS banks
-            uint32_t bits = m.n ? 1u << (((uint32_t)(p - E.lo) >> 2) & 31u) : 0u;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) bits |= (uint32_t)__shfl_xor((int)bits, d);
-            const bool poor = __builtin_popcount(__builtin_amdgcn_readfirstlane(bits)) < 12;
-            poor_seen |= poor;
-            E.sk = SK && poor;
-        }
-        return E;
-    };
-    auto issue = [&](const Ext& E, u32x4 (&v)[kStgVecs]) {
-        const uint32_t nv = (uint32_t)((E.hi - E.lo) / 16);
-#pragma unroll
-        for (int q = 0; q < kStgVecs; ++q) {
-            const uint32_t j = lane + 64u * q;  // past the extent: its first block again (no branch)
-            v[q] = ldg<true>(reinterpret_cast<const uint8_t*>(E.lo + 16ull * (j < nv ? j : 0u)));
-        }
-    };
-    auto store = [&](const Ext& E, const u32x4 (&v)[kStgVecs]) {
-#pragma unroll
-        for (int q = 0; q < kStgVecs; ++q) {
-            uint32_t at = kLead + 16u * (lane + 64u * q);
-            at = at >= kStgBytes ? 0u : at;  // the last slot, past any extent, into the slack
-            if (E.sk) {  // 4 dwords in one 128-byte line: contiguous after the skew
-                const uint32_t d = at / 4 + at / 128;
-                stage32[d] = v[q].x;
-                stage32[d + 1] = v[q].y;
-                stage32[d + 2] = v[q].z;
-                stage32[d + 3] = v[q].w;
-            } else {
-                *reinterpret_cast<u32x4*>(stage + at) = v[q];
-            }
-        }
-        wave_lds_sync();
-    };
-    auto compute = [&](uint64_t b, const Meta& m, const Ext& E) {
-        const uint64_t ri = b + lane;
-        if (ri < n_rec) {
-            uint32_t res = m.ini;
-            const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + m.o;
-            if (m.n) {
-                if (E.fits && m.n >= 4 && E.sk)
-                    res = lane_record_end<SMODE>(lds, X, Z4, kLead + (uint32_t)(p - E.lo), m.n, m.ini,
-                                                 [&](uint32_t q) { return stage32[q + (q >> 5)]; });
-                else if (E.fits && m.n >= 4)
-                    res = lane_record_end<SMODE>(lds, X, Z4, kLead + (uint32_t)(p - E.lo), m.n, m.ini, [&](uint32_t q) {
-                        return *reinterpret_cast<const uint32_t*>(stage + 4u * q);
-                    });
-                else if (E.fits)
-                    res = lane_record<8>(lds, X, Z4, TW + 1024, p, m.n, m.ini, [&](uintptr_t a) {
-                        const uint32_t at = kLead + (uint32_t)(a - E.lo);
-                        if (E.sk) {
-                            const uint32_t d = at / 4 + at / 128;
-                            return u32x4{stage32[d], stage32[d + 1], stage32[d + 2], stage32[d + 3]};
-                        }
-                        return *reinterpret_cast<const u32x4*>(stage + at);
-                    });
-                else
-                    res = lane_record<8>(lds, X, Z4, TW + 1024, p, m.n, m.ini,
-                                         [&](uintptr_t a) { return ld16(reinterpret_cast<const uint8_t*>(a)); });
-            }
-            A.out[ri] = res;
-            if (A.cmp_stored && m.n && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
-        }
-        wave_lds_sync();  // this batch's stage reads are done before the next batch is stored
-    };
-    // batch k: m0 / e0 (data in one set), batch k + 1: m1 / e1 (data in the other), batch k + 2: m2
-    Meta m0 = ld_meta(base), m1 = ld_meta(base + step), m2 = ld_meta(base + 2 * step);
-    Ext e0 = extent(m0), e1{0, 0, false, false};
-    u32x4 va[kStgVecs], vb[kStgVecs];
-    if (e0.fits) issue(e0, va);
-    const bool has1 = base + step < n_rec;
-    if (has1) {
-        e1 = extent(m1);
-        if (e1.fits) issue(e1, vb);
-    }
-    // One batch: store its set, put batch k + 2's loads into that set, step batch k.  Returns
-    // false when no batch follows.
-    auto one = [&](u32x4 (&vk)[kStgVecs]) {
-        if (e0.fits) store(e0, vk);
-        const uint64_t b2 = base + 2 * step;
-        Ext e2{0, 0, false, false};
-        Meta m3{0, 0u, 0u};
-        if (b2 < n_rec) {
-            e2 = extent(m2);
-            // batch k + 3's metadata BEFORE batch k + 2's loads: vmcnt counts in issue order, so the
-            // wait for the metadata (the loop's register moves) does not wait for those loads
-            m3 = ld_meta(b2 + step);
-            if (e2.fits) issue(e2, vk);
-        }
-        compute(base, m0, e0);
-        base += step;
-        m0 = m1;
-        e0 = e1;
-        m1 = m2;
-        e1 = e2;
-        m2 = m3;
-        return base < n_rec;
-    };
-    while (one(va) && one(vb)) {
-    }
-    if (poor_seen && A.stage_skew_seen && lane == 0) *A.stage_skew_seen = 1u;  // (benign races: all store 1)
-}
-
 }  // namespace
 
 hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
@@ -981,14 +820,8 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
 
 hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew) {
     if (a.n_rec == 0 || !a.n_dev || !a.gate_len) return hipErrorInvalidValue;
-    // (KARMA_STAGE_DEPTH=2: two batches' loads in flight per wave, k_ragged_staged_pipe2)
-    if (KARMA_AB_KNOB("KARMA_STAGE_DEPTH", KARMA_STAGE_DEPTH) == 2) {
-        if (skew)
-            hipLaunchKernelGGL((k_ragged_staged_pipe2<true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_ragged_staged_pipe2<false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
-        return hipGetLastError();
-    }
+    // (round 5 measured two batches' loads in flight per wave, a depth-2 variant of this kernel,
+    // slower: 0.1229 vs 0.1201 ms per 1M x 180 B replay call, profiles/r05_replay_depth2.txt)
     if (skew) {
         hipLaunchKernelGGL((k_ragged_staged_pipe<true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
 #ifdef KARMA_AB

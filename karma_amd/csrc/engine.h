@@ -26,9 +26,6 @@ constexpr uint32_t kStgGateLen = 183;
 #define KARMA_RAGGED_UNIT 8192  // a build-time A/B knob (tools/ragged_study.py over builds with -DKARMA_RAGGED_UNIT=...)
 #endif
 constexpr uint64_t kDefaultUnit = KARMA_RAGGED_UNIT;  // unit size for ragged batches
-#ifndef KARMA_STAGE_DEPTH
-#define KARMA_STAGE_DEPTH 1  // batches in flight per wave of the LDS-staged small-record kernel (A/B builds: 2)
-#endif
 
 // ---- table blob of the streaming kernel (uint32 words) ---------------------
 constexpr int kBlobStride = 0;     // Z_S slicing tables, 4 x 256

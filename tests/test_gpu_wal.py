@@ -55,13 +55,10 @@ WALKS = {
     "listcrc4k": (True, 4096, _lib.KARMA_WAL_CRC_INLINE), # the LDS-staged kernel (k_wal_list_crc; tools build)
     "r8": (True, 0, _lib.KARMA_WAL_CRC_PLAN),             # the plan, the plain-stage small-record kernel on the
                                                           # 8-copy image with 10 waves (KARMA_STAGE_R8; tools build)
-    "depth2": (True, 0, _lib.KARMA_WAL_CRC_PLAN),         # the plan, the staged kernel with two batches in flight
-                                                          # per wave (KARMA_STAGE_DEPTH=2; tools build)
 }
 _LIST_CRC = ("listcrc", "listcrc4k")  # KARMA_WAL_LIST_CRC=1
 _NO_STAGED = ("sepdirect4",)  # KARMA_SMALL_STAGED=0
 _R8 = ("r8",)  # KARMA_STAGE_R8=1
-_DEPTH2 = ("depth2",)  # KARMA_STAGE_DEPTH=2
 _WALK = {"name": "split"}
 
 
@@ -79,11 +76,7 @@ def _walk_env(monkeypatch, walk):
         monkeypatch.setenv("KARMA_STAGE_R8", "1")
     else:
         monkeypatch.delenv("KARMA_STAGE_R8", raising=False)
-    if walk in _DEPTH2:
-        monkeypatch.setenv("KARMA_STAGE_DEPTH", "2")
-    else:
-        monkeypatch.delenv("KARMA_STAGE_DEPTH", raising=False)
-    if WALKS[walk][0] and walk not in _LIST_CRC and walk not in _NO_STAGED and walk not in _R8 and walk not in _DEPTH2:
+    if WALKS[walk][0] and walk not in _LIST_CRC and walk not in _NO_STAGED and walk not in _R8:
         monkeypatch.setenv("KARMA_WALK_VARIANT", "1")  # read by the tools build only (ab.h)
     else:
         monkeypatch.delenv("KARMA_WALK_VARIANT", raising=False)

@@ -139,7 +139,7 @@ def main():
     for r in range(a.rounds):
         for v, (lib, sub, batch, env) in variants.items():
             for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC", "KARMA_SMALL_STAGED", "KARMA_WALK_DIRECT",
-                      "KARMA_GATHER_PARTS", "KARMA_SMALL_WHICH", "KARMA_STAGE_SKEW", "KARMA_STAGE_R8", "KARMA_STAGE_DEPTH"):
+                      "KARMA_GATHER_PARTS", "KARMA_SMALL_WHICH", "KARMA_STAGE_SKEW", "KARMA_STAGE_R8"):
                 os.environ.pop(k, None)
             if env:
                 os.environ[env[0]] = env[1]
