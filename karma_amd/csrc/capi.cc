@@ -393,7 +393,7 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 
 // ---- ragged records -------------------------------------------------------
 struct RaggedLayout {
-    size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off, total;
+    size_t fbase_off, pslot_off, tailc_off, sums_off, psums_off, desc_off, part_off, total;
 };
 
 RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
@@ -401,7 +401,8 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     const uint64_t nb = ragged_scan_blocks(n_rec);
     L.fbase_off = 0;
     L.pslot_off = L.fbase_off + align256((n_rec + 2) * sizeof(uint64_t));
-    L.sums_off = L.pslot_off + align256(2 * n_rec * sizeof(uint64_t));
+    L.tailc_off = L.pslot_off + align256(2 * n_rec * sizeof(uint64_t));
+    L.sums_off = L.tailc_off + align256(n_rec * sizeof(uint32_t));
     L.psums_off = L.sums_off + align256(nb * sizeof(uint64_t));
     L.desc_off = L.psums_off + align256(nb * sizeof(uint64_t));
     L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
@@ -413,6 +414,7 @@ void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
     char* b = static_cast<char*>(ws);
     a.fbase = reinterpret_cast<uint64_t*>(b + L.fbase_off);
     a.pslot = reinterpret_cast<uint64_t*>(b + L.pslot_off);
+    a.tailc = reinterpret_cast<uint32_t*>(b + L.tailc_off);
     a.block_sums = reinterpret_cast<uint64_t*>(b + L.sums_off);
     a.block_psums = reinterpret_cast<uint64_t*>(b + L.psums_off);
     a.desc = reinterpret_cast<UnitDesc*>(b + L.desc_off);
@@ -581,6 +583,12 @@ thread_local hipEvent_t t_units_start = nullptr, t_units_stop = nullptr;
 // its wait and at its end.
 extern "C" int karma_ab_seg_log(void* d_buf) {
     return karma::engine::set_seg_log(d_buf) == hipSuccess ? 0 : KARMA_E_HIP;
+}
+// Tools build only: k_ragged_plan writes 6 wall-clock stamps per workgroup into d_buf[8 b ..] (entry,
+// tables, block scan, look-back, entering registers, descriptors), k_ragged_finalize 3 into
+// d_buf[32768 + 8 b ..] (entry, tables, records); NULL: off.
+extern "C" int karma_ab_plan_log(void* d_buf) {
+    return karma::engine::set_plan_log(d_buf) == hipSuccess ? 0 : KARMA_E_HIP;
 }
 extern "C" int karma_ab_wave_log(void* d_buf, uint64_t cap) {
     using namespace karma::engine;

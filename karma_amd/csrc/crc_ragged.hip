@@ -60,9 +60,9 @@ __device__ __forceinline__ uint32_t lines_of(const uint8_t* us, const uint8_t* u
     return (uint32_t)((ue - floor128(us) + kChunk - 1) / kChunk);
 }
 
-__device__ __forceinline__ RecUnits rec_units(const RaggedArgs& A, uint64_t r) {
+__device__ __forceinline__ RecUnits rec_units_at(const uint8_t* p, uint32_t n) {
     RecUnits u;
-    u.g = geom(A.arena + A.off[r], A.len[r]);
+    u.g = geom(p, n);
     u.k = u.full = 0;
     u.part0 = u.part1 = u.c0 = u.c1 = u.last = 0;
     if (!u.g.is_short) {
@@ -84,6 +84,9 @@ __device__ __forceinline__ RecUnits rec_units(const RaggedArgs& A, uint64_t r) {
         u.full = u.k - u.part0 - u.part1;
     }
     return u;
+}
+__device__ __forceinline__ RecUnits rec_units(const RaggedArgs& A, uint64_t r) {
+    return rec_units_at(A.arena + A.off[r], A.len[r]);
 }
 
 // Inclusive wave scan of 64-bit values.
@@ -129,16 +132,16 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
     if (valid) {
         A.fbase[r] = fb;
         if (u.part0) {
-            const uint64_t slot = atomicAdd(&cnt[u.c0], 1ull);
-            A.pslot[2 * r] = slot;
+            const uint64_t slot0 = atomicAdd(&cnt[u.c0], 1ull);
+            A.pslot[2 * r] = slot0;
             const uintptr_t e0 = ((A0 + 1) << kUShift) < b ? ((A0 + 1) << kUShift) : b;
-            if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a), h};
+            if (slot0 < A.unit_cap) A.desc[slot0] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a), h};
         }
         if (u.part1) {
-            const uint64_t slot = atomicAdd(&cnt[u.c1], 1ull);
-            A.pslot[2 * r + 1] = slot;
+            const uint64_t slot1 = atomicAdd(&cnt[u.c1], 1ull);
+            A.pslot[2 * r + 1] = slot1;
             const uintptr_t s1 = (A0 + u.k - 1) << kUShift;
-            if (slot < A.unit_cap) A.desc[slot] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1), 0u};
+            if (slot1 < A.unit_cap) A.desc[slot1] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1), 0u};
         }
     }
     // Full units of the wave's 64 records are consecutive slots: the wave writes them together,
@@ -184,6 +187,26 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_scan(RaggedArgs A) {
     }
 }
 
+#ifdef KARMA_AB  // tools build: per-workgroup phase stamps of the plan and finalize (karma_ab_plan_log)
+__device__ uint64_t* g_plan_log;
+constexpr uint64_t kPlanLogBlocks = 4096;  // plan blocks logged; finalize's from 8 * kPlanLogBlocks on
+#define PLAN_STAMP(base, i)                                                                    \
+    do {                                                                                       \
+        if (g_plan_log && threadIdx.x == 0 && blockIdx.x < kPlanLogBlocks)                     \
+            g_plan_log[(base) + blockIdx.x * 8 + (i)] = wall_clock64();                        \
+    } while (0)
+// ... after this wave's loads and stores have completed (the stamp of a phase whose memory
+// round trip is the point: wave 0 waits, the others run on)
+#define PLAN_STAMP_DONE(base, i)                                                               \
+    do {                                                                                       \
+        if (g_plan_log && threadIdx.x < 64) __builtin_amdgcn_s_waitcnt(0);                     \
+        PLAN_STAMP(base, i);                                                                   \
+    } while (0)
+#else
+#define PLAN_STAMP(base, i) ((void)0)
+#define PLAN_STAMP_DONE(base, i) ((void)0)
+#endif
+
 // ---- the single-pass plan ----------------------------------------------------
 // Block status words for the decoupled look-back (RaggedArgs::lb): seq << 42 | flag << 40 |
 // value.  The words are read and written with agent-scope atomics (cache-coherent across
@@ -222,11 +245,19 @@ __device__ __forceinline__ uint64_t lb_wait(unsigned long long* p, uint32_t seq)
     return w;
 }
 
-// Wave 0 of plan block b: publish the block's full and partial unit counts, sum the counts
+// Wave 0 of plan block b, its counts published (lb_publish): sum the counts
 // of the blocks before it (256 per step, newest first, each array until the first block that
 // has published its inclusive total there), publish the inclusive totals and return the
 // exclusive ones (uniform).  Every block it waits for has started (ids are taken in start
 // order) and publishes its own counts before waiting on anything, so the wait ends.
+// (lb_publish: the block's own counts, stored by the caller before it does other work)
+__device__ __forceinline__ void lb_publish(const RaggedArgs& A, uint32_t seq, uint64_t b, uint64_t full_b, uint64_t part_b) {
+    const uint64_t tag = (uint64_t)seq << 42;
+    if (b > 0 && (threadIdx.x & 63u) == 0) {
+        lb_store(A.lb + 1 + b, tag | kLbAgg | full_b);
+        lb_store(A.lbp + b, tag | kLbAgg | part_b);
+    }
+}
 __device__ void lookback(const RaggedArgs& A, uint32_t seq, uint64_t b, uint64_t full_b, uint64_t part_b,
                          uint64_t& exF, uint64_t& exP) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -235,10 +266,6 @@ __device__ void lookback(const RaggedArgs& A, uint32_t seq, uint64_t b, uint64_t
     unsigned long long* lp = A.lbp;
     exF = exP = 0;
     if (b > 0) {
-        if (lane == 0) {
-            lb_store(lf + b, tag | kLbAgg | full_b);
-            lb_store(lp + b, tag | kLbAgg | part_b);
-        }
         // 256 blocks per step: every lane's 4 loads go out together (an inclusive total
         // travels back 256 blocks per memory round trip instead of 64), then the windows are
         // taken nearest first; a word is waited for only if its window is reached.
@@ -297,19 +324,31 @@ __device__ void lookback_retire(const RaggedArgs& A) {
     }
 }
 
-// One pass over the records (one thread per record, plan block b = kScanBlock records):
-// unit counts, the slots of the block's units from the look-back, the entering register
-// over each record's unaligned head, and one 16-byte descriptor per unit.  Full units take
-// slots [0, F) in record order; partial units [part_base, part_base + P), each block's run
-// sorted by chunk count, longest first (the two-pass plan's order, which the units kernel
-// streams 3 % faster on configs[2] than block-interleaved runs).  Replaces round 1's
-// k_ragged_scan + k_ragged_desc: one launch, and no block reads every other block's totals.
+// One pass over the records (plan block b = R x kScanBlock records, thread t the records
+// (b R + i) kScanBlock + t, i < R): unit counts, the slots of the block's units from the
+// look-back, the entering register over each record's unaligned head, and one 16-byte
+// descriptor per unit.  Full units take slots [0, F) in record order; partial units
+// [part_base, part_base + P), each block's run sorted by chunk count, longest first (the
+// two-pass plan's order, which the units kernel streams 3 % faster on configs[2] than
+// block-interleaved runs).  Replaces round 1's k_ragged_scan + k_ragged_desc: one launch, and
+// no block reads every other block's totals.
+// R (launch_ragged_main): enough records per thread that the plan blocks fit on the GPU at once
+// (one per CU: 70 VGPRs).  A plan block is a chain of dependent memory round trips (its ticket,
+// offsets and lengths, the look-back, the head blocks, the descriptor stores, ~16 us), so a
+// second round of blocks doubles the plan: configs[2]'s 444 one-record blocks took 31 us, the
+// last ones starting 17 us late (profiles/r05_plan_phases.json).  The head blocks are loaded
+// with the offsets, before the scan and the look-back, not after them.
+template <int R>
 __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
-    KB_SET_ARENA(A.kb_lo, A.kb_hi);
+    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.comb_blob, A.comb_blob + kCombWords);  // the blob: edge loads' dummy address
+    PLAN_STAMP(0, 0);
+    constexpr int NW = kScanBlock / 64;
+    static_assert(R * NW <= 64, "one wave scans the block's wave totals");
+    static_assert(2 * R * kScanBlock < 65536, "partial units of a block fit the packed scan's low 16 bits");
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4, byte table
     __shared__ unsigned long long cnt[kBuckets];
     __shared__ uint32_t hist[kBuckets];
-    __shared__ uint64_t sm[kScanBlock / 64];
+    __shared__ uint64_t sm[R * NW];
     __shared__ uint64_t s_id, s_fbase;
     __shared__ uint32_t s_seq;
     if (threadIdx.x == 0) {
@@ -320,20 +359,82 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
     if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
     __syncthreads();
+    PLAN_STAMP(0, 1);  // id, tag and tables
     const uint64_t b = s_id;
-    const uint64_t r = b * kScanBlock + threadIdx.x;
-    const bool valid = r < A.n_rec;
-    RecUnits u{};
-    if (valid) {
-        u = rec_units(A, r);
-        if (u.part0) atomicAdd(&hist[u.c0], 1u);
-        if (u.part1) atomicAdd(&hist[u.c1], 1u);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    // per record only its pointer, length, init and edge blocks cross the barriers; the unit
+    // geometry is recomputed from them.  The edge blocks are loaded after every record's offset
+    // and length (vmcnt counts in order: the scan then waits for those alone), the head and the
+    // tail of a record together (in a WAL image a record's tail and the next one's head share a
+    // cache line: finalize no longer reads record bytes).
+    uint64_t packed[R];
+    auto rec = [&](int i) { return (b * R + i) * kScanBlock + threadIdx.x; };
+    // Every load is issued unconditionally (past the batch: the last record; no edge: the table
+    // blob): a load under a branch is waited for where the branches join, which would put the
+    // R records' round trips one after another.
+    const uint8_t* rp[R];
+    uint32_t rn[R], ini[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const uint64_t ri = rec(i) < A.n_rec ? rec(i) : A.n_rec - 1;
+        rp[i] = A.arena + A.off[ri];
+        const uint32_t n = A.len[ri];
+        rn[i] = rec(i) < A.n_rec ? n : 0u;
+        ini[i] = A.init ? A.init[ri] : A.init_scalar;
     }
-    // full units (high bits) and partial units (low 16 bits: at most 2 per record) in one scan
-    const uint64_t packed = valid ? (u.full << 16) | (u.part0 + u.part1) : 0;
-    uint64_t tot;
-    const uint64_t ex = block_excl_scan(packed, sm, tot) >> 16;  // has barriers (hist complete after)
+    PLAN_STAMP_DONE(0, 6);  // offsets and lengths landed
+    u32x4 hv[R], tv[R];  // the blocks holding each record's unaligned head and tail
+    const uint8_t* dummy = reinterpret_cast<const uint8_t*>(A.comb_blob);
+    // (Issued after the scan instead, the edge loads no longer hold up the block's scan, by ~8 us
+    // on configs[2], but take as long themselves: the call is no faster, profiles/r05_plan_edges_ab.txt.
+    // ~454K scattered 128-byte lines at the HBM's rate.)
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const Geom g = geom(rp[i], rn[i]);
+        const bool body = rec(i) < A.n_rec && !g.is_short;
+        hv[i] = ld16(body && rp[i] < g.a ? g.a - 16 : dummy);
+        tv[i] = ld16(body && g.e > g.b ? g.b : dummy);
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const RecUnits u = rec_units_at(rp[i], rn[i]);
+        const bool valid = rec(i) < A.n_rec;
+        if (valid && u.part0) atomicAdd(&hist[u.c0], 1u);
+        if (valid && u.part1) atomicAdd(&hist[u.c1], 1u);
+        // full units (high bits) and partial units (low 16 bits: at most 2 per record)
+        packed[i] = valid ? (u.full << 16) | (u.part0 + u.part1) : 0;
+    }
+    uint64_t incl[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        incl[i] = wave_incl_scan(packed[i]);
+        if (lane == 63) sm[i * NW + wave] = incl[i];
+    }
+    PLAN_STAMP(0, 7);  // counted, wave scans
+    __syncthreads();
+    if (wave == 0) {
+        uint64_t t = lane < R * NW ? sm[lane] : 0;
+        t = wave_incl_scan(t);
+        if (lane < R * NW) sm[lane] = t;
+    }
+    __syncthreads();  // (hist complete)
+    const uint64_t tot = sm[R * NW - 1];
     const uint64_t full_b = tot >> 16, part_b = tot & 0xffffu;
+    PLAN_STAMP(0, 2);  // offsets and lengths read, block scan
+    if (threadIdx.x < 64) lb_publish(A, s_seq, b, full_b, part_b);
+    // the edges while the other blocks publish theirs (and off the look-back's registers)
+    uint32_t h[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const Geom g = geom(rp[i], rn[i]);
+        h[i] = 0;
+        if (rec(i) < A.n_rec && !g.is_short) {
+            h[i] = ~ini[i];
+            if (rp[i] < g.a) h[i] = steps_in_vec(lds, 0, 1024, h[i], hv[i], (uint32_t)(rp[i] - (g.a - 16)), 16u);
+            A.tailc[rec(i)] = steps_in_vec(lds, 0, 1024, 0u, tv[i], 0u, (uint32_t)(g.e - g.b));
+        }
+    }
+    PLAN_STAMP(0, 3);  // edges stepped
     if (threadIdx.x < 64) {
         uint64_t exF, exP;
         lookback(A, s_seq, b, full_b, part_b, exF, exP);
@@ -350,10 +451,18 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
             }
         }
     }
-    uint32_t h = 0;
-    if (valid && u.k) h = head_register(lds, 0, 1024, A.arena + A.off[r], u.g, A.init ? A.init[r] : A.init_scalar);
     __syncthreads();
-    write_unit_descs(A, u, valid, r, s_fbase + ex, cnt, A.part_base, h);
+    PLAN_STAMP(0, 4);  // look-back
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const uint64_t run = (uint64_t)i * NW + wave;
+        const uint64_t ex = ((run ? sm[run - 1] : 0) + incl[i] - packed[i]) >> 16;
+        write_unit_descs(A, rec_units_at(rp[i], rn[i]), rec(i) < A.n_rec, rec(i), s_fbase + ex, cnt, A.part_base, h[i]);
+    }
+#ifdef KARMA_AB
+    __syncthreads();
+    PLAN_STAMP_DONE(0, 4 + 1);  // descriptors stored
+#endif
 }
 
 // Units of the batch in streaming order: u in [0, U).  Full units are slots [0, F); the
@@ -503,84 +612,151 @@ __device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, 
 // One lane per record: Horner fold of the unit contributions (Z_U between unit
 // ends, Z_last before the last unit), the unaligned tail, ~R.  Records of more
 // than 64 units: the whole wave folds all but the last unit with the 64-lane tree.
+// A wave takes FR x 64 consecutive records per pass (launch_ragged_main: enough that the grid
+// fits the GPU at once, as the plan), and a record's loads go out in two dependent rounds for
+// all FR of them: offsets, lengths, first-unit slot and partial slots (before the table fill),
+// then the first ten unit contributions (the tail bytes were stepped by the plan).  (Round 4's one-record lanes took
+// four dependent rounds -- geometry, slots, contributions, tail -- and 444 blocks of them two
+// rounds of blocks on configs[2]: 22 us, profiles/r05_plan_phases.json.)
+template <int FR>
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombWords];
-    if (A.lb) lookback_retire(A);
-    load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
-    __syncthreads();
+    PLAN_STAMP(8 * kPlanLogBlocks, 0);
+    constexpr int MID = FR >= 4 ? 2 : 8;  // middle-unit contributions loaded with the first and the last
     const uint32_t lane = threadIdx.x & 63u;
     constexpr uint64_t U = kU;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t r0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; r0 < A.n_rec;
-         r0 += nwaves * 64) {
-        const uint64_t r = r0 + lane;
-        const bool valid = r < A.n_rec;
-        RecUnits u{};
-        uint64_t fb = 0, ps0 = 0, ps1 = 0;
-        uint32_t init = 0;
-        const uint8_t* p = A.arena;
-        if (valid) {
-            u = rec_units(A, r);
-            fb = A.fbase[r];
-            if (u.part0) ps0 = A.pslot[2 * r];
-            if (u.part1) ps1 = A.pslot[2 * r + 1];
-            init = A.init ? A.init[r] : A.init_scalar;
-            p = A.arena + A.off[r];
+    const uint64_t full_cap = A.part_base ? A.part_base : A.unit_cap;
+    uint64_t r0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64 * FR;
+    // per record its pointer, length and slots; the unit geometry is recomputed from them
+    bool valid[FR];
+    uint32_t rn[FR], tc[FR];
+    uint64_t fb[FR], ps0[FR], ps1[FR];
+    const uint8_t* p[FR];
+    // (every load unconditional -- past the batch: the last record; no unit: slot 0 -- so the
+    // FR records' loads go out together: loads under branches are waited for at the join)
+    auto stage1 = [&](uint64_t base) {
+#pragma unroll
+        for (int j = 0; j < FR; ++j) {
+            const uint64_t r = base + (uint64_t)j * 64 + lane;
+            valid[j] = r < A.n_rec;
+            const uint64_t rc = valid[j] ? r : A.n_rec - 1;
+            p[j] = A.arena + A.off[rc];
+            const uint32_t n = A.len[rc];
+            rn[j] = valid[j] ? n : 0u;
+            tc[j] = A.tailc[rc];
+            fb[j] = A.fbase[rc];
+            ps0[j] = A.pslot[2 * rc];  // (read whether or not the unit is partial: no wait on the geometry)
+            ps1[j] = A.pslot[2 * rc + 1];
         }
-        const bool ok = valid && fb + u.full <= (A.part_base ? A.part_base : A.unit_cap) &&
-                        (!u.part0 || ps0 < A.unit_cap) &&
-                        (!u.part1 || ps1 < A.unit_cap);
-        uint32_t acc = 0;
-        bool huge = false;
-        if (ok && u.k > 0) {
-            if (u.k <= 64) {
-                acc = A.partial[unit_slot(0, u.k, fb, ps0, ps1, u.part0, u.part1)];
-                for (uint64_t j = 1; j + 1 < u.k; j += 8) {  // middle units: Z_U steps, 8 loads in flight
+    };
+    if (r0 < A.n_rec) stage1(r0);
+    load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
+    __syncthreads();
+    PLAN_STAMP(8 * kPlanLogBlocks, 1);  // tables
+    // the plan's look-back words are retired after the first contributions are issued: its
+    // control-word load waits for every load issued before it (vmcnt counts in order)
+    bool retired = !A.lb;
+    while (r0 < A.n_rec) {  // (wave-uniform)
+        bool ok[FR];
+        uint32_t first[FR], lastc[FR], mid[FR][MID];
+#pragma unroll
+        for (int j = 0; j < FR; ++j) {
+            const RecUnits u = rec_units_at(p[j], rn[j]);
+            ok[j] = valid[j] && fb[j] + u.full <= full_cap && (!u.part0 || ps0[j] < A.unit_cap) &&
+                    (!u.part1 || ps1[j] < A.unit_cap);
+            const uint64_t k = u.k;
+            const bool any = ok[j] && k > 0;
+            const uint64_t s0 = unit_slot(0, k, fb[j], ps0[j], ps1[j], u.part0, u.part1);
+            const uint64_t s1 = unit_slot(k - 1, k, fb[j], ps0[j], ps1[j], u.part0, u.part1);
+            first[j] = A.partial[any && k <= 64 ? s0 : 0];
+            lastc[j] = A.partial[any && k >= 2 ? s1 : 0];
+#pragma unroll
+            for (int q = 0; q < MID; ++q)
+                mid[j][q] = A.partial[ok[j] && k <= 64 && (uint64_t)q + 2 < k ? fb[j] + 1 + q - u.part0 : 0];
+        }
+        if (!retired) {
+            lookback_retire(A);
+            retired = true;
+        }
+        PLAN_STAMP_DONE(8 * kPlanLogBlocks, 2);  // (first pass) contributions loaded
+        // the FR records' Horner chains (serial LDS lookups) side by side, then the rare records
+        // of more than 64 units, then the last units, tails and stores
+        uint32_t acc[FR];
+        bool huge[FR];
+#pragma unroll
+        for (int j = 0; j < FR; ++j) {
+            const RecUnits u = rec_units_at(p[j], rn[j]);
+            const uint64_t k = u.k;
+            acc[j] = 0;
+            huge[j] = ok[j] && k > 64;
+            if (ok[j] && k > 0 && k <= 64) {
+                acc[j] = first[j];
+#pragma unroll
+                for (int q = 0; q < MID; ++q)
+                    if ((uint64_t)q + 2 < k) acc[j] = zmap(lds, 0, acc[j]) ^ mid[j][q];
+                for (uint64_t m = 1 + MID; m + 1 < k; m += 8) {  // more middle units: 8 loads in flight
                     uint32_t s[8];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) s[q] = j + q + 1 < u.k ? A.partial[fb + j + q - u.part0] : 0u;
+                    for (int q = 0; q < 8; ++q) s[q] = m + q + 1 < k ? A.partial[fb[j] + m + q - u.part0] : 0u;
 #pragma unroll
                     for (int q = 0; q < 8; ++q)
-                        if (j + q + 1 < u.k) acc = zmap(lds, 0, acc) ^ s[q];
+                        if (m + q + 1 < k) acc[j] = zmap(lds, 0, acc[j]) ^ s[q];
                 }
-            } else {
-                huge = true;
             }
         }
-        uint64_t hm = __ballot(huge);
-        while (hm) {
-            const int h = __ffsll((long long)hm) - 1;
-            hm &= hm - 1;
-            const uint64_t hk = __shfl(u.k, h) - 1;  // all units but the last
-            const uint64_t hfb = __shfl(fb, h), hps0 = __shfl(ps0, h);
-            const uint32_t hp0 = __shfl(u.part0, h);
-            const uint64_t nb = (hk + 63) / 64;
-            const int64_t pad = (int64_t)(nb * 64 - hk);
-            uint32_t w = 0;
-            for (uint64_t blk = 0; blk < nb; ++blk) {
-                const int64_t idx = (int64_t)(blk * 64 + lane) - pad;
-                uint32_t v = 0;
-                if (idx >= 0) v = A.partial[idx == 0 && hp0 ? hps0 : hfb + idx - hp0];
-                v = wave_tree(lds, v);
-                w = zmap(lds, 6 * 1024, w) ^ v;
+#pragma unroll
+        for (int j = 0; j < FR; ++j) {
+            uint64_t hm = __ballot(huge[j]);
+            while (hm) {
+                const int h = __ffsll((long long)hm) - 1;
+                hm &= hm - 1;
+                const RecUnits u = rec_units_at(p[j], rn[j]);
+                const uint64_t hk = __shfl(u.k, h) - 1;  // all units but the last
+                const uint64_t hfb = __shfl(fb[j], h), hps0 = __shfl(ps0[j], h);
+                const uint32_t hp0 = __shfl(u.part0, h);
+                const uint64_t nb = (hk + 63) / 64;
+                const int64_t pad = (int64_t)(nb * 64 - hk);
+                uint32_t w = 0;
+                for (uint64_t blk = 0; blk < nb; ++blk) {
+                    const int64_t idx = (int64_t)(blk * 64 + lane) - pad;
+                    uint32_t v = 0;
+                    if (idx >= 0) v = A.partial[idx == 0 && hp0 ? hps0 : hfb + idx - hp0];
+                    v = wave_tree(lds, v);
+                    w = zmap(lds, 6 * 1024, w) ^ v;
+                }
+                w = __shfl(w, 0);
+                if ((int)lane == h) acc[j] = w;
             }
-            w = __shfl(w, 0);
-            if ((int)lane == h) acc = w;
         }
-        if (ok && u.k >= 2)  // the last unit: shift by its own length
-            acc = shift_last(lds, acc, u.last, U) ^ A.partial[unit_slot(u.k - 1, u.k, fb, ps0, ps1, u.part0, u.part1)];
-        if (ok && u.k > 0) acc = tail_register(lds, kCombZ4, kCombT8, acc, u.g);  // the unaligned tail bytes
-        if (valid) {
-            uint32_t res;
-            if (ok && u.k > 0)
-                res = ~acc;
-            else  // a short record, or (the caller's total_len was low) one whose units did not
-                  // fit the table: this lane steps it alone -- slow, but never a wrong CRC
-                res = short_record(lds, kCombZ4, kCombT8, p, A.len[r], init);
-            A.out[r] = res;
+#pragma unroll
+        for (int j = 0; j < FR; ++j) {
+            const RecUnits u = rec_units_at(p[j], rn[j]);
+            const uint64_t r = r0 + (uint64_t)j * 64 + lane;
+            const uint64_t k = u.k;
+            uint32_t c = acc[j];
+            if (ok[j] && k >= 2) c = shift_last(lds, c, u.last, U) ^ lastc[j];  // the last unit: its own length
+            if (ok[j] && k > 0 && u.g.e > u.g.b)  // the unaligned tail bytes: Z_t, then the plan's steps over them
+                c = steps_in_vec(lds, kCombZ4, kCombT8, c, u32x4{0u, 0u, 0u, 0u}, 0u, (uint32_t)(u.g.e - u.g.b)) ^ tc[j];
+            if (valid[j]) {
+                uint32_t res;
+                if (ok[j] && k > 0)
+                    res = ~c;
+                else  // a short record, or (the caller's total_len was low) one whose units did not
+                      // fit the table: this lane steps it alone -- slow, but never a wrong CRC
+                    res = short_record(lds, kCombZ4, kCombT8, p[j], rn[j], A.init ? A.init[r] : A.init_scalar);
+                A.out[r] = res;
+            }
         }
+        r0 += nwaves * 64 * FR;
+        if (r0 < A.n_rec) stage1(r0);
     }
+    if (!retired) lookback_retire(A);  // (a wave with no records)
+#ifdef KARMA_AB
+    __syncthreads();
+    PLAN_STAMP_DONE(8 * kPlanLogBlocks, 3);  // records folded and stored
+#endif
 }
 
 // Batches of small records (WAL replay of short records, the bounded ragged ABI, the
@@ -853,23 +1029,40 @@ hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     if (!a.lb || !a.lb_ctl || a.lb_seq_max < 2 || a.lb_seq_max > (1u << 22)) return hipErrorInvalidValue;
-    const uint64_t nb = ragged_scan_blocks(a.n_rec);
-    hipLaunchKernelGGL(k_ragged_plan, dim3((unsigned)nb), dim3(kScanBlock), 0, s, a);
+    // records per plan thread / finalize lane: the fewest (1, 2, 4) that fit each grid on the GPU
+    // at once, one workgroup per CU (grid_blocks = the CU count); larger batches take rounds of 4
+    const uint64_t cu = grid_blocks > 0 ? (uint64_t)grid_blocks : 1;
+    const uint64_t nb1 = ragged_scan_blocks(a.n_rec);
+    const int R = nb1 <= cu ? 1 : nb1 <= 2 * cu ? 2 : 4;
+    const unsigned pb = (unsigned)((nb1 + R - 1) / R);
+    if (R == 1)
+        hipLaunchKernelGGL(k_ragged_plan<1>, dim3(pb), dim3(kScanBlock), 0, s, a);
+    else if (R == 2)
+        hipLaunchKernelGGL(k_ragged_plan<2>, dim3(pb), dim3(kScanBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_ragged_plan<4>, dim3(pb), dim3(kScanBlock), 0, s, a);
     units_timer_begin(s);
     hipLaunchKernelGGL(k_units_ragged<>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
-    uint64_t fblocks = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
-    // at most 2 per CU (each loads the 73 KiB combine image; one or four per CU measured no
-    // better: 0.7237 / 0.7229 vs 0.7225 ms, profiles/r02_ragged_finalize_grid_ab.txt)
-    const uint64_t cap = 2 * (uint64_t)grid_blocks;
-    if (fblocks > cap) fblocks = cap;
-    hipLaunchKernelGGL(k_ragged_finalize, dim3((unsigned)fblocks), dim3(1024), 0, s, a);
+    const uint64_t fb1 = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
+    const int FR = fb1 <= cu ? 1 : fb1 <= 2 * cu ? 2 : 4;
+    const unsigned fblocks = (unsigned)std::min<uint64_t>((fb1 + FR - 1) / FR, cu);
+    if (FR == 1)
+        hipLaunchKernelGGL(k_ragged_finalize<1>, dim3(fblocks), dim3(1024), 0, s, a);
+    else if (FR == 2)
+        hipLaunchKernelGGL(k_ragged_finalize<2>, dim3(fblocks), dim3(1024), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_ragged_finalize<4>, dim3(fblocks), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 
 KB_DEFINE_COLLECT(ragged)
 #ifdef KARMA_AB
 WLOG_SETTER(ragged)
+hipError_t set_plan_log(void* p) {
+    uint64_t* q = static_cast<uint64_t*>(p);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_plan_log), &q, sizeof(q));
+}
 #endif
 
 }  // namespace engine

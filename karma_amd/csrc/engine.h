@@ -135,6 +135,8 @@ struct RaggedArgs {
     uint64_t* fbase;           // n_rec + 2: slot of the record's first full unit;
                                //   [n_rec] = total units, [n_rec+1] = full units
     uint64_t* pslot;           // 2 * n_rec: slots of the record's partial first / last unit
+    uint32_t* tailc;           // n_rec: the record's unaligned tail bytes stepped from a zero register
+                               //   (k_ragged_plan, with the head; k_ragged_finalize applies Z_t and xors it)
     uint64_t* block_sums;      // per scan block: full-unit offset
     uint64_t* block_psums;     // per scan block: partial units (k_ragged_scan)
     // Single-pass plan (k_ragged_plan): decoupled look-back over per-block status words.
@@ -183,6 +185,7 @@ struct RaggedArgs {
 hipError_t set_wave_log_ragged(void* p, uint64_t cap);  // wavelog.h (tools build)
 hipError_t set_wave_log_fixed(void* p, uint64_t cap);
 hipError_t set_seg_log(void* p);  // k_segment_once's per-workgroup stamps (8 words each)
+hipError_t set_plan_log(void* p);  // k_ragged_plan's / k_ragged_finalize's (8 words per workgroup)
 #endif
 void units_timer_begin(hipStream_t s);
 void units_timer_end(hipStream_t s);
