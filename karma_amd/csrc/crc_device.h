@@ -48,6 +48,12 @@ constexpr uint32_t kSel1 = 0x0c0c0105u;  // {X.b1, acc.b1, 0, 0}
 constexpr uint32_t kSel2 = 0x0c070204u;  // {X.b0, acc.b2, X.b3, 0}
 constexpr uint32_t kSel3 = 0x0c070305u;  // {X.b1, acc.b3, X.b3, 0}
 
+// a ^ b ^ c in one VALU instruction (gfx950's v_bitop3_b32, truth table 0x96: the parity of the
+// three input bits); the compiler does not form it from xor chains by itself.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 __device__ __forceinline__ uint32_t lds_at_byte(const uint32_t* lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(lds) + byte_addr);
 }
@@ -58,7 +64,7 @@ __device__ __forceinline__ uint32_t stride_step(const uint32_t* lds, uint32_t X,
     const uint32_t i1 = __builtin_amdgcn_perm(X, acc, kSel1);
     const uint32_t i2 = __builtin_amdgcn_perm(X, acc, kSel2);
     const uint32_t i3 = __builtin_amdgcn_perm(X, acc, kSel3);
-    return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
+    return xor3(xor3(lds_at_byte(lds, i0), lds_at_byte(lds, i1), w), lds_at_byte(lds, i2), lds_at_byte(lds, i3));
 }
 
 // The half-replicated image (16 copies, 64 KiB; the fused WAL walker, which also needs LDS
@@ -76,7 +82,7 @@ __device__ __forceinline__ uint32_t stride_step16(const uint32_t* lds, uint32_t 
     const uint32_t i1 = __builtin_amdgcn_perm(X, acc, 0x0c0c0105u);  // {X.b1, acc.b1, 0, 0}
     const uint32_t i2 = __builtin_amdgcn_perm(X, acc, 0x0c0c0206u);  // {X.b2, acc.b2, 0, 0}
     const uint32_t i3 = __builtin_amdgcn_perm(X, acc, 0x0c0c0307u);  // {X.b3, acc.b3, 0, 0}
-    return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
+    return xor3(xor3(lds_at_byte(lds, i0), lds_at_byte(lds, i1), w), lds_at_byte(lds, i2), lds_at_byte(lds, i3));
 }
 
 // The same lookups with lanes 16-31 of each 32-lane half taking the tables in the order 1, 0, 3, 2:
@@ -91,7 +97,7 @@ __device__ __forceinline__ uint32_t stride_step16s(const uint32_t* lds, uint32_t
     const uint32_t i1 = __builtin_amdgcn_perm(X, acc, s1);
     const uint32_t i2 = __builtin_amdgcn_perm(X, acc, s2);
     const uint32_t i3 = __builtin_amdgcn_perm(X, acc, s3);
-    return lds_at_byte(lds, i0) ^ lds_at_byte(lds, i1) ^ lds_at_byte(lds, i2) ^ lds_at_byte(lds, i3) ^ w;
+    return xor3(xor3(lds_at_byte(lds, i0), lds_at_byte(lds, i1), w), lds_at_byte(lds, i2), lds_at_byte(lds, i3));
 }
 
 // The 8-copy image (32 KiB: entry e, table t, copy c at byte e<<7 | t<<5 | c<<2): lane L reads
@@ -128,7 +134,7 @@ __device__ __forceinline__ void load_rep8_stride(uint32_t* lds, const uint32_t* 
 
 // Z(x) for a map stored as four plain 256-entry tables at word `base`.
 __device__ __forceinline__ uint32_t zmap(const uint32_t* lds, int base, uint32_t x) {
-    return lds[base + (x & 255u)] ^ lds[base + 256 + ((x >> 8) & 255u)] ^ lds[base + 512 + ((x >> 16) & 255u)] ^
+    return xor3(lds[base + (x & 255u)], lds[base + 256 + ((x >> 8) & 255u)], lds[base + 512 + ((x >> 16) & 255u)]) ^
            lds[base + 768 + (x >> 24)];
 }
 

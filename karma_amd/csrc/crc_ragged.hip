@@ -118,6 +118,27 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
     return pre + inc - v;
 }
 
+// An LDS counter per key, bumped by the lanes that want it: when every such lane of the wave has
+// the same key (a batch of equal records: every lane of a plan block on one bucket, whose
+// same-word atomics serialise, ~6 us of the aligned 4 KiB plan) one lane adds their number and
+// the others take consecutive slots after it; otherwise one atomic per lane.  Returns the lane's
+// slot (the counter's value for it).  Every lane calls this.
+template <typename T>
+__device__ __forceinline__ T lds_bump(T* cnt, uint32_t key, bool want) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t m = __ballot(want);
+    if (!m) return 0;
+    const int l0 = __ffsll((long long)m) - 1;
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)key, l0);
+    if (__ballot(want && key == k0) == m) {  // (uniform)
+        T base = 0;
+        if ((int)lane == l0) base = atomicAdd(&cnt[k0], (T)__popcll(m));
+        base = (T)__shfl((long long)base, l0);
+        return base + (T)__popcll(m & (lane ? (~0ull >> (64u - lane)) : 0ull));
+    }
+    return want ? atomicAdd(&cnt[key], (T)1) : (T)0;
+}
+
 // The unit descriptors of the block's records (one thread per record, every lane of the wave
 // calls this).  fb: the slot of the record's first full unit; cnt: the block's partial-run
 // cursors by chunk count (LDS); full slots at or past full_cap and any slot at or past
@@ -129,16 +150,16 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
     const uint32_t lane = threadIdx.x & 63u;
     const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
     const uint64_t A0 = a >> kUShift;
+    const uint64_t slot0 = lds_bump(cnt, u.c0, valid && u.part0);
+    const uint64_t slot1 = lds_bump(cnt, u.c1, valid && u.part1);
     if (valid) {
         A.fbase[r] = fb;
         if (u.part0) {
-            const uint64_t slot0 = atomicAdd(&cnt[u.c0], 1ull);
             A.pslot[2 * r] = slot0;
             const uintptr_t e0 = ((A0 + 1) << kUShift) < b ? ((A0 + 1) << kUShift) : b;
             if (slot0 < A.unit_cap) A.desc[slot0] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a), h};
         }
         if (u.part1) {
-            const uint64_t slot1 = atomicAdd(&cnt[u.c1], 1ull);
             A.pslot[2 * r + 1] = slot1;
             const uintptr_t s1 = (A0 + u.k - 1) << kUShift;
             if (slot1 < A.unit_cap) A.desc[slot1] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1), 0u};
@@ -399,8 +420,8 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     for (int i = 0; i < R; ++i) {
         const RecUnits u = rec_units_at(rp[i], rn[i]);
         const bool valid = rec(i) < A.n_rec;
-        if (valid && u.part0) atomicAdd(&hist[u.c0], 1u);
-        if (valid && u.part1) atomicAdd(&hist[u.c1], 1u);
+        (void)lds_bump(hist, u.c0, valid && u.part0);
+        (void)lds_bump(hist, u.c1, valid && u.part1);
         // full units (high bits) and partial units (low 16 bits: at most 2 per record)
         packed[i] = valid ? (u.full << 16) | (u.part0 + u.part1) : 0;
     }
@@ -822,7 +843,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // the next call's form from this one's records.
 // R8 (plain stage only): the 8-copy stride image (32 KiB, stride_step8) instead of the 16-copy
 // one, so kStgWaves8 waves' stages fit the LDS (the plain form's 146 VGPRs allow 3 waves per SIMD).
-template <bool SK, bool R8 = false>
+// TM (timing attribution, tools build only, wrong CRCs): 1 = no CRC steps (each lane xors one
+// stage word into its result), 2 = no record loads or stage stores (the steps run over whatever
+// the stage holds), 3 = neither.
+template <bool SK, bool R8 = false, int TM = 0>
 __global__ __launch_bounds__((R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     static_assert(!(SK && R8), "the 8-copy form has the plain stage only");
     constexpr bool END = true;
@@ -874,6 +898,7 @@ __global__ __launch_bounds__((R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_s
     };
     u32x4 v[kStgVecs];
     auto issue = [&](uintptr_t lo, uintptr_t hi) {
+        if constexpr ((TM & 2) != 0) return;
         const uint32_t nv = (uint32_t)((hi - lo) / 16);
 #pragma unroll
         for (int q = 0; q < kStgVecs; ++q) {
@@ -904,7 +929,7 @@ __global__ __launch_bounds__((R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_s
     bool sk = fits && skewed(o, n, lo);
     if (fits) issue(lo, hi);
     for (;;) {
-        if (fits) {
+        if (fits && (TM & 2) == 0) {
 #pragma unroll
             for (int q = 0; q < kStgVecs; ++q) {
                 uint32_t at = kLead + 16u * (lane + 64u * q);
@@ -938,7 +963,9 @@ __global__ __launch_bounds__((R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_s
         if (ri < n_rec) {
             uint32_t res = ini;
             const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
-            if (n) {
+            if (n && (TM & 1) != 0) {
+                res = ini ^ stage32[(kLead + (uint32_t)(p - lo)) / 4];
+            } else if (n) {
                 if (fits && END && n >= 4 && sk)
                     res = lane_record_end<SMODE>(lds, X, Z4, kLead + (uint32_t)(p - lo), n, ini,
                                                  [&](uint32_t q) { return stage32[q + (q >> 5)]; });
@@ -982,8 +1009,20 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
     // the tests hold it to parity on batches of every shape; the caller passes the lane blob)
     if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 20)
         hipLaunchKernelGGL((k_ragged_staged_pipe<true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
-    else if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 21)  // (the plain stage only)
-        hipLaunchKernelGGL((k_ragged_staged_pipe<false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 21) {  // (the plain stage only)
+#ifdef KARMA_AB
+        // (KARMA_STAGE_TIMING: the timing forms, k_ragged_staged_pipe's TM)
+        const long tm = KARMA_AB_KNOB("KARMA_STAGE_TIMING", 0);
+        if (tm == 1)
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 1>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        else if (tm == 2)
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 2>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        else if (tm == 3)
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 3>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        else
+#endif
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    }
 #ifdef KARMA_AB
     else if (KARMA_AB_KNOB("KARMA_DIRECT_VARIANT", 0) == 22)  // (the 8-copy image, kStgWaves8 waves)
         hipLaunchKernelGGL((k_ragged_staged_pipe<false, true>), dim3(grid_blocks), dim3(kStgWaves8 * 64), 0, s, a);
@@ -998,6 +1037,11 @@ hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStr
     if (a.n_rec == 0 || !a.n_dev || !a.gate_len) return hipErrorInvalidValue;
     // (round 5 measured two batches' loads in flight per wave, a depth-2 variant of this kernel,
     // slower: 0.1229 vs 0.1201 ms per 1M x 180 B replay call, profiles/r05_replay_depth2.txt)
+    // (Round 5 measured two lanes per record -- a wave staging 32 records in 6 KiB, each lane
+    // stepping half a record's windows, 12 waves per CU: 49.2 against 51.2 us on 1M x 180 B, and
+    // no faster per replay call, 0.1179 vs 0.1183 ms: profiles/r05_staged_probe_pair.json,
+    // r05_replay_pair.txt.  The staged kernel is bound by its staging round trips as much as by its
+    // steps.)
     if (skew) {
         hipLaunchKernelGGL((k_ragged_staged_pipe<true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
 #ifdef KARMA_AB
