@@ -367,8 +367,11 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     static_assert(R * NW <= 64, "one wave scans the block's wave totals");
     static_assert(2 * R * kScanBlock < 65536, "partial units of a block fit the packed scan's low 16 bits");
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4, byte table
-    __shared__ unsigned long long cnt[kBuckets];
-    __shared__ uint32_t hist[kBuckets];
+    // per round i (records (b R + i) kScanBlock + t): the partial runs are cut per kScanBlock
+    // records, so the descriptor table is laid out as with one record per thread (the units kernel
+    // measured the same either way: profiles/r05_plan_r1.txt, r05h_ragged.txt)
+    __shared__ unsigned long long cnt[R * kBuckets];
+    __shared__ uint32_t hist[R * kBuckets];
     __shared__ uint64_t sm[R * NW];
     __shared__ uint64_t s_id, s_fbase;
     __shared__ uint32_t s_seq;
@@ -378,7 +381,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
         if (s_id == 0) lb_store(A.lb_ctl + 1, s_seq);
     }
     copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
-    if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
+    if (threadIdx.x < R * kBuckets) hist[threadIdx.x] = 0;
     __syncthreads();
     PLAN_STAMP(0, 1);  // id, tag and tables
     const uint64_t b = s_id;
@@ -420,8 +423,8 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     for (int i = 0; i < R; ++i) {
         const RecUnits u = rec_units_at(rp[i], rn[i]);
         const bool valid = rec(i) < A.n_rec;
-        (void)lds_bump(hist, u.c0, valid && u.part0);
-        (void)lds_bump(hist, u.c1, valid && u.part1);
+        (void)lds_bump(hist + i * kBuckets, u.c0, valid && u.part0);
+        (void)lds_bump(hist + i * kBuckets, u.c1, valid && u.part1);
         // full units (high bits) and partial units (low 16 bits: at most 2 per record)
         packed[i] = valid ? (u.full << 16) | (u.part0 + u.part1) : 0;
     }
@@ -459,13 +462,27 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     if (threadIdx.x < 64) {
         uint64_t exF, exP;
         lookback(A, s_seq, b, full_b, part_b, exF, exP);
+        // the block's partial runs (round by round, longest bucket first): a wave scan of the
+        // R x kBuckets counts, PER consecutive ones per lane
+        {
+            constexpr int NB = R * kBuckets, PER = (NB + 63) / 64;
+            uint64_t loc[PER], sum = 0;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int o = (int)lane * PER + q, i = o / kBuckets, c = kBuckets - 1 - o % kBuckets;
+                loc[q] = o < NB ? hist[i * kBuckets + c] : 0u;
+                sum += loc[q];
+            }
+            unsigned long long run = A.part_base + exP + wave_incl_scan(sum) - sum;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int o = (int)lane * PER + q, i = o / kBuckets, c = kBuckets - 1 - o % kBuckets;
+                if (o < NB) cnt[i * kBuckets + c] = run;
+                run += loc[q];
+            }
+        }
         if (threadIdx.x == 0) {
             s_fbase = exF;
-            unsigned long long s = A.part_base + exP;  // the block's partial run, longest bucket first
-            for (int c = kBuckets - 1; c >= 0; --c) {
-                cnt[c] = s;
-                s += hist[c];
-            }
             if (b + 1 == gridDim.x) {
                 A.fbase[A.n_rec] = exF + full_b + exP + part_b;  // total units
                 A.fbase[A.n_rec + 1] = exF + full_b;             // full units
@@ -478,7 +495,8 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     for (int i = 0; i < R; ++i) {
         const uint64_t run = (uint64_t)i * NW + wave;
         const uint64_t ex = ((run ? sm[run - 1] : 0) + incl[i] - packed[i]) >> 16;
-        write_unit_descs(A, rec_units_at(rp[i], rn[i]), rec(i) < A.n_rec, rec(i), s_fbase + ex, cnt, A.part_base, h[i]);
+        write_unit_descs(A, rec_units_at(rp[i], rn[i]), rec(i) < A.n_rec, rec(i), s_fbase + ex, cnt + i * kBuckets,
+                         A.part_base, h[i]);
     }
 #ifdef KARMA_AB
     __syncthreads();
@@ -1070,6 +1088,9 @@ hipError_t launch_ragged_scan(const RaggedArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifndef KARMA_PLAN_RMAX
+#define KARMA_PLAN_RMAX 4  // most records per plan thread (a build-time A/B knob: 1 = round 4's one-record blocks)
+#endif
 hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
     if (a.n_rec == 0) return hipSuccess;
     if (!a.lb || !a.lb_ctl || a.lb_seq_max < 2 || a.lb_seq_max > (1u << 22)) return hipErrorInvalidValue;
@@ -1077,7 +1098,7 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     // at once, one workgroup per CU (grid_blocks = the CU count); larger batches take rounds of 4
     const uint64_t cu = grid_blocks > 0 ? (uint64_t)grid_blocks : 1;
     const uint64_t nb1 = ragged_scan_blocks(a.n_rec);
-    const int R = nb1 <= cu ? 1 : nb1 <= 2 * cu ? 2 : 4;
+    const int R = KARMA_PLAN_RMAX == 1 || nb1 <= cu ? 1 : KARMA_PLAN_RMAX == 2 || nb1 <= 2 * cu ? 2 : 4;
     const unsigned pb = (unsigned)((nb1 + R - 1) / R);
     if (R == 1)
         hipLaunchKernelGGL(k_ragged_plan<1>, dim3(pb), dim3(kScanBlock), 0, s, a);
