@@ -368,8 +368,10 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     static_assert(2 * R * kScanBlock < 65536, "partial units of a block fit the packed scan's low 16 bits");
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4, byte table
     // per round i (records (b R + i) kScanBlock + t): the partial runs are cut per kScanBlock
-    // records, so the descriptor table is laid out as with one record per thread (the units kernel
-    // measured the same either way: profiles/r05_plan_r1.txt, r05h_ragged.txt)
+    // records, so the descriptor table is laid out as with one record per thread.  (The event window
+    // around the units kernel still measures 0.2-2.3 % longer after an R > 1 plan on aligned
+    // layouts, with this layout or one bucket run per block; the calls are shorter:
+    // profiles/r05_plan_r1.txt, r05h_ragged.txt.)
     __shared__ unsigned long long cnt[R * kBuckets];
     __shared__ uint32_t hist[R * kBuckets];
     __shared__ uint64_t sm[R * NW];
