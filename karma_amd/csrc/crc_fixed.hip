@@ -314,7 +314,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     // The tables first, into LDS, and only then the chunk loads: issued together, the table loads
     // (L2 misses after the previous call's stream) queued at the memory channels behind the whole
     // grid's 64 MiB of chunk requests and landed ~10 us in, after the data, so no step overlapped
-    // the stream.  The call's tag, the grid's fold maps and the tail block are read after the steps.
+    // the stream.  (Round 5: the chunk loads issued after the table loads but before the table
+    // stores -- the stores then wait for the table loads alone -- measured 2 us slower per isolated
+    // 64 MiB call, profiles/r05_segment_early_ab.json.)  The call's tag, the grid's fold maps and the tail block are read after the steps.
     // 1. the table words this thread fills
     constexpr int NV16 = kRep16Words / 4, IT16 = NV16 / kBlockThreads;
     uint32_t e16[IT16];
