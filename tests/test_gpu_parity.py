@@ -160,6 +160,28 @@ def test_ragged_overlapping_large_and_end_of_buffer(raw, dev):
     _eq(got, oracle_lib.ragged_crcs(host, offs, lens))
 
 
+@pytest.mark.parametrize("n_small", [300_000, 1_200_000])
+def test_ragged_many_records_per_lane_with_huge_records(raw, dev, n_small):
+    """The plan and finalize with several records per thread / lane (300K records: R = FR = 2;
+    1.2M: R = FR = 4, finalize lanes taking two passes), with records of more than 64 units
+    (the whole wave folds them) at the start, in the middle and at the end of the batch, empty
+    and short records among them, and per-record inits."""
+    host, dbuf = raw
+    rng = np.random.default_rng(n_small)
+    lens = rng.integers(0, 300, n_small).astype(np.uint32)
+    lens[rng.integers(0, n_small, 2000)] = rng.integers(0, 16, 2000)  # short records: finalize alone
+    huge_at = [0, 1, n_small // 3, n_small // 2 + 7, n_small - 2, n_small - 1]
+    lens[huge_at] = [(1 << 23) - 3, 1 << 22, (3 << 20) + 17, 600_000, 1 << 23, (5 << 20) + 1]
+    offs = (rng.integers(0, host.size - 300, n_small)).astype(np.uint64)
+    for i in huge_at:
+        offs[i] = int(rng.integers(0, host.size - int(lens[i]) + 1))
+    init = rng.integers(0, 1 << 32, n_small, dtype=np.uint64).astype(np.uint32)
+    got = K.extend_batch_ragged(dbuf, torch.from_numpy(offs.astype(np.int64)).to(dev),
+                                torch.from_numpy(lens.astype(np.int32)).to(dev),
+                                init=torch.from_numpy(init.view(np.int32)).to(dev), total_len=int(lens.sum()))
+    _eq(got.cpu().numpy(), oracle_lib.ragged_crcs(host, offs, lens, init))
+
+
 def test_empty_batches(dev):
     buf = torch.zeros(16, dtype=torch.uint8, device=dev)
     out = torch.full((1,), 7, dtype=torch.int32, device=dev)
