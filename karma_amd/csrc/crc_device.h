@@ -108,13 +108,13 @@ __device__ __forceinline__ uint32_t stride_step16s(const uint32_t* lds, uint32_t
 constexpr int kRep8Words = 8192;
 __device__ __forceinline__ uint32_t stride_step8(const uint32_t* lds, uint32_t acc, uint32_t w) {
     const uint32_t q = (threadIdx.x >> 3) & 3u, c4 = (threadIdx.x & 7u) << 2;
-    uint32_t r = w;
+    uint32_t l[4];
 #pragma unroll
     for (uint32_t i = 0; i < 4; ++i) {
         const uint32_t t = (i + q) & 3u;
-        r ^= lds_at_byte(lds, (__builtin_amdgcn_ubfe(acc, 8u * t, 8u) << 7) | (t << 5) | c4);
+        l[i] = lds_at_byte(lds, (__builtin_amdgcn_ubfe(acc, 8u * t, 8u) << 7) | (t << 5) | c4);
     }
-    return r;
+    return xor3(xor3(l[0], l[1], w), l[2], l[3]);
 }
 template <int THREADS>
 __device__ __forceinline__ void load_rep8_stride(uint32_t* lds, const uint32_t* __restrict__ blob) {
