@@ -342,7 +342,10 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
         // (Chunk 0 under a branch, its injected word xored before the PF loads are issued: the
         // compiler then waits for chunk 0 before issuing them.  Issuing all PF + 1 loads together
         // (clamped, masked after) measured 0.7-1.2 % SLOWER on every ragged layout, and so did the
-        // kernel pipelined across units: profiles/r05_ragged_group_unit_pipe_ab.txt)
+        // kernel pipelined across units: profiles/r05_ragged_group_unit_pipe_ab.txt, DESIGN.md §4.
+        // Rechecked with a scheduling barrier after the PF loads, so that the ISA really has all
+        // seven chunk loads in flight before the first wait: still 0.5-0.8 % slower,
+        // profiles/r05_gue.txt.)
         {
             const bool ok = w >= us && w < ue;
             u32x4 v = ok ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
