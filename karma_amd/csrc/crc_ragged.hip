@@ -413,7 +413,9 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     const uint8_t* dummy = reinterpret_cast<const uint8_t*>(A.comb_blob);
     // (Issued after the scan instead, the edge loads no longer hold up the block's scan, by ~8 us
     // on configs[2], but take as long themselves: the call is no faster, profiles/r05_plan_edges_ab.txt.
-    // ~454K scattered 128-byte lines at the HBM's rate.)
+    // ~454K scattered 128-byte lines at the HBM's rate.  Issued after the look-back, with the
+    // offsets loaded beside the ticket's atomic: scan 4 us and look-back 4 us, but the edges then
+    // take 12 us alone and the call is 0.4 % slower, profiles/r05_plan_reorder_ab.txt.)
 #pragma unroll
     for (int i = 0; i < R; ++i) {
         const Geom g = geom(rp[i], rn[i]);
