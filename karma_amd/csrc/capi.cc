@@ -393,7 +393,7 @@ int fixed_locked(int dev, DevState& ds, const void* d_data, size_t rec_bytes, si
 
 // ---- ragged records -------------------------------------------------------
 struct RaggedLayout {
-    size_t fbase_off, pslot_off, tailc_off, sums_off, psums_off, desc_off, part_off, total;
+    size_t fbase_off, pslot_off, sums_off, psums_off, desc_off, part_off, total;
 };
 
 RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
@@ -401,8 +401,7 @@ RaggedLayout ragged_layout(uint64_t n_rec, uint64_t cap) {
     const uint64_t nb = ragged_scan_blocks(n_rec);
     L.fbase_off = 0;
     L.pslot_off = L.fbase_off + align256((n_rec + 2) * sizeof(uint64_t));
-    L.tailc_off = L.pslot_off + align256(2 * n_rec * sizeof(uint64_t));
-    L.sums_off = L.tailc_off + align256(n_rec * sizeof(uint32_t));
+    L.sums_off = L.pslot_off + align256(2 * n_rec * sizeof(uint64_t));
     L.psums_off = L.sums_off + align256(nb * sizeof(uint64_t));
     L.desc_off = L.psums_off + align256(nb * sizeof(uint64_t));
     L.part_off = L.desc_off + align256(cap * sizeof(UnitDesc));
@@ -414,7 +413,6 @@ void bind_ragged(RaggedArgs& a, void* ws, const RaggedLayout& L, uint64_t cap) {
     char* b = static_cast<char*>(ws);
     a.fbase = reinterpret_cast<uint64_t*>(b + L.fbase_off);
     a.pslot = reinterpret_cast<uint64_t*>(b + L.pslot_off);
-    a.tailc = reinterpret_cast<uint32_t*>(b + L.tailc_off);
     a.block_sums = reinterpret_cast<uint64_t*>(b + L.sums_off);
     a.block_psums = reinterpret_cast<uint64_t*>(b + L.psums_off);
     a.desc = reinterpret_cast<UnitDesc*>(b + L.desc_off);

@@ -314,6 +314,26 @@ __device__ __forceinline__ const uint8_t* floor_chunk(const uint8_t* p) {
     return reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(16 * G - 1));
 }
 
+// A 16-byte window with bytes [0, h) zeroed (h < 16), with its last t bytes zeroed (t < 16), and
+// with x xored into word k: the edges of a ragged record stepped over its whole 16-byte blocks.
+__device__ __forceinline__ u32x4 mask_head(const u32x4& v, uint32_t h) {
+    auto m = [&](uint32_t k) {
+        const int r = (int)h - 4 * (int)k;
+        return r <= 0 ? ~0u : r >= 4 ? 0u : (~0u << (8 * r));
+    };
+    return u32x4{v.x & m(0), v.y & m(1), v.z & m(2), v.w & m(3)};
+}
+__device__ __forceinline__ u32x4 mask_tail(const u32x4& v, uint32_t t) {
+    auto m = [&](uint32_t k) {
+        const int r = 16 - (int)t - 4 * (int)k;  // bytes of word k that stay
+        return r >= 4 ? ~0u : r <= 0 ? 0u : (~0u >> (8 * (4 - r)));
+    };
+    return u32x4{v.x & m(0), v.y & m(1), v.z & m(2), v.w & m(3)};
+}
+__device__ __forceinline__ u32x4 xor_word(const u32x4& v, uint32_t k, uint32_t x) {
+    return u32x4{v.x ^ (k == 0 ? x : 0u), v.y ^ (k == 1 ? x : 0u), v.z ^ (k == 2 ? x : 0u), v.w ^ (k == 3 ? x : 0u)};
+}
+
 // Register contribution of the 16-aligned span [us, ue).  The span is read in
 // 128-byte chunks on the ABSOLUTE 128-byte grid (every group load is one whole
 // cache line, whatever the span's alignment), 8 lanes per group, lane l owning
@@ -323,12 +343,15 @@ __device__ __forceinline__ const uint8_t* floor_chunk(const uint8_t* p) {
 // distance from ue: with m the lane holding the last window, lane l's end lies
 // 16*((m - l) mod 8) bytes before ue, and the group tree runs over the lanes
 // rotated by m + 1.  `inj` is xored into the word at `inj_at` (the body's first
-// word carries the record's entering register).  PF chunk loads stay in flight
+// word carries the record's entering register).  EDGES (the ragged units): the window at us
+// has its first `head` bytes zeroed and inj xored into its word head / 4, the window ending at
+// ue its last `tail` bytes zeroed (inj_at unused).  PF chunk loads stay in flight
 // per lane.  Every lane of the wave must call this (cross-lane shuffles); the
 // result is valid in group lane 0.
-template <int PF, bool NT>
+template <int PF, bool NT, bool EDGES = false>
 __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, uint32_t l, const uint8_t* us,
-                                               const uint8_t* ue, const uint8_t* inj_at, uint32_t inj) {
+                                               const uint8_t* ue, const uint8_t* inj_at, uint32_t inj,
+                                               uint32_t head = 0, uint32_t tail = 0) {
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     uint32_t m = kGroupLanes - 1;
     if (ue > us) {
@@ -349,7 +372,12 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
         {
             const bool ok = w >= us && w < ue;
             u32x4 v = ok ? ldg<NT>(w) : u32x4{0u, 0u, 0u, 0u};
-            if (w == inj_at) v.x ^= inj;
+            if constexpr (EDGES) {
+                if (w == ue - 16) v = mask_tail(v, tail);  // (a one-chunk unit's last window)
+                if (w == us) v = xor_word(mask_head(v, head), head >> 2, inj);
+            } else {
+                if (w == inj_at) v.x ^= inj;
+            }
             a0 = v.x;
             a1 = v.y;
             a2 = v.z;
@@ -373,6 +401,9 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
         }
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
+            if constexpr (EDGES) {
+                if (q == rem - 1 && l == m) nb[q] = mask_tail(nb[q], tail);  // the unit's last window
+            }
             if (q < rem - 1 || (q == rem - 1 && lok)) step4(lds, X, a0, a1, a2, a3, nb[q]);
         }
     }

@@ -43,11 +43,15 @@ constexpr uint64_t kU = kDefaultUnit;  // ragged units: absolute kU-byte boundar
 constexpr int kUShift = __builtin_ctzll(kDefaultUnit);
 static_assert((kU & (kU - 1)) == 0, "unit size is a power of two");
 
-// Unit layout of one record: the aligned body [a, b) cut at absolute multiples
-// of U = unit_bytes.  Unit j = [max(a, (A0+j)U), min(b, (A0+j+1)U)), A0 = a/U,
-// k = ceil(b/U) - A0.  Only the first and the last unit can be partial.
+// Unit layout of one record [p, e): its whole 16-byte blocks [a, b) = [floor16(p), ceil16(e))
+// (g.a, g.b; the h = p - a bytes before the record and the t = b - e after it are masked to zero
+// where the units kernel loads them), cut at absolute multiples of U = unit_bytes.  Unit j =
+// [max(a, (A0+j)U), min(b, (A0+j+1)U)), A0 = a/U, k = ceil(b/U) - A0.  Only the first and the
+// last unit can be partial.  Records with no aligned 16-byte block inside (g.is_short) have no
+// units: finalize steps them alone.
 struct RecUnits {
     Geom g;
+    uint32_t h, t;   // masked head / tail bytes (< 16)
     uint64_t k;      // units (0 for short records: finalize does them alone)
     uint64_t full;   // full units
     uint32_t part0;  // 1 if unit 0 is partial
@@ -65,7 +69,12 @@ __device__ __forceinline__ RecUnits rec_units_at(const uint8_t* p, uint32_t n) {
     u.g = geom(p, n);
     u.k = u.full = 0;
     u.part0 = u.part1 = u.c0 = u.c1 = u.last = 0;
+    u.h = u.t = 0;
     if (!u.g.is_short) {
+        u.g.a = floor16(p);  // the whole blocks
+        u.g.b = ceil16(u.g.e);
+        u.h = (uint32_t)(p - u.g.a);
+        u.t = (uint32_t)(u.g.b - u.g.e);
         constexpr uint64_t U = kU;
         const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
         const uint64_t A0 = a >> kUShift, A1 = (b + U - 1) >> kUShift;
@@ -143,26 +152,28 @@ __device__ __forceinline__ T lds_bump(T* cnt, uint32_t key, bool want) {
 // calls this).  fb: the slot of the record's first full unit; cnt: the block's partial-run
 // cursors by chunk count (LDS); full slots at or past full_cap and any slot at or past
 // unit_cap are dropped (a caller's total_len too low: k_ragged_finalize steps those records
-// alone).  The first unit carries h, the register entering the record's body (~init stepped
-// over the unaligned head bytes by the plan).
+// alone).  The first unit carries the masked head bytes u.h and inj (~init moved back over the
+// h % 4 masked bytes of its word by the plan), the last unit the masked tail bytes u.t.
 __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool valid, uint64_t r, uint64_t fb,
-                                 unsigned long long* cnt, uint64_t full_cap, uint32_t h) {
+                                 unsigned long long* cnt, uint64_t full_cap, uint32_t inj) {
     const uint32_t lane = threadIdx.x & 63u;
     const uintptr_t a = reinterpret_cast<uintptr_t>(u.g.a), b = reinterpret_cast<uintptr_t>(u.g.b);
     const uint64_t A0 = a >> kUShift;
+    const uint32_t hw = u.h << kDescHeadShift, tw = u.t << kDescTailShift;
     const uint64_t slot0 = lds_bump(cnt, u.c0, valid && u.part0);
     const uint64_t slot1 = lds_bump(cnt, u.c1, valid && u.part1);
     if (valid) {
         A.fbase[r] = fb;
-        if (u.part0) {
+        if (u.part0) {  // (with k == 1 also the last unit)
             A.pslot[2 * r] = slot0;
             const uintptr_t e0 = ((A0 + 1) << kUShift) < b ? ((A0 + 1) << kUShift) : b;
-            if (slot0 < A.unit_cap) A.desc[slot0] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a), h};
+            if (slot0 < A.unit_cap)
+                A.desc[slot0] = UnitDesc{(uint64_t)a, (uint32_t)(e0 - a) | hw | (u.k == 1 ? tw : 0u), inj};
         }
         if (u.part1) {
             A.pslot[2 * r + 1] = slot1;
             const uintptr_t s1 = (A0 + u.k - 1) << kUShift;
-            if (slot1 < A.unit_cap) A.desc[slot1] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1), 0u};
+            if (slot1 < A.unit_cap) A.desc[slot1] = UnitDesc{(uint64_t)s1, (uint32_t)(b - s1) | tw, 0u};
         }
     }
     // Full units of the wave's 64 records are consecutive slots: the wave writes them together,
@@ -180,10 +191,13 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
             if (__shfl(incl, o + s - 1) <= i) o += s;
         o = o < 63 ? o : 63;
         const uint64_t incl_o = __shfl(incl, o), full_o = __shfl(nfull, o), A0_o = __shfl(A0, o);
-        const uint32_t part0_o = __shfl(u.part0, o), h_o = __shfl(h, o);
+        const uint64_t k_o = __shfl(u.k, o);
+        const uint32_t part0_o = __shfl(u.part0, o), inj_o = __shfl(inj, o), hw_o = __shfl(hw, o), tw_o = __shfl(tw, o);
         const uint64_t j = i - (incl_o - full_o) + part0_o;  // unit index within the owner's record
         const uint64_t slot = F0 + i;
-        if (i < T && slot < full_cap) A.desc[slot] = UnitDesc{(A0_o + j) << kUShift, (uint32_t)kU, j == 0 ? h_o : 0u};
+        if (i < T && slot < full_cap)
+            A.desc[slot] = UnitDesc{(A0_o + j) << kUShift, (uint32_t)kU | (j == 0 ? hw_o : 0u) | (j + 1 == k_o ? tw_o : 0u),
+                                    j == 0 ? inj_o : 0u};
     }
 }
 
@@ -361,12 +375,12 @@ __device__ void lookback_retire(const RaggedArgs& A) {
 // with the offsets, before the scan and the look-back, not after them.
 template <int R>
 __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
-    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.comb_blob, A.comb_blob + kCombWords);  // the blob: edge loads' dummy address
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
     PLAN_STAMP(0, 0);
     constexpr int NW = kScanBlock / 64;
     static_assert(R * NW <= 64, "one wave scans the block's wave totals");
     static_assert(2 * R * kScanBlock < 65536, "partial units of a block fit the packed scan's low 16 bits");
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kCombCoreWords - kCombZ4];  // Z4, byte table
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2 * 1024];  // Z_1^-1, Z_2^-1
     // per round i (records (b R + i) kScanBlock + t): the partial runs are cut per kScanBlock
     // records, so the descriptor table is laid out as with one record per thread.  (The event window
     // around the units kernel still measures 0.2-2.3 % longer after an R > 1 plan on aligned
@@ -382,22 +396,20 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
         s_seq = (uint32_t)lb_load(A.lb_ctl) + 1u;  // this call's tag (RaggedArgs::lb_ctl)
         if (s_id == 0) lb_store(A.lb_ctl + 1, s_seq);
     }
-    copy_to_lds<kCombCoreWords - kCombZ4, kScanBlock>(lds, A.comb_blob + kCombZ4);
+    copy_to_lds<2 * 1024, kScanBlock>(lds, A.comb_blob + kCombInv);
     if (threadIdx.x < R * kBuckets) hist[threadIdx.x] = 0;
     __syncthreads();
     PLAN_STAMP(0, 1);  // id, tag and tables
     const uint64_t b = s_id;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    // per record only its pointer, length, init and edge blocks cross the barriers; the unit
-    // geometry is recomputed from them.  The edge blocks are loaded after every record's offset
-    // and length (vmcnt counts in order: the scan then waits for those alone), the head and the
-    // tail of a record together (in a WAL image a record's tail and the next one's head share a
-    // cache line: finalize no longer reads record bytes).
+    // per record only its pointer, length and init cross the barriers; the unit geometry is
+    // recomputed from them.  The plan reads no record bytes: the units kernel masks the bytes
+    // around a record in the blocks it loads anyway (group_unit's EDGES form).
     uint64_t packed[R];
     auto rec = [&](int i) { return (b * R + i) * kScanBlock + threadIdx.x; };
-    // Every load is issued unconditionally (past the batch: the last record; no edge: the table
-    // blob): a load under a branch is waited for where the branches join, which would put the
-    // R records' round trips one after another.
+    // Every load is issued unconditionally (past the batch: the last record): a load under a
+    // branch is waited for where the branches join, which would put the R records' round trips
+    // one after another.
     const uint8_t* rp[R];
     uint32_t rn[R], ini[R];
 #pragma unroll
@@ -409,20 +421,6 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
         ini[i] = A.init ? A.init[ri] : A.init_scalar;
     }
     PLAN_STAMP_DONE(0, 6);  // offsets and lengths landed
-    u32x4 hv[R], tv[R];  // the blocks holding each record's unaligned head and tail
-    const uint8_t* dummy = reinterpret_cast<const uint8_t*>(A.comb_blob);
-    // (Issued after the scan instead, the edge loads no longer hold up the block's scan, by ~8 us
-    // on configs[2], but take as long themselves: the call is no faster, profiles/r05_plan_edges_ab.txt.
-    // ~454K scattered 128-byte lines at the HBM's rate.  Issued after the look-back, with the
-    // offsets loaded beside the ticket's atomic: scan 4 us and look-back 4 us, but the edges then
-    // take 12 us alone and the call is 0.4 % slower, profiles/r05_plan_reorder_ab.txt.)
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-        const Geom g = geom(rp[i], rn[i]);
-        const bool body = rec(i) < A.n_rec && !g.is_short;
-        hv[i] = ld16(body && rp[i] < g.a ? g.a - 16 : dummy);
-        tv[i] = ld16(body && g.e > g.b ? g.b : dummy);
-    }
 #pragma unroll
     for (int i = 0; i < R; ++i) {
         const RecUnits u = rec_units_at(rp[i], rn[i]);
@@ -450,19 +448,18 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     const uint64_t full_b = tot >> 16, part_b = tot & 0xffffu;
     PLAN_STAMP(0, 2);  // offsets and lengths read, block scan
     if (threadIdx.x < 64) lb_publish(A, s_seq, b, full_b, part_b);
-    // the edges while the other blocks publish theirs (and off the look-back's registers)
-    uint32_t h[R];
+    // each record's injection: ~init moved back over the h % 4 masked bytes before the record
+    // within its first word (Z_1^-1, Z_2^-1; the record starts h bytes into its first block)
+    uint32_t inj[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-        const Geom g = geom(rp[i], rn[i]);
-        h[i] = 0;
-        if (rec(i) < A.n_rec && !g.is_short) {
-            h[i] = ~ini[i];
-            if (rp[i] < g.a) h[i] = steps_in_vec(lds, 0, 1024, h[i], hv[i], (uint32_t)(rp[i] - (g.a - 16)), 16u);
-            A.tailc[rec(i)] = steps_in_vec(lds, 0, 1024, 0u, tv[i], 0u, (uint32_t)(g.e - g.b));
-        }
+        const uint32_t hb = (uint32_t)(reinterpret_cast<uintptr_t>(rp[i]) & 3u);
+        uint32_t x = ~ini[i];
+        if (hb & 1u) x = zmap(lds, 0, x);
+        if (hb & 2u) x = zmap(lds, 1024, x);
+        inj[i] = x;
     }
-    PLAN_STAMP(0, 3);  // edges stepped
+    PLAN_STAMP(0, 3);  // injections
     if (threadIdx.x < 64) {
         uint64_t exF, exP;
         lookback(A, s_seq, b, full_b, part_b, exF, exP);
@@ -500,7 +497,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
         const uint64_t run = (uint64_t)i * NW + wave;
         const uint64_t ex = ((run ? sm[run - 1] : 0) + incl[i] - packed[i]) >> 16;
         write_unit_descs(A, rec_units_at(rp[i], rn[i]), rec(i) < A.n_rec, rec(i), s_fbase + ex, cnt + i * kBuckets,
-                         A.part_base, h[i]);
+                         A.part_base, inj[i]);
     }
 #ifdef KARMA_AB
     __syncthreads();
@@ -628,10 +625,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
         const uint64_t un = wb_next * kGroupsPerWave + grp;
         d = un < U ? load_desc(&KB_READ(A.desc, M.slot(un), A.unit_cap, kKbUnit)) : UnitDesc{0, 0, 0};
         const uint8_t* us = reinterpret_cast<const uint8_t*>(cur.us);
-        const uint32_t R = group_unit<PF, kRaggedNT>(lds, X, l, us, us + cur.span, us, cur.inj);
+        const uint32_t span = cur.span & kDescSpanMask;
+        const uint32_t R = group_unit<PF, kRaggedNT, true>(lds, X, l, us, us + span, us, cur.inj,
+                                                           (cur.span >> kDescHeadShift) & 15u,
+                                                           (cur.span >> kDescTailShift) & 15u);
         if (valid && l == 0) KB_WRITE(A.partial, M.slot(u), A.unit_cap, kKbUnit, R);
         WLOG_STEP();
-        WLOG_UNIT(valid && l == 0, cur.span);
+        WLOG_UNIT(valid && l == 0, span);
         wb = wb_next;
         u = un;
     }
@@ -653,14 +653,14 @@ __device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, 
 }
 
 // One lane per record: Horner fold of the unit contributions (Z_U between unit
-// ends, Z_last before the last unit), the unaligned tail, ~R.  Records of more
-// than 64 units: the whole wave folds all but the last unit with the 64-lane tree.
-// A wave takes FR x 64 consecutive records per pass (launch_ragged_main: enough that the grid
-// fits the GPU at once, as the plan), and a record's loads go out in two dependent rounds for
-// all FR of them: offsets, lengths, first-unit slot and partial slots (before the table fill),
-// then the first ten unit contributions (the tail bytes were stepped by the plan).  (Round 4's one-record lanes took
-// four dependent rounds -- geometry, slots, contributions, tail -- and 444 blocks of them two
-// rounds of blocks on configs[2]: 22 us, profiles/r05_plan_phases.json.)
+// ends, Z_last before the last unit), back over the t masked bytes after the record (Z_t^-1),
+// ~R.  Records of more than 64 units: the whole wave folds all but the last unit with the
+// 64-lane tree.  A wave takes FR x 64 consecutive records per pass (launch_ragged_main: enough
+// that the grid fits the GPU at once, as the plan), and a record's loads go out in two dependent
+// rounds for all FR of them: offsets, lengths, first-unit slot and partial slots (before the
+// table fill), then the first ten unit contributions.  No record bytes are read.  (Round 4's
+// one-record lanes took four dependent rounds -- geometry, slots, contributions, tail -- and 444
+// blocks of them two rounds of blocks on configs[2]: 22 us, profiles/r05_plan_phases.json.)
 template <int FR>
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     uint64_t r0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64 * FR;
     // per record its pointer, length and slots; the unit geometry is recomputed from them
     bool valid[FR];
-    uint32_t rn[FR], tc[FR];
+    uint32_t rn[FR];
     uint64_t fb[FR], ps0[FR], ps1[FR];
     const uint8_t* p[FR];
     // (every load unconditional -- past the batch: the last record; no unit: slot 0 -- so the
@@ -688,7 +688,6 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
             p[j] = A.arena + A.off[rc];
             const uint32_t n = A.len[rc];
             rn[j] = valid[j] ? n : 0u;
-            tc[j] = A.tailc[rc];
             fb[j] = A.fbase[rc];
             ps0[j] = A.pslot[2 * rc];  // (read whether or not the unit is partial: no wait on the geometry)
             ps1[j] = A.pslot[2 * rc + 1];
@@ -780,8 +779,11 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
             const uint64_t k = u.k;
             uint32_t c = acc[j];
             if (ok[j] && k >= 2) c = shift_last(lds, c, u.last, U) ^ lastc[j];  // the last unit: its own length
-            if (ok[j] && k > 0 && u.g.e > u.g.b)  // the unaligned tail bytes: Z_t, then the plan's steps over them
-                c = steps_in_vec(lds, kCombZ4, kCombT8, c, u32x4{0u, 0u, 0u, 0u}, 0u, (uint32_t)(u.g.e - u.g.b)) ^ tc[j];
+            if (ok[j] && k > 0) {  // back over the t masked bytes after the record: Z_t^-1 (t < 16)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if ((u.t >> i) & 1u) c = zmap(lds, kCombInv + i * 1024, c);
+            }
             if (valid[j]) {
                 uint32_t res;
                 if (ok[j] && k > 0)

@@ -57,7 +57,16 @@ constexpr int kCombSmallMaps = KARMA_RAGGED_UNIT > 8192 ? 10 : 9;  // Z_16n, n <
 // (a partial last unit is shorter than the unit: n = its length / 16 < unit / 16)
 static_assert((16ull << kCombSmallMaps) >= (unsigned long long)KARMA_RAGGED_UNIT,
               "finalize's last-unit maps Z_16n must reach a whole unit");
-constexpr int kCombWords = kCombSmall + kCombSmallMaps * 1024;
+// Z_1^-1, Z_2^-1, Z_4^-1, Z_8^-1 (the inverse zero-byte maps): ragged records are stepped over
+// their whole 16-byte blocks with the bytes outside the record masked to zero; the plan moves ~init
+// back over the 1-3 masked bytes before the record's start, finalize takes the register back over
+// the 0-15 masked bytes after its end.
+constexpr int kCombInv = kCombSmall + kCombSmallMaps * 1024;
+constexpr int kCombWords = kCombInv + 4 * 1024;
+// A unit descriptor's span word: bytes in the low 16 bits; for a record's first unit the masked head
+// bytes (the window at us holds h bytes before the record), for its last the masked tail bytes.
+constexpr uint32_t kDescSpanMask = 0xffffu, kDescHeadShift = 16, kDescTailShift = 20;
+static_assert(KARMA_RAGGED_UNIT < (1u << 16), "a unit's bytes fit the span word's low 16 bits");
 
 // ---- table blob of the one-block combine (k_combine_block) -----------------
 // For states of D bytes folded m per thread: Z_D (the in-thread Horner step),
@@ -106,12 +115,15 @@ struct FixedArgs {
     uint64_t comb_m;            // states per thread of the fused fold
 };
 
-// One unit of a ragged batch: the 16-aligned span [us, us + span) of a record body; inj is
-// xored into the span's first word: for the record's first unit the register entering the
-// body (~init stepped over the unaligned head bytes by the plan), else 0.
+// One unit of a ragged batch: the 16-aligned span [us, us + span) of a record's whole 16-byte
+// blocks.  span: bytes (kDescSpanMask), and for the record's first unit the head bytes h masked to
+// zero in the window at us (bits kDescHeadShift..+3), for its last unit the tail bytes t masked in
+// the window ending at us + span (bits kDescTailShift..+3).  inj is xored into word h / 4 of the
+// window at us: for the record's first unit ~init moved back over the h % 4 masked bytes before
+// the record (Z_{h%4}^-1(~init), the plan), else 0.
 struct UnitDesc {
     uint64_t us;
-    uint32_t span;  // bytes
+    uint32_t span;
     uint32_t inj;
 };
 static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
@@ -135,8 +147,6 @@ struct RaggedArgs {
     uint64_t* fbase;           // n_rec + 2: slot of the record's first full unit;
                                //   [n_rec] = total units, [n_rec+1] = full units
     uint64_t* pslot;           // 2 * n_rec: slots of the record's partial first / last unit
-    uint32_t* tailc;           // n_rec: the record's unaligned tail bytes stepped from a zero register
-                               //   (k_ragged_plan, with the head; k_ragged_finalize applies Z_t and xors it)
     uint64_t* block_sums;      // per scan block: full-unit offset
     uint64_t* block_psums;     // per scan block: partial units (k_ragged_scan)
     // Single-pass plan (k_ragged_plan): decoupled look-back over per-block status words.

@@ -49,6 +49,7 @@ void build_combine_blob(uint64_t unit_bytes, uint32_t* out) {
     for (int i = 0; i < 1024; ++i) out[kCombT8 + i] = 0;
     gf2::byte_table(out + kCombT8);
     for (int i = 0; i < kCombSmallMaps; ++i) gf2::slicing_tables(Map::zero_bytes(16ull << i), out + kCombSmall + i * 1024);
+    for (int i = 0; i < 4; ++i) gf2::slicing_tables(Map::inverse(Map::zero_bytes(1ull << i)), out + kCombInv + i * 1024);
 }
 
 }  // namespace engine

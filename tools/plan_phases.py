@@ -24,7 +24,7 @@ import karma_amd as K  # noqa: E402
 from karma_amd import _lib  # noqa: E402
 import synth  # noqa: E402
 
-PLAN = ["entry", "tables", "scan", "edges", "lookback", "descs"]
+PLAN = ["entry", "tables", "scan", "injections", "lookback", "descs"]
 FIN = ["entry", "tables", "loads", "records"]
 FIN_BASE = 8 * 4096
 
