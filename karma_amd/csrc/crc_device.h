@@ -346,9 +346,9 @@ __device__ __forceinline__ u32x4 xor_word(const u32x4& v, uint32_t k, uint32_t x
 // word carries the record's entering register).  EDGES (the ragged units): the window at us
 // has its first `head` bytes zeroed and inj xored into its word head / 4, the window ending at
 // ue its last `tail` bytes zeroed (inj_at unused).  PF chunk loads stay in flight
-// per lane.  Every lane of the wave must call this (cross-lane shuffles); the
-// result is valid in group lane 0.
-template <int PF, bool NT, bool EDGES = false>
+// per lane.  MODE: step4's and stream_unit's timing forms (tools build only, wrong results).
+// Every lane of the wave must call this (cross-lane shuffles); the result is valid in group lane 0.
+template <int PF, bool NT, bool EDGES = false, int MODE = 0>
 __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, uint32_t l, const uint8_t* us,
                                                const uint8_t* ue, const uint8_t* inj_at, uint32_t inj,
                                                uint32_t head = 0, uint32_t tail = 0) {
@@ -396,7 +396,7 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
 #pragma unroll
             for (int q = 0; q < PF; ++q) nb[q] = ldg<NT>(pmin(w + q * kChunk, lclamp));
 #pragma unroll
-            for (int q = 0; q < PF; ++q) step4(lds, X, a0, a1, a2, a3, cur[q]);
+            for (int q = 0; q < PF; ++q) step4<MODE>(lds, X, a0, a1, a2, a3, cur[q]);
             rem -= PF;
         }
 #pragma unroll
@@ -404,9 +404,10 @@ __device__ __forceinline__ uint32_t group_unit(const uint32_t* lds, uint32_t X, 
             if constexpr (EDGES) {
                 if (q == rem - 1 && l == m) nb[q] = mask_tail(nb[q], tail);  // the unit's last window
             }
-            if (q < rem - 1 || (q == rem - 1 && lok)) step4(lds, X, a0, a1, a2, a3, nb[q]);
+            if (q < rem - 1 || (q == rem - 1 && lok)) step4<MODE>(lds, X, a0, a1, a2, a3, nb[q]);
         }
     }
+    if constexpr ((MODE & 2) != 0) return a0 ^ a1 ^ a2 ^ a3;  // timing build only: no fold, no tree
     uint32_t c = lane_fold(lds, a0, a1, a2, a3);
     // rotate so the lane holding the last window comes last (identity when m == 7)
     const uint32_t lane = threadIdx.x & 63u;

@@ -44,7 +44,10 @@ def main():
     p.add_argument("--calls", type=int, default=10)
     p.add_argument("--no-log", action="store_true")
     p.add_argument("--json", default="")
+    p.add_argument("--lib", default="", help="another build of the library (e.g. a unit-size build)")
     a = p.parse_args()
+    if a.lib:
+        _lib.select(a.lib)
     L = _lib.lib()
     dev = torch.device("cuda:0")
     GB = 4 << 30

@@ -8,7 +8,8 @@ process, interleaved rounds.  Run on the GPU box from the repo root:
         python tools/ragged_study.py
 
 LIBS names the builds compared (name=path, comma-separated; default: the shipped library).  They
-are loaded side by side (each keeps its own kernels and state), so every layout runs through
+are loaded side by side (each keeps its own kernels and state; `name=path@KNOB=V;...` runs a build
+with A/B knobs set, e.g. a timing form of the tools build, whose CRCs then differ), so every layout runs through
 every build in the same process, rounds interleaved; every build's CRCs are compared with the
 first one's.  Builds, not environment knobs: the tools build's extra kernels change the register
 allocation of the kernels they share a file with.
@@ -27,9 +28,23 @@ from karma_amd import _lib  # noqa: E402
 import synth  # noqa: E402
 
 LIBS = {}
+KNOBS = {}  # name -> {knob: value}: name=path@KNOB=V;KNOB2=V2 runs that build with those A/B knobs set
+_loaded = {}
 for item in os.environ.get("LIBS", f"shipped={_lib.LIB_PATH}").split(","):
     name, _, path = item.partition("=")
-    LIBS[name] = _lib.load(path if os.path.isabs(path) else os.path.join(ROOT, path))
+    path, _, kn = path.partition("@")
+    path = path if os.path.isabs(path) else os.path.join(ROOT, path)
+    if path not in _loaded:
+        _loaded[path] = _lib.load(path)
+    LIBS[name] = _loaded[path]
+    KNOBS[name] = dict(kv.split("=", 1) for kv in kn.split(";") if kv)
+
+
+def set_knobs(name):
+    for kv in KNOBS.values():
+        for k in kv:
+            os.environ.pop(k, None)
+    os.environ.update(KNOBS.get(name, {}))
 dev = torch.device("cuda:0")
 GB = 4 << 30
 RAW = GB + (64 << 20)  # config 3 arena = 4.01 GiB of payload + 8-B headers
@@ -46,6 +61,7 @@ def fixed_case(L, rec):
     out = torch.empty(n, dtype=torch.uint32, device=dev)
 
     def run():
+        set_knobs(None)
         _lib.check("fixed", L.karma_crc32c_batch_fixed(raw.data_ptr(), rec, n, None, 0, out.data_ptr(), sh))
     return run, n * rec, out
 
@@ -53,7 +69,7 @@ def fixed_case(L, rec):
 _dev_layouts = {}
 
 
-def ragged_case(L, key, lens, offs):
+def ragged_case(L, key, lens, offs, lib_name=None):
     if key not in _dev_layouts:
         end = int((offs.astype(np.uint64) + lens.astype(np.uint64)).max())
         assert end <= RAW, f"layout ends at {end} > buffer {RAW}"  # checked on the host before any launch
@@ -63,6 +79,7 @@ def ragged_case(L, key, lens, offs):
     out = torch.empty(n, dtype=torch.uint32, device=dev)
 
     def run():
+        set_knobs(lib_name)
         _lib.check("ragged", L.karma_crc32c_batch_ragged(raw.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, total,
                                                          None, 0, out.data_ptr(), sh))
     return run, total, out
@@ -81,7 +98,7 @@ first = next(iter(LIBS))
 cases[f"fixed 4096 [{first}]"] = (fixed_case(LIBS[first], 4096), None)
 for name, (ln, of) in layouts.items():
     for lib_name, L in LIBS.items():
-        cases[f"ragged {name} [{lib_name}]"] = (ragged_case(L, name, ln, of), name)
+        cases[f"ragged {name} [{lib_name}]"] = (ragged_case(L, name, ln, of, lib_name), name)
 
 for name, ((run, nbytes, out), _) in cases.items():
     print("first call:", name, flush=True)
