@@ -735,9 +735,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_flat(RaggedArgs 
     auto desc_of = [&](uint64_t wstep, bool& valid) {  // unconditional: slot 0 stands in for no unit
         const uint64_t u = wstep * kGroupsPerWave + grp;
         valid = wstep < nws && u < U;
+        if constexpr ((MODE & 64) != 0)  // timing build only: unit u = arena bytes [u kU, (u + 1) kU), no loads
+            return UnitDesc{reinterpret_cast<uint64_t>(A.arena) + (valid ? u : 0) * kU, (uint32_t)kU, 0u};
         return load_desc(&KB_READ(A.desc, M.slot(valid ? u : 0), A.unit_cap, kKbUnit));
     };
-    const uint8_t* safe = reinterpret_cast<const uint8_t*>(load_desc(A.desc + M.slot(0)).us);
+    const uint8_t* safe = (MODE & 64) != 0 ? A.arena : reinterpret_cast<const uint8_t*>(load_desc(A.desc + M.slot(0)).us);
     uint64_t wn = ragged_next_step(A, &blk_next, blk_dyn, nidx, S, nws, bw0, nwaves, lane);
     uint64_t wd = ragged_next_step(A, &blk_next, blk_dyn, nidx, S, nws, bw0, nwaves, lane);
     bool vc, vn, vd;
@@ -778,7 +780,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_flat(RaggedArgs 
             t = __shfl_down(c, 4, kGroupLanes);
             c = zmap(lds, kLZ64, c) ^ t;
         }
-        if (vc && l == 0) KB_WRITE(A.partial, M.slot(wc * kGroupsPerWave + grp), A.unit_cap, kKbUnit, c);
+        if ((MODE & 128) == 0 && vc && l == 0)  // (MODE 128: timing build only, no store)
+            KB_WRITE(A.partial, M.slot(wc * kGroupsPerWave + grp), A.unit_cap, kKbUnit, c);
+        if constexpr ((MODE & 128) != 0)
+            if (c == 0x9e3779b9u && vc) A.partial[0] = c;  // (keeps the steps live)
         if (wn >= nws) break;
         cur = nxt;
         wc = wn;
@@ -1265,6 +1270,12 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
         hipLaunchKernelGGL(k_ragged_plan<2>, dim3(pb), dim3(kScanBlock), 0, s, a);
     else
         hipLaunchKernelGGL(k_ragged_plan<4>, dim3(pb), dim3(kScanBlock), 0, s, a);
+#ifdef KARMA_AB
+    // (timing: the timed units kernel follows an untimed one instead of the plan; only with
+    // KARMA_RAGGED_DYN=0 -- the first kernel takes the dynamic tail's counter to its end)
+    if (KARMA_AB_KNOB("KARMA_RAGGED_UNITS_TWICE", 0) && !a.dyn_shift)
+        hipLaunchKernelGGL(k_units_ragged<>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+#endif
     units_timer_begin(s);
 #ifdef KARMA_AB
     // timing forms (wrong results): 1 = steps without the LDS lookups, 2 = no lane fold / tree, 3 = both
@@ -1274,6 +1285,12 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
         hipLaunchKernelGGL((k_units_ragged_flat<4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (fl == 83)
         hipLaunchKernelGGL((k_units_ragged_flat<8, 3>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (fl == 864)  // arithmetic unit addresses (aligned unit-sized records only), no descriptor loads
+        hipLaunchKernelGGL((k_units_ragged_flat<8, 64>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (fl == 8128)  // no unit-state stores
+        hipLaunchKernelGGL((k_units_ragged_flat<8, 128>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (fl == 8192)  // both
+        hipLaunchKernelGGL((k_units_ragged_flat<8, 192>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (const int um = KARMA_AB_KNOB("KARMA_RAGGED_UNITS_MODE", 0); um == 1)
         hipLaunchKernelGGL((k_units_ragged<kRaggedUnitsPF, 1>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (um == 2)

@@ -245,7 +245,8 @@ def test_shipped_library_has_no_variant_knobs():
                  b"KARMA_FINALIZE_PER_CU", b"KARMA_WAL_LIST_CRC", b"KARMA_SMALL_STAGED", b"KARMA_APPEND_CALL_BYTES", b"KARMA_WALK_DIRECT",
                  b"KARMA_RAGGED_DYN", b"KARMA_GATHER_PARTS", b"KARMA_SMALL_WHICH",
                  b"KARMA_STAGE_SKEW", b"KARMA_STAGE_R8", b"KARMA_SEGMENT_ONCE", b"KARMA_RAGGED_GRID",
-                 b"KARMA_STAGE_TIMING", b"KARMA_STAGE_PAIR", b"KARMA_RAGGED_UNITS_MODE"):
+                 b"KARMA_STAGE_TIMING", b"KARMA_STAGE_PAIR", b"KARMA_RAGGED_UNITS_MODE", b"KARMA_RAGGED_UNITS_FLAT",
+                 b"KARMA_RAGGED_UNITS_TWICE"):
         assert knob not in blob, knob
 
 

@@ -12,7 +12,8 @@ for CL in $CASES; do
   C=${CL%%@*}
   LIBARG=()
   if [[ "$CL" == *@* ]]; then LIBARG=(--lib "$REPO/${CL#*@}"); fi
-  NAME=$C$( [[ "$CL" == *@* ]] && basename "${CL#*@}" .so | sed 's/libkarma_crc32c//' )
+  NAME=$C
+  if [[ "$CL" == *@* ]]; then NAME=$C$(basename "${CL#*@}" .so | sed 's/libkarma_crc32c//'); fi
   OUT=$REPO/gpurun_out/pmc_mem_$TAG/$NAME
   mkdir -p "$OUT"
   cd /tmp

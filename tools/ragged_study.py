@@ -93,6 +93,8 @@ o2, _ = synth.ragged_layout(srt, header=8)
 layouts = {"aligned 4096": (np.full(GB // 4096, 4096, np.uint32), np.arange(GB // 4096, dtype=np.uint64) * 4096),
            "aligned 2048": (np.full(GB // 2048, 2048, np.uint32), np.arange(GB // 2048, dtype=np.uint64) * 2048),
            "config3": (lens, offs), "config3 sorted desc": (srt, o2)}
+if os.environ.get("LAYOUTS"):  # a subset, e.g. LAYOUTS="aligned 4096,aligned 2048"
+    layouts = {k: v for k, v in layouts.items() if k in os.environ["LAYOUTS"].split(",")}
 cases = {}
 first = next(iter(LIBS))
 cases[f"fixed 4096 [{first}]"] = (fixed_case(LIBS[first], 4096), None)
