@@ -638,6 +638,26 @@ __device__ __forceinline__ void copy_to_lds(uint32_t* lds, const uint32_t* __res
     }
 }
 
+template <int WORDS, int THREADS>
+struct LdsCopy {  // a global -> LDS copy split in two: the loads, then (after other loads) the stores
+    static constexpr int N4 = WORDS / 4, IT = (N4 + THREADS - 1) / THREADS;
+    u32x4 v[IT];
+    __device__ __forceinline__ void load(const uint32_t* __restrict__ g) {
+#pragma unroll
+        for (int q = 0; q < IT; ++q) {  // (clamped, not branched: a load under a branch is waited for at the join)
+            const int i = (int)threadIdx.x + q * THREADS;
+            v[q] = *(const gu32x4*)(reinterpret_cast<const u32x4*>(g) + (i < N4 ? i : N4 - 1));
+        }
+    }
+    __device__ __forceinline__ void store(uint32_t* lds) const {
+#pragma unroll
+        for (int q = 0; q < IT; ++q) {
+            const int i = (int)threadIdx.x + q * THREADS;
+            if (i < N4) reinterpret_cast<u32x4*>(lds)[i] = v[q];
+        }
+    }
+};
+
 // The streaming kernels' LDS image (kBlockThreads threads).
 __device__ __forceinline__ void load_stream_tables(uint32_t* lds, const uint32_t* __restrict__ blob) {
     static_assert(kSmallWords % 4 == 0 && (kRepWords / 4) % kBlockThreads == 0, "table copy shape");

@@ -276,25 +276,6 @@ __device__ uint64_t* g_seg_log;
 #define SEG_STAMP(i) ((void)0)
 #endif
 
-template <int WORDS, int THREADS>
-struct LdsCopy {  // a global -> LDS copy split in two: the loads, then (after other loads) the stores
-    static constexpr int N4 = WORDS / 4, IT = (N4 + THREADS - 1) / THREADS;
-    u32x4 v[IT];
-    __device__ __forceinline__ void load(const uint32_t* __restrict__ g) {
-#pragma unroll
-        for (int q = 0; q < IT; ++q) {  // (clamped, not branched: a load under a branch is waited for at the join)
-            const int i = (int)threadIdx.x + q * THREADS;
-            v[q] = *(const gu32x4*)(reinterpret_cast<const u32x4*>(g) + (i < N4 ? i : N4 - 1));
-        }
-    }
-    __device__ __forceinline__ void store(uint32_t* lds) const {
-#pragma unroll
-        for (int q = 0; q < IT; ++q) {
-            const int i = (int)threadIdx.x + q * THREADS;
-            if (i < N4) reinterpret_cast<u32x4*>(lds)[i] = v[q];
-        }
-    }
-};
 
 // ARRIVE: the workgroup that arrives last folds (one ticket per workgroup from fctl[0] after its
 // state is published; the last ticket resets the counter), instead of the grid's highest-index

@@ -851,6 +851,9 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
             ps1[j] = A.pslot[2 * rc + 1];
         }
     };
+    // (Round 5 measured the first pass's unit-state loads issued before the table stores, so the
+    // table fill and those loads share a round trip: finalize 13.1 against 12.6 us, calls equal,
+    // profiles/r05_finalize_overlap_ab.txt -- its first loads are bandwidth, not latency.)
     if (r0 < A.n_rec) stage1(r0);
     load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
     __syncthreads();
