@@ -639,6 +639,88 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
 }
 
 
+#ifdef KARMA_AB
+// Tools build: k_units_fixed's own loop (stream_unit: the next unit's loads issued before the
+// current unit's last batch; the block's wave-steps from an LDS counter, no dynamic tail) over the
+// ragged units.  ARITH: unit u = arena bytes [u kU, (u + 1) kU) (aligned unit-sized layouts only,
+// timing: wrong CRCs elsewhere); else the units from the descriptor list (edges not masked: exact
+// only for records on 16-byte boundaries with 16-byte multiple lengths).
+// BIG: the fixed kernel's larger LDS allocation (kLdsWordsComb); HT: its head / tail block loads
+// per unit (both at the unit's first window here).
+template <bool ARITH, bool BIG = false, bool HT = false>
+__global__ __launch_bounds__(kBlockThreads) void k_units_ragged_fixedloop(RaggedArgs A) {
+    constexpr int PF = 4;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BIG ? kLdsWordsComb : kLdsWords];
+    __shared__ uint32_t blk_next;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & (kGroupLanes - 1);
+    const uint32_t grp = lane / kGroupLanes;
+    const uint32_t X = lane_const();
+    const UnitMap M = unit_map(A);
+    const uint64_t U = M.U;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
+    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
+    const uint32_t nidx = (uint32_t)((nws + nwaves - 1) / nwaves) * kWavesPerBlock;
+    if (threadIdx.x == 0) blk_next = kWavesPerBlock;
+    uint64_t wb = bw0 + (threadIdx.x >> 6);
+    // (ARITH: no unit past the last record's end, whatever U is)
+    const uint64_t arena_end = ARITH ? A.off[A.n_rec - 1] + A.len[A.n_rec - 1] : 0;
+    auto unit_of = [&](uint64_t w, bool& valid) {
+        const uint64_t u = w * kGroupsPerWave + grp;
+        valid = w < nws && u < U && (!ARITH || (u + 1) * kU <= arena_end);
+        const uint64_t uu = valid ? u : 0;
+        const uint8_t* us;
+        uint32_t span;
+        if constexpr (ARITH) {
+            us = A.arena + uu * kU;
+            span = (uint32_t)kU;
+        } else {
+            const UnitDesc d = load_desc(A.desc + M.slot(uu));
+            us = reinterpret_cast<const uint8_t*>(d.us);
+            span = d.span & kDescSpanMask;
+        }
+        if (!valid) span = 0;
+        return lane_unit(us, us + span, l);
+    };
+    bool valid;
+    LaneUnit L = unit_of(wb, valid);
+    u32x4 hv = u32x4{0u, 0u, 0u, 0u}, tv = hv;
+    if constexpr (HT) {
+        hv = ld16(L.us);
+        tv = ld16(L.us);
+    }
+    UnitLoads<PF> Ld;
+    issue_unit_loads<PF, kRaggedNT>(L, Ld);
+    load_stream_tables(lds, A.blob);
+    if constexpr (BIG) copy_to_lds<3 * 1024, kBlockThreads>(lds + kLdsWords, A.blob);
+    __syncthreads();
+    for (; wb < nws;) {
+        LaneUnit N;
+        bool nvalid = false;
+        uint64_t wb_next = nws;
+        const uint32_t R = stream_unit<PF, kRaggedNT>(lds, X, l, L, Ld, nullptr, 0u, [&](UnitLoads<PF>& nx) {
+            uint32_t i = 0;
+            if (lane == 0) i = atomicAdd(&blk_next, 1u);
+            i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
+            wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
+            N = unit_of(wb_next, nvalid);
+            if constexpr (HT) {
+                hv = ld16(N.us);
+                tv = ld16(N.us);
+            }
+            issue_unit_loads<PF, kRaggedNT>(N, nx);
+        });
+        if constexpr (HT)  // (keeps the head / tail loads; timing only)
+            if (hv.x == 0x9e3779b9u && tv.y == 0x7f4a7c15u) A.partial[0] = 0u;
+        if (valid && l == 0) A.partial[M.slot(wb * kGroupsPerWave + grp)] = R;
+        L = N;
+        valid = nvalid;
+        wb = wb_next;
+    }
+}
+#endif
+
 // ---- the units kernel as one chunk stream per wave -------------------------------------------------
 // k_units_ragged waits on memory three times per unit with one load in flight (its ISA: the next
 // descriptor, copied into the loop's registers right after its load, s_waitcnt vmcnt(0); chunk 0,
@@ -732,11 +814,14 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_flat(RaggedArgs 
     const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
     uint64_t wc = bw0 + (threadIdx.x >> 6);
     if (wc >= nws) return;  // (wave-uniform; U > 0 here)
+    const uint64_t arena_end = (MODE & 64) != 0 ? A.off[A.n_rec - 1] + A.len[A.n_rec - 1] : 0;
     auto desc_of = [&](uint64_t wstep, bool& valid) {  // unconditional: slot 0 stands in for no unit
         const uint64_t u = wstep * kGroupsPerWave + grp;
         valid = wstep < nws && u < U;
-        if constexpr ((MODE & 64) != 0)  // timing build only: unit u = arena bytes [u kU, (u + 1) kU), no loads
+        if constexpr ((MODE & 64) != 0) {  // timing build only: unit u = arena bytes [u kU, (u + 1) kU), no loads
+            valid = valid && (u + 1) * kU <= arena_end;  // (none past the last record's end)
             return UnitDesc{reinterpret_cast<uint64_t>(A.arena) + (valid ? u : 0) * kU, (uint32_t)kU, 0u};
+        }
         return load_desc(&KB_READ(A.desc, M.slot(valid ? u : 0), A.unit_cap, kKbUnit));
     };
     const uint8_t* safe = (MODE & 64) != 0 ? A.arena : reinterpret_cast<const uint8_t*>(load_desc(A.desc + M.slot(0)).us);
@@ -1282,7 +1367,17 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     units_timer_begin(s);
 #ifdef KARMA_AB
     // timing forms (wrong results): 1 = steps without the LDS lookups, 2 = no lane fold / tree, 3 = both
-    if (const int fl = KARMA_AB_KNOB("KARMA_RAGGED_UNITS_FLAT", 0); fl == 8)
+    if (const int fx = KARMA_AB_KNOB("KARMA_RAGGED_UNITS_FIXEDLOOP", 0); fx == 1)
+        hipLaunchKernelGGL(k_units_ragged_fixedloop<false>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (fx == 2)
+        hipLaunchKernelGGL(k_units_ragged_fixedloop<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (fx == 3)
+        hipLaunchKernelGGL((k_units_ragged_fixedloop<true, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (fx == 4)
+        hipLaunchKernelGGL((k_units_ragged_fixedloop<true, false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (fx == 5)
+        hipLaunchKernelGGL((k_units_ragged_fixedloop<false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (const int fl = KARMA_AB_KNOB("KARMA_RAGGED_UNITS_FLAT", 0); fl == 8)
         hipLaunchKernelGGL((k_units_ragged_flat<8>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (fl == 4)
         hipLaunchKernelGGL((k_units_ragged_flat<4>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
