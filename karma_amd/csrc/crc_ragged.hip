@@ -649,6 +649,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
 // per unit (both at the unit's first window here).
 template <bool ARITH, bool BIG = false, bool HT = false>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged_fixedloop(RaggedArgs A) {
+    KB_SET_ARENA(A.kb_lo, A.kb_hi);
     constexpr int PF = 4;
     __shared__ __attribute__((aligned(16))) uint32_t lds[BIG ? kLdsWordsComb : kLdsWords];
     __shared__ uint32_t blk_next;
