@@ -946,13 +946,21 @@ def main():
     # ---- single-segment latency: isolated calls, each waited for ------------------------------
     extra = {}
     if wl == "segment" and rank == 0:
+        # the library call alone between the events: its pointers computed beforehand (the
+        # harness's own Python -- the step pipeline, torch's data_ptr() -- is not the call's latency)
+        stream_fn, a_base, o_base = L.karma_crc32c_stream, arena.data_ptr(), cur["out"].data_ptr()
         lat = []
         for _ in range(20):
+            i = seg_i["i"] % nseg
+            seg_i["i"] += 1
+            pa, po = a_base + i * seg, o_base + 4 * i
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
-            crc_step()
+            st = stream_fn(0, pa, seg, po, sh)
             b.record(stream)
             torch.cuda.synchronize()
+            if st:
+                _lib.check("stream", st)
             lat.append(a.elapsed_time(b))
         extra["single_segment_latency_us"] = round(float(np.median(lat)) * 1e3, 2)
         extra["single_segment_latency_gibs"] = round(payload / (float(np.median(lat)) * 1e-3) / GIB, 1)
