@@ -640,248 +640,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
 
 
 #ifdef KARMA_AB
-// Tools build: k_units_fixed's own loop (stream_unit: the next unit's loads issued before the
-// current unit's last batch; the block's wave-steps from an LDS counter, no dynamic tail) over the
-// ragged units.  ARITH: unit u = arena bytes [u kU, (u + 1) kU) (aligned unit-sized layouts only,
-// timing: wrong CRCs elsewhere); else the units from the descriptor list (edges not masked: exact
-// only for records on 16-byte boundaries with 16-byte multiple lengths).
-// BIG: the fixed kernel's larger LDS allocation (kLdsWordsComb); HT: its head / tail block loads
-// per unit (both at the unit's first window here).
-template <bool ARITH, bool BIG = false, bool HT = false>
-__global__ __launch_bounds__(kBlockThreads) void k_units_ragged_fixedloop(RaggedArgs A) {
-    KB_SET_ARENA(A.kb_lo, A.kb_hi);
-    constexpr int PF = 4;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[BIG ? kLdsWordsComb : kLdsWords];
-    __shared__ uint32_t blk_next;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t l = lane & (kGroupLanes - 1);
-    const uint32_t grp = lane / kGroupLanes;
-    const uint32_t X = lane_const();
-    const UnitMap M = unit_map(A);
-    const uint64_t U = M.U;
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
-    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
-    const uint32_t nidx = (uint32_t)((nws + nwaves - 1) / nwaves) * kWavesPerBlock;
-    if (threadIdx.x == 0) blk_next = kWavesPerBlock;
-    uint64_t wb = bw0 + (threadIdx.x >> 6);
-    // (ARITH: no unit past the last record's end, whatever U is)
-    const uint64_t arena_end = ARITH ? A.off[A.n_rec - 1] + A.len[A.n_rec - 1] : 0;
-    auto unit_of = [&](uint64_t w, bool& valid) {
-        const uint64_t u = w * kGroupsPerWave + grp;
-        valid = w < nws && u < U && (!ARITH || (u + 1) * kU <= arena_end);
-        const uint64_t uu = valid ? u : 0;
-        const uint8_t* us;
-        uint32_t span;
-        if constexpr (ARITH) {
-            us = A.arena + uu * kU;
-            span = (uint32_t)kU;
-        } else {
-            const UnitDesc d = load_desc(A.desc + M.slot(uu));
-            us = reinterpret_cast<const uint8_t*>(d.us);
-            span = d.span & kDescSpanMask;
-        }
-        if (!valid) span = 0;
-        return lane_unit(us, us + span, l);
-    };
-    bool valid;
-    LaneUnit L = unit_of(wb, valid);
-    u32x4 hv = u32x4{0u, 0u, 0u, 0u}, tv = hv;
-    if constexpr (HT) {
-        hv = ld16(L.us);
-        tv = ld16(L.us);
-    }
-    UnitLoads<PF> Ld;
-    issue_unit_loads<PF, kRaggedNT>(L, Ld);
-    load_stream_tables(lds, A.blob);
-    if constexpr (BIG) copy_to_lds<3 * 1024, kBlockThreads>(lds + kLdsWords, A.blob);
-    __syncthreads();
-    for (; wb < nws;) {
-        LaneUnit N;
-        bool nvalid = false;
-        uint64_t wb_next = nws;
-        const uint32_t R = stream_unit<PF, kRaggedNT>(lds, X, l, L, Ld, nullptr, 0u, [&](UnitLoads<PF>& nx) {
-            uint32_t i = 0;
-            if (lane == 0) i = atomicAdd(&blk_next, 1u);
-            i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
-            wb_next = i < nidx ? bw0 + (i % kWavesPerBlock) + (uint64_t)(i / kWavesPerBlock) * nwaves : nws;
-            N = unit_of(wb_next, nvalid);
-            if constexpr (HT) {
-                hv = ld16(N.us);
-                tv = ld16(N.us);
-            }
-            issue_unit_loads<PF, kRaggedNT>(N, nx);
-        });
-        if constexpr (HT)  // (keeps the head / tail loads; timing only)
-            if (hv.x == 0x9e3779b9u && tv.y == 0x7f4a7c15u) A.partial[0] = 0u;
-        if (valid && l == 0) A.partial[M.slot(wb * kGroupsPerWave + grp)] = R;
-        L = N;
-        valid = nvalid;
-        wb = wb_next;
-    }
-}
+#include "ragged_ab.inc"  // the round-5 experiment forms of the units kernel (tools build only)
 #endif
-
-// ---- the units kernel as one chunk stream per wave -------------------------------------------------
-// k_units_ragged waits on memory three times per unit with one load in flight (its ISA: the next
-// descriptor, copied into the loop's registers right after its load, s_waitcnt vmcnt(0); chunk 0,
-// waited for before the unit's other loads issue; the unit's last batch before the fold), and with
-// the lookups and the fold removed it is no faster (profiles/r05_units_modes.txt): the gap to
-// k_units_fixed is that schedule.  Here a wave's steps are one stream of chunk iterations: a ring of
-// D loads per lane, chunk i + D issued when chunk i is stepped -- into the next step's unit for the
-// last D chunks of a step -- so loads stay in flight across unit boundaries.  Each ring slot is
-// consumed before its next load is issued into the same registers (no loop-carried copy waits on a
-// fresh load), descriptors are loaded two steps ahead and read a step later, and a step runs
-// L = max(D, wave max of its units' chunk counts) rounded up to D iterations, groups past their
-// unit's end stepping nothing (their loads clamped to their last window).
-struct FlatUnit {
-    const uint8_t* cb;   // the unit's first chunk on the absolute 128-byte grid
-    const uint8_t* us;   // [us, ue): the unit's whole 16-byte blocks
-    const uint8_t* ue;
-    const uint8_t* lcl;  // the last window this lane loads (a valid address)
-    uint32_t nch;        // chunks (0: no unit)
-    uint32_t m;          // group lane holding the unit's last window
-    uint32_t edge;       // head bytes | tail bytes << 4 | (this lane's last window inside) << 8
-    uint32_t inj;
-    uint32_t L;          // the step's chunk iterations (wave-uniform)
-};
-
-template <int D>
-__device__ __forceinline__ FlatUnit flat_unit(const UnitDesc& d, bool valid, const uint8_t* safe, uint32_t l) {
-    FlatUnit f;
-    const uint32_t span = valid ? (d.span & kDescSpanMask) : 0u;
-    f.us = valid && span ? reinterpret_cast<const uint8_t*>(d.us) : safe;
-    f.ue = f.us + span;
-    f.cb = floor128(f.us);
-    f.nch = span ? (uint32_t)((uint64_t)(f.ue - f.cb + kChunk - 1) / kChunk) : 0u;
-    f.m = span ? (uint32_t)((reinterpret_cast<uintptr_t>(f.ue) - 16) >> 4) & (kGroupLanes - 1) : kGroupLanes - 1;
-    const uint8_t* wl = f.cb + (int64_t)(f.nch ? f.nch - 1 : 0) * kChunk + 16 * l;
-    const bool lok = span && wl < f.ue;
-    f.lcl = lok ? wl : span ? f.ue - 16 : f.us;
-    f.edge = (span ? ((d.span >> kDescHeadShift) & 15u) | (((d.span >> kDescTailShift) & 15u) << 4) : 0u) |
-             (lok ? 256u : 0u);
-    f.inj = span ? d.inj : 0u;
-    uint32_t x = f.nch;  // the wave's longest unit
-    x = max(x, (uint32_t)__shfl_xor((int)x, 8));
-    x = max(x, (uint32_t)__shfl_xor((int)x, 16));
-    x = max(x, (uint32_t)__shfl_xor((int)x, 32));
-    x = __builtin_amdgcn_readfirstlane(x);
-    f.L = x <= (uint32_t)D ? (uint32_t)D : (x + D - 1) / D * D;
-    return f;
-}
-
-// This lane's window of chunk j, clamped into [us, lcl] (always a valid address).
-__device__ __forceinline__ const uint8_t* flat_addr(const FlatUnit& f, uint32_t j, uint32_t l) {
-    return pmin(pmax(f.cb + (int64_t)j * kChunk + 16 * l, f.us), f.lcl);
-}
-
-// Chunk i of the step's unit: windows outside [us, ue) are zero, the edge windows masked, the
-// entering register injected; lanes past the unit's end step nothing.
-template <int MODE>
-__device__ __forceinline__ void flat_chunk(const uint32_t* lds, uint32_t X, uint32_t& a0, uint32_t& a1, uint32_t& a2,
-                                           uint32_t& a3, u32x4 v, const FlatUnit& f, uint32_t i, uint32_t l) {
-    const uint8_t* w = f.cb + (int64_t)i * kChunk + 16 * l;
-    if (!(w >= f.us && w < f.ue)) v = u32x4{0u, 0u, 0u, 0u};
-    if (w == f.ue - 16) v = mask_tail(v, (f.edge >> 4) & 15u);
-    if (w == f.us) v = xor_word(mask_head(v, f.edge & 15u), (f.edge & 15u) >> 2, f.inj);
-    if (i + 1 < f.nch || (i + 1 == f.nch && (f.edge & 256u))) step4<MODE>(lds, X, a0, a1, a2, a3, v);
-}
-
-template <int D = 8, int MODE = 0>
-__global__ __launch_bounds__(kBlockThreads) void k_units_ragged_flat(RaggedArgs A) {
-    KB_SET_ARENA(A.kb_lo, A.kb_hi);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
-    __shared__ uint32_t blk_next;
-    __shared__ uint32_t blk_dyn[kDynChunks];
-    if (threadIdx.x == 0) blk_next = kWavesPerBlock;
-    for (uint32_t c = threadIdx.x; c < kDynChunks; c += blockDim.x) blk_dyn[c] = ~0u;
-    load_stream_tables(lds, A.blob);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t l = lane & (kGroupLanes - 1);
-    const uint32_t grp = lane / kGroupLanes;
-    const uint32_t X = lane_const();
-    const UnitMap M = unit_map(A);
-    const uint64_t U = M.U;
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t nws = (U + kGroupsPerWave - 1) / kGroupsPerWave;
-    uint64_t S = nws;
-    if (A.dyn_shift) {
-        const uint64_t d = min(nws >> A.dyn_shift, (uint64_t)kDynMaxSteps);
-        const uint64_t s = (nws - d) / nwaves * nwaves;
-        S = s >= nwaves ? s : nws;
-    }
-    const uint32_t nidx = (uint32_t)((S + nwaves - 1) / nwaves) * kWavesPerBlock;
-    const uint64_t bw0 = (uint64_t)blockIdx.x * kWavesPerBlock;
-    uint64_t wc = bw0 + (threadIdx.x >> 6);
-    if (wc >= nws) return;  // (wave-uniform; U > 0 here)
-    const uint64_t arena_end = (MODE & 64) != 0 ? A.off[A.n_rec - 1] + A.len[A.n_rec - 1] : 0;
-    auto desc_of = [&](uint64_t wstep, bool& valid) {  // unconditional: slot 0 stands in for no unit
-        const uint64_t u = wstep * kGroupsPerWave + grp;
-        valid = wstep < nws && u < U;
-        if constexpr ((MODE & 64) != 0) {  // timing build only: unit u = arena bytes [u kU, (u + 1) kU), no loads
-            valid = valid && (u + 1) * kU <= arena_end;  // (none past the last record's end)
-            return UnitDesc{reinterpret_cast<uint64_t>(A.arena) + (valid ? u : 0) * kU, (uint32_t)kU, 0u};
-        }
-        return load_desc(&KB_READ(A.desc, M.slot(valid ? u : 0), A.unit_cap, kKbUnit));
-    };
-    const uint8_t* safe = (MODE & 64) != 0 ? A.arena : reinterpret_cast<const uint8_t*>(load_desc(A.desc + M.slot(0)).us);
-    uint64_t wn = ragged_next_step(A, &blk_next, blk_dyn, nidx, S, nws, bw0, nwaves, lane);
-    uint64_t wd = ragged_next_step(A, &blk_next, blk_dyn, nidx, S, nws, bw0, nwaves, lane);
-    bool vc, vn, vd;
-    const UnitDesc dc = desc_of(wc, vc), dn = desc_of(wn, vn);
-    UnitDesc dd = desc_of(wd, vd);  // read one step later
-    FlatUnit cur = flat_unit<D>(dc, vc, safe, l);
-    FlatUnit nxt = flat_unit<D>(dn, vn, safe, l);
-    u32x4 ring[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) ring[q] = ldg<kRaggedNT>(flat_addr(cur, q, l));
-    for (;;) {
-        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-        uint32_t base = 0;
-        for (; base + D < cur.L; base += D) {
-#pragma unroll
-            for (int q = 0; q < D; ++q) {
-                flat_chunk<MODE>(lds, X, a0, a1, a2, a3, ring[q], cur, base + q, l);
-                __builtin_amdgcn_sched_barrier(0);
-                ring[q] = ldg<kRaggedNT>(flat_addr(cur, base + q + D, l));
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < D; ++q) {  // the step's last D chunks; the next step's first D issued
-            flat_chunk<MODE>(lds, X, a0, a1, a2, a3, ring[q], cur, base + q, l);
-            __builtin_amdgcn_sched_barrier(0);
-            ring[q] = ldg<kRaggedNT>(flat_addr(nxt, q, l));
-        }
-        uint32_t c;
-        if constexpr ((MODE & 2) != 0) {
-            c = a0 ^ a1 ^ a2 ^ a3;  // timing build only: no fold, no tree
-        } else {
-            c = lane_fold(lds, a0, a1, a2, a3);
-            c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + cur.m + 1) & (kGroupLanes - 1))), 64);
-            uint32_t t = __shfl_down(c, 1, kGroupLanes);
-            c = zmap(lds, kLZ16, c) ^ t;
-            t = __shfl_down(c, 2, kGroupLanes);
-            c = zmap(lds, kLZ32, c) ^ t;
-            t = __shfl_down(c, 4, kGroupLanes);
-            c = zmap(lds, kLZ64, c) ^ t;
-        }
-        if ((MODE & 128) == 0 && vc && l == 0)  // (MODE 128: timing build only, no store)
-            KB_WRITE(A.partial, M.slot(wc * kGroupsPerWave + grp), A.unit_cap, kKbUnit, c);
-        if constexpr ((MODE & 128) != 0)
-            if (c == 0x9e3779b9u && vc) A.partial[0] = c;  // (keeps the steps live)
-        if (wn >= nws) break;
-        cur = nxt;
-        wc = wn;
-        vc = vn;
-        nxt = flat_unit<D>(dd, vd, safe, l);
-        wn = wd;
-        vn = vd;
-        wd = ragged_next_step(A, &blk_next, blk_dyn, nidx, S, nws, bw0, nwaves, lane);
-        dd = desc_of(wd, vd);
-    }
-}
-
 
 // Slot of unit j of a record (full units from fb in order, partial ones bucketed).
 __device__ __forceinline__ uint64_t unit_slot(uint64_t j, uint64_t k, uint64_t fb, uint64_t ps0, uint64_t ps1,
