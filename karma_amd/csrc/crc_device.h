@@ -758,6 +758,42 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
     return ((uint64_t)h << 32) | l;
 }
 
+// One DPP move of a 64-bit value (both halves; lanes the row pattern leaves without a source, or
+// rows outside RM, take `old`).
+template <int CTRL, int RM>
+__device__ __forceinline__ uint64_t dpp64(uint64_t old, uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)old, (int)(uint32_t)x, CTRL, RM, 0xf, false);
+    const uint32_t hi =
+        (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(old >> 32), (int)(uint32_t)(x >> 32), CTRL, RM, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+// Inclusive prefix min of lo and max of hi over the wave's lanes, through DPP (row shifts 1, 2, 4,
+// 8, then the gfx9 row broadcasts): VALU steps instead of six dependent rounds of ds_bpermute,
+// which share the LDS pipe and its counter with the stride lookups.
+__device__ __forceinline__ void wave_prefix_minmax(uint64_t& lo, uint64_t& hi) {
+    auto step = [&](uint64_t a, uint64_t b) {
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    };
+    step(dpp64<0x111, 0xf>(~0ull, lo), dpp64<0x111, 0xf>(0ull, hi));  // row_shr:1
+    step(dpp64<0x112, 0xf>(~0ull, lo), dpp64<0x112, 0xf>(0ull, hi));  // row_shr:2
+    step(dpp64<0x114, 0xf>(~0ull, lo), dpp64<0x114, 0xf>(0ull, hi));  // row_shr:4
+    step(dpp64<0x118, 0xf>(~0ull, lo), dpp64<0x118, 0xf>(0ull, hi));  // row_shr:8
+    step(dpp64<0x142, 0xa>(~0ull, lo), dpp64<0x142, 0xa>(0ull, hi));  // row_bcast:15 -> rows 1, 3
+    step(dpp64<0x143, 0xc>(~0ull, lo), dpp64<0x143, 0xc>(0ull, hi));  // row_bcast:31 -> rows 2, 3
+}
+
+// OR of a 32-bit value over the wave (DPP prefix, lane 63 read back): uniform.
+__device__ __forceinline__ uint32_t wave_or32(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 struct StgBatch {
     uintptr_t p;    // this lane's record
     uint32_t n, init;
@@ -775,14 +811,11 @@ __device__ __forceinline__ StgBatch stg_meta(const RaggedArgs& A, uint64_t n_rec
     B.init = B.vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
     const bool live = B.vi && B.n;
     uint64_t lo = live ? (B.p & ~uintptr_t(15)) : ~0ull, hi = live ? ((B.p + B.n + 15) & ~uintptr_t(15)) : 0ull;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t ol = (uint64_t)__shfl_xor((long long)lo, d), oh = (uint64_t)__shfl_xor((long long)hi, d);
-        lo = ol < lo ? ol : lo;
-        hi = oh > hi ? oh : hi;
-    }
-    B.lo = uniform64(lo);
-    B.hi = uniform64(hi);
+    wave_prefix_minmax(lo, hi);  // lane 63: the whole wave's
+    B.lo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lo >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lo, 63);
+    B.hi = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hi >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hi, 63);
     return B;
 }
 __device__ __forceinline__ bool stg_fits(const StgBatch& B) { return B.hi != 0 && B.hi - B.lo <= kStgBytes; }
@@ -824,14 +857,7 @@ struct StgSpan {
 };
 __device__ __forceinline__ StgSpan stg_prefix(uintptr_t p, uint32_t n, bool live, uint32_t lane) {
     uint64_t lo = live ? (p & ~uintptr_t(15)) : ~0ull, hi = live ? ((p + n + 15) & ~uintptr_t(15)) : 0ull;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {  // inclusive prefix min / max
-        const uint64_t ol = (uint64_t)__shfl_up((long long)lo, d), oh = (uint64_t)__shfl_up((long long)hi, d);
-        if (lane >= (uint32_t)d) {
-            lo = ol < lo ? ol : lo;
-            hi = oh > hi ? oh : hi;
-        }
-    }
+    wave_prefix_minmax(lo, hi);  // inclusive prefix min / max
     const bool fits = hi == 0 || hi - lo <= kStgBytes;  // monotonic in the lane
     const uint32_t cnt = (uint32_t)__popcll(__ballot(fits));
     StgSpan S;

@@ -98,6 +98,19 @@ __device__ __forceinline__ RecUnits rec_units(const RaggedArgs& A, uint64_t r) {
     return rec_units_at(A.arena + A.off[r], A.len[r]);
 }
 
+// Inclusive wave scan of 32-bit values through DPP (row shifts, then the row broadcasts of gfx9):
+// six VALU steps instead of six dependent cross-lane LDS round trips (ds_bpermute) of the 64-bit
+// scan below.
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 // Inclusive wave scan of 64-bit values.
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
     const int lane = threadIdx.x & 63;
@@ -180,7 +193,7 @@ __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool va
     // lane i taking slot F0 + i and finding its record by a search over the lanes' inclusive
     // unit counts, so the stores are coalesced and balanced however skewed the record sizes are.
     const uint64_t nfull = valid ? u.full : 0;
-    const uint64_t incl = wave_incl_scan(nfull);
+    const uint64_t incl = wave_incl_scan32((uint32_t)nfull);  // (a record's full units < 2^19: a wave's < 2^25)
     const uint64_t T = __shfl(incl, 63);
     const uint64_t F0 = __shfl(fb, 0);
     for (uint64_t base = 0; base < T; base += 64) {  // uniform trip count: shuffles see every lane
@@ -433,7 +446,10 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
     uint64_t incl[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-        incl[i] = wave_incl_scan(packed[i]);
+        // full units (< 2^19 per record, < 2^25 per wave) and partial ones (<= 2 per record) scanned
+        // apart in 32 bits, then packed as packed[i] is
+        incl[i] = ((uint64_t)wave_incl_scan32((uint32_t)(packed[i] >> 16)) << 16) |
+                  wave_incl_scan32((uint32_t)(packed[i] & 0xffffu));
         if (lane == 63) sm[i * NW + wave] = incl[i];
     }
     PLAN_STAMP(0, 7);  // counted, wave scans
@@ -474,7 +490,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
                 loc[q] = o < NB ? hist[i * kBuckets + c] : 0u;
                 sum += loc[q];
             }
-            unsigned long long run = A.part_base + exP + wave_incl_scan(sum) - sum;
+            unsigned long long run = A.part_base + exP + wave_incl_scan32((uint32_t)sum) - sum;  // (<= 2 R kScanBlock)
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
                 const int o = (int)lane * PER + q, i = o / kBuckets, c = kBuckets - 1 - o % kBuckets;
@@ -918,14 +934,11 @@ __global__ __launch_bounds__((R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_s
     auto extent = [&](uint64_t o, uint32_t n, uintptr_t& lo, uintptr_t& hi) {
         const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
         uint64_t l = n ? (p & ~uintptr_t(15)) : ~0ull, h = n ? ((p + n + 15) & ~uintptr_t(15)) : 0ull;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t ol = (uint64_t)__shfl_xor((long long)l, d), oh = (uint64_t)__shfl_xor((long long)h, d);
-            l = ol < l ? ol : l;
-            h = oh > h ? oh : h;
-        }
-        lo = uniform64(l);
-        hi = uniform64(h);
+        wave_prefix_minmax(l, h);  // (DPP; lane 63 holds the wave's)
+        lo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(l >> 32), 63) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)l, 63);
+        hi = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(h >> 32), 63) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)h, 63);
     };
     u32x4 v[kStgVecs];
     auto issue = [&](uintptr_t lo, uintptr_t hi) {
@@ -951,9 +964,8 @@ __global__ __launch_bounds__((R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_s
         if (!SK && !A.stage_skew_seen) return false;
         const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
         uint32_t bits = n ? 1u << (((uint32_t)(p - lo) >> 2) & 31u) : 0u;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) bits |= (uint32_t)__shfl_xor((int)bits, d);
-        const bool poor = __builtin_popcount(__builtin_amdgcn_readfirstlane(bits)) < 12;
+        bits = wave_or32(bits);
+        const bool poor = __builtin_popcount(bits) < 12;
         poor_seen |= poor;
         return SK && poor;
     };
