@@ -729,15 +729,33 @@ __device__ __forceinline__ uint32_t zshift16(const uint32_t* lds, uint32_t x, ui
     return x;
 }
 
+// Lane i + D's x for the lanes a reduction tree keeps (lane 0 at the last level; at level D the
+// lanes that are multiples of 2D): D = 1, 2, 4, 8 through DPP row shifts (VALU, within the lane's
+// row of 16), D = 16 and 32 through v_readlane -- instead of ds_bpermute round trips, which a
+// chain of tree levels waits on one after another.  Other lanes get values the tree never uses.
+template <int D>
+__device__ __forceinline__ uint32_t tree_down(uint32_t x) {
+    static_assert(D == 1 || D == 2 || D == 4 || D == 8 || D == 16 || D == 32, "tree levels");
+    if constexpr (D <= 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + D, 0xf, 0xf, false);  // row_shl:D
+    } else if constexpr (D == 16) {  // lanes 0 and 32 take lanes 16 and 48
+        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+        return (threadIdx.x & 32u) ? b : a;
+    } else {
+        return (uint32_t)__builtin_amdgcn_readlane((int)x, 32);
+    }
+}
+
 // Tree over the 64 lanes of a wave with maps Z_{D*2^d}: lane 0 gets
 // XOR_l Z_{D*(63-l)}(v_l).
 __device__ __forceinline__ uint32_t wave_tree(const uint32_t* lds, uint32_t v) {
-#pragma unroll
-    for (int d = 0; d < 6; ++d) {
-        const uint32_t t = __shfl_down(v, 1u << d, 64);
-        v = zmap(lds, d * 1024, v) ^ t;
-    }
-    return v;
+    v = zmap(lds, 0, v) ^ tree_down<1>(v);
+    v = zmap(lds, 1024, v) ^ tree_down<2>(v);
+    v = zmap(lds, 2 * 1024, v) ^ tree_down<4>(v);
+    v = zmap(lds, 3 * 1024, v) ^ tree_down<8>(v);
+    v = zmap(lds, 4 * 1024, v) ^ tree_down<16>(v);
+    return zmap(lds, 5 * 1024, v) ^ tree_down<32>(v);
 }
 
 // ---- small records staged through LDS (k_ragged_staged, k_wal_list_crc) ----------------
@@ -757,6 +775,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
     const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
     return ((uint64_t)h << 32) | l;
 }
+
 
 // One DPP move of a 64-bit value (both halves; lanes the row pattern leaves without a source, or
 // rows outside RM, take `old`).

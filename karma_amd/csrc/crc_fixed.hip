@@ -108,11 +108,7 @@ __device__ void fused_record_fold(const FixedArgs& A, uint32_t* lds, uint32_t* w
             acc = zmap(lds, kBcZD, acc) ^ (uint32_t)w[q];
         }
     }
-#pragma unroll
-    for (int d = 0; d < 6; ++d) {
-        const uint32_t t = __shfl_down(acc, 1u << d, 64);
-        acc = zmap(lds, kBcTree + d * 1024, acc) ^ t;
-    }
+    acc = wave_tree(lds + kBcTree, acc);
     if (lane == 0) wv[wave] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -192,12 +188,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
             issue_unit_loads<PF, NT>(N.L, nx);
         });
         if constexpr (WAVE_COMB) {  // unit states sit in lanes 8g; fold g = 0..7 (g = 7 ends last)
-            uint32_t t = __shfl_down(R, 8, 64);
-            R = zmap(lds, kCombLdsBase, R) ^ t;
-            t = __shfl_down(R, 16, 64);
-            R = zmap(lds, kCombLdsBase + 1024, R) ^ t;
-            t = __shfl_down(R, 32, 64);
-            R = zmap(lds, kCombLdsBase + 2048, R) ^ t;
+            R = zmap(lds, kCombLdsBase, R) ^ tree_down<8>(R);
+            R = zmap(lds, kCombLdsBase + 1024, R) ^ tree_down<16>(R);
+            R = zmap(lds, kCombLdsBase + 2048, R) ^ tree_down<32>(R);
             if constexpr (FUSE) {  // tagged, visible to the last workgroup without a fence
                 if (P.valid && lane == 0)
                     __hip_atomic_store(reinterpret_cast<unsigned long long*>(A.partial) + wb,
@@ -354,19 +347,14 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
         tag = __hip_atomic_load(reinterpret_cast<const uint32_t*>(A.fctl + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     uint32_t c = lane_fold_at(lds, kSegZ4, a0, a1, a2, a3);
     c = __shfl(c, (int)((lane & ~(kGroupLanes - 1u)) | ((l + L.m + 1) & (kGroupLanes - 1))), 64);
-    uint32_t t = __shfl_down(c, 1, kGroupLanes);
-    c = zmap(lds, kSegZ4 + 1024, c) ^ t;
-    t = __shfl_down(c, 2, kGroupLanes);
-    c = zmap(lds, kSegZ4 + 2048, c) ^ t;
-    t = __shfl_down(c, 4, kGroupLanes);
-    c = zmap(lds, kSegZ4 + 3072, c) ^ t;
+    // (the tree levels through DPP / readlane, tree_down: no LDS round trip between levels)
+    c = zmap(lds, kSegZ4 + 1024, c) ^ tree_down<1>(c);
+    c = zmap(lds, kSegZ4 + 2048, c) ^ tree_down<2>(c);
+    c = zmap(lds, kSegZ4 + 3072, c) ^ tree_down<4>(c);
     // 6. the wave's 8 units (Z_U, Z_2U, Z_4U), the workgroup's 16 waves (Z_8U .. Z_64U)
-    t = __shfl_down(c, 8, 64);
-    c = zmap(lds, kSegComb, c) ^ t;
-    t = __shfl_down(c, 16, 64);
-    c = zmap(lds, kSegComb + 1024, c) ^ t;
-    t = __shfl_down(c, 32, 64);
-    c = zmap(lds, kSegComb + 2048, c) ^ t;
+    c = zmap(lds, kSegComb, c) ^ tree_down<8>(c);
+    c = zmap(lds, kSegComb + 1024, c) ^ tree_down<16>(c);
+    c = zmap(lds, kSegComb + 2048, c) ^ tree_down<32>(c);
     if (lane == 0) wst[wave] = c;
     if (ARRIVE || last_wg) grid.store(lds + kSegGrid);
     SEG_STAMP(2);
@@ -376,11 +364,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     if (wave == 0) {
         const uint32_t my_tag = tag ? tag : 1u;
         uint32_t s = lane < kWavesPerBlock ? wst[lane] : 0u;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const uint32_t o = __shfl_down(s, 1u << d, kWavesPerBlock);
-            s = zmap(lds, kSegComb + (3 + d) * 1024, s) ^ o;
-        }
+        s = zmap(lds, kSegComb + 3 * 1024, s) ^ tree_down<1>(s);
+        s = zmap(lds, kSegComb + 4 * 1024, s) ^ tree_down<2>(s);
+        s = zmap(lds, kSegComb + 5 * 1024, s) ^ tree_down<4>(s);
+        s = zmap(lds, kSegComb + 6 * 1024, s) ^ tree_down<8>(s);
         if (lane == 0)  // tagged: visible to the last workgroup without a fence
             __hip_atomic_store(reinterpret_cast<unsigned long long*>(A.partial) + blockIdx.x,
                                ((unsigned long long)my_tag << 32) | s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -413,11 +400,12 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
         s = (uint32_t)w;
     }
     if (wave < nw) {
-#pragma unroll
-        for (int d = 0; d < 6; ++d) {
-            const uint32_t o = __shfl_down(s, 1u << d, 64);
-            s = zmap(lds, kSegGrid + d * 1024, s) ^ o;
-        }
+        s = zmap(lds, kSegGrid, s) ^ tree_down<1>(s);
+        s = zmap(lds, kSegGrid + 1024, s) ^ tree_down<2>(s);
+        s = zmap(lds, kSegGrid + 2 * 1024, s) ^ tree_down<4>(s);
+        s = zmap(lds, kSegGrid + 3 * 1024, s) ^ tree_down<8>(s);
+        s = zmap(lds, kSegGrid + 4 * 1024, s) ^ tree_down<16>(s);
+        s = zmap(lds, kSegGrid + 5 * 1024, s) ^ tree_down<32>(s);
         if (lane == 0) wst[wave] = s;
     }
     __syncthreads();
@@ -562,11 +550,7 @@ __global__ __launch_bounds__(1024) void k_combine_block(FixedArgs A, const uint3
         for (int q = 0; q < 8; ++q)
             if (i + q < m) acc = zmap(lds, kBcZD, acc) ^ sv[q];
     }
-#pragma unroll
-    for (int d = 0; d < 6; ++d) {
-        const uint32_t t = __shfl_down(acc, 1u << d, 64);
-        acc = zmap(lds, kBcTree + d * 1024, acc) ^ t;
-    }
+    acc = wave_tree(lds + kBcTree, acc);
     if (lane == 0) wv[wave] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -27,7 +27,10 @@ dev = torch.device("cuda:0")
 arena = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
 K.fill_splitmix64(arena, 42)
 sh = torch.cuda.current_stream().cuda_stream
-cases = {"1M x 4 KiB": (4096, 1 << 20), "256K x 16 KiB": (16384, 1 << 18), "4M x 1 KiB": (1024, 1 << 22)}
+cases = {"1M x 4 KiB": (4096, 1 << 20), "256K x 16 KiB": (16384, 1 << 18), "4M x 1 KiB": (1024, 1 << 22),
+         "64 x 64 MiB": (64 << 20, 64)}  # (the last: configs[3], wave-folded units + k_combine_block)
+if os.environ.get("CASES"):  # a subset, e.g. CASES="1M x 4 KiB,64 x 64 MiB"
+    cases = {k: v for k, v in cases.items() if k in os.environ["CASES"].split(",")}
 outs = {n: {v: torch.empty(c[1], dtype=torch.int32, device=dev) for v in LIBS} for n, c in cases.items()}
 
 
