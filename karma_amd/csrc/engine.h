@@ -361,6 +361,10 @@ hipError_t launch_wal_plan(const WalArgs& a, uint64_t nseg, hipStream_t s);
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, int cu, hipStream_t s);
 // The first of n candidates whose payload CRC differs from the stored one (atomicMin into *first_bad).
 hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);
+// The summary (device memory) into page-locked host memory by one wave's stores: the host reads it
+// after the stream syncs.  A 56-byte hipMemcpyAsync D2H is a copy kernel of its own (~4 us on the
+// replay's stream); this is one small launch (wal.cc's summary readback).
+hipError_t launch_wal_publish(const WalSummary* src, WalSummary* dst_host, hipStream_t s);
 
 // ---- KFP frames (kfp.cc) ----------------------------------------------------
 struct KfpWalk {

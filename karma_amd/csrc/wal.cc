@@ -450,9 +450,8 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
                                                   &A.sum->stage_skew))
             return rc;
     }
-    WalSummary* S = c.h_small.as<WalSummary>();
-    if (hipMemcpyAsync(S, A.sum, sizeof(WalSummary), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
-        hipStreamSynchronize(c.st) != hipSuccess)
+    WalSummary* S = c.h_small.as<WalSummary>();  // (page-locked: the device writes it, launch_wal_publish)
+    if (launch_wal_publish(A.sum, S, c.st) != hipSuccess || hipStreamSynchronize(c.st) != hipSuccess)
         return fail(KARMA_E_HIP, "wal_replay: walk + plan");
     T.mark(inline_crc ? "walk + inline CRCs + plan (device)"
                       : dev_plan ? "walk + plan + gather + CRCs (device)" : "walk + plan (device)");

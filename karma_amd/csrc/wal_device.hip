@@ -1247,6 +1247,24 @@ hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, i
     return hipGetLastError();
 }
 
+namespace {
+// One wave: word i of the summary to the host copy (system scope: written through to host memory).
+__global__ __launch_bounds__(64) void k_wal_publish(const WalSummary* src, WalSummary* dst) {
+    constexpr uint32_t kWords = sizeof(WalSummary) / 4;
+    static_assert(sizeof(WalSummary) % 4 == 0 && kWords <= 64, "one word per lane");
+    const uint32_t i = threadIdx.x;
+    if (i < kWords) {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(src)[i];
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(dst) + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+}  // namespace
+
+hipError_t launch_wal_publish(const WalSummary* src, WalSummary* dst_host, hipStream_t s) {
+    hipLaunchKernelGGL(k_wal_publish, dim3(1), dim3(64), 0, s, src, dst_host);
+    return hipGetLastError();
+}
+
 hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s) {
     if (!n) return hipSuccess;
     uint64_t blocks = (n + 255) / 256;

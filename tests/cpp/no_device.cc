@@ -29,6 +29,7 @@ hipError_t launch_ragged_staged_dev(const RaggedArgs&, int, hipStream_t, bool) {
 hipError_t launch_wal_plan(const WalArgs&, uint64_t, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_wal_gather(const WalArgs&, uint64_t, bool, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_wal_compare(const WalArgs&, uint64_t, int, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_wal_publish(const WalSummary*, WalSummary*, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_fill_splitmix(uint8_t*, uint64_t, uint64_t, uint64_t, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_stream_probe(const uint8_t*, uint64_t, uint32_t*, int, hipStream_t) { return hipErrorNoDevice; }
 

@@ -1,0 +1,6 @@
+# round 5: the replay summary published by a one-wave kernel instead of a D2H hipMemcpyAsync
+set -o pipefail
+O=gpurun_out
+mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_wal.py tests/test_gpu_wal_api.py tests/test_gpu_multi_host.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/r05z_wal_tests.log 2>&1 || exit 10
+timeout -k 10 400 python3 -u tools/replay_study.py --variants shipped,lib=tools/lib/libkarma_crc32c_prev.so --rounds 7 --calls 20 > $O/r05_replay_publish_ab.txt 2>&1 || exit 15
