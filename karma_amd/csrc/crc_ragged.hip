@@ -98,19 +98,6 @@ __device__ __forceinline__ RecUnits rec_units(const RaggedArgs& A, uint64_t r) {
     return rec_units_at(A.arena + A.off[r], A.len[r]);
 }
 
-// Inclusive wave scan of 32-bit values through DPP (row shifts, then the row broadcasts of gfx9):
-// six VALU steps instead of six dependent cross-lane LDS round trips (ds_bpermute) of the 64-bit
-// scan below.
-__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
-    return x;
-}
-
 // Inclusive wave scan of 64-bit values.
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
     const int lane = threadIdx.x & 63;

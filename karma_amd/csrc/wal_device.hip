@@ -869,12 +869,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
         const uint32_t f = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;  // lanes < f follow the serial loop
         const bool take = lane < f && acc;
         const uint32_t n = take ? m.count : 0u;
-        uint32_t pre = n;  // inclusive prefix of n
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t t = __shfl_up(pre, d);
-            if ((int)lane >= d) pre += t;
-        }
+        const uint32_t pre = wave_incl_scan32(n);  // inclusive prefix of n (DPP)
         if (in && lane < f) {
             KB_WRITE(A.span, 2 * (s * P + jj), 2 * A.nwork * P, kKbSpan, (uint32_t)(jj * A.sub_cap));
             KB_WRITE(A.span, 2 * (s * P + jj) + 1, 2 * A.nwork * P, kKbSpan, count + pre - n);
@@ -882,22 +877,12 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
         {  // (count: the candidates before this batch of runs)
             const uint32_t f0 = m.pad[0];
             const bool unk = take && n != 0 && f0 == kCrcUnknown;
-            uint32_t ord = take && f0 < kCrcUnknown ? count + pre - n + f0 : kNoBad;
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                const uint32_t o = __shfl_xor(ord, d);
-                ord = o < ord ? o : ord;
-            }
+            const uint32_t ord = wave_min32(take && f0 < kCrcUnknown ? count + pre - n + f0 : kNoBad);
             if (__ballot(unk)) sunk = true;
             sfb = ord < sfb ? ord : sfb;
         }
-        count += __shfl(pre, 63);
-        uint32_t vmx = take ? m.max_len : 0u;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            const uint32_t o = __shfl_xor(vmx, d);
-            vmx = o > vmx ? o : vmx;
-        }
+        count += (uint32_t)__builtin_amdgcn_readlane((int)pre, 63);
+        const uint32_t vmx = wave_max32(take ? m.max_len : 0u);
         mx = vmx > mx ? vmx : mx;
         const uint64_t kt = __ballot(take && m.kind != 0);
         if (kt) {
