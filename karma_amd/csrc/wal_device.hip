@@ -584,11 +584,7 @@ __device__ WalkEnd walk_range(WaveLds& W, const Seg& S, uint32_t lane, uint32_t 
     if (lane < k) put(E.count + lane, myrec, mylen, mycrc);  // the last, partial run
     E.count += k;
     E.pos = pos;
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t o = __shfl_xor(vmax, d);
-        vmax = o > vmax ? o : vmax;
-    }
-    E.max_len = __builtin_amdgcn_readfirstlane(vmax);
+    E.max_len = wave_max32(vmax);  // (DPP)
     return E;
 }
 
@@ -1090,12 +1086,10 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
         __syncthreads();
         const uint32_t w1 = s_w1;
         if (blockIdx.x >= w1 && blockIdx.x != 0) return;  // replay does not enter this segment
-        unsigned long long pre = tid < blockIdx.x ? m.count : 0, all = tid < w1 ? m.count : 0;
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) {
-            pre += __shfl_xor(pre, d);
-            all += __shfl_xor(all, d);
-        }
+        // (32-bit sums through DPP: the device-planned path has images <= 256 MiB, so fewer than
+        // 2^26 candidates in all)
+        const unsigned long long pre = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(tid < blockIdx.x ? m.count : 0u), 63);
+        const unsigned long long all = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(tid < w1 ? m.count : 0u), 63);
         if (lane == 0) {
             s_pre[wave] = pre;
             s_all[wave] = all;
