@@ -98,15 +98,22 @@ __device__ __forceinline__ RecUnits rec_units(const RaggedArgs& A, uint64_t r) {
     return rec_units_at(A.arena + A.off[r], A.len[r]);
 }
 
-// Inclusive wave scan of 64-bit values.
+// Inclusive wave scan of 64-bit values, through DPP as wave_incl_scan32 (each step moves both
+// halves).  Every lane of the wave must be active.
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t t = __shfl_up(x, d);
-        if (lane >= d) x += t;
-    }
+    x += dpp64<0x111, 0xf>(0ull, x);  // row_shr:1
+    x += dpp64<0x112, 0xf>(0ull, x);  // row_shr:2
+    x += dpp64<0x114, 0xf>(0ull, x);  // row_shr:4
+    x += dpp64<0x118, 0xf>(0ull, x);  // row_shr:8
+    x += dpp64<0x142, 0xa>(0ull, x);  // row_bcast:15 -> rows 1, 3
+    x += dpp64<0x143, 0xc>(0ull, x);  // row_bcast:31 -> rows 2, 3
     return x;
+}
+// The sum over the wave (uniform).
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+    x = wave_incl_scan(x);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
 }
 
 // Exclusive block scan (blockDim.x a multiple of 64, <= 1024).
@@ -264,10 +271,7 @@ __device__ __forceinline__ bool lb_take(uint64_t w, uint64_t& excl) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t incl = __ballot(((w >> 40) & 3u) == 2u);
     const uint32_t k = incl ? (uint32_t)(__ffsll((long long)incl) - 1) : 63u;
-    uint64_t v = lane <= k ? (w & kLbValueMask) : 0;
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
-    excl += v;
+    excl += wave_sum64(lane <= k ? (w & kLbValueMask) : 0);  // (DPP)
     return incl != 0;
 }
 
