@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """bench.py -- CRC32C GiB/s, device-resident, batched WAL records, on 1..8 MI355X.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
-``torch.distributed.run`` with one rank per GPU.  One "step" = one pass of the hot path over
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 either launched
+by ``torch.distributed.run`` with one rank per GPU, or run as a plain command, in which case this
+process starts the N ranks itself (``launch_ranks``: the same arguments, torch.distributed.run's
+environment contract, before anything touches a GPU) and exits with the worst rank's status.
+One "step" = one pass of the hot path over
 one batch: every rank checksums its shard of records (``karma_crc32c_batch_fixed``) and, for
 N > 1, the per-record CRCs are gathered to rank 0 over RCCL (``karma_crc32c_gather_u32``).
 Rank 0 prints ONE JSON line.
@@ -64,7 +67,72 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on (affinity)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_fixed_4k.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/profile.sh)")
+    p.add_argument("--dry-backend", choices=["gloo"], default=None,
+                   help="test the N-rank plumbing on CPU (tests/test_bench_launch.py): ranks over gloo, the "
+                        "device batch replaced by the library's host crc32c::Value, the RCCL gather by "
+                        "torch.distributed.gather; no GPU is touched and the line is not a measurement")
+    p.add_argument("--dry-fail-rank", type=int, default=-1,
+                   help="--dry-backend only: this rank exits with status 3 before joining the group "
+                        "(the launcher must end the others and report 3)")
     return p.parse_args()
+
+
+# ---------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _exit_status(code: int) -> int:
+    """A child's return code as a shell exit status (a signal -S becomes 128 + S)."""
+    return 128 - code if code < 0 else code
+
+
+def launch_ranks(argv, n: int, grace_s: float = 20.0) -> int:
+    """Start N ranks of this script as child processes with torch.distributed.run's environment
+    (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), the same
+    arguments, and wait for them.  Called before torch is imported: the parent never initialises
+    a GPU or loads the HIP library, so starting children is safe.  When a rank fails, the others
+    would block in their next collective: they get `grace_s` to finish, then are terminated (the
+    exact PIDs started here).  Returns the worst exit status of the ranks that ended on their own
+    (0 only if every rank returned 0); ranks terminated here do not mask the failure's status."""
+    import subprocess
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    script = os.path.abspath(__file__)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    codes = [None] * n
+    failed_at = own = None
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        if failed_at is None and any(c not in (None, 0) for c in codes):
+            failed_at = time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            own = [_exit_status(c) for c in codes if c is not None]
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(10)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+        time.sleep(0.05)
+    statuses = [_exit_status(c) for c in codes]
+    if any(statuses):
+        print(f"bench.py: rank exit statuses {statuses}", file=sys.stderr, flush=True)
+    return max(own) if own is not None else max(statuses)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -669,17 +737,125 @@ def aggregate_self_checks(checks, gathered=None, n_rec: int = 0):
     return per_rank, total
 
 
-def main():
-    args = parse()
+class HostSync:
+    """GatherPipeline's streams and events for the dry run: work runs at once on the host, so
+    events only need to exist and be recorded before they are waited on."""
+
+    compute_stream, gather_stream = "compute", "gather"
+
+    def event(self):
+        return {"recorded": False}
+
+    def record(self, ev, stream):
+        ev["recorded"] = True
+
+    def wait(self, stream, ev):
+        assert ev["recorded"], "waits on an event never recorded"
+
+
+def dry_main(args, world: int, rank: int):
+    """--dry-backend gloo: the N-rank path of main() -- rank launch, GatherPipeline, barrier +
+    synchronise around K steps, max-over-ranks time, every rank's self-check aggregated on rank 0,
+    one JSON line from rank 0 -- on CPU processes over gloo (tests/test_bench_launch.py).  The
+    device batch is replaced by the product library's host crc32c::Value per record
+    (host_crc32c.cc), the RCCL gather by torch.distributed.gather.  Nothing touches a GPU; the
+    line is marked dry and is not a measurement.  It carries a digest of the CRCs rank 0 gathered,
+    so the test can check every shard against the oracle."""
+    import hashlib
+
     import torch
     import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import synth
 
+    import karma_amd as K
+    if rank == args.dry_fail_rank:
+        raise SystemExit(3)
+    if world > 1:
+        dist.init_process_group("gloo")
+    n_rec = args.records_per_gpu or 2048
+    rec = args.rec_bytes
+    payload = n_rec * rec
+    host = synth.splitmix_np(args.seed, rank * payload, payload).copy()  # bench's fill: first_byte = rank * payload
+    arena = torch.from_numpy(host)
+    outs = [torch.zeros(n_rec, dtype=torch.int64) for _ in range(2 if world > 1 else 1)]
+    gathered = {"last": None}
+
+    def compute(o):
+        o.copy_(torch.from_numpy(np.array([K.Value(host[i * rec:(i + 1) * rec]) for i in range(n_rec)],
+                                          dtype=np.int64)))
+
+    def gather(o, stream):
+        full = [torch.zeros(n_rec, dtype=torch.int64) for _ in range(world)] if rank == 0 else None
+        dist.gather(o, full, dst=0)
+        if rank == 0:
+            gathered["last"] = torch.cat(full)
+
+    pipe = GatherPipeline(outs, compute, gather if world > 1 else None, HostSync())
+    for _ in range(args.warmup):
+        pipe.crc_step()
+        pipe.gather_step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.crc_step()
+        pipe.gather_step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    mine = shard_self_check(arena, pipe.current, rec, n_rec, K.Value, seed=1 + rank)
+    res = None
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        checks = [None] * world
+        dist.all_gather_object(checks, mine)
+        if rank == 0:
+            g = gathered["last"].numpy()
+            per, check = aggregate_self_checks(checks, g, n_rec)
+            res = {"per_rank": {"self_check": per}, "self_check": check,
+                   "gathered_crcs": int(g.size),
+                   "gathered_sha256_16": hashlib.sha256(g.astype("<u4").tobytes()).hexdigest()[:16]}
+    elif rank == 0:
+        g = pipe.current.numpy()
+        res = {"self_check": {"sampled_records": len(mine["idx"]), "mismatches": mine["mismatches"]},
+               "gathered_crcs": int(g.size),
+               "gathered_sha256_16": hashlib.sha256(g.astype("<u4").tobytes()).hexdigest()[:16]}
+    if rank == 0:
+        line = {"metric": METRIC + " [dry run: gloo ranks on CPU, host crc32c::Value; not a measurement]",
+                "value": round(payload * world * args.steps / elapsed / GIB, 4), "unit": "GiB/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "u8", "data": "synthetic splitmix64 records on the host",
+                "config": {"workload": f"{n_rec} x {rec} B records per rank", "records_per_gpu": n_rec,
+                           "rec_bytes": rec, "parallelism": f"record-sharded x{world}"
+                           + (" + gloo gather to rank 0" if world > 1 else "")},
+                "roofline": None, "dry_backend": args.dry_backend, "rccl_nranks": None,
+                "dry_nranks": dist.get_world_size() if world > 1 else 1,
+                "launched_by": os.environ.get("KARMA_BENCH_LAUNCHER", "external")}
+        line.update(res)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # a plain `python bench.py --gpus N`: start the N ranks here, before torch is imported
+        os.environ["KARMA_BENCH_LAUNCHER"] = "bench.py"
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus, float(os.environ.get("KARMA_BENCH_GRACE_S", "20"))))
+    if args.dry_backend:
+        return dry_main(args, world, rank)
+    import torch
+    import torch.distributed as dist
+
     ndev = torch.cuda.device_count()
     local = local % max(ndev, 1)  # one rank per GPU; several ranks per GPU only for plumbing checks
     torch.cuda.set_device(local)
