@@ -457,7 +457,11 @@ int ragged_locked(int dev, DevState& ds, const void* d_arena, const uint64_t* d_
     uint64_t cap_full, cap;
     void* ws = nullptr;
     if (total_len > 0) {
-        cap_full = std::max<uint64_t>(1, ceil_div(total_len, kDefaultUnit));
+        // A record's units cover its whole 16-byte blocks [floor16(p), ceil16(p + n)): at most
+        // n + 30 bytes, so its full (aligned, whole) units number at most (n + 30) / U, and the
+        // batch's at most (total_len + 30 n_rec) / U.  (A record of U - 8 bytes at offset 8 mod U,
+        // the WAL framing at stride U, fills a whole unit: ceil(total_len / U) alone undercounts.)
+        cap_full = std::max<uint64_t>(1, ceil_div(total_len + 30 * (uint64_t)n_rec, kDefaultUnit));
         cap = cap_full + 2 * n_rec;
         const RaggedLayout L = ragged_layout(n_rec, cap);
         KARMA_RC(workspace(dev, s, L.total, &ws));

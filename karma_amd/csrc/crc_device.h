@@ -48,6 +48,11 @@ constexpr uint32_t kSel1 = 0x0c0c0105u;  // {X.b1, acc.b1, 0, 0}
 constexpr uint32_t kSel2 = 0x0c070204u;  // {X.b0, acc.b2, X.b3, 0}
 constexpr uint32_t kSel3 = 0x0c070305u;  // {X.b1, acc.b3, X.b3, 0}
 
+// The engine is written for CDNA4 alone: v_bitop3_b32 below (and the LDS sizes) are gfx950's.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "karma_amd kernels target gfx950 (MI355X) only: build with --offload-arch=gfx950"
+#endif
+
 // a ^ b ^ c in one VALU instruction (gfx950's v_bitop3_b32, truth table 0x96: the parity of the
 // three input bits); the compiler does not form it from xor chains by itself.
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -488,15 +493,23 @@ __device__ __forceinline__ void issue_unit_loads(const LaneUnit& L, UnitLoads<PF
 // Every lane of the wave must call this (cross-lane shuffles); the result is
 // valid in group lane 0.
 // (G < 8: the LDS image's stride tables must be Z_{16 G}, and the tree takes log2 G levels.)
-template <int PF, bool NT, int MODE = 0, int G = kGroupLanes, typename IssueNext>
+// EDGES (the ragged units): as group_unit's, the window at L.us has its first `head` bytes zeroed
+// and inj xored into its word head / 4, the window ending at L.ue its last `tail` bytes zeroed
+// (inj_at unused).
+template <int PF, bool NT, int MODE = 0, int G = kGroupLanes, bool EDGES = false, typename IssueNext>
 __device__ __forceinline__ uint32_t stream_unit(const uint32_t* lds, uint32_t X, uint32_t l, const LaneUnit& L,
                                                 UnitLoads<PF>& Ld, const uint8_t* inj_at, uint32_t inj,
-                                                IssueNext&& issue_next) {
+                                                IssueNext&& issue_next, uint32_t head = 0, uint32_t tail = 0) {
     static_assert(G == 8 || G == 4 || G == 2, "groups of 8, 4 or 2 lanes");
     constexpr int C = 16 * G;
     const bool ok0 = L.nch > 0 && L.w >= L.us && L.w < L.ue;
     u32x4 v = ok0 ? Ld.v0 : u32x4{0u, 0u, 0u, 0u};
-    if (ok0 && L.w == inj_at) v.x ^= inj;
+    if constexpr (EDGES) {
+        if (ok0 && L.w == L.ue - 16) v = mask_tail(v, tail);  // (a one-chunk unit's last window)
+        if (ok0 && L.w == L.us) v = xor_word(mask_head(v, head), head >> 2, inj);
+    } else {
+        if (ok0 && L.w == inj_at) v.x ^= inj;
+    }
     uint32_t a0 = v.x, a1 = v.y, a2 = v.z, a3 = v.w;
     int64_t rem = L.nch - 1;  // chunks after chunk 0; the final one is masked per lane
     const uint8_t* w = L.w + C;
@@ -517,8 +530,12 @@ __device__ __forceinline__ uint32_t stream_unit(const uint32_t* lds, uint32_t X,
     for (int q = 0; q < D; ++q) cur[q] = Ld.nb[q];
     issue_next(Ld);
 #pragma unroll
-    for (int q = 0; q < D; ++q)
+    for (int q = 0; q < D; ++q) {
+        if constexpr (EDGES) {
+            if (q == rem - 1 && l == L.m) cur[q] = mask_tail(cur[q], tail);  // the unit's last window
+        }
         if (q < rem - 1 || (q == rem - 1 && L.lok)) step4<MODE>(lds, X, a0, a1, a2, a3, cur[q]);
+    }
     // lane fold (crc32c.cc STEP4W order), then the 8-lane tree with the lane
     // holding the unit's last window rotated to the end
     if constexpr ((MODE & 2) != 0) return a0 ^ a1 ^ a2 ^ a3;  // timing build only: no fold, no tree

@@ -158,7 +158,8 @@ __device__ __forceinline__ T lds_bump(T* cnt, uint32_t key, bool want) {
 // The unit descriptors of the block's records (one thread per record, every lane of the wave
 // calls this).  fb: the slot of the record's first full unit; cnt: the block's partial-run
 // cursors by chunk count (LDS); full slots at or past full_cap and any slot at or past
-// unit_cap are dropped (a caller's total_len too low: k_ragged_finalize steps those records
+// unit_cap are dropped (only when a caller's total_len is below the true payload sum: capi.cc
+// sizes full_cap for each record's widened block span; k_ragged_finalize steps such records
 // alone).  The first unit carries the masked head bytes u.h and inj (~init moved back over the
 // h % 4 masked bytes of its word by the plan), the last unit the masked tail bytes u.t.
 __device__ void write_unit_descs(const RaggedArgs& A, const RecUnits& u, bool valid, uint64_t r, uint64_t fb,
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(kScanBlock) void k_ragged_plan(RaggedArgs A) {
         if (s_id == 0) lb_store(A.lb_ctl + 1, s_seq);
     }
     copy_to_lds<2 * 1024, kScanBlock>(lds, A.comb_blob + kCombInv);
-    if (threadIdx.x < R * kBuckets) hist[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i < R * kBuckets; i += kScanBlock) hist[i] = 0;  // (R kBuckets may pass kScanBlock)
     __syncthreads();
     PLAN_STAMP(0, 1);  // id, tag and tables
     const uint64_t b = s_id;
@@ -1141,6 +1142,14 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
         hipLaunchKernelGGL((k_units_ragged_fixedloop<true, false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (fx == 5)
         hipLaunchKernelGGL((k_units_ragged_fixedloop<false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (const int st = KARMA_AB_KNOB("KARMA_RAGGED_UNITS_STREAM", 0); st == 40)  // PF, dynamic tail
+        hipLaunchKernelGGL((k_units_ragged_stream<4, false>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (st == 41)
+        hipLaunchKernelGGL((k_units_ragged_stream<4, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (st == 60)
+        hipLaunchKernelGGL((k_units_ragged_stream<6, false>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (st == 61)
+        hipLaunchKernelGGL((k_units_ragged_stream<6, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (const int fl = KARMA_AB_KNOB("KARMA_RAGGED_UNITS_FLAT", 0); fl == 8)
         hipLaunchKernelGGL((k_units_ragged_flat<8>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (fl == 4)

@@ -26,6 +26,9 @@ constexpr uint32_t kStgGateLen = 183;
 #define KARMA_RAGGED_UNIT 8192  // a build-time A/B knob (tools/ragged_study.py over builds with -DKARMA_RAGGED_UNIT=...)
 #endif
 constexpr uint64_t kDefaultUnit = KARMA_RAGGED_UNIT;  // unit size for ragged batches
+// WAL images up to this take replay's device-planned path (wal.cc); wal_device.hip's fused plan
+// sums its candidate counts in 32 bits on that bound (static_assert there).
+constexpr uint64_t kDevicePlanMax = uint64_t(256) << 20;
 
 // ---- table blob of the streaming kernel (uint32 words) ---------------------
 constexpr int kBlobStride = 0;     // Z_S slicing tables, 4 x 256

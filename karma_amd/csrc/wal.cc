@@ -151,7 +151,6 @@ struct DevBuf {
 // Walkers switch to direct header rounds after a fast round of this many headers.
 constexpr uint32_t kDirectStreak = 8;
 constexpr uint32_t kSmallRecordMax = 1024;      // payloads up to this take the one-record-per-group batch
-constexpr uint64_t kDevicePlanMax = uint64_t(256) << 20;  // images up to this: the device-planned path
 struct ReplayCtx {
     std::mutex mu;
     bool ready = false;

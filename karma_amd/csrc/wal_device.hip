@@ -1088,8 +1088,9 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
         __syncthreads();
         const uint32_t w1 = s_w1;
         if (blockIdx.x >= w1 && blockIdx.x != 0) return;  // replay does not enter this segment
-        // (32-bit sums through DPP: the device-planned path has images <= 256 MiB, so fewer than
-        // 2^26 candidates in all)
+        // (32-bit sums through DPP: the device-planned path has images <= kDevicePlanMax, and a
+        // candidate takes at least 8 image bytes, so the counts fit in 32 bits)
+        static_assert(kDevicePlanMax / 8 < (1ull << 32), "fused-plan candidate sums are 32-bit");
         const unsigned long long pre = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(tid < blockIdx.x ? m.count : 0u), 63);
         const unsigned long long all = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(tid < w1 ? m.count : 0u), 63);
         if (lane == 0) {

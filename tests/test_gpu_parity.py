@@ -510,6 +510,27 @@ def _variants_match_oracle(raw, dev):
     _eq(got, oracle_lib.ragged_crcs(host, offs, lens, ini.astype(np.uint32)))
 
 
+@pytest.mark.parametrize("form", ["40", "41", "60", "61"])
+def test_ragged_units_stream_form_matches_oracle(raw, dev, form, monkeypatch):
+    """The tools build's descriptor-driven stream form of the ragged units kernel
+    (k_units_ragged_stream: stream_unit with masked edges, KARMA_RAGGED_UNITS_STREAM = PF, dynamic
+    tail) is held to the shipped kernel's parity: every length 0..300 at every alignment with
+    per-record inits, records of many units and of one, WAL-framed whole units, the variants mix."""
+    host, dbuf = raw
+    monkeypatch.setenv("KARMA_RAGGED_UNITS_STREAM", form)
+    with _lib.using(_lib.AB_LIB_PATH):
+        test_ragged_edge_lengths_every_alignment(raw, dev)
+        test_ragged_overlapping_large_and_end_of_buffer(raw, dev)
+        test_ragged_many_records_per_lane_with_huge_records(raw, dev, 300_000)
+        test_ragged_wal_framed_units_fill_whole_units(raw, dev, 8)
+        _variants_match_oracle(raw, dev)
+        shorts = np.full(5000, 9, np.uint32)  # only short records: no units at all
+        soffs = (np.arange(5000, dtype=np.uint64) * 37).astype(np.uint64)
+        _eq(K.extend_batch_ragged(dbuf, torch.from_numpy(soffs.astype(np.int64)).to(dev),
+                                  torch.from_numpy(shorts.astype(np.int32)).to(dev), total_len=int(shorts.sum()))
+            .cpu().numpy(), oracle_lib.ragged_crcs(host, soffs, shorts))
+
+
 @pytest.mark.parametrize("build", ["shipped", "tag_wrap"])
 def test_ragged_plan_many_blocks_lookback(raw, dev, build, monkeypatch):
     """The single-pass plan (k_ragged_plan) chains its blocks' unit counts by a decoupled
@@ -624,6 +645,25 @@ def test_ragged_low_total_len_is_still_exact(raw, dev):
     for total in (int(lens.sum()), int(lens.sum()) // 3, 1, 8192):
         got = K.extend_batch_ragged(dbuf[:arena], d_off, d_len, total_len=total).cpu().numpy()
         _eq(got, want)
+
+
+@pytest.mark.parametrize("head", [8, 15, 1])
+def test_ragged_wal_framed_units_fill_whole_units(raw, dev, head):
+    """Records of U - head bytes at offset head mod U (U = 8 KiB ragged unit; head 8 = the WAL's
+    [crc][len|type] header at stride U): each record's whole 16-byte blocks span a full unit, so
+    the batch has n full units for a payload sum below n U.  With the exact total_len the unit
+    table must still hold them all (capi.cc sizes it for the widened spans); CRCs bit-exact."""
+    host, dbuf = raw
+    U = 8192
+    shift = (-dbuf.data_ptr()) % U  # absolute unit boundaries: offsets are relative to the arena base
+    n = (host.size - shift) // U - 1
+    offs = (shift + head + np.arange(n, dtype=np.uint64) * np.uint64(U)).astype(np.uint64)
+    lens = np.full(n, U - head, dtype=np.uint32)
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    want = oracle_lib.ragged_crcs(host, offs, lens)
+    _eq(K.extend_batch_ragged(dbuf, d_off, d_len, total_len=int(lens.sum())).cpu().numpy(), want)
+    _eq(K.extend_batch_ragged(dbuf, d_off, d_len).cpu().numpy(), want)
 
 
 @pytest.mark.parametrize("variant", ["shipped", "20", "21", "22"])
