@@ -562,7 +562,9 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
         b.blob = L.ds->lane_blob;
         b.gate_max = stg_max;
         b.stage_skew_seen = d_skew_seen;
-        const uint64_t sblocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_cap, 64 * kStgWaves));
+        uint64_t sblocks = std::min<uint64_t>((uint64_t)L.ds->cu, ceil_div(n_cap, 64 * kStgWaves));
+        if (const long g = KARMA_AB_KNOB("KARMA_STAGE_BLOCKS", 0); g > 0)  // (A/B: fewer CUs for the batch)
+            sblocks = std::min<uint64_t>(sblocks, (uint64_t)g);
         units_timer_begin(s);  // (karma_crc32c_time_next_units: the replay's CRC kernel)
         KARMA_HIP(launch_ragged_staged_dev(b, (int)sblocks, s, stage_skew));
         units_timer_end(s);

@@ -885,11 +885,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // TM (timing attribution, tools build only, wrong CRCs): 1 = no CRC steps (each lane xors one
 // stage word into its result), 2 = no record loads or stage stores (the steps run over whatever
 // the stage holds), 3 = neither.
-template <bool SK, bool R8 = false, int TM = 0>
-__global__ __launch_bounds__((R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
+// NWO (tools build A/B, with R8): that many waves instead of kStgWaves8, leaving LDS for another
+// kernel's workgroups on the same CU (the sliced WAL replay's walkers, wal.cc).
+template <bool SK, bool R8 = false, int TM = 0, int NWO = 0>
+__global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     static_assert(!(SK && R8), "the 8-copy form has the plain stage only");
     constexpr bool END = true;
-    constexpr int NW = R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : 24;
+    constexpr int NW = NWO ? NWO : R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : 24;
     constexpr int TW = R8 ? kRep8Words : kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
     constexpr uint32_t kLead = 16u, kFit = kStgBytes - 32u;
     constexpr uint32_t kStride = SK ? kStgBytes + kStgBytes / 32 : kStgBytes;  // bytes per wave's stage
@@ -1080,7 +1082,14 @@ hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStr
     if (skew) {
         hipLaunchKernelGGL((k_ragged_staged_pipe<true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
 #ifdef KARMA_AB
-    } else if (KARMA_AB_KNOB("KARMA_STAGE_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves; not
+    } else if (const long r8 = KARMA_AB_KNOB("KARMA_STAGE_R8", 0); r8 == 6 || r8 == 4) {
+        // (A/B, round 6: the 8-copy image with 6 or 4 waves, 109 / 85 KiB of LDS: room beside it
+        // for 12 / 18 of the sliced replay's 4 KiB walkers per CU)
+        if (r8 == 6)
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, true, 0, 6>), dim3(grid_blocks), dim3(6 * 64), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, true, 0, 4>), dim3(grid_blocks), dim3(4 * 64), 0, s, a);
+    } else if (r8) {  // (A/B: the 8-copy image, kStgWaves8 waves; not
         // shipped: 1M x 180 B 0.1219 vs 0.1215 ms per replay call, 100-B payloads 0.0978 vs 0.1007)
         const uint64_t g = std::min<uint64_t>((uint64_t)grid_blocks, (a.n_rec + 64 * kStgWaves8 - 1) / (64 * kStgWaves8));
         hipLaunchKernelGGL((k_ragged_staged_pipe<false, true>), dim3((unsigned)g), dim3(kStgWaves8 * 64), 0, s, a);

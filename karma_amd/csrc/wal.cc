@@ -156,6 +156,10 @@ struct ReplayCtx {
     bool ready = false;
     int cu = 1;
     hipStream_t st = nullptr;
+    // the sliced pass (tools build, KARMA_WAL_SLICES=2): the CRC batches' stream and the events
+    // ordering them after their slice's gather
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, sum;
     DevBuf h_small;                             // pinned readback of the summary
     uint64_t img_gen = 0;                       // uploads of a host image into img so far
@@ -184,6 +188,16 @@ struct ReplayCtx {
             b->release();
         (void)hipStreamDestroy(st);
         st = nullptr;
+        if (st2) {
+            (void)hipStreamSynchronize(st2);
+            (void)karma::engine::release_internal_stream(dev, st2);
+            (void)hipStreamDestroy(st2);
+            st2 = nullptr;
+        }
+        for (hipEvent_t& e : ev) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
         ++img_gen;  // a replay between passes must not take the freed image for its own
         ready = false;
     }
@@ -295,6 +309,137 @@ int karma_wal_replay_tuned(const void* h_wal, const void* d_wal, size_t wal_byte
 
 namespace {
 
+#ifdef KARMA_AB
+// The device-planned pass in two slices of segments (tools build A/B, KARMA_WAL_SLICES=2; round 6,
+// DESIGN.md §8a): slice k's walk and gather on the replay stream, its staged CRC batch on a second
+// stream ordered after that gather by an event, so slice 1's walk can run beside slice 0's CRCs.
+// Each slice is replayed as an image of its own (its lists, its summary); replay enters slice 1 at
+// offset 0 exactly when slice 0's walk ended cleanly at its last segment's end (status END: no
+// stop, no spill), and its results then follow slice 0's.  Otherwise slice 1's work was
+// speculative and slice 0's result is the pass's (a spill continues in replay_core as usual).
+// Taken only when the previous pass's largest payload went to the staged kernel; returns 1 when a
+// slice's payloads were not covered by it (the caller then runs the pass unsliced).
+int sliced_pass(ReplayCtx& c, const karma::engine::WalArgs& A, const karma_wal_tuning* tuning, uint64_t* h_n_records,
+                uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap) {
+    using namespace karma::engine;
+    const uint64_t seg = A.seg_bytes, nwork = A.nwork;
+    const uint64_t n0 = (nwork + 1) / 2, ns[2] = {n0, nwork - n0};
+    const WalWalkPlan plan = wal_walk_plan(seg, n0, c.cu, tuning ? tuning->walk_sub_bytes : 0, false, false);
+    const uint64_t cap[2] = {ns[0] * seg / 8 + ns[0], ns[1] * seg / 8 + ns[1]};
+    if (!c.st2 && hipStreamCreateWithFlags(&c.st2, hipStreamNonBlocking) != hipSuccess) {
+        c.st2 = nullptr;
+        return fail(KARMA_E_HIP, "wal_replay: stream");
+    }
+    for (hipEvent_t& e : c.ev)
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            e = nullptr;
+            return fail(KARMA_E_HIP, "wal_replay: event");
+        }
+    for (auto [b, bytes] : {std::pair<DevBuf*, size_t>{&c.crec, nwork * plan.cand_cap * 4}, {&c.clen, nwork * plan.cand_cap * 4},
+                            {&c.ccrc, nwork * plan.cand_cap * 4}, {&c.meta, nwork * sizeof(WalSegMeta)},
+                            {&c.sub, nwork * plan.nsub * sizeof(WalSubMeta)}, {&c.span, nwork * plan.nsub * 8},
+                            {&c.cbase, nwork * 8}, {&c.sum, 2 * sizeof(WalSummary)}, {&c.off, (cap[0] + cap[1]) * 8},
+                            {&c.len, (cap[0] + cap[1]) * 4}, {&c.stored, (cap[0] + cap[1]) * 4}, {&c.crc, (cap[0] + cap[1]) * 4}})
+        if (const int rc = b->ensure(bytes)) return rc;
+    if (const int rc = c.h_small.ensure(2 * sizeof(WalSummary), true)) return rc;
+    WalArgs S[2];
+    for (int k = 0; k < 2; ++k) {
+        const uint64_t s0 = k ? n0 : 0, l0 = k ? cap[0] : 0;
+        WalArgs& a = S[k];
+        a = A;
+        a.wal = A.wal + s0 * seg;
+        a.base0 = A.base0 + s0 * seg;
+        a.first_pos = k ? 0 : A.first_pos;
+        a.nwork = ns[k];
+        a.img_bytes = ns[k] * seg;
+        a.wal_end = a.base0 + a.img_bytes;
+        a.nsub = plan.nsub;
+        a.sub_bytes = plan.sub_bytes;
+        a.sub_cap = plan.sub_cap;
+        a.cand_cap = plan.cand_cap;
+        a.cand_rec = c.crec.as<uint32_t>() + s0 * plan.cand_cap;
+        a.cand_len = c.clen.as<uint32_t>() + s0 * plan.cand_cap;
+        a.cand_crc = c.ccrc.as<uint32_t>() + s0 * plan.cand_cap;
+        a.meta = c.meta.as<WalSegMeta>() + s0;
+        a.sub = c.sub.as<WalSubMeta>() + s0 * plan.nsub;
+        a.span = c.span.as<uint32_t>() + s0 * plan.nsub * 2;
+        a.cand_base = c.cbase.as<uint64_t>() + s0;
+        a.sum = c.sum.as<WalSummary>() + k;
+        a.first_bad = &a.sum->first_bad;
+        a.off = c.off.as<uint64_t>() + l0;
+        a.len = c.len.as<uint32_t>() + l0;
+        a.stored = c.stored.as<uint32_t>() + l0;
+        a.crc = c.crc.as<uint32_t>() + l0;
+        a.n_all = cap[k];
+    }
+    const long skew_knob = KARMA_AB_KNOB("KARMA_STAGE_SKEW", -1);
+    for (int k = 0; k < 2; ++k) {
+        WalArgs& a = S[k];
+        if (launch_wal_walk(a, ns[k], plan, c.st) != hipSuccess || launch_wal_gather(a, ns[k], true, c.cu, c.st) != hipSuccess ||
+            hipEventRecord(c.ev[k], c.st) != hipSuccess || hipStreamWaitEvent(c.st2, c.ev[k], 0) != hipSuccess)
+            return fail(KARMA_E_HIP, "wal_replay: sliced walk");
+        if (const int rc = ragged_small_batch_dev(a.wal + 8, a.off, a.len, &a.sum->n_all, cap[k], &a.sum->max_len,
+                                                  kSmallRecordMax, const_cast<uint32_t*>(a.crc), a.stored, a.first_bad,
+                                                  c.st2, kSmallStaged, skew_knob >= 0 ? skew_knob != 0 : c.skew_hint,
+                                                  &a.sum->stage_skew))
+            return rc;
+    }
+    WalSummary* H = c.h_small.as<WalSummary>();
+    if (hipEventRecord(c.ev[2], c.st2) != hipSuccess || hipStreamWaitEvent(c.st, c.ev[2], 0) != hipSuccess ||
+        launch_wal_publish(S[0].sum, H, c.st) != hipSuccess || launch_wal_publish(S[1].sum, H + 1, c.st) != hipSuccess ||
+        hipStreamSynchronize(c.st) != hipSuccess)
+        return fail(KARMA_E_HIP, "wal_replay: sliced pass");
+    const WalSummary a = H[0], b = H[1];
+    const bool whole = a.status == KARMA_WAL_END;  // replay entered slice 1 at its first byte
+    const uint32_t max_len = std::max(a.n_all ? a.max_len : 0u, whole && b.n_all ? b.max_len : 0u);
+    if (max_len > kStgGateLen) return 1;  // not all payloads were checksummed by the staged batch
+    c.have_len_hint = a.n_all || (whole && b.n_all) ? true : c.have_len_hint;
+    if (c.have_len_hint) c.len_hint = max_len;
+    c.skew_hint = a.stage_skew != 0 || (whole && b.stage_skew != 0);
+    const uint64_t n_all[2] = {a.n_all, whole ? b.n_all : 0};
+    uint64_t accepted = n_all[0] + n_all[1];
+    int status = (int)(whole ? b.status : a.status);
+    uint64_t end = whole ? b.end : a.end;
+    int bad_k = -1;
+    uint64_t bad_i = 0;
+    if (a.first_bad < n_all[0]) {
+        bad_k = 0;
+        bad_i = a.first_bad;
+        accepted = a.first_bad;
+    } else if (whole && b.first_bad < n_all[1]) {
+        bad_k = 1;
+        bad_i = b.first_bad;
+        accepted = n_all[0] + b.first_bad;
+    }
+    if (bad_k >= 0) {  // the first mismatch in WAL order: "Corrupt record"
+        uint64_t at = 0;
+        if (hipMemcpyAsync(&at, S[bad_k].off + bad_i, 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+            hipStreamSynchronize(c.st) != hipSuccess)
+            return fail(KARMA_E_HIP, "wal_replay: D2H");
+        status = KARMA_WAL_CORRUPT;
+        end = S[bad_k].base0 + at;
+    }
+    if (h_rec_off && rec_cap && accepted) {  // slice 0's offsets, then slice 1's
+        uint64_t done = 0;
+        for (int k = 0; k < 2 && done < std::min<uint64_t>(accepted, rec_cap); ++k) {
+            const uint64_t m = std::min<uint64_t>({n_all[k], accepted - done, rec_cap - done});
+            if (!m) continue;
+            if (hipMemcpyAsync(h_rec_off + done, S[k].off, m * 8, hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+                hipStreamSynchronize(c.st) != hipSuccess)
+                return fail(KARMA_E_HIP, "wal_replay: D2H offsets");
+            const uint64_t base = S[k].base0;
+            uint64_t* o = h_rec_off + done;
+            parallel_for(0, m, 1 << 16, [&](uint64_t i) { o[i] += base; });
+            done += m;
+        }
+    }
+    *h_n_records = accepted;
+    *h_stop = end;
+    *h_status = status;
+    return 0;
+}
+#endif
+
 // One replay pass (replay_core): the image is d_wal, or produced by fill and streamed into
 // HBM (or, h_pinned: the same image in page-locked host memory, one DMA).  Offsets in and
 // out are relative to the image start.
@@ -378,6 +523,14 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         }
 #endif
     }
+#ifdef KARMA_AB
+    if (KARMA_AB_KNOB("KARMA_WAL_SLICES", 1) == 2 && dev_plan && !inline_crc && batch == KARMA_WAL_CRC_PLAN &&
+        nwork >= 2 && (nwork + 1) / 2 <= 1024 && c.have_len_hint && c.len_hint <= kStgGateLen) {
+        const int rc = sliced_pass(c, A, tuning, h_n_records, h_stop, h_status, h_rec_off, rec_cap);
+        if (rc != 1) return rc;
+        c.have_len_hint = false;  // the unsliced pass below launches both small-record kernels
+    }
+#endif
     // 1. segment-parallel header walk (sub-range walkers when there are few segments)
     const WalWalkPlan plan =
         wal_walk_plan(seg_bytes, nwork, c.cu, tuning ? tuning->walk_sub_bytes : 0, inline_crc, list_crc);

@@ -55,10 +55,15 @@ WALKS = {
     "listcrc4k": (True, 4096, _lib.KARMA_WAL_CRC_INLINE), # the LDS-staged kernel (k_wal_list_crc; tools build)
     "r8": (True, 0, _lib.KARMA_WAL_CRC_PLAN),             # the plan, the plain-stage small-record kernel on the
                                                           # 8-copy image with 10 waves (KARMA_STAGE_R8; tools build)
+    "sliced": (True, 0, _lib.KARMA_WAL_CRC_PLAN),         # the pass in two slices of segments, slice 1's walk beside
+                                                          # slice 0's CRCs (KARMA_WAL_SLICES=2; tools build)
+    "sliced_r8": (True, 0, _lib.KARMA_WAL_CRC_PLAN),      # the same with the 6-wave 8-copy staged kernel
 }
 _LIST_CRC = ("listcrc", "listcrc4k")  # KARMA_WAL_LIST_CRC=1
 _NO_STAGED = ("sepdirect4",)  # KARMA_SMALL_STAGED=0
 _R8 = ("r8",)  # KARMA_STAGE_R8=1
+_SLICED = {"sliced": {"KARMA_WAL_SLICES": "2"},
+           "sliced_r8": {"KARMA_WAL_SLICES": "2", "KARMA_STAGE_R8": "6", "KARMA_STAGE_SKEW": "0"}}
 _WALK = {"name": "split"}
 
 
@@ -76,7 +81,11 @@ def _walk_env(monkeypatch, walk):
         monkeypatch.setenv("KARMA_STAGE_R8", "1")
     else:
         monkeypatch.delenv("KARMA_STAGE_R8", raising=False)
-    if WALKS[walk][0] and walk not in _LIST_CRC and walk not in _NO_STAGED and walk not in _R8:
+    for k in ("KARMA_WAL_SLICES", "KARMA_STAGE_SKEW"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in _SLICED.get(walk, {}).items():
+        monkeypatch.setenv(k, v)
+    if WALKS[walk][0] and walk not in _LIST_CRC and walk not in _NO_STAGED and walk not in _R8 and walk not in _SLICED:
         monkeypatch.setenv("KARMA_WALK_VARIANT", "1")  # read by the tools build only (ab.h)
     else:
         monkeypatch.delenv("KARMA_WALK_VARIANT", raising=False)
@@ -440,7 +449,7 @@ def test_replay_randomized_against_model(lib, monkeypatch):
             assert got == (list(want[0]), want[1], want[2]), (case, walk, seg, mix)
 
 
-@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc", "r8"])
+@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc", "r8", "sliced", "sliced_r8"])
 @pytest.mark.parametrize("seg", [4096 + 4, 65536, 1 << 20])
 def test_replay_uniform_runs_speculative_walk(lib, seg, walk, monkeypatch):
     """Runs of one record size (the walker reads a round of headers at the last stride, lane j at
@@ -534,7 +543,7 @@ def test_replay_accepted_size0_records_advance_12(lib, seg, walk, monkeypatch):
     assert spills > 0, "some size-0 record must carry the chain into the next segment"
 
 
-@pytest.mark.parametrize("walk", ["split", "sep", "split4k", "r8"])
+@pytest.mark.parametrize("walk", ["split", "sep", "split4k", "r8", "sliced"])
 def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
     """The device-planned replay launches one small-record kernel, chosen by the largest payload of
     the previous call on the same device (the staged kernel up to 183 B, the 4-lane kernel up to
@@ -567,7 +576,7 @@ def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
         assert got == (list(w[0]), w[1], w[2]), (i, name, walk)
 
 
-@pytest.mark.parametrize("walk", ["split", "sep", "r8"])
+@pytest.mark.parametrize("walk", ["split", "sep", "r8", "sliced"])
 def test_replay_stage_skew_hint_between_calls(lib, walk, monkeypatch):
     """The staged small-record kernel comes in two forms, with the bank-skewed stage (records on
     few LDS banks: strides that are multiples of 32 bytes) and without it; a call takes the form
@@ -596,3 +605,44 @@ def test_replay_stage_skew_hint_between_calls(lib, walk, monkeypatch):
     for i, name in enumerate(order):
         w = want[name]
         assert _replay(lib, wals[name], d_wal=dev[name], seg=seg, host=False) == (list(w[0]), w[1], w[2]), (i, name)
+
+
+@pytest.mark.parametrize("walk", ["sliced", "sliced_r8"])
+@pytest.mark.parametrize("nseg", [2, 7, 40])
+def test_replay_sliced_pass_every_stop(lib, walk, nseg, monkeypatch):
+    """The tools build's sliced pass (wal.cc sliced_pass: slice 1's walk beside slice 0's staged
+    CRCs): small payloads (<= 180 B, so the previous call's hint takes the sliced path), replayed
+    twice each, from the start and from checkpoints in either slice, with every kind of stop in
+    either slice -- a corrupt payload, a bad type, a zero tail (the never-written rest) ending
+    slice 0 early (slice 1's work is then speculative and must not count) -- against the model."""
+    _walk_env(monkeypatch, walk)
+    seg = 16 << 10
+    n = nseg * seg // 100
+    src, offs, lens = _payloads(nseg + len(walk), n, 1, 180)
+    wal = np.zeros(nseg * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    h = [int(x) for x in rec]
+    half = (nseg + 1) // 2 * seg  # slice 1's first byte
+    in0 = [i for i, x in enumerate(h) if x < half]
+    in1 = [i for i, x in enumerate(h) if x >= half]
+    images = {"clean": wal}
+    for name, k in (("bad0", in0[len(in0) // 2]), ("bad1", in1[len(in1) // 3] if in1 else None)):
+        if k is None:
+            continue
+        img = wal.copy()
+        img[h[k] + 8 + int(lens[k]) // 2] ^= 0x20
+        images[name] = img
+    img = wal.copy()
+    img[h[in0[len(in0) // 3]] + 4] = 9
+    images["badtype0"] = img
+    img = wal.copy()
+    img[h[in0[-5]]:half] = 0  # the WAL ends inside slice 0
+    images["tail0"] = img
+    d = {k: torch.from_numpy(v).cuda() for k, v in images.items()}
+    for name, img in images.items():
+        starts = [0, h[in0[len(in0) // 4]]] + ([h[in1[len(in1) // 2]]] if in1 else [])
+        for start in starts:
+            w = wal_model.replay(img.tobytes(), seg, start)
+            for _ in range(2):  # (the first call may take the unsliced path: the previous call's hint)
+                got = _replay(lib, img, start=start, seg=seg, d_wal=d[name], host=False)
+                assert got == (list(w[0]), w[1], w[2]), (name, start)

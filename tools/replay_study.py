@@ -117,9 +117,8 @@ def main():
             variants[v] = (L, 0, 3, None)
         elif v.startswith("sub="):
             variants[v] = (L, int(v[4:]), 0, None)
-        elif v.startswith("ab:"):  # tools build, default plan, one knob: ab:NAME=VALUE
-            name, _, val = v[3:].partition("=")
-            variants[v] = (AB, 0, 0, (name, val))
+        elif v.startswith("ab:"):  # tools build, default plan, knobs: ab:NAME=VALUE[+NAME2=VALUE2...]
+            variants[v] = (AB, 0, 0, [tuple(kv.split("=", 1)) for kv in v[3:].split("+")])
         elif v.startswith("lib="):  # another build's default plan, loaded beside the shipped one
             path = v[4:]
             variants[v] = (_lib.load(path if os.path.isabs(path) else os.path.join(ROOT, path)), 0, 0, None)
@@ -139,15 +138,17 @@ def main():
     for r in range(a.rounds):
         for v, (lib, sub, batch, env) in variants.items():
             for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC", "KARMA_SMALL_STAGED", "KARMA_WALK_DIRECT",
-                      "KARMA_GATHER_PARTS", "KARMA_SMALL_WHICH", "KARMA_STAGE_SKEW", "KARMA_STAGE_R8"):
+                      "KARMA_GATHER_PARTS", "KARMA_SMALL_WHICH", "KARMA_STAGE_SKEW", "KARMA_STAGE_R8",
+                      "KARMA_WAL_SLICES", "KARMA_STAGE_BLOCKS"):
                 os.environ.pop(k, None)
-            if env:
-                os.environ[env[0]] = env[1]
+            pairs = env if isinstance(env, list) else [env] if env else []
+            for name, val in pairs:
+                os.environ[name] = val
             res[v].append(timed(lib, sub, batch, False))
             if a.single:
                 res1[v].append(timed(lib, sub, batch, True))
-            if env:
-                del os.environ[env[0]]
+            for name, _ in pairs:
+                del os.environ[name]
         print(f"round {r}: " + "  ".join(f"{v} {res[v][-1]:.4f}" + (f" (single {res1[v][-1]:.4f})" if a.single else "")
                                          for v in variants), flush=True)
     print(f"images: {len(d_wals)} x {wal_bytes / 1e6:.1f} MB rotated ({len(d_wals) * wal_bytes / 2**20:.0f} MiB)")
