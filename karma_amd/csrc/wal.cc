@@ -324,7 +324,9 @@ int sliced_pass(ReplayCtx& c, const karma::engine::WalArgs& A, const karma_wal_t
     using namespace karma::engine;
     const uint64_t seg = A.seg_bytes, nwork = A.nwork;
     const uint64_t n0 = (nwork + 1) / 2, ns[2] = {n0, nwork - n0};
-    const WalWalkPlan plan = wal_walk_plan(seg, n0, c.cu, tuning ? tuning->walk_sub_bytes : 0, false, false);
+    // (KARMA_WAL_SLICE_PLAN=1: the sub-range split of the whole image's plan, not of a slice's)
+    const uint64_t plan_nseg = KARMA_AB_KNOB("KARMA_WAL_SLICE_PLAN", 0) ? nwork : n0;
+    const WalWalkPlan plan = wal_walk_plan(seg, plan_nseg, c.cu, tuning ? tuning->walk_sub_bytes : 0, false, false);
     const uint64_t cap[2] = {ns[0] * seg / 8 + ns[0], ns[1] * seg / 8 + ns[1]};
     if (!c.st2 && hipStreamCreateWithFlags(&c.st2, hipStreamNonBlocking) != hipSuccess) {
         c.st2 = nullptr;

@@ -37,7 +37,7 @@ for item in os.environ.get("LIBS", f"shipped={_lib.LIB_PATH}").split(","):
     if path not in _loaded:
         _loaded[path] = _lib.load(path)
     LIBS[name] = _loaded[path]
-    KNOBS[name] = dict(kv.split("=", 1) for kv in kn.split(";") if kv)
+    KNOBS[name] = dict(kv.split("=", 1) for kv in kn.replace("+", ";").split(";") if kv)
 
 
 def set_knobs(name):

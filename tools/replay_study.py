@@ -139,7 +139,7 @@ def main():
         for v, (lib, sub, batch, env) in variants.items():
             for k in ("KARMA_DIRECT_VARIANT", "KARMA_WAL_LIST_CRC", "KARMA_SMALL_STAGED", "KARMA_WALK_DIRECT",
                       "KARMA_GATHER_PARTS", "KARMA_SMALL_WHICH", "KARMA_STAGE_SKEW", "KARMA_STAGE_R8",
-                      "KARMA_WAL_SLICES", "KARMA_STAGE_BLOCKS"):
+                      "KARMA_WAL_SLICES", "KARMA_STAGE_BLOCKS", "KARMA_WAL_SLICE_PLAN"):
                 os.environ.pop(k, None)
             pairs = env if isinstance(env, list) else [env] if env else []
             for name, val in pairs:
