@@ -275,8 +275,13 @@ __device__ uint64_t* g_seg_log;
 // workgroup waiting for the others: no workgroup waits on one that may not have been scheduled, so
 // the forward-progress contract of include/karma_crc32c.h is not needed.  Every workgroup then
 // loads the grid fold maps (any may fold).
-template <bool NT, bool ARRIVE = false>
+// R8 (tools build A/B, round 6): the 8-copy stride image (32 KiB, stride_step8) instead of the
+// 16-copy one (64 KiB): half the table fill the chunk loads queue behind.
+template <bool NT, bool ARRIVE = false, bool R8 = false>
 __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
+    constexpr int TW = R8 ? kRep8Words : kRep16Words;
+    constexpr int kSegZ4 = TW, kSegComb = kSegZ4 + kSmallWords, kSegGrid = kSegComb + kCombMaps * 1024;
+    constexpr int kSegLdsWords = kSegGrid + kCombMaps * 1024;
     KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
                  (reinterpret_cast<uintptr_t>(A.arena + A.rec_bytes) + 15) & ~uintptr_t(15));
     __shared__ __attribute__((aligned(16))) uint32_t lds[kSegLdsWords];
@@ -292,11 +297,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     // stores -- the stores then wait for the table loads alone -- measured 2 us slower per isolated
     // 64 MiB call, profiles/r05_segment_early_ab.json.)  The call's tag, the grid's fold maps and the tail block are read after the steps.
     // 1. the table words this thread fills
-    constexpr int NV16 = kRep16Words / 4, IT16 = NV16 / kBlockThreads;
+    constexpr int NV16 = TW / 4, IT16 = NV16 / kBlockThreads;
     uint32_t e16[IT16];
 #pragma unroll
     for (int q = 0; q < IT16; ++q) {
-        const int v = (int)threadIdx.x + q * kBlockThreads, row = v >> 4, k = (v >> 2) & 3;
+        const int v = (int)threadIdx.x + q * kBlockThreads;
+        // (16-copy: row e = v >> 4, table k; 8-copy, load_rep8_stride's layout: entry v >> 3, table (v >> 1) & 3)
+        const int row = R8 ? v >> 3 : v >> 4, k = R8 ? (v >> 1) & 3 : (v >> 2) & 3;
         e16[q] = *(const __attribute__((address_space(1))) uint32_t*)(A.blob + kBlobStride + k * 256 + row);
     }
     LdsCopy<kSmallWords, kBlockThreads> small;
@@ -339,7 +346,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     uint32_t a0 = x0.x, a1 = x0.y, a2 = x0.z, a3 = x0.w;
 #pragma unroll
     for (int q = 1; q < kSegMaxChunks; ++q)
-        if (q < L.nch - 1 || (q == L.nch - 1 && L.lok)) step4<24>(lds, X, a0, a1, a2, a3, v[q]);
+        if (q < L.nch - 1 || (q == L.nch - 1 && L.lok)) step4<R8 ? 32 : 24>(lds, X, a0, a1, a2, a3, v[q]);
     LdsCopy<kCombMaps * 1024, kBlockThreads> grid;  // the last workgroup's fold maps, in flight meanwhile
     if (ARRIVE || last_wg) grid.load(A.block_blob);
     uint32_t tag = 0;  // wave 0 publishes the workgroup's state, tagged with the call's tag
@@ -652,6 +659,10 @@ hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t 
     units_timer_begin(s);
     if (arrive)
         hipLaunchKernelGGL((k_segment_once<true, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+#ifdef KARMA_AB
+    else if (KARMA_AB_KNOB("KARMA_SEGMENT_R8", 0))  // (A/B: the 8-copy stride image)
+        hipLaunchKernelGGL((k_segment_once<true, false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+#endif
     else
         hipLaunchKernelGGL((k_segment_once<true, false>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);

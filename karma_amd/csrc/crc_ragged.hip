@@ -673,7 +673,10 @@ __device__ __forceinline__ uint32_t shift_last(const uint32_t* lds, uint32_t x, 
 // table fill), then the first ten unit contributions.  No record bytes are read.  (Round 4's
 // one-record lanes took four dependent rounds -- geometry, slots, contributions, tail -- and 444
 // blocks of them two rounds of blocks on configs[2]: 22 us, profiles/r05_plan_phases.json.)
-template <int FR>
+// LITE (tools build A/B, round 6): the LDS fill skips the maps Z_{2U} .. Z_{64U} (24 of its 88 KiB),
+// which only records of more than 64 units use; those fold with the maps read from the blob in
+// global memory instead.
+template <int FR, bool LITE = false>
 __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kCombWords];
@@ -709,7 +712,13 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
     // table fill and those loads share a round trip: finalize 13.1 against 12.6 us, calls equal,
     // profiles/r05_finalize_overlap_ab.txt -- its first loads are bandwidth, not latency.)
     if (r0 < A.n_rec) stage1(r0);
-    load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
+    if constexpr (LITE) {
+        load_comb_tables<1024, 1024>(lds, A.comb_blob);
+        load_comb_tables<kCombWords - kCombZ4, 1024>(lds + kCombZ4, A.comb_blob + kCombZ4);
+    } else {
+        load_comb_tables<kCombWords, 1024>(lds, A.comb_blob);
+    }
+    const uint32_t* big = LITE ? A.comb_blob : lds;  // the maps Z_{2^k U} of the huge records' fold
     __syncthreads();
     PLAN_STAMP(8 * kPlanLogBlocks, 1);  // tables
     // the plan's look-back words are retired after the first contributions are issued: its
@@ -780,8 +789,8 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
                     const int64_t idx = (int64_t)(blk * 64 + lane) - pad;
                     uint32_t v = 0;
                     if (idx >= 0) v = A.partial[idx == 0 && hp0 ? hps0 : hfb + idx - hp0];
-                    v = wave_tree(lds, v);
-                    w = zmap(lds, 6 * 1024, w) ^ v;
+                    v = wave_tree(big, v);
+                    w = zmap(big, 6 * 1024, w) ^ v;
                 }
                 w = __shfl(w, 0);
                 if ((int)lane == h) acc[j] = w;
@@ -1184,6 +1193,17 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     const uint64_t fb1 = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
     const int FR = fb1 <= cu ? 1 : fb1 <= 2 * cu ? 2 : 4;
     const unsigned fblocks = (unsigned)std::min<uint64_t>((fb1 + FR - 1) / FR, cu);
+#ifdef KARMA_AB
+    if (KARMA_AB_KNOB("KARMA_FINALIZE_LITE", 0)) {  // (A/B: the LDS fill without the huge records' maps)
+        if (FR == 1)
+            hipLaunchKernelGGL((k_ragged_finalize<1, true>), dim3(fblocks), dim3(1024), 0, s, a);
+        else if (FR == 2)
+            hipLaunchKernelGGL((k_ragged_finalize<2, true>), dim3(fblocks), dim3(1024), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_ragged_finalize<4, true>), dim3(fblocks), dim3(1024), 0, s, a);
+        return hipGetLastError();
+    }
+#endif
     if (FR == 1)
         hipLaunchKernelGGL(k_ragged_finalize<1>, dim3(fblocks), dim3(1024), 0, s, a);
     else if (FR == 2)

@@ -285,6 +285,14 @@ def test_segment_once_sizes_and_alignments(dev):
         assert got == oracle_lib.extend(0x7A5C31E9, host[off: off + m].tobytes()), ("init array", off, m)
 
 
+def test_segment_once_8copy_tables(dev, monkeypatch):
+    """The tools build's k_segment_once on the 8-copy stride image (KARMA_SEGMENT_R8=1: half the
+    table fill) is held to the shipped form's parity: every size, alignment and init case above."""
+    monkeypatch.setenv("KARMA_SEGMENT_R8", "1")
+    with _lib.using(_lib.AB_LIB_PATH):
+        test_segment_once_sizes_and_alignments(dev)
+
+
 def test_segment_once_arrival_fold(dev, monkeypatch):
     """k_segment_once with the last-ARRIVING workgroup folding (one ticket per workgroup; the
     tools build's KARMA_SEGMENT_ONCE=2): sizes at the thresholds and unaligned, repeated calls
@@ -529,6 +537,19 @@ def test_ragged_units_stream_form_matches_oracle(raw, dev, form, monkeypatch):
         _eq(K.extend_batch_ragged(dbuf, torch.from_numpy(soffs.astype(np.int64)).to(dev),
                                   torch.from_numpy(shorts.astype(np.int32)).to(dev), total_len=int(shorts.sum()))
             .cpu().numpy(), oracle_lib.ragged_crcs(host, soffs, shorts))
+
+
+def test_ragged_finalize_lite_fill_matches_oracle(raw, dev, monkeypatch):
+    """The tools build's finalize with the smaller LDS fill (KARMA_FINALIZE_LITE=1: records of more
+    than 64 units fold with the maps read from global memory): huge records at the batch's start,
+    middle and end with FR = 2 and 4 records per lane, every edge length and alignment."""
+    monkeypatch.setenv("KARMA_FINALIZE_LITE", "1")
+    with _lib.using(_lib.AB_LIB_PATH):
+        test_ragged_many_records_per_lane_with_huge_records(raw, dev, 300_000)
+        test_ragged_many_records_per_lane_with_huge_records(raw, dev, 1_200_000)
+        test_ragged_edge_lengths_every_alignment(raw, dev)
+        test_ragged_overlapping_large_and_end_of_buffer(raw, dev)
+        test_ragged_low_total_len_is_still_exact(raw, dev)
 
 
 @pytest.mark.parametrize("build", ["shipped", "tag_wrap"])

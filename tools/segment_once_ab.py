@@ -33,7 +33,8 @@ def main():
     p.add_argument("--libs", default="", help="name=path,... : builds compared at their defaults "
                    "(instead of the tools build's KARMA_SEGMENT_ONCE=1 / 0)")
     p.add_argument("--variants", default="1,0", help="KARMA_SEGMENT_ONCE values of the tools build (1 = the grid's "
-                   "last workgroup folds, 2 = the last-arriving one, 0 = the looping fused kernel)")
+                   "last workgroup folds, 2 = the last-arriving one, 0 = the looping fused kernel; r8 = 1 on the "
+                   "8-copy stride image)")
     a = p.parse_args()
     dev = torch.device("cuda:0")
     nseg, top = 64, 64 << 20
@@ -55,8 +56,12 @@ def main():
 
         def call(v):
             lib = libs.get(v, L)
-            if not libs:
-                os.environ["KARMA_SEGMENT_ONCE"] = v
+            if not libs:  # (r8: KARMA_SEGMENT_ONCE=1 on the 8-copy stride image, KARMA_SEGMENT_R8=1)
+                os.environ["KARMA_SEGMENT_ONCE"] = "1" if v == "r8" else v
+                if v == "r8":
+                    os.environ["KARMA_SEGMENT_R8"] = "1"
+                else:
+                    os.environ.pop("KARMA_SEGMENT_R8", None)
             i = state["i"] % nseg
             state["i"] += 1
             _lib.check("stream", lib.karma_crc32c_stream(0, arena.data_ptr() + i * top, seg,
@@ -97,6 +102,7 @@ def main():
         # one logged call of k_segment_once: per-workgroup stamps (us from the earliest entry)
         if hasattr(L, "karma_ab_seg_log") and not libs:
             os.environ["KARMA_SEGMENT_ONCE"] = "1"
+            os.environ.pop("KARMA_SEGMENT_R8", None)
             log = torch.zeros(256 * 8, dtype=torch.int64, device=dev)
             torch.cuda.synchronize()
             L.karma_ab_seg_log(ctypes.c_void_p(log.data_ptr()))

@@ -53,7 +53,8 @@ def main():
     for r in rows:
         name = r["Kernel_Name"]
         fam = "A" if any(k in name for k in fa) else "B" if any(k in name for k in fb) else None
-        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), fam, name.split("(")[0][:48], r.get(q, "")))
+        short = name.replace("(anonymous namespace)::", "").replace("karma::engine::", "").replace("void ", "")
+        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), fam, short.split("(")[0][:56], r.get(q, "")))
     ev.sort()
     t0 = ev[-a.show][0] if len(ev) >= a.show else ev[0][0]
     for s, e, fam, name, qq in ev[-a.show:]:
