@@ -38,12 +38,12 @@ for s in "$@"; do
     smoke) step smoke 300 "python3 -u -c 'import __graft_entry__ as g; g.smoke()'" ;;
     bench) step bench 600 "python3 -u bench.py" ;;
     bench_driver) step bench_driver 300 "python3 -u bench.py --steps 20 --warmup 5" ;;
-    bench_*) step "$s" 400 "python3 -u bench.py --workload ${s#bench_}" ;;
-    profile_*) step "$s" 600 "bash tools/profile_round.sh $TAG ${s#profile_}" ;;
-    *=*)
+    *=*)  # (before the bench_* / profile_* names: a custom step's name may start with them)
       lhs=${s%%=*}; cmd=${s#*=}; name=${lhs%%:*}; secs=400
       [ "$lhs" != "$name" ] && secs=${lhs#*:}
       step "$name" "$secs" "$cmd" ;;
+    bench_*) step "$s" 400 "python3 -u bench.py --workload ${s#bench_}" ;;
+    profile_*) step "$s" 600 "bash tools/profile_round.sh $TAG ${s#profile_}" ;;
     *) echo "unknown step: $s"; exit 2 ;;
   esac
 done
