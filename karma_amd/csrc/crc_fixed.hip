@@ -242,7 +242,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
 }
 
 // ---- one segment, one wave-step per wave (karma_crc32c_stream up to grid x 16 x 8 units) ------
-// DESIGN.md §4 "The single segment": a 64 MiB scan is 4,096 wave-steps of 8 x 2 KiB units, one per
+// DESIGN.md Appendix B "One segment (round 4)": a 64 MiB scan is 4,096 wave-steps of 8 x 2 KiB units, one per
 // wave of a 256-workgroup grid, so the looping kernel above spends its time in latency: the LDS
 // table fill behind the first chunk loads (~4.7 us), four batches of chunk loads one round trip
 // each, and a last-workgroup fold of 4,096 wave states (~4.8 us).  Here every lane issues the

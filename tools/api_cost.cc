@@ -1,5 +1,5 @@
 // tools/api_cost.cc -- host cost of the HIP calls on the library's enqueue path (one 64 MiB
-// segment call enqueues in ~3.3 us from C++, DESIGN.md §4 "One segment"): hipGetDeviceCount,
+// segment call enqueues in ~3.3 us from C++, DESIGN.md Appendix B "One segment"): hipGetDeviceCount,
 // hipGetDevice, hipStreamIsCapturing, an empty kernel launch, and karma_crc32c_stream itself.
 //   hipcc --offload-arch=gfx950 -O2 -o build/api_cost tools/api_cost.cc -Iinclude -Lkarma_amd/lib -lkarma_crc32c \
 //         -Wl,-rpath,$PWD/karma_amd/lib && build/api_cost
