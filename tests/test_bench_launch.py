@@ -44,13 +44,13 @@ def _json_lines(out: str):
     return [json.loads(s) for s in out.splitlines() if s.startswith("{")]
 
 
-def _check_line(line, launcher):
-    assert line["n_gpus"] == 2 and line["dry_nranks"] == 2 and line["dry_backend"] == "gloo"
+def _check_line(line, launcher, n=2):
+    assert line["n_gpus"] == n and line["dry_nranks"] == n and line["dry_backend"] == "gloo"
     assert line["launched_by"] == launcher
     assert line["self_check"]["mismatches"] == 0 and line["self_check"]["gather_mismatches"] == 0
-    assert [p["mismatches"] for p in line["per_rank"]["self_check"]] == [0, 0]
-    want = oracle_lib.splitmix_fixed_crcs(42, REC, 0, 2 * N_REC)
-    assert line["gathered_crcs"] == 2 * N_REC
+    assert [p["mismatches"] for p in line["per_rank"]["self_check"]] == [0] * n
+    want = oracle_lib.splitmix_fixed_crcs(42, REC, 0, n * N_REC)
+    assert line["gathered_crcs"] == n * N_REC
     assert line["gathered_sha256_16"] == hashlib.sha256(want.astype("<u4").tobytes()).hexdigest()[:16]
     assert line["steps"] == 3 and line["value"] > 0
 
@@ -63,6 +63,17 @@ def test_plain_command_launches_its_own_ranks():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout
     _check_line(lines[0], "bench.py")
+
+
+def test_plain_command_four_ranks():
+    """`python bench.py --gpus 4`: four self-launched ranks, every shard in the gathered CRCs."""
+    args = [a if a != "2" else "4" for a in ARGS]
+    r = subprocess.run([sys.executable, BENCH] + args, cwd=ROOT, env=_env(), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    _check_line(lines[0], "bench.py", n=4)
 
 
 def test_torch_distributed_run_launch():
