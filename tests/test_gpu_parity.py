@@ -685,6 +685,28 @@ def test_ragged_wal_framed_units_fill_whole_units(raw, dev, head):
     want = oracle_lib.ragged_crcs(host, offs, lens)
     _eq(K.extend_batch_ragged(dbuf, d_off, d_len, total_len=int(lens.sum())).cpu().numpy(), want)
     _eq(K.extend_batch_ragged(dbuf, d_off, d_len).cpu().numpy(), want)
+    # no record may take finalize's one-lane fallback (a record whose units did not fit the table
+    # is stepped serially by one lane: ~8 KiB of byte-block steps, tens of us): with the exact
+    # total_len the call must run about as fast as with a generous one (twice the payload)
+    out = torch.empty(n, dtype=torch.uint32, device=dev)
+
+    def t(total):
+        ms = []
+        for _ in range(7):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            K.extend_batch_ragged(dbuf, d_off, d_len, out=out, total_len=total)
+            b.record()
+            b.synchronize()
+            ms.append(a.elapsed_time(b))
+        return float(np.median(ms))
+
+    t(2 * int(lens.sum()))  # (warm: workspaces sized)
+    exact, generous = t(int(lens.sum())), t(2 * int(lens.sum()))
+    # (the check's sensitivity: a total_len 16 units short makes 16 records take the fallback)
+    short = t(int(lens.sum()) - 16 * U)
+    assert short > 1.5 * generous + 0.015, (short, generous)
+    assert exact <= 1.5 * generous + 0.015, (exact, generous)
 
 
 @pytest.mark.parametrize("variant", ["shipped", "20", "21", "22"])
