@@ -14,6 +14,8 @@ Default workload = BASELINE.json configs[1]: 1M x 4 KiB records per GPU (weak sc
 of the splitmix64 stream generated on the device before timing (inputs resident in HBM).
 Other workloads (``--workload ragged|stream|host``) measure configs[2], configs[3] and the
 PCIe-inclusive host-memory path; they are reported in DESIGN.md, not by the driver.
+``--dry-backend gloo`` runs the N-rank plumbing on CPU processes (tests/test_bench_launch.py): no
+GPU, the host crc32c::Value for the batch, a gloo gather for RCCL; its line is not a measurement.
 """
 from __future__ import annotations
 
