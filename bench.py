@@ -327,6 +327,26 @@ def pmc_traffic(path: str, workload: str, n_bytes_per_launch: int):
     return d.get("hbm_bytes_per_launch")
 
 
+REPLAY_PMC = "r06final_wal_replay_pmc.json"  # tools/pmc_replay.sh + tools/pmc_kernels.py, the final tree
+
+
+def replay_pmc_traffic(n_rec: int, rec_bytes: int):
+    """(HBM bytes of the replay's CRC kernel per launch, of the whole call) from the per-kernel PMC
+    file of tools/pmc_replay.sh (FETCH_SIZE x 2 + WRITE_SIZE per dispatch; the call: walk,
+    resolve, gather and the CRC batch summed), whose calls replay tools/replay_study.py's default
+    image: 1M x 180 B records in 1 MiB segments.  (None, None) for another shape (not measured)."""
+    if (n_rec, rec_bytes) != (1 << 20, 180):
+        return None, None
+    try:
+        with open(os.path.join(ROOT, "profiles", REPLAY_PMC)) as f:
+            ks = json.load(f)["kernels"]
+        crc = ks["k_ragged_staged_pipe"]
+        return (float(crc["hbm_read_bytes"] + crc["hbm_write_bytes"]),
+                float(sum(k["hbm_read_bytes"] + k["hbm_write_bytes"] for k in ks.values())))
+    except (OSError, ValueError, KeyError, TypeError):
+        return None, None
+
+
 # ---------------------------------------------------------------------------------------------
 def wal_bench(args, L, rank):
     """configs[0] shape end to end from host memory: karma_wal_append_batch (sivir::build_sqe +
@@ -511,11 +531,14 @@ def wal_bench(args, L, rank):
         algo = payload + 20 * n
         achieved = algo / (crc_kernel_ms * 1e-3) / 1e9
         call_s = payload / (dev_rate * GIB)
-        pm = pmc_traffic(os.path.join(ROOT, "profiles", "r04g_wal_replay_pmc.json"), "wal_replay", wal_bytes)
+        pm, pm_call = replay_pmc_traffic(n, size) if size else (None, None)
         res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
-                           "frac": round(achieved / 8000.0, 4), "traffic": pm,
-                           "traffic_source": "profiles/r04g_wal_replay_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, "
-                                             "every kernel of one rotated call)" if pm is not None else None,
+                           "frac": round(achieved / 8000.0, 4), "traffic": round(pm) if pm is not None else None,
+                           "traffic_source": f"profiles/{REPLAY_PMC} (FETCH_SIZE x 2 + WRITE_SIZE of the CRC "
+                                             f"kernel per launch; a separate rocprofv3 --pmc pass, not this run)"
+                           if pm is not None else None,
+                           "call_traffic": round(pm_call) if pm_call is not None else None,
+                           "call_traffic_vs_image": round(pm_call / wal_bytes, 3) if pm_call is not None else None,
                            "kernel": "the replay's payload CRC batch (k_ragged_staged_pipe)",
                            "kernel_ms_avg": round(crc_kernel_ms, 4), "algorithmic_bytes_per_launch": algo,
                            "achieved_source": "algorithmic bytes / the CRC kernel's HIP-event time inside "
