@@ -100,12 +100,28 @@ def launch_ranks(argv, n: int, grace_s: float = 20.0) -> int:
     arguments, and wait for them.  Called before torch is imported: the parent never initialises
     a GPU or loads the HIP library, so starting children is safe.  When a rank fails, the others
     would block in their next collective: they get `grace_s` to finish, then are terminated (the
-    exact PIDs started here).  Returns the worst exit status of the ranks that ended on their own
+    exact PIDs started here); a SIGTERM / SIGINT / SIGHUP to this process is passed on to the ranks
+    before it exits.  Returns the worst exit status of the ranks that ended on their own
     (0 only if every rank returned 0); ranks terminated here do not mask the failure's status."""
+    import signal
     import subprocess
     port = int(os.environ.get("MASTER_PORT") or _free_port())
     script = os.path.abspath(__file__)
     procs = []
+
+    def forward(signum, frame):  # a launcher told to stop stops its ranks first (no orphan holds a GPU)
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        sys.exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

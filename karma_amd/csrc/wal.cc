@@ -395,8 +395,10 @@ int sliced_pass(ReplayCtx& c, const karma::engine::WalArgs& A, const karma_wal_t
     const bool whole = a.status == KARMA_WAL_END;  // replay entered slice 1 at its first byte
     const uint32_t max_len = std::max(a.n_all ? a.max_len : 0u, whole && b.n_all ? b.max_len : 0u);
     if (max_len > kStgGateLen) return 1;  // not all payloads were checksummed by the staged batch
-    c.have_len_hint = a.n_all || (whole && b.n_all) ? true : c.have_len_hint;
-    if (c.have_len_hint) c.len_hint = max_len;
+    if (a.n_all || (whole && b.n_all)) {
+        c.have_len_hint = true;
+        c.len_hint = max_len;
+    }
     c.skew_hint = a.stage_skew != 0 || (whole && b.stage_skew != 0);
     const uint64_t n_all[2] = {a.n_all, whole ? b.n_all : 0};
     uint64_t accepted = n_all[0] + n_all[1];

@@ -106,3 +106,33 @@ def test_single_rank_dry_line():
     assert line["n_gpus"] == 1 and line["launched_by"] == "external" and line["self_check"]["mismatches"] == 0
     want = oracle_lib.splitmix_fixed_crcs(42, REC, 0, N_REC)
     assert line["gathered_sha256_16"] == hashlib.sha256(want.astype("<u4").tobytes()).hexdigest()[:16]
+
+
+def test_plain_command_stop_signal_reaches_the_ranks():
+    """SIGTERM to a self-launching bench.py (a driver's time limit) ends its ranks too: no rank is
+    left running, holding a GPU, after the launcher has gone."""
+    import signal
+    import time
+
+    import psutil
+    args = [a if a != "3" else "100000" for a in ARGS]  # --steps 100000: the ranks keep running
+    p = subprocess.Popen([sys.executable, BENCH] + args, cwd=ROOT, env=_env(), stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL)
+    try:
+        t0 = time.time()
+        kids = []
+        while time.time() - t0 < 120:
+            kids = psutil.Process(p.pid).children()
+            if len(kids) == 2:
+                break
+            time.sleep(0.2)
+        assert len(kids) == 2, kids
+        time.sleep(3)  # the ranks are in their timed loop
+        assert all(k.is_running() for k in kids)
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(60) == 128 + signal.SIGTERM
+        gone, alive = psutil.wait_procs(kids, timeout=30)
+        assert not alive, alive
+    finally:
+        if p.poll() is None:
+            p.kill()
