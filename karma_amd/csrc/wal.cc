@@ -85,15 +85,6 @@ WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t su
 
 namespace {
 
-inline void put32(uint8_t* p, uint32_t v) {
-    p[0] = uint8_t(v);
-    p[1] = uint8_t(v >> 8);
-    p[2] = uint8_t(v >> 16);
-    p[3] = uint8_t(v >> 24);
-}
-
-constexpr uint64_t kHeader = 8;  // store::RECORD_HEADER_LENGTH (common.h:11)
-
 // body(i) for i in [lo, hi) on up to 16 std::threads, at least `grain` items each.
 template <typename F>
 void parallel_for(uint64_t lo, uint64_t hi, uint64_t grain, F&& body) {
