@@ -340,6 +340,10 @@ struct WalArgs {
     uint32_t direct_streak;    // the walkers read headers straight from global memory after a fast round
                                // of at least this many headers (0: tiles only; wal.cc kDirectStreak)
     uintptr_t kb_lo, kb_hi;    // bounds build: the image's allocation (the inline CRC loads)
+    // the fused resolve + gather (k_wal_resolve_gather): per segment two tagged words (count and
+    // stop flag; largest payload), and this call's tag (1..65535; the words are zeroed when it wraps)
+    unsigned long long* rg_words;
+    uint32_t rg_tag;
 };
 constexpr uint32_t kWalkTile = 4096;  // the one-wave walker's LDS tile (wal_device.hip)
 constexpr uint32_t kMaxSub = 4096;    // sub-ranges per segment (k_wal_gather stages their runs in LDS)
@@ -355,13 +359,19 @@ struct WalWalkPlan {
 WalWalkPlan wal_walk_plan(uint64_t seg_bytes, uint64_t nseg, int cu, uint64_t sub_bytes, bool inline_crc = false,
                           bool list_crc = false);
 constexpr int kWalFuseWaves = 15;  // walkers per workgroup of k_wal_walk_crc (wal_device.hip)
-hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s);
+hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s,
+                           bool resolve = true);
 // The replay plan on the device: a.sum, a.cand_base (first list slot per segment) and
 // *a.first_bad = ~0, from the walk's metas of nseg segments.
 hipError_t launch_wal_plan(const WalArgs& a, uint64_t nseg, hipStream_t s);
 // Gather: one block per segment of the nseg walked; segments from sum->w1 on do nothing.
 // fused_plan (nseg <= 1024): the gather computes the plan itself (no launch_wal_plan before it).
 hipError_t launch_wal_gather(const WalArgs& a, uint64_t nseg, bool fused_plan, int cu, hipStream_t s);
+// The resolve (sub-range walkers, nsub > 1) and the fused-plan gather in one launch, one 1024-thread
+// block per segment (nseg <= 1024): wave 0 resolves the segment, the block's list offset comes from
+// the earlier segments' tagged counts (a look-back), then the block gathers.  Replaces
+// k_wal_resolve + k_wal_gather<true>; a.rg_words / a.rg_tag set.
+hipError_t launch_wal_resolve_gather(const WalArgs& a, uint64_t nseg, hipStream_t s);
 // The first of n candidates whose payload CRC differs from the stored one (atomicMin into *first_bad).
 hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t s);
 // The summary (device memory) into page-locked host memory by one wave's stores: the host reads it

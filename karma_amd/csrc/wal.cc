@@ -152,6 +152,11 @@ struct ReplayCtx {
     hipStream_t st2 = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     DevBuf img, crec, clen, ccrc, meta, sub, span, cbase, off, len, stored, crc, sum;
+    // the fused resolve + gather's tagged words (WalArgs::rg_words), zeroed when (re)allocated and
+    // when the 16-bit call tag wraps
+    DevBuf rgw;
+    void* rgw_zeroed = nullptr;
+    uint32_t rg_seq = 0;
     DevBuf h_small;                             // pinned readback of the summary
     uint64_t img_gen = 0;                       // uploads of a host image into img so far
     // the largest payload of the last device-planned pass on this context: the next pass
@@ -175,8 +180,11 @@ struct ReplayCtx {
         if (!ready) return;
         (void)hipStreamSynchronize(st);
         (void)karma::engine::release_internal_stream(dev, st);
-        for (DevBuf* b : {&img, &crec, &clen, &ccrc, &meta, &sub, &span, &cbase, &off, &len, &stored, &crc, &sum, &h_small})
+        for (DevBuf* b : {&img, &crec, &clen, &ccrc, &meta, &sub, &span, &cbase, &off, &len, &stored, &crc, &sum, &h_small,
+                          &rgw})
             b->release();
+        rgw_zeroed = nullptr;
+        rg_seq = 0;
         (void)hipStreamDestroy(st);
         st = nullptr;
         if (st2) {
@@ -577,12 +585,27 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     const uint64_t cap_all = img_bytes / 8 + nwork;
     // (up to 1024 segments the device-planned gather reduces the metas itself: no plan launch)
     const bool fused_plan = dev_plan && !inline_crc && nwork <= 1024;
-    if (launch_wal_walk(A, nwork, plan, c.st) != hipSuccess ||
+    // (tools build A/B, KARMA_WAL_RG=1: the resolve and the fused-plan gather in one launch)
+    const bool rg = fused_plan && plan.nsub > 1 && plan.nsub <= kMaxSub && KARMA_AB_KNOB("KARMA_WAL_RG", 0) != 0;
+    if (rg) {
+        constexpr size_t kRgBytes = 2 * 1024 * sizeof(unsigned long long);
+        if (const int rc = c.rgw.ensure(kRgBytes)) return rc;
+        if (++c.rg_seq >= (1u << 16)) c.rg_seq = 1;
+        if (c.rgw.p != c.rgw_zeroed || c.rg_seq == 1) {
+            if (hipMemsetAsync(c.rgw.p, 0, kRgBytes, c.st) != hipSuccess)
+                return fail(KARMA_E_HIP, "wal_replay: hipMemsetAsync");
+            c.rgw_zeroed = c.rgw.p;
+        }
+        A.rg_words = c.rgw.as<unsigned long long>();
+        A.rg_tag = c.rg_seq;
+    }
+    if (launch_wal_walk(A, nwork, plan, c.st, !rg) != hipSuccess ||
         (!fused_plan && launch_wal_plan(A, nwork, c.st) != hipSuccess))
         return fail(KARMA_E_HIP, "wal_replay: header walk");
     if (dev_plan && !inline_crc) {
         if (const int rc = bind_lists(cap_all)) return rc;
-        if (launch_wal_gather(A, nwork, fused_plan, c.cu, c.st) != hipSuccess)
+        if ((rg ? launch_wal_resolve_gather(A, nwork, c.st) : launch_wal_gather(A, nwork, fused_plan, c.cu, c.st)) !=
+            hipSuccess)
             return fail(KARMA_E_HIP, "wal_replay: gather");
         // the CRC batch is also the check (first mismatch into the summary): no compare launch.
         // Which kernel covers the largest payload is known on the device only; the last pass's

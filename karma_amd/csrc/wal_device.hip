@@ -828,10 +828,13 @@ __global__ __launch_bounds__(kStgWaves * 64) void k_wal_list_crc(WalArgs A) {
 // that run is accepted; when pos is not in the list (walker j started on a wrong
 // header, or none), this wave walks the sub-range itself from pos, into the same
 // slots.  Writes the segment's count / stop and the accepted run per sub-range.
-__global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
-    __shared__ __attribute__((aligned(16))) WaveLds W;
-    const uint32_t lane = threadIdx.x;
-    const uint64_t P = A.nsub, s = blockIdx.x;
+// The resolver's body for segment s, run by one wave (lane = its lane): WG as walk_range's (a
+// wave alone in its workgroup: false; one wave of a larger workgroup: true).  lspan: the
+// segment's runs also into LDS (the fused resolve + gather), else nullptr.  Returns the meta.
+template <bool WG>
+__device__ __forceinline__ WalSegMeta resolve_segment(const WalArgs& A, WaveLds& W, uint64_t s, uint32_t lane,
+                                                      uint2* lspan) {
+    const uint64_t P = A.nsub;
     const uint64_t rel = s * A.seg_bytes;
     const Seg S = make_seg(A, s);
     const uint32_t seg = S.seg;
@@ -871,6 +874,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
         if (in && lane < f) {
             KB_WRITE(A.span, 2 * (s * P + jj), 2 * A.nwork * P, kKbSpan, (uint32_t)(jj * A.sub_cap));
             KB_WRITE(A.span, 2 * (s * P + jj) + 1, 2 * A.nwork * P, kKbSpan, count + pre - n);
+            if (lspan) lspan[jj] = uint2{(uint32_t)(jj * A.sub_cap), count + pre - n};
         }
         {  // (count: the candidates before this batch of runs)
             const uint32_t f0 = m.pad[0];
@@ -947,7 +951,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
                     stop = m.stop;
                 }
             } else {
-                const WalkEnd E = walk_range(W, S, lane, pos, hi, A, c0 + st, A.sub_cap);
+                const WalkEnd E = walk_range<WG>(W, S, lane, pos, hi, A, c0 + st, A.sub_cap);
                 n = E.count;
                 if (n) sunk = true;  // no inline CRCs for this run
                 pos = E.pos;
@@ -961,6 +965,7 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
         if (lane == 0) {
             KB_WRITE(A.span, 2 * (s * P + j), 2 * A.nwork * P, kKbSpan, st);
             KB_WRITE(A.span, 2 * (s * P + j) + 1, 2 * A.nwork * P, kKbSpan, count);  // candidates before the run
+            if (lspan) lspan[j] = uint2{st, count};
         }
         count += n;
     }
@@ -968,9 +973,14 @@ __global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
         kind = kWalSpill;
         stop = pos;
     }
-    if (lane == 0)
-        KB_WRITE(A.meta, s, A.nwork, kKbMeta,
-                 (WalSegMeta{count, kind, A.base0 + rel + (kind ? stop : seg), mx, sunk ? kCrcUnknown : sfb}));
+    const WalSegMeta out{count, kind, A.base0 + rel + (kind ? stop : seg), mx, sunk ? kCrcUnknown : sfb};
+    if (lane == 0) KB_WRITE(A.meta, s, A.nwork, kKbMeta, out);
+    return out;
+}
+
+__global__ __launch_bounds__(64) void k_wal_resolve(WalArgs A) {
+    __shared__ __attribute__((aligned(16))) WaveLds W;
+    (void)resolve_segment<false>(A, W, blockIdx.x, threadIdx.x, nullptr);
 }
 
 // The replay plan on the device (one block): replay enters segment s + 1 only when segment s
@@ -1162,6 +1172,121 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
     }
 }
 
+// Resolve and gather in one launch (round 6; the device-planned replay with sub-range walkers and
+// at most 1024 segments).  Block s: wave 0 resolves segment s (resolve_segment, its runs also into
+// LDS) and publishes two tagged words -- the segment's candidate count with a flag for "did not end
+// cleanly", and its largest payload -- then sums the words of segments [0, s) (each lane a stride of
+// them, loads issued together, a word not yet tagged with this call's tag waited for): the block's
+// list offset, whether replay stops before segment s (replay enters s only if every earlier segment
+// ended cleanly), and the largest payload so far.  Every block it waits on has a lower index, so it
+// was dispatched earlier and publishes before waiting on anything: the waits end.  The segment
+// replay stops in (or the last one) writes the summary, as k_wal_gather<true>'s block 0 does; the
+// other blocks gather their candidates exactly as k_wal_gather does.  Replaces k_wal_resolve's
+// launch and k_wal_gather<true>'s re-reduction of every segment's meta in every block.
+constexpr uint64_t kRgTagShift = 48, kRgStop = 1ull << 47, kRgValue = (1ull << 47) - 1;
+__global__ __launch_bounds__(1024) void k_wal_resolve_gather(WalArgs A) {
+    __shared__ __attribute__((aligned(16))) WaveLds W;
+    __shared__ uint2 spans[kMaxSub];
+    __shared__ unsigned long long s_pre;
+    __shared__ uint32_t s_count, s_stop_before;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint64_t s = blockIdx.x;
+    if (wave == 0) {
+        const WalSegMeta m = resolve_segment<true>(A, W, s, lane, spans);
+        const unsigned long long tag = (unsigned long long)A.rg_tag << kRgTagShift;
+        if (lane == 0) {
+            __hip_atomic_store(A.rg_words + 2 * s, tag | (m.kind != KARMA_WAL_END ? kRgStop : 0ull) | m.count,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.rg_words + 2 * s + 1, tag | m.max_len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        uint32_t cnt = 0, stop = 0, mx = 0;  // (counts: < 2^25 candidates in an image of <= 256 MiB)
+        constexpr int kQ = 16;               // 16 x 64 = 1024 segments, every load out at once
+        unsigned long long wc[kQ], wm[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const uint64_t i = lane + 64ull * q;
+            wc[q] = wm[q] = tag;  // (segments at or past s: nothing)
+            if (i < s) {
+                wc[q] = __hip_atomic_load(A.rg_words + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wm[q] = __hip_atomic_load(A.rg_words + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const uint64_t i = lane + 64ull * q;
+            if (i < s) {
+                while ((wc[q] >> kRgTagShift) != A.rg_tag) {  // not published yet
+                    __builtin_amdgcn_s_sleep(1);
+                    wc[q] = __hip_atomic_load(A.rg_words + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                while ((wm[q] >> kRgTagShift) != A.rg_tag) {
+                    __builtin_amdgcn_s_sleep(1);
+                    wm[q] = __hip_atomic_load(A.rg_words + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                cnt += (uint32_t)(wc[q] & kRgValue);
+                stop |= (wc[q] & kRgStop) ? 1u : 0u;
+                mx = (uint32_t)wm[q] > mx ? (uint32_t)wm[q] : mx;
+            }
+        }
+        cnt = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(cnt), 63);
+        stop = wave_or32(stop);
+        mx = wave_max32(mx);
+        mx = m.max_len > mx ? m.max_len : mx;
+        if (lane == 0) {
+            s_pre = cnt;
+            s_count = m.count;
+            s_stop_before = stop;
+            // the segment replay stops in, or the last one: the summary (k_wal_gather<true>'s)
+            if (!stop && (m.kind != KARMA_WAL_END || s + 1 == A.nwork)) {
+                WalSummary S{(uint64_t)cnt + m.count, A.wal_end, (uint32_t)(s + 1), KARMA_WAL_END, mx, 1u, ~0ull, 0ull};
+                if (m.kind != KARMA_WAL_END) {
+                    S.status = m.kind;
+                    S.end = m.stop;
+                }
+                *A.sum = S;
+            }
+        }
+    }
+    __syncthreads();
+    if (s_stop_before) return;  // replay does not enter this segment
+    const uint64_t g0 = s_pre;
+    const uint32_t P = (uint32_t)A.nsub, count = s_count;
+    const uint64_t rel = s * A.seg_bytes;
+    const uint32_t* crec = A.cand_rec + s * A.cand_cap;
+    const uint32_t* clen = A.cand_len + s * A.cand_cap;
+    const uint32_t* ccrc = A.cand_crc + s * A.cand_cap;
+    constexpr int kGatherU = 8;  // (as k_wal_gather)
+    for (uint32_t i0 = tid; i0 < count; i0 += kGatherU * blockDim.x) {
+        uint32_t vr[kGatherU], vn[kGatherU], vc[kGatherU];
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            if (i >= count) break;
+            uint32_t a = 0, b = P;  // the last run whose prefix is <= i: [a, b)
+            while (b - a > 1) {
+                const uint32_t mid = (a + b) / 2;
+                if (spans[mid].y <= i) a = mid;
+                else b = mid;
+            }
+            const uint32_t slot = spans[a].x + (i - spans[a].y);
+#ifdef KARMA_BOUNDS
+            kb_ok(slot >= a * A.sub_cap && slot < (a + 1) * A.sub_cap, kKbRunSlot, slot, A.sub_cap);
+#endif
+            vr[u] = KB_READ(crec, slot, A.cand_cap, kKbCand);
+            vn[u] = KB_READ(clen, slot, A.cand_cap, kKbCand);
+            vc[u] = KB_READ(ccrc, slot, A.cand_cap, kKbCand);
+        }
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            if (i >= count) break;
+            KB_WRITE(A.off, g0 + i, A.n_all, kKbList, rel + vr[u]);
+            KB_WRITE(A.len, g0 + i, A.n_all, kKbList, vn[u]);
+            KB_WRITE(A.stored, g0 + i, A.n_all, kKbList, vc[u]);
+        }
+    }
+}
+
 // The first candidate (in WAL order) whose payload CRC differs from the stored
 // one; size-0 records were checked by the walk.
 __global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n) {
@@ -1177,7 +1302,7 @@ __global__ __launch_bounds__(256) void k_wal_compare(WalArgs A, uint64_t n) {
 
 }  // namespace
 
-hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s) {
+hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& plan, hipStream_t s, bool resolve) {
     if (!nseg) return hipSuccess;
 #ifdef KARMA_AB
     if (plan.kernel == 1) {
@@ -1200,7 +1325,7 @@ hipError_t launch_wal_walk(const WalArgs& a, uint64_t nseg, const WalWalkPlan& p
         if (blocks > (uint64_t)plan.cu) blocks = (uint64_t)plan.cu;
         hipLaunchKernelGGL(k_wal_list_crc, dim3((unsigned)blocks), dim3(kStgWaves * 64), 0, s, a);
     }
-    if (plan.nsub > 1) hipLaunchKernelGGL(k_wal_resolve, dim3((unsigned)nseg), dim3(64), 0, s, a);
+    if (plan.nsub > 1 && resolve) hipLaunchKernelGGL(k_wal_resolve, dim3((unsigned)nseg), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
@@ -1244,6 +1369,13 @@ __global__ __launch_bounds__(64) void k_wal_publish(const WalSummary* src, WalSu
 
 hipError_t launch_wal_publish(const WalSummary* src, WalSummary* dst_host, hipStream_t s) {
     hipLaunchKernelGGL(k_wal_publish, dim3(1), dim3(64), 0, s, src, dst_host);
+    return hipGetLastError();
+}
+
+hipError_t launch_wal_resolve_gather(const WalArgs& a, uint64_t nseg, hipStream_t s) {
+    if (!nseg) return hipSuccess;
+    if (nseg > 1024 || a.nsub > kMaxSub || !a.rg_words || !a.rg_tag || a.rg_tag >= (1u << 16)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_wal_resolve_gather, dim3((unsigned)nseg), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 
