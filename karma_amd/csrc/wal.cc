@@ -585,8 +585,10 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     const uint64_t cap_all = img_bytes / 8 + nwork;
     // (up to 1024 segments the device-planned gather reduces the metas itself: no plan launch)
     const bool fused_plan = dev_plan && !inline_crc && nwork <= 1024;
-    // (tools build A/B, KARMA_WAL_RG=1: the resolve and the fused-plan gather in one launch)
-    const bool rg = fused_plan && plan.nsub > 1 && plan.nsub <= kMaxSub && KARMA_AB_KNOB("KARMA_WAL_RG", 0) != 0;
+    // the resolve and the fused-plan gather in one launch (k_wal_resolve_gather: 0.1084 vs 0.1106 ms
+    // per rotated 1M x 180 B call, profiles/r06_replay_rg_ab.txt); the tools build's KARMA_WAL_RG=0
+    // keeps round 5's two launches for A/B
+    const bool rg = fused_plan && plan.nsub > 1 && plan.nsub <= kMaxSub && KARMA_AB_KNOB("KARMA_WAL_RG", 1) != 0;
     if (rg) {
         constexpr size_t kRgBytes = 2 * 1024 * sizeof(unsigned long long);
         if (const int rc = c.rgw.ensure(kRgBytes)) return rc;

@@ -58,15 +58,15 @@ WALKS = {
     "sliced": (True, 0, _lib.KARMA_WAL_CRC_PLAN),         # the pass in two slices of segments, slice 1's walk beside
                                                           # slice 0's CRCs (KARMA_WAL_SLICES=2; tools build)
     "sliced_r8": (True, 0, _lib.KARMA_WAL_CRC_PLAN),      # the same with the 6-wave 8-copy staged kernel
-    "rg": (True, 0, _lib.KARMA_WAL_CRC_PLAN),             # the resolve and the gather in one launch
-                                                          # (k_wal_resolve_gather, KARMA_WAL_RG=1; tools build)
+    "rg0": (True, 0, _lib.KARMA_WAL_CRC_PLAN),            # the resolve and the gather as two launches (round 5's;
+                                                          # the plan fuses them, k_wal_resolve_gather): KARMA_WAL_RG=0
 }
 _LIST_CRC = ("listcrc", "listcrc4k")  # KARMA_WAL_LIST_CRC=1
 _NO_STAGED = ("sepdirect4",)  # KARMA_SMALL_STAGED=0
 _R8 = ("r8",)  # KARMA_STAGE_R8=1
 _SLICED = {"sliced": {"KARMA_WAL_SLICES": "2"},
            "sliced_r8": {"KARMA_WAL_SLICES": "2", "KARMA_STAGE_R8": "6", "KARMA_STAGE_SKEW": "0"},
-           "rg": {"KARMA_WAL_RG": "1"}}
+           "rg0": {"KARMA_WAL_RG": "0"}}
 _WALK = {"name": "split"}
 
 
@@ -305,7 +305,7 @@ def test_replay_large_records_jumps(lib, seg, walk, monkeypatch):
         assert got == (list(w[0]), w[1], w[2])
 
 
-@pytest.mark.parametrize("walk", ["split", "split4k", "sep", "inline", "inline4k", "listcrc", "listcrc4k", "rg"])
+@pytest.mark.parametrize("walk", ["split", "split4k", "sep", "inline", "inline4k", "listcrc", "listcrc4k", "rg0"])
 def test_replay_payloads_that_look_like_wal_records(lib, walk, monkeypatch):
     """Payloads that are themselves WAL images (valid header chains inside records): a sub-range
     walker can start on a header inside a payload, and the resolver must then walk the sub-range
@@ -452,7 +452,7 @@ def test_replay_randomized_against_model(lib, monkeypatch):
             assert got == (list(want[0]), want[1], want[2]), (case, walk, seg, mix)
 
 
-@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc", "r8", "sliced", "sliced_r8", "rg"])
+@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc", "r8", "sliced", "sliced_r8", "rg0"])
 @pytest.mark.parametrize("seg", [4096 + 4, 65536, 1 << 20])
 def test_replay_uniform_runs_speculative_walk(lib, seg, walk, monkeypatch):
     """Runs of one record size (the walker reads a round of headers at the last stride, lane j at
@@ -546,7 +546,7 @@ def test_replay_accepted_size0_records_advance_12(lib, seg, walk, monkeypatch):
     assert spills > 0, "some size-0 record must carry the chain into the next segment"
 
 
-@pytest.mark.parametrize("walk", ["split", "sep", "split4k", "r8", "sliced", "rg"])
+@pytest.mark.parametrize("walk", ["split", "sep", "split4k", "r8", "sliced", "rg0"])
 def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
     """The device-planned replay launches one small-record kernel, chosen by the largest payload of
     the previous call on the same device (the staged kernel up to 183 B, the 4-lane kernel up to
@@ -579,7 +579,7 @@ def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
         assert got == (list(w[0]), w[1], w[2]), (i, name, walk)
 
 
-@pytest.mark.parametrize("walk", ["split", "sep", "r8", "sliced", "rg"])
+@pytest.mark.parametrize("walk", ["split", "sep", "r8", "sliced", "rg0"])
 def test_replay_stage_skew_hint_between_calls(lib, walk, monkeypatch):
     """The staged small-record kernel comes in two forms, with the bank-skewed stage (records on
     few LDS banks: strides that are multiples of 32 bytes) and without it; a call takes the form
@@ -610,7 +610,7 @@ def test_replay_stage_skew_hint_between_calls(lib, walk, monkeypatch):
         assert _replay(lib, wals[name], d_wal=dev[name], seg=seg, host=False) == (list(w[0]), w[1], w[2]), (i, name)
 
 
-@pytest.mark.parametrize("walk", ["sliced", "sliced_r8", "rg"])
+@pytest.mark.parametrize("walk", ["sliced", "sliced_r8", "rg0"])
 @pytest.mark.parametrize("nseg", [2, 7, 40])
 def test_replay_sliced_pass_every_stop(lib, walk, nseg, monkeypatch):
     """The tools build's sliced pass (wal.cc sliced_pass: slice 1's walk beside slice 0's staged
@@ -651,14 +651,16 @@ def test_replay_sliced_pass_every_stop(lib, walk, nseg, monkeypatch):
                 assert got == (list(w[0]), w[1], w[2]), (name, start)
 
 
+@pytest.mark.parametrize("walk", ["split", "rg0"])
 @pytest.mark.parametrize("nseg", [1, 2, 300, 1024])
-def test_replay_resolve_gather_fused_many_segments(lib, nseg, monkeypatch):
-    """The tools build's one-launch resolve + gather (k_wal_resolve_gather, KARMA_WAL_RG=1) over 1
-    to 1024 segments of 64 KiB (4 sub-range walkers each, so the resolve runs): every block's list
-    offset comes from the earlier segments' tagged counts.  From the start, from a checkpoint, with
-    a corrupted payload, with a bad type that stops replay in the first third (later blocks must
-    gather nothing), and repeated calls (the call tag changes), against the model."""
-    _walk_env(monkeypatch, "rg")
+def test_replay_resolve_gather_fused_many_segments(lib, nseg, walk, monkeypatch):
+    """The one-launch resolve + gather (k_wal_resolve_gather, the plan's default; rg0: the tools
+    build's two launches) over 1 to 1024 segments of 64 KiB (4 sub-range walkers each, so the
+    resolve runs): every block's list offset comes from the earlier segments' tagged counts.  From
+    the start, from a checkpoint, with a corrupted payload, with a bad type that stops replay in the
+    first third (later blocks must gather nothing), and repeated calls (the call tag changes),
+    against the model."""
+    _walk_env(monkeypatch, walk)
     seg = 64 << 10
     src, offs, lens = _payloads(nseg + 3, nseg * 420, 1, 300)
     wal = np.zeros(nseg * seg, np.uint8)
