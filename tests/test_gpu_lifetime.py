@@ -108,8 +108,8 @@ def test_thousand_streams_released(dev):
     # warm-up: what a process keeps once it has used a device (the per-device tables, the code
     # objects of every kernel launched) exists before the baseline.  Streams share the runtime's
     # hardware queues (GPU_MAX_HW_QUEUES, 4 here) round robin, and each queue keeps the scratch
-    # memory its kernels once needed (the bounds-checked build's WAL kernels use 280-360 B of
-    # scratch per lane: ~150 MiB a queue), so every queue runs the calls once before the baseline
+    # memory its kernels once needed (the bounds-checked build's WAL kernels use up to 504 B of
+    # scratch per lane: ~256 MiB a queue), so every queue runs the calls once before the baseline
     # (a trim destroys the WAL contexts' streams: the next replay's stream takes the next queue).
     for _ in range(8):
         s0 = ctypes.c_void_p()
@@ -138,11 +138,12 @@ def test_thousand_streams_released(dev):
         assert hip.hipStreamDestroy(s) == 0
     assert L.karma_crc32c_trim(-1) == 0
     after = _free()
-    # The bounds-checked build's WAL kernels use 280-360 B of scratch per lane; the HIP runtime
-    # keeps a queue's scratch (288 B x 64 lanes x 8,192 wave slots = 144 MiB) after the library
-    # freed everything it allocated, so that build is allowed one such block on top.  The shipped
-    # build's kernels use no scratch and are held to 16 MiB.
-    slack = 16 * MIB + (144 * MIB if hasattr(L, "karma_debug_bounds_report") else 0)
+    # The bounds-checked build's WAL kernels spill to scratch (k_wal_resolve_gather, capped at 128
+    # VGPRs by its 1024-thread blocks: 504 B per lane); the HIP runtime keeps a queue's scratch
+    # (504 B x 64 lanes x 8,192 wave slots = 252 MiB, 256 as allocated) after the library freed
+    # everything it allocated, so that build is allowed one such block on top.  The shipped build's
+    # kernels use no scratch and are held to 16 MiB.
+    slack = 16 * MIB + (256 * MIB if hasattr(L, "karma_debug_bounds_report") else 0)
     assert base - after < slack, f"{(base - after) / MIB:.1f} MiB not returned (peak {(worst) / MIB:.1f} MiB)"
 
 
