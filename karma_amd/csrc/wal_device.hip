@@ -1175,10 +1175,10 @@ __global__ __launch_bounds__(1024) void k_wal_gather(WalArgs A) {
 // Resolve and gather in one launch (round 6; the device-planned replay with sub-range walkers and
 // at most 1024 segments).  Block s: wave 0 resolves segment s (resolve_segment, its runs also into
 // LDS) and publishes two tagged words -- the segment's candidate count with a flag for "did not end
-// cleanly", and its largest payload -- then sums the words of segments [0, s) (each lane a stride of
-// them, loads issued together, a word not yet tagged with this call's tag waited for): the block's
-// list offset, whether replay stops before segment s (replay enters s only if every earlier segment
-// ended cleanly), and the largest payload so far.  Every block it waits on has a lower index, so it
+// cleanly", and its largest payload; meanwhile wave 1 sums the words of segments [0, s) (each lane a
+// stride of them, loads issued together, a word not yet tagged with this call's tag waited for):
+// the block's list offset, whether replay stops before segment s (replay enters s only if every
+// earlier segment ended cleanly), and the largest payload so far.  Every block it waits on has a lower index, so it
 // was dispatched earlier and publishes before waiting on anything: the waits end.  The segment
 // replay stops in (or the last one) writes the summary, as k_wal_gather<true>'s block 0 does; the
 // other blocks gather their candidates exactly as k_wal_gather does.  Replaces k_wal_resolve's
@@ -1188,17 +1188,23 @@ __global__ __launch_bounds__(1024) void k_wal_resolve_gather(WalArgs A) {
     __shared__ __attribute__((aligned(16))) WaveLds W;
     __shared__ uint2 spans[kMaxSub];
     __shared__ unsigned long long s_pre;
-    __shared__ uint32_t s_count, s_stop_before;
+    __shared__ uint32_t s_count, s_stop_before, s_mx, s_mx_pred, s_kind;
+    __shared__ uint64_t s_stop_off;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint64_t s = blockIdx.x;
-    if (wave == 0) {
+    const unsigned long long tag = (unsigned long long)A.rg_tag << kRgTagShift;
+    if (wave == 0) {  // the segment's resolve, then its words
         const WalSegMeta m = resolve_segment<true>(A, W, s, lane, spans);
-        const unsigned long long tag = (unsigned long long)A.rg_tag << kRgTagShift;
         if (lane == 0) {
             __hip_atomic_store(A.rg_words + 2 * s, tag | (m.kind != KARMA_WAL_END ? kRgStop : 0ull) | m.count,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(A.rg_words + 2 * s + 1, tag | m.max_len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_count = m.count;
+            s_kind = m.kind;
+            s_stop_off = m.stop;
+            s_mx = m.max_len;
         }
+    } else if (wave == 1) {  // meanwhile, the earlier segments' words (they publish before waiting)
         uint32_t cnt = 0, stop = 0, mx = 0;  // (counts: < 2^25 candidates in an image of <= 256 MiB)
         constexpr int kQ = 16;               // 16 x 64 = 1024 segments, every load out at once
         unsigned long long wc[kQ], wm[kQ];
@@ -1231,23 +1237,23 @@ __global__ __launch_bounds__(1024) void k_wal_resolve_gather(WalArgs A) {
         cnt = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(cnt), 63);
         stop = wave_or32(stop);
         mx = wave_max32(mx);
-        mx = m.max_len > mx ? m.max_len : mx;
         if (lane == 0) {
             s_pre = cnt;
-            s_count = m.count;
             s_stop_before = stop;
-            // the segment replay stops in, or the last one: the summary (k_wal_gather<true>'s)
-            if (!stop && (m.kind != KARMA_WAL_END || s + 1 == A.nwork)) {
-                WalSummary S{(uint64_t)cnt + m.count, A.wal_end, (uint32_t)(s + 1), KARMA_WAL_END, mx, 1u, ~0ull, 0ull};
-                if (m.kind != KARMA_WAL_END) {
-                    S.status = m.kind;
-                    S.end = m.stop;
-                }
-                *A.sum = S;
-            }
+            s_mx_pred = mx;
         }
     }
     __syncthreads();
+    // the segment replay stops in, or the last one: the summary (k_wal_gather<true>'s)
+    if (tid == 0 && !s_stop_before && (s_kind != KARMA_WAL_END || s + 1 == A.nwork)) {
+        const uint32_t mx = s_mx > s_mx_pred ? s_mx : s_mx_pred;
+        WalSummary S{(uint64_t)s_pre + s_count, A.wal_end, (uint32_t)(s + 1), KARMA_WAL_END, mx, 1u, ~0ull, 0ull};
+        if (s_kind != KARMA_WAL_END) {
+            S.status = s_kind;
+            S.end = s_stop_off;
+        }
+        *A.sum = S;
+    }
     if (s_stop_before) return;  // replay does not enter this segment
     const uint64_t g0 = s_pre;
     const uint32_t P = (uint32_t)A.nsub, count = s_count;
