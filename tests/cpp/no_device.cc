@@ -23,11 +23,12 @@ hipError_t launch_combine_block(const FixedArgs&, const uint32_t*, uint64_t, uin
 hipError_t launch_ragged_scan(const RaggedArgs&, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_ragged_main(const RaggedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_ragged_direct(const RaggedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
-hipError_t launch_wal_walk(const WalArgs&, uint64_t, const WalWalkPlan&, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_wal_walk(const WalArgs&, uint64_t, const WalWalkPlan&, hipStream_t, bool) { return hipErrorNoDevice; }
 hipError_t launch_ragged_direct_dev(const RaggedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_ragged_staged_dev(const RaggedArgs&, int, hipStream_t, bool) { return hipErrorNoDevice; }
 hipError_t launch_wal_plan(const WalArgs&, uint64_t, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_wal_gather(const WalArgs&, uint64_t, bool, int, hipStream_t) { return hipErrorNoDevice; }
+hipError_t launch_wal_resolve_gather(const WalArgs&, uint64_t, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_wal_compare(const WalArgs&, uint64_t, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_wal_publish(const WalSummary*, WalSummary*, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_fill_splitmix(uint8_t*, uint64_t, uint64_t, uint64_t, hipStream_t) { return hipErrorNoDevice; }
