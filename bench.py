@@ -69,6 +69,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on (affinity)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_fixed_4k.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/profile.sh)")
+    p.add_argument("--streams", type=int, choices=[1, 2], default=1,
+                   help="fixed workload, one GPU: consecutive batches on 1 or 2 streams (2: each into its own "
+                        "output buffer, so batch i + 1 may start while batch i drains)")
     p.add_argument("--dry-backend", choices=["gloo"], default=None,
                    help="test the N-rank plumbing on CPU (tests/test_bench_launch.py): ranks over gloo, the "
                         "device batch replaced by the library's host crc32c::Value, the RCCL gather by "
@@ -954,7 +957,8 @@ def main():
         out = torch.empty(n_rec, dtype=torch.uint32, device=dev)
 
         def crc_step():
-            st = L.karma_crc32c_batch_fixed(arena.data_ptr(), rec, n_rec, None, 0, cur['out'].data_ptr(), sh)
+            st = L.karma_crc32c_batch_fixed(arena.data_ptr(), rec, n_rec, None, 0, cur['out'].data_ptr(),
+                                            cur.get('sh', sh))
             if st:
                 _lib.check("batch_fixed", st)
 
@@ -1075,6 +1079,17 @@ def main():
     pipe = GatherPipeline(outs, compute, gather if (comm is not None and out is not None) else None,
                           TorchSync(torch, stream))
     crc_step, gather_step = pipe.crc_step, pipe.gather_step
+    if args.streams == 2 and wl == "fixed" and comm is None:
+        # consecutive batches on two streams, each into its own output: batch i + 1's workgroups
+        # take the CUs batch i's last ones leave, instead of waiting for the whole of batch i
+        s2 = torch.cuda.Stream()
+        alt = {"i": 0, "outs": [out, torch.empty_like(out)], "sh": [sh, s2.cuda_stream]}
+
+        def crc_step():
+            k = alt["i"] % 2
+            alt["i"] += 1
+            cur["sh"] = alt["sh"][k]
+            compute(alt["outs"][k])
 
     # ---- pre-warm: the batch alone (no collective: ranks stop at different counts) for a fixed
     # time, so the clocks settle before --warmup (tools/ramp_probe.py) -----------
@@ -1254,6 +1269,10 @@ def main():
         }
         if per_rank is not None:
             res["per_rank"] = per_rank
+        if args.streams == 2 and wl == "fixed" and comm is None:
+            res["config"]["streams"] = 2
+            res["roofline"]["streams_note"] = ("two streams: consecutive launches overlap, so kernel_ms_avg spans "
+                                               "both and frac understates the kernel; read it from a --streams 1 line")
         if config5:  # the N = 8 default is configs[4]'s shard, not configs[1]'s 1M records per GPU
             res["config"]["records_per_gpu_n1_equivalent"] = 1 << 20
             anchor = config5_anchor()
