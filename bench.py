@@ -465,6 +465,27 @@ def wal_bench(args, L, rank):
                 dev_rate = r
             else:
                 dev_single = r
+        # the same rotated images through the walk (the path of WALs whose records vary in size):
+        # a forced sub-range size -- the planner's own for these images -- skips the uniform-stride pass
+        walk_rate = None
+        if size:
+            rot["k"] = len(d_wals)
+            tune = _lib.WalTuning(40960, _lib.KARMA_WAL_CRC_PLAN, 0)
+
+            def replay_walk():
+                d_wal = d_wals[rot["i"] % rot["k"]]
+                rot["i"] += 1
+                _lib.check("wal_replay_tuned", L.karma_wal_replay_tuned(
+                    None, d_wal.data_ptr(), wal_bytes, seg, 0, ctypes.byref(nrec), ctypes.byref(stop),
+                    ctypes.byref(status), None, 0, local, ctypes.byref(tune)))
+                assert nrec.value == n
+
+            for _ in range(args.warmup):
+                replay_walk()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                replay_walk()
+            walk_rate = payload / ((time.perf_counter() - t0) / args.steps) / GIB
         # the replay's CRC kernel alone (HIP events the library records on its replay stream
         # around that launch: karma_crc32c_time_next_units), rotated images, after the timed loop
         rot["k"] = len(d_wals)
@@ -532,6 +553,13 @@ def wal_bench(args, L, rank):
            "device_resident_image_tbs": round(wal_bytes / (payload / dev_rate / GIB) / 1e12, 3)
            if dev_rate is not None else None,
            "device_resident_single_image_value": round(dev_single, 3) if dev_single is not None else None,
+           "device_resident_walk_value": round(walk_rate, 3) if walk_rate is not None else None,
+           "device_resident_walk_image_tbs": round(wal_bytes / (payload / walk_rate / GIB) / 1e12, 3)
+           if walk_rate is not None else None,
+           "device_resident_walk_note": "the same rotated images with the uniform-stride pass skipped (a forced "
+                                        "40 KiB sub-range walk: the planner's own plan for them), i.e. the rate of "
+                                        "the walk, gather and CRC batch that WALs of varying record sizes take"
+           if walk_rate is not None else None,
            "device_resident_note": "karma_wal_replay over WAL images already in HBM, 4 distinct ~%d MB images "
                                    "in rotation (none left in the 256 MB MALL by the previous call); host wall "
                                    "clock over --steps synchronous calls; image TB/s = wal_bytes / call time; the "
@@ -544,10 +572,11 @@ def wal_bench(args, L, rank):
                       "record_bytes": size},
            "roofline": None}
     if args.workload == "wal_replay" and dev_rate is not None:
-        # the dominant kernel of a device-resident replay: the payload CRC batch over the gathered
-        # lists (payload bytes + offset 8 B, length 4 B, stored CRC 4 B, result 4 B per record);
-        # the whole call's image rate beside it
-        algo = payload + 20 * n
+        # the dominant kernel of a device-resident replay: for records of one size the
+        # uniform-stride pass's CRC batch (each record's 8-byte header and payload, read once; no
+        # lists), else the payload CRC batch over the gathered lists (payload bytes + offset 8 B,
+        # length 4 B, stored CRC 4 B, result 4 B per record); the whole call's image rate beside it
+        algo = n * (size + 8) if size else payload + 20 * n
         achieved = algo / (crc_kernel_ms * 1e-3) / 1e9
         call_s = payload / (dev_rate * GIB)
         pm, pm_call = replay_pmc_traffic(n, size) if size else (None, None)
@@ -558,7 +587,8 @@ def wal_bench(args, L, rank):
                            if pm is not None else None,
                            "call_traffic": round(pm_call) if pm_call is not None else None,
                            "call_traffic_vs_image": round(pm_call / wal_bytes, 3) if pm_call is not None else None,
-                           "kernel": "the replay's payload CRC batch (k_ragged_staged_pipe)",
+                           "kernel": "the replay's CRC batch (k_ragged_staged_pipe" +
+                                     (", uniform-stride form: headers and payloads of the slots)" if size else ")"),
                            "kernel_ms_avg": round(crc_kernel_ms, 4), "algorithmic_bytes_per_launch": algo,
                            "achieved_source": "algorithmic bytes / the CRC kernel's HIP-event time inside "
                                               "karma_wal_replay (rotated device-resident images)",

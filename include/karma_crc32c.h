@@ -194,7 +194,11 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
 /* Batched replay (sivir::open's wal::scan_record loop, wal.cc:34-87) from WAL offset
  * `start`, entirely on the device: segment-parallel header walk (sub-range walkers
  * stitched along the real chain when there are few segments), all payload CRCs in one
- * GPU batch, first mismatch.  The image is d_wal when the caller already holds a device
+ * GPU batch, first mismatch.  A replay from a segment boundary whose first record has a
+ * payload of at most 183 bytes first tries the uniform-stride pass: every segment read as
+ * records of that size, each header and CRC checked in one batch with no walk; its result
+ * is used only when it is scan_record's (nothing before replay's stop breaks the stride),
+ * otherwise the walk decides.  The image is d_wal when the caller already holds a device
  * copy (h_wal may then be NULL), else h_wal is streamed into HBM (pinned staging, no
  * page-locking of the caller's buffer).  seg_bytes < 2^31.
  * Outputs: *h_n_records type-0 records accepted, their header offsets in h_rec_off
@@ -230,7 +234,8 @@ int karma_wal_replay_multi(const void* h_wal, size_t wal_bytes, size_t seg_bytes
                                    (k_wal_walk_crc: faster when the image is cache-resident, slower from HBM) */
 typedef struct karma_wal_tuning {
     uint64_t walk_sub_bytes; /* header-walk sub-range size, rounded down to a 4 KiB multiple (>= 4 KiB);
-                                >= seg_bytes: one walker per segment; 0 = planned */
+                                >= seg_bytes: one walker per segment; 0 = planned (non-zero also
+                                skips the uniform-stride pass: always the walk) */
     int32_t crc_batch;       /* KARMA_WAL_CRC_* */
     int32_t reserved;        /* 0 */
 } karma_wal_tuning;

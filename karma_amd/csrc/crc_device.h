@@ -819,6 +819,14 @@ __device__ __forceinline__ void wave_prefix_minmax(uint64_t& lo, uint64_t& hi) {
     step(dpp64<0x143, 0xc>(~0ull, lo), dpp64<0x143, 0xc>(0ull, hi));  // row_bcast:31 -> rows 2, 3
 }
 
+// Min of a 64-bit value over the wave (DPP prefix, lane 63 read back): uniform.
+__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
+    uint64_t hi = 0;
+    wave_prefix_minmax(x, hi);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+}
+
 // Inclusive wave scan of 32-bit values through DPP (row shifts, then the row broadcasts of gfx9):
 // six VALU steps instead of six dependent cross-lane LDS round trips (ds_bpermute) of the 64-bit
 // scan below.

@@ -896,9 +896,16 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // the stage holds), 3 = neither.
 // NWO (tools build A/B, with R8): that many waves instead of kStgWaves8, leaving LDS for another
 // kernel's workgroups on the same CU (the sliced WAL replay's walkers, wal.cc).
-template <bool SK, bool R8 = false, int TM = 0, int NWO = 0>
+// SPEC (the uniform-stride WAL replay, engine.h WalSpec): the records are the probe's slots, a batch
+// the 64 slots of one segment from 64 j (batch b: segment b / B, j = b % B), each with its 8-byte
+// header in front (arena = image + 8; the extent starts at the first header); no lists are read
+// and no CRCs stored.  Per slot: its header against (n, type 0) and its payload CRC against the
+// header's field; the wave's smallest keys go to spec->stop_key / dev_key by one atomicMin each,
+// once per wave (a wave's slots only grow).
+template <bool SK, bool R8 = false, int TM = 0, int NWO = 0, bool SPEC = false>
 __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     static_assert(!(SK && R8), "the 8-copy form has the plain stage only");
+    static_assert(!(SPEC && (R8 || TM || NWO)), "the uniform-stride form is the shipped stage only");
     constexpr bool END = true;
     constexpr int NW = NWO ? NWO : R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : 24;
     constexpr int TW = R8 ? kRep8Words : kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
@@ -908,6 +915,16 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
     if (A.n_dev) {
         if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
         n_rec = *A.n_dev;
+    }
+    if (n_rec == 0) return;  // (uniform: a device-sized batch with nothing in it skips the table fill)
+    // SPEC: the stride, slots and batches per segment, segment bytes (uniform)
+    uint32_t sp_n = 0, sp_m = 1, sp_B = 1;
+    uint64_t sp_S = 0;
+    if constexpr (SPEC) {
+        sp_n = A.spec->n;
+        sp_m = A.spec->m;
+        sp_B = A.spec->B;
+        sp_S = A.spec->seg;
     }
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[BUF + NW * (int)(kStride / 4)];
@@ -928,6 +945,14 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
     uint64_t base = ((uint64_t)blockIdx.x * NW + wave) * 64;
     if (base >= n_rec) return;
     auto ld_meta = [&](uint64_t b, uint64_t& o, uint32_t& n, uint32_t& ini) {
+        if constexpr (SPEC) {  // slot 64 j + lane of segment s: arithmetic, no loads
+            const uint32_t bi = (uint32_t)(b >> 6), sg = bi / sp_B, i = 64u * (bi - sg * sp_B) + lane;
+            const bool v = b + lane < n_rec && i < sp_m;
+            o = (uint64_t)sg * sp_S + (uint64_t)i * (sp_n + 8u);
+            n = v ? sp_n : 0u;
+            ini = 0u;
+            return;
+        }
         const uint64_t ri = b + lane;
         const bool v = ri < n_rec;
         o = v ? A.off[ri] : 0;
@@ -936,7 +961,8 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
     };
     auto extent = [&](uint64_t o, uint32_t n, uintptr_t& lo, uintptr_t& hi) {
         const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
-        uint64_t l = n ? (p & ~uintptr_t(15)) : ~0ull, h = n ? ((p + n + 15) & ~uintptr_t(15)) : 0ull;
+        const uintptr_t p0 = SPEC ? p - 8 : p;  // (SPEC: from the record's header)
+        uint64_t l = n ? (p0 & ~uintptr_t(15)) : ~0ull, h = n ? ((p + n + 15) & ~uintptr_t(15)) : 0ull;
         wave_prefix_minmax(l, h);  // (DPP; lane 63 holds the wave's)
         lo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(l >> 32), 63) << 32) |
              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)l, 63);
@@ -974,6 +1000,7 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
     };
     bool sk = fits && skewed(o, n, lo);
     if (fits) issue(lo, hi);
+    bool rep_stop = false, rep_dev = false;  // (SPEC) this wave has reported a key of that kind
     for (;;) {
         if (fits && (TM & 2) == 0) {
 #pragma unroll
@@ -1006,6 +1033,7 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
             ld_meta(nb + step, o3, n3, ini3);
         }
         const uint64_t ri = base + lane;
+        [[maybe_unused]] uint32_t spec_res = 0;
         if (ri < n_rec) {
             uint32_t res = ini;
             const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
@@ -1032,8 +1060,58 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
                     res = lane_record<R8 ? 32 : 8>(lds, X, Z4, T8, p, n, ini,
                                       [&](uintptr_t a) { return ld16(reinterpret_cast<const uint8_t*>(a)); });
             }
-            A.out[ri] = res;
-            if (A.cmp_stored && n && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
+            if constexpr (SPEC) {
+                spec_res = res;  // (checked below, with every lane of the wave)
+            } else {
+                A.out[ri] = res;
+                if (A.cmp_stored && n && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
+            }
+        }
+        if constexpr (SPEC) {
+            // the slot's header: its CRC field and len/type word, from the stage (or global memory)
+            unsigned long long kstop = ~0ull, kdev = ~0ull;
+            if (ri < n_rec && n) {
+                const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
+                uint32_t hc, hs;
+                if (fits) {
+                    const uint32_t at = kLead + (uint32_t)(p - 8 - lo), q = at >> 2, sh = at & 3u;
+                    uint32_t d0, d1, d2;
+                    if (sk) {
+                        d0 = stage32[q + (q >> 5)];
+                        d1 = stage32[(q + 1) + ((q + 1) >> 5)];
+                        d2 = stage32[(q + 2) + ((q + 2) >> 5)];
+                    } else {
+                        d0 = stage32[q];
+                        d1 = stage32[q + 1];
+                        d2 = stage32[q + 2];
+                    }
+                    hc = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                    hs = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                } else {
+                    const uint8_t* hp = KB_BYTES(reinterpret_cast<const uint8_t*>(p - 8), 8);
+                    hc = (uint32_t)hp[0] | (uint32_t)hp[1] << 8 | (uint32_t)hp[2] << 16 | (uint32_t)hp[3] << 24;
+                    hs = (uint32_t)hp[4] | (uint32_t)hp[5] << 8 | (uint32_t)hp[6] << 16 | (uint32_t)hp[7] << 24;
+                }
+                const uint32_t bi = (uint32_t)(base >> 6), sg = bi / sp_B;
+                const uint64_t g = (uint64_t)sg * sp_m + 64u * (bi - sg * sp_B) + lane;
+                if (hs == (sp_n << 8)) {  // the record the stride says: scan_record checks its CRC
+                    if (spec_res != hc) kstop = 2 * g;
+                } else if (hs == 0 && hc == 0) {  // an all-zero header: "Corrupt record" (size-0 quirk)
+                    kstop = 2 * g;
+                } else {  // anything else: the stride's assumption ends here
+                    kdev = 2 * g;
+                }
+            }
+            kstop = wave_min64(kstop);
+            kdev = wave_min64(kdev);
+            if (kstop != ~0ull && !rep_stop) {
+                if (lane == 0) atomicMin(&A.spec->stop_key, kstop);
+                rep_stop = true;
+            }
+            if (kdev != ~0ull && !rep_dev) {
+                if (lane == 0) atomicMin(&A.spec->dev_key, kdev);
+                rep_dev = true;
+            }
         }
         wave_lds_sync();
         if (!more) break;
@@ -1106,6 +1184,15 @@ hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStr
     } else {
         hipLaunchKernelGGL((k_ragged_staged_pipe<false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew) {
+    if (!a.spec || !a.n_dev || !a.gate_len || grid_blocks <= 0) return hipErrorInvalidValue;
+    if (skew)
+        hipLaunchKernelGGL((k_ragged_staged_pipe<true, false, 0, 0, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 0, 0, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     return hipGetLastError();
 }
 

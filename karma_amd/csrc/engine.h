@@ -139,6 +139,7 @@ static_assert(sizeof(UnitDesc) == 16, "one 16-byte load per unit descriptor");
 constexpr int kBuckets = (int)(kDefaultUnit / kChunk) + 1;  // chunk counts of a partial unit (index = chunks; 65 for 8 KiB units)
 static_assert(kDefaultUnit / kChunk < kBuckets, "a partial unit has at most unit/kChunk chunks");
 
+struct WalSpec;  // the uniform-stride WAL replay's probe result (below)
 struct RaggedArgs {
     const uint8_t* arena;
     const uint64_t* off;       // payload offset per record
@@ -190,6 +191,9 @@ struct RaggedArgs {
     // k_ragged_staged_pipe: set to 1 when a batch's records start on few LDS banks (the skewed
     // stage's case), whichever stage the kernel has; nullptr: not reported
     uint32_t* stage_skew_seen;
+    // the uniform-stride WAL replay (k_ragged_staged_pipe's SPEC form, wal.cc): the records are
+    // slots of the probe's stride (WalSpec), not lists; nullptr otherwise
+    WalSpec* spec;
 };
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
@@ -267,6 +271,26 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
                            const uint32_t* d_stored, uint64_t* d_first_bad, hipStream_t s, int which = kSmallBoth,
                            bool stage_skew = true, uint32_t* d_skew_seen = nullptr);
 
+// ---- the uniform-stride WAL replay (wal.cc replay_pass) ------------------------
+// Segment 0's first header (type 0, payload n, 1 <= n <= kStgGateLen) gives a stride sigma = n + 8;
+// the pass assumes every segment holds m = seg / sigma records at slots i * sigma and checks it.
+// Slot g = s * m + i; events are keyed 2 g (slot g) and 2 (s + 1) m - 1 (segment s's tail, after
+// its last slot).  stop_key: the first exact stop scan_record makes there (a CRC mismatch, an
+// all-zero header: "Corrupt record"); dev_key: the first place the assumption breaks (any other
+// header).  The result is scan_record's whenever stop_key <= dev_key; otherwise the walk runs.
+struct WalSpec {
+    uint32_t n, m, B, seg;   // payload, slots per segment, 64-slot batches per segment, segment bytes
+    uint64_t nslots;         // slots the CRC kernel checks (0: the probe declined)
+    unsigned long long stop_key, dev_key;
+    uint32_t nseg_eff;       // segments before the first one whose first header is all zero
+    uint32_t ok;             // segment 0's header gave a stride
+};
+// The SPEC form of k_ragged_staged_pipe over a.spec's slots: per slot the header check, the
+// payload CRC against the header's field, one atomicMin per wave and key (a.arena = image + 8).
+hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew);
+// ... enqueued by the library (capi.cc): the lane blob, the grid, the gate on spec->nslots.
+int ragged_spec_batch_dev(const void* d_wal, WalSpec* d_spec, uint32_t* d_skew_seen, hipStream_t s, bool stage_skew);
+
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {
     uint32_t count;  // type-0 records (candidates) the walk found
@@ -299,7 +323,9 @@ struct WalSummary {
     uint64_t first_bad;  // the first candidate whose payload CRC differs (~0: none), set by the CRC check
     uint64_t bad_off;    // inline CRCs: that candidate's header offset relative to wal (k_wal_plan)
     uint32_t stage_skew; // the staged small-record batch met records on few LDS banks (RaggedArgs::stage_skew_seen)
-    uint32_t pad;
+    uint32_t spec;       // the uniform-stride pass (k_wal_spec_finish): 0 not run, 1 its result is final
+                         // (n_all accepted records, w1 = slots per segment, max_len = payload,
+                         // bad_off = the stop's header offset relative to wal), 2 declined: the walk decides
 };
 static_assert(sizeof(WalSummary) == 56, "one 56-byte summary, read back in one copy");
 
@@ -344,6 +370,7 @@ struct WalArgs {
     // stop flag; largest payload), and this call's tag (1..65535; the words are zeroed when it wraps)
     unsigned long long* rg_words;
     uint32_t rg_tag;
+    WalSpec* spec;             // the uniform-stride pass (k_wal_spec_probe / k_wal_spec_finish)
 };
 constexpr uint32_t kWalkTile = 4096;  // the one-wave walker's LDS tile (wal_device.hip)
 constexpr uint32_t kMaxSub = 4096;    // sub-ranges per segment (k_wal_gather stages their runs in LDS)
@@ -378,6 +405,12 @@ hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t 
 // after the stream syncs.  A 56-byte hipMemcpyAsync D2H is a copy kernel of its own (~4 us on the
 // replay's stream); this is one small launch (wal.cc's summary readback).
 hipError_t launch_wal_publish(const WalSummary* src, WalSummary* dst_host, hipStream_t s);
+// The uniform-stride pass around its CRC kernel: the probe (one block: the stride, the segment
+// tails, the first all-zero segment; a.spec, a.sum->stage_skew = 0) and the finish (one wave: the
+// summary from the keys).  nseg = a.nwork <= kSpecMaxSeg, a.first_pos == 0.
+constexpr uint64_t kSpecMaxSeg = 1u << 20;
+hipError_t launch_wal_spec_probe(const WalArgs& a, hipStream_t s);
+hipError_t launch_wal_spec_finish(const WalArgs& a, hipStream_t s);
 
 // ---- KFP frames (kfp.cc) ----------------------------------------------------
 struct KfpWalk {

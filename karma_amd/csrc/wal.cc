@@ -141,6 +141,12 @@ struct DevBuf {
 
 // Walkers switch to direct header rounds after a fast round of this many headers.
 constexpr uint32_t kDirectStreak = 8;
+// Passes that skip the uniform-stride pass after it declined (a WAL of mixed sizes declines in
+// its probe: ~10 us of a call that then walks).
+constexpr uint32_t kSpecSkip = 16;
+#ifdef KARMA_AB
+std::atomic<int> g_spec_last{0};  // the last pass's uniform-stride outcome (karma_ab_wal_spec_last)
+#endif
 constexpr uint32_t kSmallRecordMax = 1024;      // payloads up to this take the one-record-per-group batch
 struct ReplayCtx {
     std::mutex mu;
@@ -166,6 +172,10 @@ struct ReplayCtx {
     // whether the last pass's staged batch met records on few LDS banks: this pass then launches
     // the staged kernel with the skewed stage (else the plain-stage form, 3-5 us faster)
     bool skew_hint = true;
+    // the uniform-stride pass (WalSpec): its probe result on the device; after it declines, the
+    // next kSpecSkip passes go straight to the walk
+    DevBuf spec;
+    uint32_t spec_skip = 0;
     int init(int dev) {
         if (ready) return 0;
         hipDeviceProp_t prop;
@@ -181,7 +191,7 @@ struct ReplayCtx {
         (void)hipStreamSynchronize(st);
         (void)karma::engine::release_internal_stream(dev, st);
         for (DevBuf* b : {&img, &crec, &clen, &ccrc, &meta, &sub, &span, &cbase, &off, &len, &stored, &crc, &sum, &h_small,
-                          &rgw})
+                          &rgw, &spec})
             b->release();
         rgw_zeroed = nullptr;
         rg_seq = 0;
@@ -276,6 +286,12 @@ int replay_core(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
 }  // namespace
 
 extern "C" {
+
+#ifdef KARMA_AB
+// Tools build only: the last replay pass's uniform-stride outcome on any device (0 not tried,
+// 1 its result taken, 2 declined: the walk decided).
+int karma_ab_wal_spec_last(void) { return g_spec_last.load(); }
+#endif
 
 int karma_wal_replay(const void* h_wal, const void* d_wal, size_t wal_bytes, size_t seg_bytes, uint64_t start,
                      uint64_t* h_n_records, uint64_t* h_stop, int* h_status, uint64_t* h_rec_off, size_t rec_cap,
@@ -534,6 +550,56 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         c.have_len_hint = false;  // the unsliced pass below launches both small-record kernels
     }
 #endif
+#ifdef KARMA_AB
+    g_spec_last = 0;
+#endif
+    // 0b. the uniform-stride pass (engine.h WalSpec): when segment 0 starts with a
+    //     record of n <= kStgGateLen bytes, check every segment as m = seg / (n + 8) such records and
+    //     their CRCs in one staged batch, with no walk, gather or lists.  Its result is final when
+    //     the first place that breaks the assumption (if any) comes after replay's stop; otherwise
+    //     the walk below decides (one host round trip spent).  The tools build's KARMA_WAL_SPEC: 0
+    //     never, 2 every pass (no skipping after a decline).
+    const long spec_knob = KARMA_AB_KNOB("KARMA_WAL_SPEC", 1);
+    // (a caller's forced sub-range size asks for the walk: karma_wal_tuning)
+    const bool spec_try = spec_knob != 0 && dev_plan && !inline_crc && batch == KARMA_WAL_CRC_PLAN && A.first_pos == 0 &&
+                          !(tuning && tuning->walk_sub_bytes) && nwork <= kSpecMaxSeg &&
+                          (spec_knob == 2 || c.spec_skip == 0);
+    if (!spec_try && c.spec_skip) --c.spec_skip;
+    if (spec_try) {
+        if (const int rc = c.sum.ensure(sizeof(WalSummary))) return rc;
+        if (const int rc = c.h_small.ensure(64, true)) return rc;
+        if (const int rc = c.spec.ensure(sizeof(WalSpec))) return rc;
+        A.sum = c.sum.as<WalSummary>();
+        A.spec = c.spec.as<WalSpec>();
+        A.wal_end = wal_bytes;
+        WalSummary* S = c.h_small.as<WalSummary>();
+        if (launch_wal_spec_probe(A, c.st) != hipSuccess)
+            return fail(KARMA_E_HIP, "wal_replay: uniform-stride probe");
+        if (const int rc = ragged_spec_batch_dev(A.wal, A.spec, &A.sum->stage_skew, c.st, c.skew_hint)) return rc;
+        if (launch_wal_spec_finish(A, c.st) != hipSuccess || launch_wal_publish(A.sum, S, c.st) != hipSuccess ||
+            hipStreamSynchronize(c.st) != hipSuccess)
+            return fail(KARMA_E_HIP, "wal_replay: uniform-stride pass");
+        T.mark("uniform-stride pass (device)");
+#ifdef KARMA_AB
+        g_spec_last = (int)S->spec;
+#endif
+        if (S->spec == 1) {
+            const uint64_t accepted = S->n_all, m = S->w1, sig = (uint64_t)S->max_len + 8;
+            c.have_len_hint = true;
+            c.len_hint = S->max_len;
+            c.skew_hint = S->stage_skew != 0;
+            if (h_rec_off && rec_cap && accepted) {  // slot g = s m + i: base0 + s seg + i sigma
+                const uint64_t k = std::min<uint64_t>(accepted, rec_cap);
+                parallel_for(0, k, 1 << 16, [&](uint64_t g) { h_rec_off[g] = base0 + (g / m) * seg_bytes + (g % m) * sig; });
+                T.mark("offsets");
+            }
+            *h_n_records = accepted;
+            *h_stop = S->end;
+            *h_status = (int)S->status;
+            return 0;
+        }
+        c.spec_skip = kSpecSkip;
+    }
     // 1. segment-parallel header walk (sub-range walkers when there are few segments)
     const WalWalkPlan plan =
         wal_walk_plan(seg_bytes, nwork, c.cu, tuning ? tuning->walk_sub_bytes : 0, inline_crc, list_crc);

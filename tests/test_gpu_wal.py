@@ -60,13 +60,18 @@ WALKS = {
     "sliced_r8": (True, 0, _lib.KARMA_WAL_CRC_PLAN),      # the same with the 6-wave 8-copy staged kernel
     "rg0": (True, 0, _lib.KARMA_WAL_CRC_PLAN),            # the resolve and the gather as two launches (round 5's;
                                                           # the plan fuses them, k_wal_resolve_gather): KARMA_WAL_RG=0
+    "spec": (True, 0, _lib.KARMA_WAL_CRC_PLAN),           # the uniform-stride pass tried on every call (KARMA_WAL_SPEC=2;
+                                                          # the plan tries it unless the last try declined)
+    "spec0": (True, 0, _lib.KARMA_WAL_CRC_PLAN),          # the plan with the uniform-stride pass off: the walk always
 }
 _LIST_CRC = ("listcrc", "listcrc4k")  # KARMA_WAL_LIST_CRC=1
 _NO_STAGED = ("sepdirect4",)  # KARMA_SMALL_STAGED=0
 _R8 = ("r8",)  # KARMA_STAGE_R8=1
 _SLICED = {"sliced": {"KARMA_WAL_SLICES": "2"},
            "sliced_r8": {"KARMA_WAL_SLICES": "2", "KARMA_STAGE_R8": "6", "KARMA_STAGE_SKEW": "0"},
-           "rg0": {"KARMA_WAL_RG": "0"}}
+           "rg0": {"KARMA_WAL_RG": "0"},
+           "spec": {"KARMA_WAL_SPEC": "2"},
+           "spec0": {"KARMA_WAL_SPEC": "0"}}
 _WALK = {"name": "split"}
 
 
@@ -84,7 +89,7 @@ def _walk_env(monkeypatch, walk):
         monkeypatch.setenv("KARMA_STAGE_R8", "1")
     else:
         monkeypatch.delenv("KARMA_STAGE_R8", raising=False)
-    for k in ("KARMA_WAL_SLICES", "KARMA_STAGE_SKEW", "KARMA_WAL_RG"):
+    for k in ("KARMA_WAL_SLICES", "KARMA_STAGE_SKEW", "KARMA_WAL_RG", "KARMA_WAL_SPEC"):
         monkeypatch.delenv(k, raising=False)
     for k, v in _SLICED.get(walk, {}).items():
         monkeypatch.setenv(k, v)
@@ -452,7 +457,8 @@ def test_replay_randomized_against_model(lib, monkeypatch):
             assert got == (list(want[0]), want[1], want[2]), (case, walk, seg, mix)
 
 
-@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc", "r8", "sliced", "sliced_r8", "rg0"])
+@pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc", "r8", "sliced", "sliced_r8", "rg0",
+                                  "spec", "spec0"])
 @pytest.mark.parametrize("seg", [4096 + 4, 65536, 1 << 20])
 def test_replay_uniform_runs_speculative_walk(lib, seg, walk, monkeypatch):
     """Runs of one record size (the walker reads a round of headers at the last stride, lane j at
@@ -546,7 +552,7 @@ def test_replay_accepted_size0_records_advance_12(lib, seg, walk, monkeypatch):
     assert spills > 0, "some size-0 record must carry the chain into the next segment"
 
 
-@pytest.mark.parametrize("walk", ["split", "sep", "split4k", "r8", "sliced", "rg0"])
+@pytest.mark.parametrize("walk", ["split", "sep", "split4k", "r8", "sliced", "rg0", "spec", "spec0"])
 def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
     """The device-planned replay launches one small-record kernel, chosen by the largest payload of
     the previous call on the same device (the staged kernel up to 183 B, the 4-lane kernel up to
@@ -579,7 +585,7 @@ def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
         assert got == (list(w[0]), w[1], w[2]), (i, name, walk)
 
 
-@pytest.mark.parametrize("walk", ["split", "sep", "r8", "sliced", "rg0"])
+@pytest.mark.parametrize("walk", ["split", "sep", "r8", "sliced", "rg0", "spec", "spec0"])
 def test_replay_stage_skew_hint_between_calls(lib, walk, monkeypatch):
     """The staged small-record kernel comes in two forms, with the bank-skewed stage (records on
     few LDS banks: strides that are multiples of 32 bytes) and without it; a call takes the form
@@ -680,3 +686,105 @@ def test_replay_resolve_gather_fused_many_segments(lib, nseg, walk, monkeypatch)
         w = wal_model.replay(bad.tobytes(), seg)
         assert len(w[0]) == k
         assert _replay(lib, bad, seg=seg) == (list(w[0]), w[1], w[2]), what
+
+
+def _uniform_wal(lib, size, seg, n, seed):
+    """n records of one payload size framed into segments (footers as append writes them), one
+    never-written segment after them."""
+    lens = np.full(n, size, np.uint32)
+    offs = (np.arange(n, dtype=np.uint64) * size).astype(np.uint64)
+    src = synth.splitmix_np(seed, 0, n * size + 16).copy()
+    per = seg // (size + 8)
+    wal = np.zeros(((n + per - 1) // per + 1) * seg, np.uint8)
+    cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+    assert len(rec) == n
+    return wal, [int(x) for x in rec]
+
+
+_SPEC_CASES = ([(4096 + 4, s) for s in (1, 3, 4, 5, 15, 16, 17, 56, 120, 180, 182, 183)] +
+               [(65536, s) for s in (4, 17, 120, 180, 183)] + [(1 << 20, s) for s in (100, 180)])
+
+
+@pytest.mark.parametrize("seg,size", _SPEC_CASES)
+def test_replay_uniform_stride_pass(lib, seg, size, monkeypatch):
+    """The uniform-stride pass (engine.h WalSpec; tools build, KARMA_WAL_SPEC=2: tried on every call)
+    over WALs of one payload size.  Its result is taken (karma_ab_wal_spec_last 1) for the zero tail
+    after the last record (CORRUPT at the first unwritten header), segments filled to the image end
+    (END), a corrupt payload or CRC field at a segment's first, middle or last slot, an empty record
+    (all-zero header) and a zeroed padding header; it declines (2) and the walk decides for a changed
+    length, a bad type, padding mid-segment, a size-0 record with the stale-word CRC (accepted, 12
+    bytes), a length past the segment and a smaller record in a segment's tail; it is not tried (0)
+    from a checkpoint.  Every result against the model, over the host image and the device copy."""
+    _walk_env(monkeypatch, "spec")
+    ab = _lib.load(_lib.AB_LIB_PATH)
+    sig = size + 8
+    per = seg // sig
+    tail = seg - per * sig
+    n = per * 3 + per // 2
+    wal, h = _uniform_wal(lib, size, seg, n, seed=size * 7 + seg)
+
+    def check(img, spec, start=0, device=False):
+        w = wal_model.replay(img.tobytes(), seg, start)
+        got = _replay(lib, img, start=start, seg=seg)
+        assert got == (list(w[0]), w[1], w[2]), (spec, start)
+        assert ab.karma_ab_wal_spec_last() == spec
+        if device:
+            d = torch.from_numpy(img).cuda()
+            assert _replay(lib, img, d_wal=d, host=False, seg=seg) == (list(w[0]), w[1], w[2])
+            assert ab.karma_ab_wal_spec_last() == spec
+        return w
+
+    w = check(wal, 1, device=True)
+    assert w[2] == wal_model.CORRUPT and len(w[0]) == n and w[1] == h[-1] + sig
+    full = wal[: 3 * seg].copy()  # three full segments: END
+    w = check(full, 1, device=True)
+    assert w[2] == wal_model.END and len(w[0]) == 3 * per
+    img = full.copy()  # ... with a corrupt payload and no other stop: every slot was checked
+    img[h[per + 3] + 8] ^= 0x01
+    w = check(img, 1)
+    assert w[2] == wal_model.CORRUPT and len(w[0]) == per + 3
+    img = full.copy()  # ... with a changed length and no stop: declined
+    img[h[2 * per + 1] + 5] ^= 0x01
+    check(img, 2)
+    taken = {"payload_mid": (2 * per + per // 3, "payload"), "crc_first": (per, "crc"),
+             "crc_last": (2 * per - 1, "crc"), "payload_first": (0, "payload"), "empty": (per + 7, "zero")}
+    for name, (k, what) in taken.items():
+        img = wal.copy()
+        if what == "payload":
+            img[h[k] + 8 + size // 2] ^= 0x20
+        elif what == "crc":
+            img[h[k]] ^= 0x01
+        else:
+            img[h[k]: h[k] + 8] = 0
+        w = check(img, 1)
+        assert w[2] == wal_model.CORRUPT and len(w[0]) == k, name
+    if tail >= 8:  # segment 1's padding header zeroed: "Corrupt record" there
+        img = wal.copy()
+        img[seg + per * sig: seg + per * sig + 8] = 0
+        w = check(img, 1)
+        assert w[2] == wal_model.CORRUPT and w[1] == seg + per * sig and len(w[0]) == 2 * per
+    k = per + per // 2
+    declined = {"length": lambda img: img.__setitem__(h[k] + 5, img[h[k] + 5] ^ 0x01),
+                "bad_type": lambda img: img.__setitem__(h[k] + 4, 3),
+                "padding": lambda img: img.__setitem__(h[k] + 4, 1),
+                "past_segment": lambda img: img.__setitem__(slice(h[k] + 4, h[k] + 8),
+                                                            np.frombuffer(np.uint32(seg << 8).tobytes(), np.uint8)),
+                "stale_empty": lambda img: img.__setitem__(slice(h[k], h[k] + 8),
+                                                           np.frombuffer(np.array([0x48674BC7, 0], np.uint32).tobytes(),
+                                                                         np.uint8))}
+    for name, edit in declined.items():
+        img = wal.copy()
+        edit(img)
+        check(img, 2)
+    if tail >= 9:  # a record of tail - 8 bytes fills segment 1's tail instead of the padding
+        img = wal.copy()
+        t = seg + per * sig
+        body = synth.splitmix_np(5, 0, tail - 8).copy()
+        import oracle_lib
+        img[t: t + 8] = np.frombuffer(np.array([oracle_lib.extend(0, body.tobytes()), (tail - 8) << 8], np.uint32)
+                                      .tobytes(), np.uint8)
+        img[t + 8: t + tail] = body
+        w = check(img, 2)
+        assert t in w[0]
+    check(wal, 0, start=h[5])  # from a checkpoint: not tried
+    check(wal, 1)  # and taken again on the next call

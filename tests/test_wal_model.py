@@ -1,5 +1,7 @@
 """The WAL restatement itself (CPU): framing round-trips through replay, and the reference's
 own end-of-log behaviour (zero tail -> "Corrupt record") holds."""
+import struct
+
 import numpy as np
 
 import synth
@@ -55,3 +57,55 @@ def test_reference_append_harness_matches_model():
     # and the replay harness accepts exactly the records the model replays
     recs, _, _ = wal_model.replay(bytes(model), SEG)
     assert ref.ref_wal_replay_mt(wal.ctypes.data, wal.nbytes, SEG, 1, 1) == len(recs) == n
+
+
+def test_spec_replay_is_scan_record_whenever_it_decides():
+    """The uniform-stride pass's decision rule (wal_model.spec_replay, the CPU restatement of
+    k_wal_spec_probe + the SPEC slot checks + k_wal_spec_finish): over uniform WALs with random
+    edits (flipped bytes, zeroed / retyped / resized headers, accepted size-0 records, zeroed
+    rests, padding headers), WALs of mixed sizes and sizes past the stage gate, every result it
+    takes equals the model's replay, and it takes the clean and the simply-corrupted ones."""
+    rng = np.random.default_rng(77)
+    taken = declined = 0
+    for case in range(400):
+        seg = int(rng.choice([64, 100, 256, 1000, 4096]))
+        size = int(rng.choice([1, 2, 5, 16, 20, 56, 100, 120, 183, 184, 300])) if case % 5 else 0
+        if size + 8 > seg:
+            continue
+        nseg = int(rng.integers(1, 7))
+        if size:
+            per = seg // (size + 8)
+            count = int(rng.integers(1, nseg * per + 1))
+            lens = [size] * count
+        else:  # mixed sizes
+            lens = [int(x) for x in rng.integers(1, min(300, seg - 8) + 1, int(rng.integers(1, 200)))]
+        data = synth.splitmix(case, 0, sum(lens) + 16)
+        pos = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        wal = bytearray(nseg * seg)
+        cur, offs = wal_model.append([data[int(p): int(p) + n] for p, n in zip(pos, lens)], wal, seg, 0)
+        if case % 3 and offs:
+            for _ in range(int(rng.integers(1, 3))):
+                k = int(offs[int(rng.integers(0, len(offs)))])
+                kind = int(rng.integers(0, 7))
+                if kind == 0:
+                    wal[int(rng.integers(0, max(cur, 1)))] ^= 1 << int(rng.integers(0, 8))
+                elif kind == 1:
+                    wal[k: k + 8] = bytes(8)
+                elif kind == 2:
+                    wal[k + 4] = int(rng.choice([1, 2, 9]))
+                elif kind == 3:
+                    wal[k + 5] ^= 1
+                elif kind == 4:
+                    wal[k: k + 8] = struct.pack("<II", 0x48674BC7, 0)
+                elif kind == 5:
+                    wal[k:] = bytes(len(wal) - k)
+                else:
+                    s = k // seg * seg
+                    wal[s + seg - 8: s + seg] = bytes(8) if rng.integers(0, 2) else struct.pack("<II", 0, (0 << 8) | 1)
+        got = wal_model.spec_replay(bytes(wal), seg)
+        if got is None:
+            declined += 1
+            continue
+        taken += 1
+        assert got == wal_model.replay(bytes(wal), seg), (case, seg, size)
+    assert taken > 100 and declined > 50, (taken, declined)

@@ -72,3 +72,65 @@ def replay(wal: bytes, seg: int, start: int = 0):
             off = base + seg
         else:
             return recs, off, BAD_TYPE
+
+
+def spec_replay(wal: bytes, seg: int, gate: int = 183):
+    """The uniform-stride pass (engine.h WalSpec) restated: k_wal_spec_probe (segment 0's first
+    header gives the stride; the header after each segment's last slot; the first segment whose
+    first header is all zero), the per-slot checks of k_ragged_staged_pipe's SPEC form and
+    k_wal_spec_finish's decision.  (records, stop, status) as replay(wal, seg) from 0 -- or None
+    when the pass declines and the walk decides.  Keys: 2 g for slot g, 2 (s + 1) m - 1 for the
+    header after segment s's last slot; stop = scan_record's "Corrupt record" there (a CRC
+    mismatch, an all-zero header), dev = any other header."""
+    inf = 1 << 64
+    nseg = len(wal) // seg
+    if nseg == 0:
+        return None
+    c0, st0 = struct.unpack_from("<II", wal, 0)
+    n = st0 >> 8
+    if st0 & 0xFF or not 1 <= n <= gate or n + HEADER > seg:
+        return None
+    sig = n + HEADER
+    m = seg // sig
+    t = m * sig
+    stop = dev = inf
+    nz = nseg
+    for s in range(nseg):
+        c, st = struct.unpack_from("<II", wal, s * seg)
+        if c == 0 and st == 0:
+            nz = min(nz, s)
+        if seg - t >= HEADER:
+            c, st = struct.unpack_from("<II", wal, s * seg + t)
+            key = 2 * (s + 1) * m - 1
+            if st & 0xFF == 1:
+                pass
+            elif c == 0 and st == 0:
+                stop = min(stop, key)
+            else:
+                dev = min(dev, key)
+    if nz < nseg:
+        stop = min(stop, 2 * nz * m)
+    if dev < stop:
+        return None
+    for g in range(nz * m):
+        if 2 * g >= min(stop, dev):
+            break
+        off = g // m * seg + g % m * sig
+        c, st = struct.unpack_from("<II", wal, off)
+        if st == n << 8:
+            if oracle_lib.extend(0, bytes(wal[off + HEADER: off + HEADER + n])) != c:
+                stop = min(stop, 2 * g)
+        elif c == 0 and st == 0:
+            stop = min(stop, 2 * g)
+        else:
+            dev = min(dev, 2 * g)
+    if dev < stop:
+        return None
+    if stop == inf:
+        return [g // m * seg + g % m * sig for g in range(nseg * m)], len(wal), END
+    acc = (stop + 1) // 2
+    if stop % 2 == 0:
+        at = acc // m * seg + acc % m * sig
+    else:
+        at = (acc // m - 1) * seg + t
+    return [g // m * seg + g % m * sig for g in range(acc)], at, CORRUPT
