@@ -346,14 +346,15 @@ def pmc_traffic(path: str, workload: str, n_bytes_per_launch: int):
     return d.get("hbm_bytes_per_launch")
 
 
-REPLAY_PMC = "r06final_wal_replay_pmc.json"  # tools/pmc_replay.sh + tools/pmc_kernels.py, the final tree
+REPLAY_PMC = "r06spec_wal_replay_pmc.json"  # tools/pmc_replay.sh + tools/pmc_kernels.py: the uniform-stride pass
 
 
 def replay_pmc_traffic(n_rec: int, rec_bytes: int):
     """(HBM bytes of the replay's CRC kernel per launch, of the whole call) from the per-kernel PMC
-    file of tools/pmc_replay.sh (FETCH_SIZE x 2 + WRITE_SIZE per dispatch; the call: walk,
-    resolve, gather and the CRC batch summed), whose calls replay tools/replay_study.py's default
-    image: 1M x 180 B records in 1 MiB segments.  (None, None) for another shape (not measured)."""
+    file of tools/pmc_replay.sh (FETCH_SIZE x 2 + WRITE_SIZE per dispatch; the call: the kernels
+    the file lists, summed -- for the uniform-stride pass its one kernel), whose calls replay
+    tools/replay_study.py's default image: 1M x 180 B records in 1 MiB segments.  (None, None) for
+    another shape (not measured)."""
     if (n_rec, rec_bytes) != (1 << 20, 180):
         return None, None
     try:

@@ -575,18 +575,20 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
     KARMA_HIP(launch_ragged_direct_dev(a, (int)blocks, s));
     return 0;
 }
-int ragged_spec_batch_dev(const void* d_wal, WalSpec* d_spec, uint32_t* d_skew_seen, hipStream_t s, bool stage_skew) {
+int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, uint64_t base0, uint64_t wal_end,
+                          WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew) {
     Locked L;
     if (L.rc) return L.rc;
     RaggedArgs a{};
     a.arena = static_cast<const uint8_t*>(d_wal) + 8;  // payloads: the image shifted by the header
-    a.n_rec = 1;  // (the slot count is on the device: spec->nslots)
+    a.n_rec = 1;  // (the slot count comes from segment 0's header, in the kernel)
     a.blob = L.ds->lane_blob;
     a.spec = d_spec;
-    a.n_dev = &d_spec->nslots;
-    a.gate_len = &d_spec->n;
-    a.gate_max = kStgGateLen;
-    a.stage_skew_seen = d_skew_seen;
+    a.spec_nseg = nseg;
+    a.spec_seg = seg_bytes;
+    a.spec_base0 = base0;
+    a.spec_wal_end = wal_end;
+    a.spec_out = h_out;
     bind_arena_bounds(a);
     units_timer_begin(s);  // (karma_crc32c_time_next_units: the replay's CRC kernel)
     KARMA_HIP(launch_ragged_staged_spec(a, L.ds->cu, s, stage_skew));

@@ -22,6 +22,7 @@
 #include "ab.h"
 #include "crc_device.h"
 #include "engine.h"
+#include "karma_crc32c.h"
 #include "wavelog.h"
 
 namespace karma {
@@ -875,6 +876,63 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
     }
 }
 
+// The uniform-stride pass's summary (engine.h WalSummary::spec), by wave 0 of the SPEC kernel's last
+// workgroup: from the keys, written word by word to the page-locked A.spec_out (system scope, as
+// k_wal_publish); then the keys, the flag and the ticket counter are reset for the next call.
+// scratch: 16 dwords of this wave's LDS stage.
+__device__ void spec_finish(const RaggedArgs& A, bool ok, uint32_t n, uint32_t m32, uint32_t lane, uint32_t* scratch) {
+    WalSpec* P = A.spec;
+    if (lane == 0) {
+        const unsigned long long ks = __hip_atomic_load(&P->stop_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long kd = __hip_atomic_load(&P->dev_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t skew = __hip_atomic_load(&P->skew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t S = A.spec_seg, sig = (uint64_t)n + 8, m = m32;
+        WalSummary r{};
+        r.stage_skew = skew;
+        r.first_bad = ~0ull;
+        if (!ok || kd < ks) {
+            r.spec = 2;  // declined: the walk decides
+        } else {
+            r.spec = 1;
+            r.w1 = m32;
+            r.max_len = n;
+            if (ks == ~0ull) {  // every segment ended cleanly
+                r.n_all = A.spec_nseg * m;
+                r.status = KARMA_WAL_END;
+                r.end = A.spec_wal_end;
+            } else {
+                uint64_t rel;
+                if ((ks & 1) == 0) {  // slot g's header
+                    const uint64_t g = ks / 2;
+                    rel = (g / m) * S + (g % m) * sig;
+                    r.n_all = g;
+                } else {  // the header after segment s's last slot
+                    rel = ((ks + 1) / (2 * m) - 1) * S + m * sig;
+                    r.n_all = (ks + 1) / 2;
+                }
+                r.status = KARMA_WAL_CORRUPT;
+                r.end = A.spec_base0 + rel;
+                r.bad_off = rel;
+            }
+        }
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&r);
+        for (uint32_t i = 0; i < sizeof(WalSummary) / 4; ++i) scratch[i] = w[i];
+        __hip_atomic_store(&P->stop_key, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&P->dev_key, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&P->skew, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&P->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    wave_lds_sync();
+    // every word but `spec`, then (their stores complete) `spec`: a host that sees spec != 0 sees the rest
+    constexpr uint32_t kWords = sizeof(WalSummary) / 4, kSpecWord = offsetof(WalSummary, spec) / 4;
+    static_assert(sizeof(WalSummary) % 4 == 0 && kWords <= 64, "one word per lane");
+    uint32_t* out = reinterpret_cast<uint32_t*>(A.spec_out);
+    if (lane < kWords && lane != kSpecWord)
+        __hip_atomic_store(out + lane, scratch[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_s_waitcnt(0);
+    if (lane == 0) __hip_atomic_store(out + kSpecWord, scratch[kSpecWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The staged kernel software-pipelined across batches: batch k + 1's extent and batch k + 2's
 // offsets / lengths are in flight while batch k is stepped (a wave's batches are otherwise one
 // chain of three memory latencies and the steps: DESIGN.md §8a), plain scalars across the loop.
@@ -896,12 +954,15 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // the stage holds), 3 = neither.
 // NWO (tools build A/B, with R8): that many waves instead of kStgWaves8, leaving LDS for another
 // kernel's workgroups on the same CU (the sliced WAL replay's walkers, wal.cc).
-// SPEC (the uniform-stride WAL replay, engine.h WalSpec): the records are the probe's slots, a batch
-// the 64 slots of one segment from 64 j (batch b: segment b / B, j = b % B), each with its 8-byte
-// header in front (arena = image + 8; the extent starts at the first header); no lists are read
-// and no CRCs stored.  Per slot: its header against (n, type 0) and its payload CRC against the
-// header's field; the wave's smallest keys go to spec->stop_key / dev_key by one atomicMin each,
-// once per wave (a wave's slots only grow).
+// SPEC (the uniform-stride WAL replay, engine.h WalSpec): every workgroup reads segment 0's first
+// header (the stride; a header that gives none ends the kernel, workgroup 0 records it), the
+// records are then the slots of a_spec_nseg segments, a batch the 64 slots of one segment from
+// 64 j (batch b: segment b / B, j = b % B), each with its 8-byte header in front (arena = image
+// + 8; the extent starts at the first header); no lists are read and no CRCs stored.  Per slot:
+// its header against (n, type 0) and its payload CRC against the header's field; a segment's last
+// batch also classifies the header after its last slot.  The wave's smallest keys go to
+// spec->stop_key / dev_key by one atomicMin, and the wave then ends: its later slots have larger
+// keys, which can change neither the first stop nor whether a break comes before it.
 template <bool SK, bool R8 = false, int TM = 0, int NWO = 0, bool SPEC = false>
 __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     static_assert(!(SK && R8), "the 8-copy form has the plain stage only");
@@ -917,16 +978,13 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         n_rec = *A.n_dev;
     }
     if (n_rec == 0) return;  // (uniform: a device-sized batch with nothing in it skips the table fill)
-    // SPEC: the stride, slots and batches per segment, segment bytes (uniform)
-    uint32_t sp_n = 0, sp_m = 1, sp_B = 1;
-    uint64_t sp_S = 0;
-    if constexpr (SPEC) {
-        sp_n = A.spec->n;
-        sp_m = A.spec->m;
-        sp_B = A.spec->B;
-        sp_S = A.spec->seg;
-    }
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
+    // SPEC: segment 0's first len/type word, loaded beside the table fill
+    uint32_t sp_st = 0;
+    if constexpr (SPEC) {
+        const uint8_t* h0 = KB_BYTES(A.arena - 8, 8);
+        sp_st = (uint32_t)h0[4] | (uint32_t)h0[5] << 8 | (uint32_t)h0[6] << 16 | (uint32_t)h0[7] << 24;
+    }
     __shared__ __attribute__((aligned(16))) uint32_t lds[BUF + NW * (int)(kStride / 4)];
     static_assert((BUF + NW * (int)(kStride / 4)) * 4 <= 160 * 1024, "LDS of one workgroup");
     if constexpr (R8) {
@@ -943,16 +1001,53 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
     uint32_t* stage32 = reinterpret_cast<uint32_t*>(stage);
     const uint64_t step = (uint64_t)gridDim.x * NW * 64;
     uint64_t base = ((uint64_t)blockIdx.x * NW + wave) * 64;
-    if (base >= n_rec) return;
-    auto ld_meta = [&](uint64_t b, uint64_t& o, uint32_t& n, uint32_t& ini) {
+    // SPEC: the stride, slots and batches per segment (uniform); every wave reaches the epilogue
+    uint32_t sp_n = 0, sp_m = 1, sp_B = 1;
+    const uint64_t sp_S = A.spec_seg;
+    bool sp_ok = false;
+    if constexpr (SPEC) {
+        sp_n = sp_st >> 8;
+        sp_ok = (sp_st & 0xffu) == 0 && sp_n >= 1 && sp_n <= kStgGateLen && (uint64_t)sp_n + 8 <= sp_S;
+        if (sp_ok) {
+            sp_m = (uint32_t)(sp_S / (sp_n + 8));
+            sp_B = (sp_m + 63) / 64;
+        }
+        n_rec = sp_ok ? A.spec_nseg * sp_B * 64 : 0;
+    } else if (base >= n_rec) {
+        return;
+    }
+    // SPEC: the segment and batch of the wave's next ld_meta (batch w + k W: segment (w + k W) / B,
+    // batch (w + k W) % B), advanced by W = all waves per call: no division per batch (uniform)
+    uint32_t cur_sg = 0, cur_j = 0, adv_q = 0, adv_r = 0;
+    if constexpr (SPEC) {
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * NW + wave));
+        const uint32_t W = gridDim.x * NW;
+        cur_sg = w / sp_B;
+        cur_j = w - cur_sg * sp_B;
+        adv_q = W / sp_B;
+        adv_r = W - adv_q * sp_B;
+    }
+    // (SPEC: g0 the batch's first slot, lastf this lane's slot is its segment's last)
+    auto ld_meta = [&](uint64_t b, uint64_t& o, uint32_t& n, uint32_t& ini, uint64_t& g0, bool& lastf) {
         if constexpr (SPEC) {  // slot 64 j + lane of segment s: arithmetic, no loads
-            const uint32_t bi = (uint32_t)(b >> 6), sg = bi / sp_B, i = 64u * (bi - sg * sp_B) + lane;
-            const bool v = b + lane < n_rec && i < sp_m;
-            o = (uint64_t)sg * sp_S + (uint64_t)i * (sp_n + 8u);
+            (void)b;
+            const uint32_t i = 64u * cur_j + lane;
+            const bool v = cur_sg < A.spec_nseg && i < sp_m;
+            o = (uint64_t)cur_sg * sp_S + (uint64_t)i * (sp_n + 8u);
             n = v ? sp_n : 0u;
             ini = 0u;
+            g0 = (uint64_t)cur_sg * sp_m + 64u * cur_j;
+            lastf = v && i == sp_m - 1;
+            cur_j += adv_r;
+            cur_sg += adv_q;
+            if (cur_j >= sp_B) {
+                cur_j -= sp_B;
+                ++cur_sg;
+            }
             return;
         }
+        (void)g0;
+        (void)lastf;
         const uint64_t ri = b + lane;
         const bool v = ri < n_rec;
         o = v ? A.off[ri] : 0;
@@ -980,11 +1075,12 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         }
     };
     // batch `base`: meta (o, n, ini), extent; batch base + step: meta (o2, n2, ini2)
-    uint64_t o, o2;
+    uint64_t o, o2, gq = 0, gq2 = 0;
     uint32_t n, ini, n2, ini2;
+    bool lf = false, lf2 = false;
     uintptr_t lo, hi;
-    ld_meta(base, o, n, ini);
-    ld_meta(base + step, o2, n2, ini2);
+    ld_meta(base, o, n, ini, gq, lf);
+    ld_meta(base + step, o2, n2, ini2, gq2, lf2);
     extent(o, n, lo, hi);
     bool fits = hi != 0 && hi - lo <= kFit;
     // does the batch at (o, n, lo) need the skewed stage?  (banks of the records' first dwords)
@@ -994,14 +1090,16 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
         uint32_t bits = n ? 1u << (((uint32_t)(p - lo) >> 2) & 31u) : 0u;
         bits = wave_or32(bits);
-        const bool poor = __builtin_popcount(bits) < 12;
+        // (a batch of fewer than 12 records -- a segment's last slots, the batch's end -- is poor
+        // only when its records share banks)
+        const uint32_t live = (uint32_t)__popcll(__ballot(n != 0));
+        const bool poor = (uint32_t)__builtin_popcount(bits) < (live < 12u ? live : 12u);
         poor_seen |= poor;
         return SK && poor;
     };
     bool sk = fits && skewed(o, n, lo);
     if (fits) issue(lo, hi);
-    bool rep_stop = false, rep_dev = false;  // (SPEC) this wave has reported a key of that kind
-    for (;;) {
+    for (bool run = !SPEC || base < n_rec; run;) {
         if (fits && (TM & 2) == 0) {
 #pragma unroll
             for (int q = 0; q < kStgVecs; ++q) {
@@ -1023,14 +1121,15 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         const bool more = nb < n_rec;
         uintptr_t lo2 = 0, hi2 = 0;
         bool fits2 = false, sk2 = false;
-        uint64_t o3 = 0;
+        uint64_t o3 = 0, gq3 = 0;
         uint32_t n3 = 0, ini3 = 0;
+        bool lf3 = false;
         if (more) {
             extent(o2, n2, lo2, hi2);
             fits2 = hi2 != 0 && hi2 - lo2 <= kFit;
             sk2 = fits2 && skewed(o2, n2, lo2);
             if (fits2) issue(lo2, hi2);
-            ld_meta(nb + step, o3, n3, ini3);
+            ld_meta(nb + step, o3, n3, ini3, gq3, lf3);
         }
         const uint64_t ri = base + lane;
         [[maybe_unused]] uint32_t spec_res = 0;
@@ -1069,6 +1168,7 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         }
         if constexpr (SPEC) {
             // the slot's header: its CRC field and len/type word, from the stage (or global memory)
+            // (read after the CRC steps: read before them, the kernel measured 4 us slower)
             unsigned long long kstop = ~0ull, kdev = ~0ull;
             if (ri < n_rec && n) {
                 const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
@@ -1092,8 +1192,7 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
                     hc = (uint32_t)hp[0] | (uint32_t)hp[1] << 8 | (uint32_t)hp[2] << 16 | (uint32_t)hp[3] << 24;
                     hs = (uint32_t)hp[4] | (uint32_t)hp[5] << 8 | (uint32_t)hp[6] << 16 | (uint32_t)hp[7] << 24;
                 }
-                const uint32_t bi = (uint32_t)(base >> 6), sg = bi / sp_B;
-                const uint64_t g = (uint64_t)sg * sp_m + 64u * (bi - sg * sp_B) + lane;
+                const uint64_t g = gq + lane;
                 if (hs == (sp_n << 8)) {  // the record the stride says: scan_record checks its CRC
                     if (spec_res != hc) kstop = 2 * g;
                 } else if (hs == 0 && hc == 0) {  // an all-zero header: "Corrupt record" (size-0 quirk)
@@ -1101,24 +1200,58 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
                 } else {  // anything else: the stride's assumption ends here
                     kdev = 2 * g;
                 }
+                // a segment's last slot: the header after it (scan_record at m sigma), key 2 g + 1
+                if (lf && sp_S - (uint64_t)sp_m * (sp_n + 8u) >= 8) {
+                    const uint8_t* tp = KB_BYTES(reinterpret_cast<const uint8_t*>(p + n), 8);
+                    const uint32_t tc = (uint32_t)tp[0] | (uint32_t)tp[1] << 8 | (uint32_t)tp[2] << 16 | (uint32_t)tp[3] << 24;
+                    const uint32_t ts = (uint32_t)tp[4] | (uint32_t)tp[5] << 8 | (uint32_t)tp[6] << 16 | (uint32_t)tp[7] << 24;
+                    const unsigned long long key = 2 * g + 1;
+                    if ((ts & 0xffu) == 1u) {
+                        // padding: the next segment
+                    } else if (tc == 0 && ts == 0) {
+                        kstop = key < kstop ? key : kstop;
+                    } else {
+                        kdev = key < kdev ? key : kdev;
+                    }
+                }
             }
-            kstop = wave_min64(kstop);
-            kdev = wave_min64(kdev);
-            if (kstop != ~0ull && !rep_stop) {
-                if (lane == 0) atomicMin(&A.spec->stop_key, kstop);
-                rep_stop = true;
-            }
-            if (kdev != ~0ull && !rep_dev) {
-                if (lane == 0) atomicMin(&A.spec->dev_key, kdev);
-                rep_dev = true;
+            if (__ballot(kstop != ~0ull || kdev != ~0ull)) {  // (uniform) a key: report it, the wave is done
+                kstop = wave_min64(kstop);
+                kdev = wave_min64(kdev);
+                if (lane == 0) {
+                    // (the returning forms: the epilogue's wait covers them)
+                    unsigned long long r0 = 0, r1 = 0;
+                    if (kstop != ~0ull)
+                        r0 = __hip_atomic_fetch_min(&A.spec->stop_key, kstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (kdev != ~0ull)
+                        r1 = __hip_atomic_fetch_min(&A.spec->dev_key, kdev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("" ::"v"(r0), "v"(r1));
+                }
+                break;
             }
         }
         wave_lds_sync();
         if (!more) break;
         base = nb;
-        o = o2; n = n2; ini = ini2;
-        o2 = o3; n2 = n3; ini2 = ini3;
+        o = o2; n = n2; ini = ini2; gq = gq2; lf = lf2;
+        o2 = o3; n2 = n3; ini2 = ini3; gq2 = gq3; lf2 = lf3;
         lo = lo2; hi = hi2; fits = fits2; sk = sk2;
+    }
+    if constexpr (SPEC) {
+        if (poor_seen && lane == 0) {
+            const uint32_t r = __hip_atomic_fetch_or(&A.spec->skew, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("" ::"v"(r));
+        }
+        // The last workgroup to finish writes the summary: every wave's key atomics have returned
+        // before its workgroup takes a ticket, so the last ticket's loads see the final keys.
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        __shared__ uint32_t s_last;
+        if (threadIdx.x == 0)
+            s_last = __hip_atomic_fetch_add(&A.spec->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x;
+        __syncthreads();
+        if (s_last && wave == 0) spec_finish(A, sp_ok, sp_n, sp_m, lane, stage32);
+        return;
     }
     if (poor_seen && A.stage_skew_seen && lane == 0) *A.stage_skew_seen = 1u;  // (benign races: all store 1)
 }
@@ -1188,7 +1321,9 @@ hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStr
 }
 
 hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew) {
-    if (!a.spec || !a.n_dev || !a.gate_len || grid_blocks <= 0) return hipErrorInvalidValue;
+    if (!a.spec || !a.spec_out || !a.spec_nseg || a.spec_seg < 9 || a.spec_seg >= (1ull << 31) || grid_blocks <= 0 ||
+        a.n_dev)
+        return hipErrorInvalidValue;
     if (skew)
         hipLaunchKernelGGL((k_ragged_staged_pipe<true, false, 0, 0, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else

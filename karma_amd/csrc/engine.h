@@ -192,8 +192,12 @@ struct RaggedArgs {
     // stage's case), whichever stage the kernel has; nullptr: not reported
     uint32_t* stage_skew_seen;
     // the uniform-stride WAL replay (k_ragged_staged_pipe's SPEC form, wal.cc): the records are
-    // slots of the probe's stride (WalSpec), not lists; nullptr otherwise
+    // the slots of spec_nseg segments of spec_seg bytes at arena - 8 (WalSpec), not lists;
+    // nullptr otherwise
     WalSpec* spec;
+    uint64_t spec_nseg, spec_seg;
+    uint64_t spec_base0, spec_wal_end;  // WAL offsets of the image start and end (the summary's)
+    struct WalSummary* spec_out;        // page-locked: the pass's summary (its last workgroup writes it)
 };
 
 // Instrumentation (capi.cc): events armed by karma_crc32c_time_next_units are
@@ -274,22 +278,24 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
 // ---- the uniform-stride WAL replay (wal.cc replay_pass) ------------------------
 // Segment 0's first header (type 0, payload n, 1 <= n <= kStgGateLen) gives a stride sigma = n + 8;
 // the pass assumes every segment holds m = seg / sigma records at slots i * sigma and checks it.
-// Slot g = s * m + i; events are keyed 2 g (slot g) and 2 (s + 1) m - 1 (segment s's tail, after
-// its last slot).  stop_key: the first exact stop scan_record makes there (a CRC mismatch, an
+// Slot g = s * m + i; events are keyed 2 g (slot g) and 2 (s + 1) m - 1 (the header after segment
+// s's last slot).  stop_key: the first exact stop scan_record makes there (a CRC mismatch, an
 // all-zero header: "Corrupt record"); dev_key: the first place the assumption breaks (any other
 // header).  The result is scan_record's whenever stop_key <= dev_key; otherwise the walk runs.
+// (tests/wal_model.py spec_replay restates the rule; tests/test_wal_model.py holds it to the model.)
 struct WalSpec {
-    uint32_t n, m, B, seg;   // payload, slots per segment, 64-slot batches per segment, segment bytes
-    uint64_t nslots;         // slots the CRC kernel checks (0: the probe declined)
-    unsigned long long stop_key, dev_key;
-    uint32_t nseg_eff;       // segments before the first one whose first header is all zero
-    uint32_t ok;             // segment 0's header gave a stride
+    unsigned long long stop_key, dev_key;  // ~0 between calls
+    uint32_t done;                         // workgroups finished (0 between calls)
+    uint32_t skew;                         // a batch's records started on few LDS banks (0 between calls)
 };
-// The SPEC form of k_ragged_staged_pipe over a.spec's slots: per slot the header check, the
-// payload CRC against the header's field, one atomicMin per wave and key (a.arena = image + 8).
+// The SPEC form of k_ragged_staged_pipe over the slots of a.spec_nseg segments of a.spec_seg bytes
+// (a.arena = image + 8): every workgroup reads the stride from segment 0's first header; per slot
+// the header check and the payload CRC against the header's field, one atomicMin per wave; the
+// last workgroup writes the summary to a.spec_out and resets a.spec.  One launch per pass.
 hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew);
-// ... enqueued by the library (capi.cc): the lane blob, the grid, the gate on spec->nslots.
-int ragged_spec_batch_dev(const void* d_wal, WalSpec* d_spec, uint32_t* d_skew_seen, hipStream_t s, bool stage_skew);
+// ... enqueued by the library (capi.cc): the lane blob, one workgroup per CU.
+int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, uint64_t base0, uint64_t wal_end,
+                          WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew);
 
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {
@@ -370,7 +376,6 @@ struct WalArgs {
     // stop flag; largest payload), and this call's tag (1..65535; the words are zeroed when it wraps)
     unsigned long long* rg_words;
     uint32_t rg_tag;
-    WalSpec* spec;             // the uniform-stride pass (k_wal_spec_probe / k_wal_spec_finish)
 };
 constexpr uint32_t kWalkTile = 4096;  // the one-wave walker's LDS tile (wal_device.hip)
 constexpr uint32_t kMaxSub = 4096;    // sub-ranges per segment (k_wal_gather stages their runs in LDS)
@@ -405,12 +410,8 @@ hipError_t launch_wal_compare(const WalArgs& a, uint64_t n, int cu, hipStream_t 
 // after the stream syncs.  A 56-byte hipMemcpyAsync D2H is a copy kernel of its own (~4 us on the
 // replay's stream); this is one small launch (wal.cc's summary readback).
 hipError_t launch_wal_publish(const WalSummary* src, WalSummary* dst_host, hipStream_t s);
-// The uniform-stride pass around its CRC kernel: the probe (one block: the stride, the segment
-// tails, the first all-zero segment; a.spec, a.sum->stage_skew = 0) and the finish (one wave: the
-// summary from the keys).  nseg = a.nwork <= kSpecMaxSeg, a.first_pos == 0.
+// Segments the uniform-stride pass takes at most (its slot keys stay far below 2^64).
 constexpr uint64_t kSpecMaxSeg = 1u << 20;
-hipError_t launch_wal_spec_probe(const WalArgs& a, hipStream_t s);
-hipError_t launch_wal_spec_finish(const WalArgs& a, hipStream_t s);
 
 // ---- KFP frames (kfp.cc) ----------------------------------------------------
 struct KfpWalk {

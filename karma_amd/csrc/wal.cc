@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -175,6 +176,7 @@ struct ReplayCtx {
     // the uniform-stride pass (WalSpec): its probe result on the device; after it declines, the
     // next kSpecSkip passes go straight to the walk
     DevBuf spec;
+    void* spec_init = nullptr;  // spec holds the between-calls state (keys ~0, counters 0) for this allocation
     uint32_t spec_skip = 0;
     int init(int dev) {
         if (ready) return 0;
@@ -195,6 +197,7 @@ struct ReplayCtx {
             b->release();
         rgw_zeroed = nullptr;
         rg_seq = 0;
+        spec_init = nullptr;
         (void)hipStreamDestroy(st);
         st = nullptr;
         if (st2) {
@@ -566,19 +569,35 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
                           (spec_knob == 2 || c.spec_skip == 0);
     if (!spec_try && c.spec_skip) --c.spec_skip;
     if (spec_try) {
-        if (const int rc = c.sum.ensure(sizeof(WalSummary))) return rc;
         if (const int rc = c.h_small.ensure(64, true)) return rc;
         if (const int rc = c.spec.ensure(sizeof(WalSpec))) return rc;
-        A.sum = c.sum.as<WalSummary>();
-        A.spec = c.spec.as<WalSpec>();
-        A.wal_end = wal_bytes;
+        WalSpec* d_spec = c.spec.as<WalSpec>();
+        if (c.spec.p != c.spec_init) {  // a fresh allocation: the state each pass leaves for the next
+            static const WalSpec kFresh{~0ull, ~0ull, 0u, 0u};
+            if (hipMemcpyAsync(d_spec, &kFresh, sizeof(kFresh), hipMemcpyHostToDevice, c.st) != hipSuccess ||
+                hipStreamSynchronize(c.st) != hipSuccess)
+                return fail(KARMA_E_HIP, "wal_replay: uniform-stride state");
+            c.spec_init = c.spec.p;
+        }
         WalSummary* S = c.h_small.as<WalSummary>();
-        if (launch_wal_spec_probe(A, c.st) != hipSuccess)
-            return fail(KARMA_E_HIP, "wal_replay: uniform-stride probe");
-        if (const int rc = ragged_spec_batch_dev(A.wal, A.spec, &A.sum->stage_skew, c.st, c.skew_hint)) return rc;
-        if (launch_wal_spec_finish(A, c.st) != hipSuccess || launch_wal_publish(A.sum, S, c.st) != hipSuccess ||
-            hipStreamSynchronize(c.st) != hipSuccess)
-            return fail(KARMA_E_HIP, "wal_replay: uniform-stride pass");
+        S->spec = 0;  // (the kernel's last workgroup overwrites it: 0 after the sync would be no result)
+        // one launch: its workgroups read the stride from segment 0's first header, check every
+        // slot, and the last one writes the summary straight into page-locked memory
+        if (const int rc = ragged_spec_batch_dev(A.wal, nwork, seg_bytes, base0, wal_bytes, d_spec, S, c.st, c.skew_hint))
+            return rc;
+        // The host waits for the summary word itself, the kernel's last write, not for the stream
+        // (0.0579 vs 0.0636 ms per rotated 1M x 180 B call, profiles/r06_replay_uniform_stride_ab.txt):
+        // every read of the image is done by then, and later work on the stream is ordered after the
+        // kernel anyway.  The stream sync follows only if the word never comes (a fault: its error).
+        // (tools build: KARMA_WAL_SPEC_POLL=0 syncs the stream instead)
+        bool seen = false;
+        if (KARMA_AB_KNOB("KARMA_WAL_SPEC_POLL", 1)) {
+            const auto t0 = std::chrono::steady_clock::now();
+            while (!(seen = __atomic_load_n(&S->spec, __ATOMIC_ACQUIRE) != 0) &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50)) {
+            }
+        }
+        if (!seen && hipStreamSynchronize(c.st) != hipSuccess) return fail(KARMA_E_HIP, "wal_replay: uniform-stride pass");
         T.mark("uniform-stride pass (device)");
 #ifdef KARMA_AB
         g_spec_last = (int)S->spec;

@@ -1373,151 +1373,6 @@ __global__ __launch_bounds__(64) void k_wal_publish(const WalSummary* src, WalSu
 }
 }  // namespace
 
-namespace {
-// ---- the uniform-stride pass (engine.h WalSpec, wal.cc replay_pass) ----------------------------
-__device__ __forceinline__ void read_header(const uint8_t* h, uint32_t& crc, uint32_t& st) {
-    crc = uint32_t(h[0]) | uint32_t(h[1]) << 8 | uint32_t(h[2]) << 16 | uint32_t(h[3]) << 24;
-    st = uint32_t(h[4]) | uint32_t(h[5]) << 8 | uint32_t(h[6]) << 16 | uint32_t(h[7]) << 24;
-}
-
-// One block.  Segment 0's first header gives the stride; per segment the header after its last
-// slot (scan_record at m sigma: padding or a short rest end the segment cleanly, an all-zero
-// header is "Corrupt record", anything else breaks the assumption) and whether its first header
-// is all zero (nothing from that segment on needs a CRC: replay stops there at the latest).
-// When a break comes before every stop, the CRC kernel is skipped (nslots = 0).
-__global__ __launch_bounds__(1024) void k_wal_spec_probe(WalArgs A) {
-    WalSpec* P = A.spec;
-    __shared__ uint32_t s_n, s_ok, s_z[16];
-    __shared__ unsigned long long s_stop[16], s_dev[16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint64_t S = A.seg_bytes;
-    if (tid == 0) {
-        uint32_t crc, st;
-        read_header(seg_at(make_seg(A, 0), 0, 8), crc, st);
-        const uint32_t n = st >> 8;
-        s_ok = (st & 0xffu) == 0 && n >= 1 && n <= kStgGateLen && (uint64_t)n + 8 <= S ? 1u : 0u;
-        s_n = n;
-        A.sum->stage_skew = 0u;
-    }
-    __syncthreads();
-    const uint32_t n = s_n, ok = s_ok, sig = n + 8;
-    const uint32_t m = ok ? (uint32_t)(S / sig) : 1u;
-    const uint64_t T = (uint64_t)m * sig, rest = S - T;
-    unsigned long long kstop = ~0ull, kdev = ~0ull;
-    uint32_t zs = ~0u;
-    if (ok) {
-        for (uint64_t sg = tid; sg < A.nwork; sg += blockDim.x) {
-            const Seg G = make_seg(A, sg);
-            uint32_t crc, st;
-            read_header(seg_at(G, 0, 8), crc, st);
-            if (crc == 0 && st == 0 && sg < zs) zs = (uint32_t)sg;
-            if (rest >= 8) {  // (rest < 8: the short rest, the next segment)
-                read_header(seg_at(G, T, 8), crc, st);
-                const unsigned long long key = 2ull * (sg + 1) * m - 1;
-                if ((st & 0xffu) == 1u) {
-                    // padding: the next segment
-                } else if (crc == 0 && st == 0) {
-                    kstop = key < kstop ? key : kstop;
-                } else {
-                    kdev = key < kdev ? key : kdev;
-                }
-            }
-        }
-    }
-    kstop = wave_min64(kstop);
-    kdev = wave_min64(kdev);
-    zs = wave_min32(zs);
-    if (lane == 0) {
-        s_stop[wave] = kstop;
-        s_dev[wave] = kdev;
-        s_z[wave] = zs;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        for (uint32_t w = 1; w < blockDim.x / 64; ++w) {
-            kstop = s_stop[w] < kstop ? s_stop[w] : kstop;
-            kdev = s_dev[w] < kdev ? s_dev[w] : kdev;
-            zs = s_z[w] < zs ? s_z[w] : zs;
-        }
-        const uint32_t nz = zs < A.nwork ? zs : (uint32_t)A.nwork;
-        if (nz < A.nwork) {  // slot 0 of that segment: the latest stop
-            const unsigned long long key = 2ull * nz * m;
-            kstop = key < kstop ? key : kstop;
-        }
-        // nothing after the segment of the first stop known here needs a CRC
-        uint32_t nslot_seg = nz;
-        if (kstop != ~0ull) {
-            const uint64_t sstop = (kstop & 1) ? (kstop + 1) / (2ull * m) - 1 : kstop / 2 / m;
-            if (sstop + 1 < nz) nslot_seg = (uint32_t)(sstop + 1);
-        }
-        const uint32_t B = (m + 63) / 64;
-        WalSpec R;
-        R.n = n;
-        R.m = m;
-        R.B = B;
-        R.seg = (uint32_t)S;
-        R.nslots = ok && kdev >= kstop ? (uint64_t)nslot_seg * B * 64 : 0;
-        R.stop_key = kstop;
-        R.dev_key = kdev;
-        R.nseg_eff = nz;
-        R.ok = ok;
-        *P = R;
-    }
-}
-
-// One lane: the summary from the keys (engine.h WalSummary::spec).
-__global__ __launch_bounds__(64) void k_wal_spec_finish(WalArgs A) {
-    if (threadIdx.x != 0) return;
-    const WalSpec P = *A.spec;
-    WalSummary R{};
-    R.stage_skew = A.sum->stage_skew;
-    R.first_bad = ~0ull;
-    if (!P.ok || P.dev_key < P.stop_key) {  // declined: the walk decides
-        R.spec = 2;
-        *A.sum = R;
-        return;
-    }
-    const uint64_t m = P.m, sig = P.n + 8, S = P.seg;
-    R.w1 = P.m;
-    R.max_len = P.n;
-    R.spec = 1;
-    if (P.stop_key == ~0ull) {  // every segment ended cleanly
-        R.n_all = (uint64_t)P.nseg_eff * m;
-        R.status = KARMA_WAL_END;
-        R.end = A.wal_end;
-    } else {
-        const unsigned long long K = P.stop_key;
-        uint64_t rel;
-        if ((K & 1) == 0) {  // slot g's header
-            const uint64_t g = K / 2;
-            rel = (g / m) * S + (g % m) * sig;
-            R.n_all = g;
-        } else {  // the header after segment s's last slot
-            const uint64_t sg = (K + 1) / (2 * m) - 1;
-            rel = sg * S + m * sig;
-            R.n_all = (K + 1) / 2;
-        }
-        R.status = KARMA_WAL_CORRUPT;
-        R.end = A.base0 + rel;
-        R.bad_off = rel;
-    }
-    *A.sum = R;
-}
-}  // namespace
-
-hipError_t launch_wal_spec_probe(const WalArgs& a, hipStream_t s) {
-    if (!a.spec || !a.sum || !a.nwork || a.nwork > kSpecMaxSeg || a.first_pos != 0 || a.seg_bytes >= (1ull << 31))
-        return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_wal_spec_probe, dim3(1), dim3(1024), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_wal_spec_finish(const WalArgs& a, hipStream_t s) {
-    if (!a.spec || !a.sum) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_wal_spec_finish, dim3(1), dim3(64), 0, s, a);
-    return hipGetLastError();
-}
-
 hipError_t launch_wal_publish(const WalSummary* src, WalSummary* dst_host, hipStream_t s) {
     hipLaunchKernelGGL(k_wal_publish, dim3(1), dim3(64), 0, s, src, dst_host);
     return hipGetLastError();

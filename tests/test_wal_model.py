@@ -60,8 +60,8 @@ def test_reference_append_harness_matches_model():
 
 
 def test_spec_replay_is_scan_record_whenever_it_decides():
-    """The uniform-stride pass's decision rule (wal_model.spec_replay, the CPU restatement of
-    k_wal_spec_probe + the SPEC slot checks + k_wal_spec_finish): over uniform WALs with random
+    """The uniform-stride pass's decision rule (wal_model.spec_replay, the CPU restatement of the
+    SPEC form of k_ragged_staged_pipe and k_wal_spec_finish): over uniform WALs with random
     edits (flipped bytes, zeroed / retyped / resized headers, accepted size-0 records, zeroed
     rests, padding headers), WALs of mixed sizes and sizes past the stage gate, every result it
     takes equals the model's replay, and it takes the clean and the simply-corrupted ones."""

@@ -75,13 +75,14 @@ def replay(wal: bytes, seg: int, start: int = 0):
 
 
 def spec_replay(wal: bytes, seg: int, gate: int = 183):
-    """The uniform-stride pass (engine.h WalSpec) restated: k_wal_spec_probe (segment 0's first
-    header gives the stride; the header after each segment's last slot; the first segment whose
-    first header is all zero), the per-slot checks of k_ragged_staged_pipe's SPEC form and
-    k_wal_spec_finish's decision.  (records, stop, status) as replay(wal, seg) from 0 -- or None
-    when the pass declines and the walk decides.  Keys: 2 g for slot g, 2 (s + 1) m - 1 for the
-    header after segment s's last slot; stop = scan_record's "Corrupt record" there (a CRC
-    mismatch, an all-zero header), dev = any other header."""
+    """The uniform-stride pass (engine.h WalSpec) restated: segment 0's first header gives the
+    stride (k_ragged_staged_pipe's SPEC prologue), every slot's header and CRC and every segment's
+    header after its last slot are classified (the SPEC batches), and k_wal_spec_finish decides.
+    (records, stop, status) as replay(wal, seg) from 0 -- or None when the pass declines and the
+    walk decides.  Keys: 2 g for slot g, 2 (s + 1) m - 1 for the header after segment s's last
+    slot; stop = scan_record's "Corrupt record" there (a CRC mismatch, an all-zero header), dev =
+    any other header.  (The kernel's waves end at their first key: later keys are larger and
+    change nothing, as the early break below.)"""
     inf = 1 << 64
     nseg = len(wal) // seg
     if nseg == 0:
@@ -94,25 +95,7 @@ def spec_replay(wal: bytes, seg: int, gate: int = 183):
     m = seg // sig
     t = m * sig
     stop = dev = inf
-    nz = nseg
-    for s in range(nseg):
-        c, st = struct.unpack_from("<II", wal, s * seg)
-        if c == 0 and st == 0:
-            nz = min(nz, s)
-        if seg - t >= HEADER:
-            c, st = struct.unpack_from("<II", wal, s * seg + t)
-            key = 2 * (s + 1) * m - 1
-            if st & 0xFF == 1:
-                pass
-            elif c == 0 and st == 0:
-                stop = min(stop, key)
-            else:
-                dev = min(dev, key)
-    if nz < nseg:
-        stop = min(stop, 2 * nz * m)
-    if dev < stop:
-        return None
-    for g in range(nz * m):
+    for g in range(nseg * m):
         if 2 * g >= min(stop, dev):
             break
         off = g // m * seg + g % m * sig
@@ -124,6 +107,15 @@ def spec_replay(wal: bytes, seg: int, gate: int = 183):
             stop = min(stop, 2 * g)
         else:
             dev = min(dev, 2 * g)
+        if g % m == m - 1 and seg - t >= HEADER:  # the header after the segment's last slot
+            c, st = struct.unpack_from("<II", wal, g // m * seg + t)
+            key = 2 * (g // m + 1) * m - 1
+            if st & 0xFF == 1:
+                pass
+            elif c == 0 and st == 0:
+                stop = min(stop, key)
+            else:
+                dev = min(dev, key)
     if dev < stop:
         return None
     if stop == inf:
