@@ -966,7 +966,7 @@ __device__ void spec_finish(const RaggedArgs& A, bool ok, uint32_t n, uint32_t m
 template <bool SK, bool R8 = false, int TM = 0, int NWO = 0, bool SPEC = false>
 __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     static_assert(!(SK && R8), "the 8-copy form has the plain stage only");
-    static_assert(!(SPEC && (R8 || TM || NWO)), "the uniform-stride form is the shipped stage only");
+    static_assert(!(SPEC && (TM || NWO)), "the uniform-stride form has no timing forms");
     constexpr bool END = true;
     constexpr int NW = NWO ? NWO : R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : 24;
     constexpr int TW = R8 ? kRep8Words : kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
@@ -1324,6 +1324,12 @@ hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipSt
     if (!a.spec || !a.spec_out || !a.spec_nseg || a.spec_seg < 9 || a.spec_seg >= (1ull << 31) || grid_blocks <= 0 ||
         a.n_dev)
         return hipErrorInvalidValue;
+#ifdef KARMA_AB
+    if (KARMA_AB_KNOB("KARMA_SPEC_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves, plain stage)
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false, true, 0, 0, true>), dim3(grid_blocks), dim3(kStgWaves8 * 64), 0, s, a);
+        return hipGetLastError();
+    }
+#endif
     if (skew)
         hipLaunchKernelGGL((k_ragged_staged_pipe<true, false, 0, 0, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
     else
