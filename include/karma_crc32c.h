@@ -194,11 +194,11 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
 /* Batched replay (sivir::open's wal::scan_record loop, wal.cc:34-87) from WAL offset
  * `start`, entirely on the device: segment-parallel header walk (sub-range walkers
  * stitched along the real chain when there are few segments), all payload CRCs in one
- * GPU batch, first mismatch.  A replay from a segment boundary whose first record has a
- * payload of at most 183 bytes first tries the uniform-stride pass: every segment read as
- * records of that size, each header and CRC checked in one batch with no walk; its result
- * is used only when it is scan_record's (nothing before replay's stop breaks the stride),
- * otherwise the walk decides.  The image is d_wal when the caller already holds a device
+ * GPU batch, first mismatch.  A replay whose first record (at `start`) has a payload of at
+ * most 183 bytes first tries the uniform-stride pass: the segments read as records of that
+ * size, each header and CRC checked in one batch with no walk; its result is used only when
+ * it is scan_record's (nothing before replay's stop breaks the stride), otherwise the walk
+ * decides.  The image is d_wal when the caller already holds a device
  * copy (h_wal may then be NULL), else h_wal is streamed into HBM (pinned staging, no
  * page-locking of the caller's buffer).  seg_bytes < 2^31.
  * Outputs: *h_n_records type-0 records accepted, their header offsets in h_rec_off

@@ -575,8 +575,8 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
     KARMA_HIP(launch_ragged_direct_dev(a, (int)blocks, s));
     return 0;
 }
-int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, uint64_t base0, uint64_t wal_end,
-                          WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew) {
+int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, uint64_t first_pos, uint64_t base0,
+                          uint64_t wal_end, WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew) {
     Locked L;
     if (L.rc) return L.rc;
     RaggedArgs a{};
@@ -586,6 +586,7 @@ int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, 
     a.spec = d_spec;
     a.spec_nseg = nseg;
     a.spec_seg = seg_bytes;
+    a.spec_first = first_pos;
     a.spec_base0 = base0;
     a.spec_wal_end = wal_end;
     a.spec_out = h_out;

@@ -876,17 +876,29 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
     }
 }
 
-// The uniform-stride pass's summary (engine.h WalSummary::spec), by wave 0 of the SPEC kernel's last
-// workgroup: from the keys, written word by word to the page-locked A.spec_out (system scope, as
-// k_wal_publish); then the keys, the flag and the ticket counter are reset for the next call.
-// scratch: 16 dwords of this wave's LDS stage.
-__device__ void spec_finish(const RaggedArgs& A, bool ok, uint32_t n, uint32_t m32, uint32_t lane, uint32_t* scratch) {
+// The uniform-stride pass's slots (engine.h WalSpec): segment 0's start at f (replay's start), m0
+// slots there, m in every later segment, sigma = n + 8 bytes apart; slot g in WAL order, its
+// header at rel(g) bytes from the image start; B0 / B batches of 64 slots per segment.
+struct SpecGeom {
+    uint64_t S, f;
+    uint32_t n, sig, m, m0, B, B0;
+    __device__ __forceinline__ uint64_t rel(uint64_t g) const {
+        if (g < m0) return f + g * sig;
+        const uint64_t h = g - m0;
+        return (1 + h / m) * S + (h % m) * sig;
+    }
+};
+
+// The summary (engine.h WalSummary::spec), by wave 0 of the SPEC kernel's last workgroup: from the
+// keys, written word by word to the page-locked A.spec_out (system scope, as k_wal_publish); then
+// the keys, the flag and the ticket counter are reset for the next call.  scratch: 16 dwords of
+// this wave's LDS stage.
+__device__ void spec_finish(const RaggedArgs& A, bool ok, const SpecGeom& G, uint32_t lane, uint32_t* scratch) {
     WalSpec* P = A.spec;
     if (lane == 0) {
         const unsigned long long ks = __hip_atomic_load(&P->stop_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long kd = __hip_atomic_load(&P->dev_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t skew = __hip_atomic_load(&P->skew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t S = A.spec_seg, sig = (uint64_t)n + 8, m = m32;
         WalSummary r{};
         r.stage_skew = skew;
         r.first_bad = ~0ull;
@@ -894,22 +906,16 @@ __device__ void spec_finish(const RaggedArgs& A, bool ok, uint32_t n, uint32_t m
             r.spec = 2;  // declined: the walk decides
         } else {
             r.spec = 1;
-            r.w1 = m32;
-            r.max_len = n;
+            r.w1 = G.m;
+            r.max_len = G.n;
             if (ks == ~0ull) {  // every segment ended cleanly
-                r.n_all = A.spec_nseg * m;
+                r.n_all = G.m0 + (A.spec_nseg - 1) * (uint64_t)G.m;
                 r.status = KARMA_WAL_END;
                 r.end = A.spec_wal_end;
             } else {
-                uint64_t rel;
-                if ((ks & 1) == 0) {  // slot g's header
-                    const uint64_t g = ks / 2;
-                    rel = (g / m) * S + (g % m) * sig;
-                    r.n_all = g;
-                } else {  // the header after segment s's last slot
-                    rel = ((ks + 1) / (2 * m) - 1) * S + m * sig;
-                    r.n_all = (ks + 1) / 2;
-                }
+                // slot g's header (key 2 g), or the header after a segment's last slot g (2 g + 1)
+                const uint64_t g = ks / 2, rel = G.rel(g) + ((ks & 1) ? G.sig : 0u);
+                r.n_all = (ks + 1) / 2;
                 r.status = KARMA_WAL_CORRUPT;
                 r.end = A.spec_base0 + rel;
                 r.bad_off = rel;
@@ -982,7 +988,7 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
     // SPEC: segment 0's first len/type word, loaded beside the table fill
     uint32_t sp_st = 0;
     if constexpr (SPEC) {
-        const uint8_t* h0 = KB_BYTES(A.arena - 8, 8);
+        const uint8_t* h0 = KB_BYTES(A.arena - 8 + A.spec_first, 8);
         sp_st = (uint32_t)h0[4] | (uint32_t)h0[5] << 8 | (uint32_t)h0[6] << 16 | (uint32_t)h0[7] << 24;
     }
     __shared__ __attribute__((aligned(16))) uint32_t lds[BUF + NW * (int)(kStride / 4)];
@@ -1001,49 +1007,45 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
     uint32_t* stage32 = reinterpret_cast<uint32_t*>(stage);
     const uint64_t step = (uint64_t)gridDim.x * NW * 64;
     uint64_t base = ((uint64_t)blockIdx.x * NW + wave) * 64;
-    // SPEC: the stride, slots and batches per segment (uniform); every wave reaches the epilogue
-    uint32_t sp_n = 0, sp_m = 1, sp_B = 1;
-    const uint64_t sp_S = A.spec_seg;
+    // SPEC: the slots (uniform); every wave reaches the epilogue
+    SpecGeom G{A.spec_seg, A.spec_first, 0u, 8u, 1u, 1u, 1u, 1u};
     bool sp_ok = false;
     if constexpr (SPEC) {
-        sp_n = sp_st >> 8;
-        sp_ok = (sp_st & 0xffu) == 0 && sp_n >= 1 && sp_n <= kStgGateLen && (uint64_t)sp_n + 8 <= sp_S;
+        G.n = sp_st >> 8;
+        G.sig = G.n + 8;
+        sp_ok = (sp_st & 0xffu) == 0 && G.n >= 1 && G.n <= kStgGateLen && G.f + G.sig <= G.S;
         if (sp_ok) {
-            sp_m = (uint32_t)(sp_S / (sp_n + 8));
-            sp_B = (sp_m + 63) / 64;
+            G.m = (uint32_t)(G.S / G.sig);
+            G.m0 = (uint32_t)((G.S - G.f) / G.sig);
+            G.B = (G.m + 63) / 64;
+            G.B0 = (G.m0 + 63) / 64;
         }
-        n_rec = sp_ok ? A.spec_nseg * sp_B * 64 : 0;
+        n_rec = sp_ok ? (G.B0 + (A.spec_nseg - 1) * (uint64_t)G.B) * 64 : 0;
     } else if (base >= n_rec) {
         return;
     }
-    // SPEC: the segment and batch of the wave's next ld_meta (batch w + k W: segment (w + k W) / B,
-    // batch (w + k W) % B), advanced by W = all waves per call: no division per batch (uniform)
-    uint32_t cur_sg = 0, cur_j = 0, adv_q = 0, adv_r = 0;
-    if constexpr (SPEC) {
-        const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * NW + wave));
-        const uint32_t W = gridDim.x * NW;
-        cur_sg = w / sp_B;
-        cur_j = w - cur_sg * sp_B;
-        adv_q = W / sp_B;
-        adv_r = W - adv_q * sp_B;
-    }
-    // (SPEC: g0 the batch's first slot, lastf this lane's slot is its segment's last)
+    // (SPEC: g0 the batch's first slot, lastf this lane's slot is its segment's last and a header
+    // follows it in the segment)
     auto ld_meta = [&](uint64_t b, uint64_t& o, uint32_t& n, uint32_t& ini, uint64_t& g0, bool& lastf) {
-        if constexpr (SPEC) {  // slot 64 j + lane of segment s: arithmetic, no loads
-            (void)b;
-            const uint32_t i = 64u * cur_j + lane;
-            const bool v = cur_sg < A.spec_nseg && i < sp_m;
-            o = (uint64_t)cur_sg * sp_S + (uint64_t)i * (sp_n + 8u);
-            n = v ? sp_n : 0u;
-            ini = 0u;
-            g0 = (uint64_t)cur_sg * sp_m + 64u * cur_j;
-            lastf = v && i == sp_m - 1;
-            cur_j += adv_r;
-            cur_sg += adv_q;
-            if (cur_j >= sp_B) {
-                cur_j -= sp_B;
-                ++cur_sg;
+        if constexpr (SPEC) {  // batch b / 64: segment 0's B0, then B per segment; arithmetic, no loads
+            const uint32_t bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 6));
+            uint32_t sg = 0, j = bi, mm = G.m0;
+            uint64_t pos0 = G.f, gb = 0;
+            if (bi >= G.B0) {
+                const uint32_t t = bi - G.B0;
+                sg = 1 + t / G.B;
+                j = t - (sg - 1) * G.B;
+                mm = G.m;
+                pos0 = (uint64_t)sg * G.S;
+                gb = G.m0 + (uint64_t)(sg - 1) * G.m;
             }
+            const uint32_t i = 64u * j + lane;
+            const bool v = sg < A.spec_nseg && i < mm;
+            o = pos0 + (uint64_t)i * G.sig;
+            n = v ? G.n : 0u;
+            ini = 0u;
+            g0 = gb + 64u * j;
+            lastf = v && i == mm - 1 && (uint64_t)sg * G.S + G.S - (pos0 + (uint64_t)mm * G.sig) >= 8;
             return;
         }
         (void)g0;
@@ -1193,7 +1195,7 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
                     hs = (uint32_t)hp[4] | (uint32_t)hp[5] << 8 | (uint32_t)hp[6] << 16 | (uint32_t)hp[7] << 24;
                 }
                 const uint64_t g = gq + lane;
-                if (hs == (sp_n << 8)) {  // the record the stride says: scan_record checks its CRC
+                if (hs == (G.n << 8)) {  // the record the stride says: scan_record checks its CRC
                     if (spec_res != hc) kstop = 2 * g;
                 } else if (hs == 0 && hc == 0) {  // an all-zero header: "Corrupt record" (size-0 quirk)
                     kstop = 2 * g;
@@ -1201,7 +1203,7 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
                     kdev = 2 * g;
                 }
                 // a segment's last slot: the header after it (scan_record at m sigma), key 2 g + 1
-                if (lf && sp_S - (uint64_t)sp_m * (sp_n + 8u) >= 8) {
+                if (lf) {
                     const uint8_t* tp = KB_BYTES(reinterpret_cast<const uint8_t*>(p + n), 8);
                     const uint32_t tc = (uint32_t)tp[0] | (uint32_t)tp[1] << 8 | (uint32_t)tp[2] << 16 | (uint32_t)tp[3] << 24;
                     const uint32_t ts = (uint32_t)tp[4] | (uint32_t)tp[5] << 8 | (uint32_t)tp[6] << 16 | (uint32_t)tp[7] << 24;
@@ -1250,7 +1252,7 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         if (threadIdx.x == 0)
             s_last = __hip_atomic_fetch_add(&A.spec->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x;
         __syncthreads();
-        if (s_last && wave == 0) spec_finish(A, sp_ok, sp_n, sp_m, lane, stage32);
+        if (s_last && wave == 0) spec_finish(A, sp_ok, G, lane, stage32);
         return;
     }
     if (poor_seen && A.stage_skew_seen && lane == 0) *A.stage_skew_seen = 1u;  // (benign races: all store 1)
@@ -1322,7 +1324,7 @@ hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStr
 
 hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew) {
     if (!a.spec || !a.spec_out || !a.spec_nseg || a.spec_seg < 9 || a.spec_seg >= (1ull << 31) || grid_blocks <= 0 ||
-        a.n_dev)
+        a.n_dev || a.spec_first + 8 > a.spec_seg)
         return hipErrorInvalidValue;
 #ifdef KARMA_AB
     if (KARMA_AB_KNOB("KARMA_SPEC_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves, plain stage)

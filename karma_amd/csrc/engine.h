@@ -196,6 +196,7 @@ struct RaggedArgs {
     // nullptr otherwise
     WalSpec* spec;
     uint64_t spec_nseg, spec_seg;
+    uint64_t spec_first;                // where replay enters segment 0 (its first slot)
     uint64_t spec_base0, spec_wal_end;  // WAL offsets of the image start and end (the summary's)
     struct WalSummary* spec_out;        // page-locked: the pass's summary (its last workgroup writes it)
 };
@@ -294,8 +295,8 @@ struct WalSpec {
 // last workgroup writes the summary to a.spec_out and resets a.spec.  One launch per pass.
 hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew);
 // ... enqueued by the library (capi.cc): the lane blob, one workgroup per CU.
-int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, uint64_t base0, uint64_t wal_end,
-                          WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew);
+int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, uint64_t first_pos, uint64_t base0,
+                          uint64_t wal_end, WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew);
 
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {

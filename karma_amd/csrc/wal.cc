@@ -556,16 +556,16 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
 #ifdef KARMA_AB
     g_spec_last = 0;
 #endif
-    // 0b. the uniform-stride pass (engine.h WalSpec): when segment 0 starts with a
-    //     record of n <= kStgGateLen bytes, check every segment as m = seg / (n + 8) such records and
-    //     their CRCs in one staged batch, with no walk, gather or lists.  Its result is final when
-    //     the first place that breaks the assumption (if any) comes after replay's stop; otherwise
-    //     the walk below decides (one host round trip spent).  The tools build's KARMA_WAL_SPEC: 0
-    //     never, 2 every pass (no skipping after a decline).
+    // 0b. the uniform-stride pass (engine.h WalSpec): when replay's first header (at
+    //     `start`) is a record of n <= kStgGateLen bytes, check the rest of its segment and every later
+    //     segment as records of that size and their CRCs in one staged batch, with no walk, gather or
+    //     lists.  Its result is final when the first place that breaks the assumption (if any) comes
+    //     after replay's stop; otherwise the walk below decides (one host round trip spent).  The
+    //     tools build's KARMA_WAL_SPEC: 0 never, 2 every pass (no skipping after a decline).
     const long spec_knob = KARMA_AB_KNOB("KARMA_WAL_SPEC", 1);
     // (a caller's forced sub-range size asks for the walk: karma_wal_tuning)
-    const bool spec_try = spec_knob != 0 && dev_plan && !inline_crc && batch == KARMA_WAL_CRC_PLAN && A.first_pos == 0 &&
-                          !(tuning && tuning->walk_sub_bytes) && nwork <= kSpecMaxSeg &&
+    const bool spec_try = spec_knob != 0 && dev_plan && !inline_crc && batch == KARMA_WAL_CRC_PLAN &&
+                          A.first_pos + 8 <= seg_bytes && !(tuning && tuning->walk_sub_bytes) && nwork <= kSpecMaxSeg &&
                           (spec_knob == 2 || c.spec_skip == 0);
     if (!spec_try && c.spec_skip) --c.spec_skip;
     if (spec_try) {
@@ -583,7 +583,8 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         S->spec = 0;  // (the kernel's last workgroup overwrites it: 0 after the sync would be no result)
         // one launch: its workgroups read the stride from segment 0's first header, check every
         // slot, and the last one writes the summary straight into page-locked memory
-        if (const int rc = ragged_spec_batch_dev(A.wal, nwork, seg_bytes, base0, wal_bytes, d_spec, S, c.st, c.skew_hint))
+        if (const int rc = ragged_spec_batch_dev(A.wal, nwork, seg_bytes, A.first_pos, base0, wal_bytes, d_spec, S, c.st,
+                                                 c.skew_hint))
             return rc;
         // The host waits for the summary word itself, the kernel's last write, not for the stream
         // (0.0579 vs 0.0636 ms per rotated 1M x 180 B call, profiles/r06_replay_uniform_stride_ab.txt):
@@ -603,13 +604,16 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         g_spec_last = (int)S->spec;
 #endif
         if (S->spec == 1) {
-            const uint64_t accepted = S->n_all, m = S->w1, sig = (uint64_t)S->max_len + 8;
+            const uint64_t accepted = S->n_all, m = S->w1, sig = (uint64_t)S->max_len + 8, f = A.first_pos;
+            const uint64_t m0 = (seg_bytes - f) / sig;  // segment 0's slots, from replay's start
             c.have_len_hint = true;
             c.len_hint = S->max_len;
             c.skew_hint = S->stage_skew != 0;
-            if (h_rec_off && rec_cap && accepted) {  // slot g = s m + i: base0 + s seg + i sigma
+            if (h_rec_off && rec_cap && accepted) {  // slot g: f + g sigma in segment 0, then m per segment
                 const uint64_t k = std::min<uint64_t>(accepted, rec_cap);
-                parallel_for(0, k, 1 << 16, [&](uint64_t g) { h_rec_off[g] = base0 + (g / m) * seg_bytes + (g % m) * sig; });
+                parallel_for(0, k, 1 << 16, [&](uint64_t g) {
+                    h_rec_off[g] = base0 + (g < m0 ? f + g * sig : (1 + (g - m0) / m) * seg_bytes + (g - m0) % m * sig);
+                });
                 T.mark("offsets");
             }
             *h_n_records = accepted;

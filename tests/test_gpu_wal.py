@@ -713,8 +713,9 @@ def test_replay_uniform_stride_pass(lib, seg, size, monkeypatch):
     (END), a corrupt payload or CRC field at a segment's first, middle or last slot, an empty record
     (all-zero header) and a zeroed padding header; it declines (2) and the walk decides for a changed
     length, a bad type, padding mid-segment, a size-0 record with the stale-word CRC (accepted, 12
-    bytes), a length past the segment and a smaller record in a segment's tail; it is not tried (0)
-    from a checkpoint.  Every result against the model, over the host image and the device copy."""
+    bytes), a length past the segment and a smaller record in a segment's tail; from checkpoints
+    (records in segments 0-2) it is taken too.  Every result against the model, over the host image
+    and the device copy."""
     _walk_env(monkeypatch, "spec")
     ab = _lib.load(_lib.AB_LIB_PATH)
     sig = size + 8
@@ -786,5 +787,17 @@ def test_replay_uniform_stride_pass(lib, seg, size, monkeypatch):
         img[t + 8: t + tail] = body
         w = check(img, 2)
         assert t in w[0]
-    check(wal, 0, start=h[5])  # from a checkpoint: not tried
-    check(wal, 1)  # and taken again on the next call
+    # from checkpoints (sivir::open starts at the WAL's checkpoint, sivir.cc:31): a record in
+    # segment 0, segment 0's last record, a record in segment 2, segment 1's first; a corrupt
+    # payload after the checkpoint; a start inside a payload (decided either way, always exact)
+    for k in (5, per - 1, 2 * per + per // 2, per):
+        w = check(wal, 1, start=h[k])
+        assert w[2] == wal_model.CORRUPT and len(w[0]) == n - k
+    img = wal.copy()
+    img[h[per + 9] + 8] ^= 0x04
+    w = check(img, 1, start=h[per // 2])
+    assert w[2] == wal_model.CORRUPT and w[1] == h[per + 9]
+    for start in (h[7] + 3, h[per + 2] + 8):
+        w = wal_model.replay(wal.tobytes(), seg, start)
+        assert _replay(lib, wal, start=start, seg=seg) == (list(w[0]), w[1], w[2])
+    check(wal, 1)  # and from the start again

@@ -63,10 +63,12 @@ def test_spec_replay_is_scan_record_whenever_it_decides():
     """The uniform-stride pass's decision rule (wal_model.spec_replay, the CPU restatement of the
     SPEC form of k_ragged_staged_pipe and k_wal_spec_finish): over uniform WALs with random
     edits (flipped bytes, zeroed / retyped / resized headers, accepted size-0 records, zeroed
-    rests, padding headers), WALs of mixed sizes and sizes past the stage gate, every result it
-    takes equals the model's replay, and it takes the clean and the simply-corrupted ones."""
+    rests, padding headers), WALs of mixed sizes and sizes past the stage gate, from the start, a
+    record and an arbitrary byte, every result it takes equals the model's replay, and it takes the
+    clean and the simply-corrupted ones."""
     rng = np.random.default_rng(77)
     taken = declined = 0
+    taken_mid = [0]
     for case in range(400):
         seg = int(rng.choice([64, 100, 256, 1000, 4096]))
         size = int(rng.choice([1, 2, 5, 16, 20, 56, 100, 120, 183, 184, 300])) if case % 5 else 0
@@ -102,10 +104,17 @@ def test_spec_replay_is_scan_record_whenever_it_decides():
                 else:
                     s = k // seg * seg
                     wal[s + seg - 8: s + seg] = bytes(8) if rng.integers(0, 2) else struct.pack("<II", 0, (0 << 8) | 1)
-        got = wal_model.spec_replay(bytes(wal), seg)
-        if got is None:
-            declined += 1
-            continue
-        taken += 1
-        assert got == wal_model.replay(bytes(wal), seg), (case, seg, size)
-    assert taken > 100 and declined > 50, (taken, declined)
+        # from the start, from a record (a checkpoint) and from an arbitrary byte
+        starts = [0]
+        if offs:
+            starts += [int(offs[int(rng.integers(0, len(offs)))]), int(rng.integers(0, len(wal)))]
+        for start in starts:
+            got = wal_model.spec_replay(bytes(wal), seg, start)
+            if got is None:
+                declined += 1
+                continue
+            taken += 1
+            if start:
+                taken_mid[0] += 1
+            assert got == wal_model.replay(bytes(wal), seg, start), (case, seg, size, start)
+    assert taken > 200 and declined > 100 and taken_mid[0] > 50, (taken, declined, taken_mid)

@@ -74,31 +74,38 @@ def replay(wal: bytes, seg: int, start: int = 0):
             return recs, off, BAD_TYPE
 
 
-def spec_replay(wal: bytes, seg: int, gate: int = 183):
-    """The uniform-stride pass (engine.h WalSpec) restated: segment 0's first header gives the
-    stride (k_ragged_staged_pipe's SPEC prologue), every slot's header and CRC and every segment's
-    header after its last slot are classified (the SPEC batches), and k_wal_spec_finish decides.
-    (records, stop, status) as replay(wal, seg) from 0 -- or None when the pass declines and the
-    walk decides.  Keys: 2 g for slot g, 2 (s + 1) m - 1 for the header after segment s's last
-    slot; stop = scan_record's "Corrupt record" there (a CRC mismatch, an all-zero header), dev =
-    any other header.  (The kernel's waves end at their first key: later keys are larger and
-    change nothing, as the early break below.)"""
+def spec_replay(wal: bytes, seg: int, start: int = 0, gate: int = 183):
+    """The uniform-stride pass (engine.h WalSpec) restated: replay's first header (at `start`) gives
+    the stride (k_ragged_staged_pipe's SPEC prologue); the slots are the rest of that segment from
+    `start`, then every later segment from its first byte; every slot's header and CRC and every
+    segment's header after its last slot are classified (the SPEC batches), and the last
+    workgroup decides (spec_finish).  (records, stop, status) as replay(wal, seg, start) -- or None
+    when the pass declines and the walk decides.  Keys: 2 g for slot g, 2 g + 1 for the header
+    after a segment's last slot g; stop = scan_record's "Corrupt record" there (a CRC mismatch, an
+    all-zero header), dev = any other header.  (The kernel's waves end at their first key: later
+    keys are larger and change nothing, as the early break below.)"""
     inf = 1 << 64
-    nseg = len(wal) // seg
-    if nseg == 0:
+    s0, f = start // seg, start % seg
+    nseg = len(wal) // seg - s0
+    if nseg <= 0 or f + HEADER > seg:
         return None
-    c0, st0 = struct.unpack_from("<II", wal, 0)
+    base0 = s0 * seg
+    c0, st0 = struct.unpack_from("<II", wal, base0 + f)
     n = st0 >> 8
-    if st0 & 0xFF or not 1 <= n <= gate or n + HEADER > seg:
+    if st0 & 0xFF or not 1 <= n <= gate or f + n + HEADER > seg:
         return None
     sig = n + HEADER
-    m = seg // sig
-    t = m * sig
+    m, m0 = seg // sig, (seg - f) // sig
+
+    def rel(g):
+        return f + g * sig if g < m0 else (1 + (g - m0) // m) * seg + (g - m0) % m * sig
+
+    total = m0 + (nseg - 1) * m
     stop = dev = inf
-    for g in range(nseg * m):
+    for g in range(total):
         if 2 * g >= min(stop, dev):
             break
-        off = g // m * seg + g % m * sig
+        off = base0 + rel(g)
         c, st = struct.unpack_from("<II", wal, off)
         if st == n << 8:
             if oracle_lib.extend(0, bytes(wal[off + HEADER: off + HEADER + n])) != c:
@@ -107,22 +114,19 @@ def spec_replay(wal: bytes, seg: int, gate: int = 183):
             stop = min(stop, 2 * g)
         else:
             dev = min(dev, 2 * g)
-        if g % m == m - 1 and seg - t >= HEADER:  # the header after the segment's last slot
-            c, st = struct.unpack_from("<II", wal, g // m * seg + t)
-            key = 2 * (g // m + 1) * m - 1
+        last = g == m0 - 1 or (g >= m0 and (g - m0) % m == m - 1)
+        seg_end = (off - base0) // seg * seg + seg
+        if last and seg_end - (off - base0 + sig) >= HEADER:  # the header after the segment's last slot
+            c, st = struct.unpack_from("<II", wal, off + sig)
             if st & 0xFF == 1:
                 pass
             elif c == 0 and st == 0:
-                stop = min(stop, key)
+                stop = min(stop, 2 * g + 1)
             else:
-                dev = min(dev, key)
+                dev = min(dev, 2 * g + 1)
     if dev < stop:
         return None
     if stop == inf:
-        return [g // m * seg + g % m * sig for g in range(nseg * m)], len(wal), END
-    acc = (stop + 1) // 2
-    if stop % 2 == 0:
-        at = acc // m * seg + acc % m * sig
-    else:
-        at = (acc // m - 1) * seg + t
-    return [g // m * seg + g % m * sig for g in range(acc)], at, CORRUPT
+        return [base0 + rel(g) for g in range(total)], len(wal), END
+    g = stop // 2
+    return [base0 + rel(i) for i in range((stop + 1) // 2)], base0 + rel(g) + (sig if stop & 1 else 0), CORRUPT
