@@ -576,13 +576,14 @@ int ragged_small_batch_dev(const void* d_arena, const uint64_t* d_off, const uin
     return 0;
 }
 int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, uint64_t first_pos, uint64_t base0,
-                          uint64_t wal_end, WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew) {
+                          uint64_t wal_end, WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew,
+                          bool direct) {
     Locked L;
     if (L.rc) return L.rc;
     RaggedArgs a{};
     a.arena = static_cast<const uint8_t*>(d_wal) + 8;  // payloads: the image shifted by the header
     a.n_rec = 1;  // (the slot count comes from segment 0's header, in the kernel)
-    a.blob = L.ds->lane_blob;
+    a.blob = direct ? L.ds->quad_blob : L.ds->lane_blob;
     a.spec = d_spec;
     a.spec_nseg = nseg;
     a.spec_seg = seg_bytes;
@@ -592,7 +593,10 @@ int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, 
     a.spec_out = h_out;
     bind_arena_bounds(a);
     units_timer_begin(s);  // (karma_crc32c_time_next_units: the replay's CRC kernel)
-    KARMA_HIP(launch_ragged_staged_spec(a, L.ds->cu, s, stage_skew));
+    if (direct)
+        KARMA_HIP(launch_ragged_direct_spec(a, L.ds->cu, s));
+    else
+        KARMA_HIP(launch_ragged_staged_spec(a, L.ds->cu, s, stage_skew));
     units_timer_end(s);
     return 0;
 }

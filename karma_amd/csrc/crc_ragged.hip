@@ -829,59 +829,13 @@ __global__ __launch_bounds__(1024) void k_ragged_finalize(RaggedArgs A) {
 #endif
 }
 
-// Batches of small records (WAL replay of short records, the bounded ragged ABI, the
-// writer's CRC blocks): one record per group of G = 4 lanes, its whole body one unit, no
-// plan kernels (scan, descriptors and finalize cost more than the CRCs of 180-byte
-// records).  Chunks are 64 bytes on the absolute 64-byte grid, read with the quad blob's
-// Z_64 stride tables; the group tree has two levels.  The head and tail byte steps are
-// serial LDS lookups with a per-record trip count, so a wave does them for 64 records at
-// once (lane i: record base + i), then streams the 64 bodies in 4 rounds of 16 groups,
-// passing each record's entering register in and its body register out by shuffles.
-// The rounds are software-pipelined (stream_unit): round r + 1's loads are issued before
-// round r's last chunks are stepped, and each record's tail block is loaded with its
-// extent.  A group with no body in a round (a short record, or past the batch) streams an
-// empty unit at a valid address (the table blob): every load is issued unconditionally.
-// Correct for any length; balanced when every record is small.
-// Why 4 lanes: the kernel is instruction-bound on small records, and the per-round set-up,
-// lane fold and tree are shared by 16 records instead of 8 (8-lane groups: 0.237 ms per
-// replay call of 1M x 180 B, 4: 0.202, 2: 0.222 -- their loads then spread over 32 cache
-// lines per instruction; one record per lane: 0.327, DESIGN.md §8a).
-__global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) {
-    constexpr int G = 4;
-    uint64_t n_rec = A.n_rec;
-    if (A.n_dev) {  // a device-sized batch: the count is known on the device only
-        if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
-        n_rec = *A.n_dev;
-    }
-    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.blob, A.blob + kBlobWords);  // the blob: empty units' address
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
-    load_stream_tables(lds, A.blob);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t X = lane_const();
-    const uint8_t* safe = reinterpret_cast<const uint8_t*>(A.blob);  // 16-aligned, always mapped
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; base < n_rec;
-         base += nwaves * 64) {
-        const uint64_t ri = base + lane;
-        const bool vi = ri < n_rec;
-        const uint8_t* pi = vi ? A.arena + A.off[ri] : A.arena;
-        const uint32_t ni = vi ? A.len[ri] : 0u;
-        const uint32_t initi = vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
-        const uint32_t res = direct_batch<G, kRaggedPF, kRaggedNT, 0>(lds, X, safe, pi, ni, initi, vi);
-        if (vi) {
-            A.out[ri] = res;
-            if (A.cmp_stored && ni && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
-        }
-    }
-}
-
 // The uniform-stride pass's slots (engine.h WalSpec): segment 0's start at f (replay's start), m0
 // slots there, m in every later segment, sigma = n + 8 bytes apart; slot g in WAL order, its
 // header at rel(g) bytes from the image start; B0 / B batches of 64 slots per segment.
 struct SpecGeom {
     uint64_t S, f;
     uint32_t n, sig, m, m0, B, B0;
+    bool type0;  // the first header's type is 0
     __device__ __forceinline__ uint64_t rel(uint64_t g) const {
         if (g < m0) return f + g * sig;
         const uint64_t h = g - m0;
@@ -902,7 +856,11 @@ __device__ void spec_finish(const RaggedArgs& A, bool ok, const SpecGeom& G, uin
         WalSummary r{};
         r.stage_skew = skew;
         r.first_bad = ~0ull;
-        if (!ok || kd < ks) {
+        if (!ok) {  // no stride for this kernel: 3 = a record of another size class (the host
+                    // takes the other kernel next call), 2 = none at all
+            r.spec = G.n >= 1 && G.n <= kSpecDirectMax && G.f + G.sig <= G.S && G.type0 ? 3 : 2;
+            r.max_len = G.n;
+        } else if (kd < ks) {
             r.spec = 2;  // declined: the walk decides
         } else {
             r.spec = 1;
@@ -937,6 +895,198 @@ __device__ void spec_finish(const RaggedArgs& A, bool ok, const SpecGeom& G, uin
         __hip_atomic_store(out + lane, scratch[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_s_waitcnt(0);
     if (lane == 0) __hip_atomic_store(out + kSpecWord, scratch[kSpecWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+
+// The geometry from replay's first len/type word st (uniform): a stride for payloads in [lo, hi].
+__device__ __forceinline__ bool spec_geom(const RaggedArgs& A, uint32_t st, uint32_t lo, uint32_t hi, SpecGeom& G) {
+    G = SpecGeom{A.spec_seg, A.spec_first, st >> 8, (st >> 8) + 8, 1u, 1u, 1u, 1u, (st & 0xffu) == 0};
+    const bool ok = G.type0 && G.n >= lo && G.n <= hi && G.f + G.sig <= G.S;
+    if (ok) {
+        G.m = (uint32_t)(G.S / G.sig);
+        G.m0 = (uint32_t)((G.S - G.f) / G.sig);
+        G.B = (G.m + 63) / 64;
+        G.B0 = (G.m0 + 63) / 64;
+    }
+    return ok;
+}
+__device__ __forceinline__ uint64_t spec_batches(const RaggedArgs& A, const SpecGeom& G) {
+    return G.B0 + (A.spec_nseg - 1) * (uint64_t)G.B;
+}
+
+// Batch bi (uniform): segment 0's B0 batches, then B per segment.  This lane's slot: its header
+// offset o (from the image start = arena - 8), payload n (0: no slot), the batch's first slot g0
+// and whether the slot is its segment's last with a header after it in the segment.
+__device__ __forceinline__ void spec_slot(const RaggedArgs& A, const SpecGeom& G, uint32_t bi, uint32_t lane, uint64_t& o,
+                                          uint32_t& n, uint64_t& g0, bool& lastf) {
+    uint32_t sg = 0, j = bi, mm = G.m0;
+    uint64_t pos0 = G.f, gb = 0;
+    if (bi >= G.B0) {
+        const uint32_t t = bi - G.B0;
+        sg = 1 + t / G.B;
+        j = t - (sg - 1) * G.B;
+        mm = G.m;
+        pos0 = (uint64_t)sg * G.S;
+        gb = G.m0 + (uint64_t)(sg - 1) * G.m;
+    }
+    const uint32_t i = 64u * j + lane;
+    const bool v = sg < A.spec_nseg && i < mm;
+    o = pos0 + (uint64_t)i * G.sig;
+    n = v ? G.n : 0u;
+    g0 = gb + 64u * j;
+    lastf = v && i == mm - 1 && (uint64_t)sg * G.S + G.S - (pos0 + (uint64_t)mm * G.sig) >= 8;
+}
+
+__device__ __forceinline__ void read_hdr(const uint8_t* hp, uint32_t& hc, uint32_t& hs) {
+    hc = (uint32_t)hp[0] | (uint32_t)hp[1] << 8 | (uint32_t)hp[2] << 16 | (uint32_t)hp[3] << 24;
+    hs = (uint32_t)hp[4] | (uint32_t)hp[5] << 8 | (uint32_t)hp[6] << 16 | (uint32_t)hp[7] << 24;
+}
+
+// Slot g against its header (hc, hs) and payload CRC res; when lastf, also the header after the
+// segment's last slot, at tp (key 2 g + 1).
+__device__ __forceinline__ void spec_keys(const SpecGeom& G, uint32_t hc, uint32_t hs, uint32_t res, uint64_t g,
+                                          bool lastf, const uint8_t* tp, unsigned long long& kstop,
+                                          unsigned long long& kdev) {
+    if (hs == (G.n << 8)) {  // the record the stride says: scan_record checks its CRC
+        if (res != hc) kstop = 2 * g;
+    } else if (hs == 0 && hc == 0) {  // an all-zero header: "Corrupt record" (size-0 quirk)
+        kstop = 2 * g;
+    } else {  // anything else: the stride's assumption ends here
+        kdev = 2 * g;
+    }
+    if (lastf) {  // scan_record at the header after the segment's last slot
+        uint32_t tc, ts;
+        read_hdr(tp, tc, ts);
+        const unsigned long long key = 2 * g + 1;
+        if ((ts & 0xffu) == 1u) {
+            // padding: the next segment
+        } else if (tc == 0 && ts == 0) {
+            kstop = key < kstop ? key : kstop;
+        } else {
+            kdev = key < kdev ? key : kdev;
+        }
+    }
+}
+
+// The wave's smallest keys to spec->stop_key / dev_key (returning atomics: the epilogue's wait
+// covers them); true when it had any (uniform): the wave is then done -- its later slots have
+// larger keys, which change neither the first stop nor whether a break comes before it.
+__device__ __forceinline__ bool spec_report(const RaggedArgs& A, unsigned long long kstop, unsigned long long kdev,
+                                            uint32_t lane) {
+    if (!__ballot(kstop != ~0ull || kdev != ~0ull)) return false;
+    kstop = wave_min64(kstop);
+    kdev = wave_min64(kdev);
+    if (lane == 0) {
+        unsigned long long r0 = 0, r1 = 0;
+        if (kstop != ~0ull) r0 = __hip_atomic_fetch_min(&A.spec->stop_key, kstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (kdev != ~0ull) r1 = __hip_atomic_fetch_min(&A.spec->dev_key, kdev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(r0), "v"(r1));
+    }
+    return true;
+}
+
+// Every thread of the workgroup: the stage flag, then a ticket; the last workgroup to finish writes
+// the summary (spec_finish, wave 0, scratch: 16 dwords of LDS).  Every wave's key atomics have
+// returned before its workgroup takes a ticket, so the last ticket's loads see the final keys.
+__device__ void spec_epilogue(const RaggedArgs& A, bool ok, const SpecGeom& G, bool poor_seen, uint32_t* scratch) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (poor_seen && lane == 0) {
+        const uint32_t r = __hip_atomic_fetch_or(&A.spec->skew, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(r));
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    __shared__ uint32_t s_last;
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(&A.spec->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x;
+    __syncthreads();
+    if (s_last && threadIdx.x < 64) spec_finish(A, ok, G, lane, scratch);
+}
+
+// Batches of small records (WAL replay of short records, the bounded ragged ABI, the
+// writer's CRC blocks): one record per group of G = 4 lanes, its whole body one unit, no
+// plan kernels (scan, descriptors and finalize cost more than the CRCs of 180-byte
+// records).  Chunks are 64 bytes on the absolute 64-byte grid, read with the quad blob's
+// Z_64 stride tables; the group tree has two levels.  The head and tail byte steps are
+// serial LDS lookups with a per-record trip count, so a wave does them for 64 records at
+// once (lane i: record base + i), then streams the 64 bodies in 4 rounds of 16 groups,
+// passing each record's entering register in and its body register out by shuffles.
+// The rounds are software-pipelined (stream_unit): round r + 1's loads are issued before
+// round r's last chunks are stepped, and each record's tail block is loaded with its
+// extent.  A group with no body in a round (a short record, or past the batch) streams an
+// empty unit at a valid address (the table blob): every load is issued unconditionally.
+// Correct for any length; balanced when every record is small.
+// Why 4 lanes: the kernel is instruction-bound on small records, and the per-round set-up,
+// lane fold and tree are shared by 16 records instead of 8 (8-lane groups: 0.237 ms per
+// replay call of 1M x 180 B, 4: 0.202, 2: 0.222 -- their loads then spread over 32 cache
+// lines per instruction; one record per lane: 0.327, DESIGN.md §8a).
+// SPEC (the uniform-stride WAL replay, payloads up to kSpecDirectMax): the slots of spec_slot, 64 per
+// wave as k_ragged_staged_pipe's SPEC form takes them, each slot's header read from global memory
+// beside its CRC; the same keys, wave exit and last-workgroup summary.
+template <bool SPEC = false>
+__global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) {
+    constexpr int G = 4;
+    uint64_t n_rec = A.n_rec;
+    if (A.n_dev) {  // a device-sized batch: the count is known on the device only
+        if (*A.gate_len > A.gate_max || *A.gate_len < A.gate_min) return;
+        n_rec = *A.n_dev;
+    }
+    KB_SET_ARENA_SAFE(A.kb_lo, A.kb_hi, A.blob, A.blob + kBlobWords);  // the blob: empty units' address
+    uint32_t sp_st = 0;  // (SPEC: replay's first len/type word, loaded beside the table fill)
+    if constexpr (SPEC) {
+        uint32_t crc0;
+        read_hdr(KB_BYTES(A.arena - 8 + A.spec_first, 8), crc0, sp_st);
+    }
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
+    load_stream_tables(lds, A.blob);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t X = lane_const();
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(A.blob);  // 16-aligned, always mapped
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    SpecGeom SG{};
+    bool sp_ok = false;
+    if constexpr (SPEC) {
+        sp_ok = spec_geom(A, sp_st, 1u, kSpecDirectMax, SG);
+        n_rec = sp_ok ? spec_batches(A, SG) * 64 : 0;
+    }
+    for (uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64; base < n_rec;
+         base += nwaves * 64) {
+        const uint64_t ri = base + lane;
+        bool vi = ri < n_rec;
+        const uint8_t* pi;
+        uint32_t ni, initi;
+        uint64_t g0 = 0;
+        bool lastf = false;
+        if constexpr (SPEC) {
+            uint64_t o;
+            spec_slot(A, SG, (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(base >> 6)), lane, o, ni, g0, lastf);
+            vi = ni != 0;
+            pi = A.arena + o;
+            initi = 0u;
+        } else {
+            pi = vi ? A.arena + A.off[ri] : A.arena;
+            ni = vi ? A.len[ri] : 0u;
+            initi = vi ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
+        }
+        const uint32_t res = direct_batch<G, kRaggedPF, kRaggedNT, 0>(lds, X, safe, pi, ni, initi, vi);
+        if constexpr (SPEC) {
+            unsigned long long kstop = ~0ull, kdev = ~0ull;
+            if (vi) {
+                uint32_t hc, hs;
+                read_hdr(KB_BYTES(pi - 8, 8), hc, hs);
+                spec_keys(SG, hc, hs, res, g0 + lane, lastf, KB_BYTES(pi + ni, lastf ? 8u : 0u), kstop, kdev);
+            }
+            if (spec_report(A, kstop, kdev, lane)) break;
+        } else if (vi) {
+            A.out[ri] = res;
+            if (A.cmp_stored && ni && res != A.cmp_stored[ri]) atomicMin(A.cmp_bad, (unsigned long long)ri);
+        }
+    }
+    if constexpr (SPEC) {
+        __shared__ uint32_t scratch[16];
+        spec_epilogue(A, sp_ok, SG, false, scratch);
+    }
 }
 
 // The staged kernel software-pipelined across batches: batch k + 1's extent and batch k + 2's
@@ -1008,44 +1158,20 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
     const uint64_t step = (uint64_t)gridDim.x * NW * 64;
     uint64_t base = ((uint64_t)blockIdx.x * NW + wave) * 64;
     // SPEC: the slots (uniform); every wave reaches the epilogue
-    SpecGeom G{A.spec_seg, A.spec_first, 0u, 8u, 1u, 1u, 1u, 1u};
+    SpecGeom G{};
     bool sp_ok = false;
     if constexpr (SPEC) {
-        G.n = sp_st >> 8;
-        G.sig = G.n + 8;
-        sp_ok = (sp_st & 0xffu) == 0 && G.n >= 1 && G.n <= kStgGateLen && G.f + G.sig <= G.S;
-        if (sp_ok) {
-            G.m = (uint32_t)(G.S / G.sig);
-            G.m0 = (uint32_t)((G.S - G.f) / G.sig);
-            G.B = (G.m + 63) / 64;
-            G.B0 = (G.m0 + 63) / 64;
-        }
-        n_rec = sp_ok ? (G.B0 + (A.spec_nseg - 1) * (uint64_t)G.B) * 64 : 0;
+        sp_ok = spec_geom(A, sp_st, 1u, kStgGateLen, G);
+        n_rec = sp_ok ? spec_batches(A, G) * 64 : 0;
     } else if (base >= n_rec) {
         return;
     }
     // (SPEC: g0 the batch's first slot, lastf this lane's slot is its segment's last and a header
     // follows it in the segment)
     auto ld_meta = [&](uint64_t b, uint64_t& o, uint32_t& n, uint32_t& ini, uint64_t& g0, bool& lastf) {
-        if constexpr (SPEC) {  // batch b / 64: segment 0's B0, then B per segment; arithmetic, no loads
-            const uint32_t bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 6));
-            uint32_t sg = 0, j = bi, mm = G.m0;
-            uint64_t pos0 = G.f, gb = 0;
-            if (bi >= G.B0) {
-                const uint32_t t = bi - G.B0;
-                sg = 1 + t / G.B;
-                j = t - (sg - 1) * G.B;
-                mm = G.m;
-                pos0 = (uint64_t)sg * G.S;
-                gb = G.m0 + (uint64_t)(sg - 1) * G.m;
-            }
-            const uint32_t i = 64u * j + lane;
-            const bool v = sg < A.spec_nseg && i < mm;
-            o = pos0 + (uint64_t)i * G.sig;
-            n = v ? G.n : 0u;
+        if constexpr (SPEC) {  // arithmetic, no loads
+            spec_slot(A, G, (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 6)), lane, o, n, g0, lastf);
             ini = 0u;
-            g0 = gb + 64u * j;
-            lastf = v && i == mm - 1 && (uint64_t)sg * G.S + G.S - (pos0 + (uint64_t)mm * G.sig) >= 8;
             return;
         }
         (void)g0;
@@ -1190,47 +1316,12 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
                     hc = __builtin_amdgcn_alignbyte(d1, d0, sh);
                     hs = __builtin_amdgcn_alignbyte(d2, d1, sh);
                 } else {
-                    const uint8_t* hp = KB_BYTES(reinterpret_cast<const uint8_t*>(p - 8), 8);
-                    hc = (uint32_t)hp[0] | (uint32_t)hp[1] << 8 | (uint32_t)hp[2] << 16 | (uint32_t)hp[3] << 24;
-                    hs = (uint32_t)hp[4] | (uint32_t)hp[5] << 8 | (uint32_t)hp[6] << 16 | (uint32_t)hp[7] << 24;
+                    read_hdr(KB_BYTES(reinterpret_cast<const uint8_t*>(p - 8), 8), hc, hs);
                 }
-                const uint64_t g = gq + lane;
-                if (hs == (G.n << 8)) {  // the record the stride says: scan_record checks its CRC
-                    if (spec_res != hc) kstop = 2 * g;
-                } else if (hs == 0 && hc == 0) {  // an all-zero header: "Corrupt record" (size-0 quirk)
-                    kstop = 2 * g;
-                } else {  // anything else: the stride's assumption ends here
-                    kdev = 2 * g;
-                }
-                // a segment's last slot: the header after it (scan_record at m sigma), key 2 g + 1
-                if (lf) {
-                    const uint8_t* tp = KB_BYTES(reinterpret_cast<const uint8_t*>(p + n), 8);
-                    const uint32_t tc = (uint32_t)tp[0] | (uint32_t)tp[1] << 8 | (uint32_t)tp[2] << 16 | (uint32_t)tp[3] << 24;
-                    const uint32_t ts = (uint32_t)tp[4] | (uint32_t)tp[5] << 8 | (uint32_t)tp[6] << 16 | (uint32_t)tp[7] << 24;
-                    const unsigned long long key = 2 * g + 1;
-                    if ((ts & 0xffu) == 1u) {
-                        // padding: the next segment
-                    } else if (tc == 0 && ts == 0) {
-                        kstop = key < kstop ? key : kstop;
-                    } else {
-                        kdev = key < kdev ? key : kdev;
-                    }
-                }
+                spec_keys(G, hc, hs, spec_res, gq + lane, lf, KB_BYTES(reinterpret_cast<const uint8_t*>(p + n), lf ? 8u : 0u),
+                          kstop, kdev);
             }
-            if (__ballot(kstop != ~0ull || kdev != ~0ull)) {  // (uniform) a key: report it, the wave is done
-                kstop = wave_min64(kstop);
-                kdev = wave_min64(kdev);
-                if (lane == 0) {
-                    // (the returning forms: the epilogue's wait covers them)
-                    unsigned long long r0 = 0, r1 = 0;
-                    if (kstop != ~0ull)
-                        r0 = __hip_atomic_fetch_min(&A.spec->stop_key, kstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (kdev != ~0ull)
-                        r1 = __hip_atomic_fetch_min(&A.spec->dev_key, kdev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    asm volatile("" ::"v"(r0), "v"(r1));
-                }
-                break;
-            }
+            if (spec_report(A, kstop, kdev, lane)) break;
         }
         wave_lds_sync();
         if (!more) break;
@@ -1240,19 +1331,7 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         lo = lo2; hi = hi2; fits = fits2; sk = sk2;
     }
     if constexpr (SPEC) {
-        if (poor_seen && lane == 0) {
-            const uint32_t r = __hip_atomic_fetch_or(&A.spec->skew, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("" ::"v"(r));
-        }
-        // The last workgroup to finish writes the summary: every wave's key atomics have returned
-        // before its workgroup takes a ticket, so the last ticket's loads see the final keys.
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        __shared__ uint32_t s_last;
-        if (threadIdx.x == 0)
-            s_last = __hip_atomic_fetch_add(&A.spec->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x;
-        __syncthreads();
-        if (s_last && wave == 0) spec_finish(A, sp_ok, G, lane, stage32);
+        spec_epilogue(A, sp_ok, G, poor_seen, stage32);
         return;
     }
     if (poor_seen && A.stage_skew_seen && lane == 0) *A.stage_skew_seen = 1u;  // (benign races: all store 1)
@@ -1287,7 +1366,7 @@ hipError_t launch_ragged_direct(const RaggedArgs& a, int grid_blocks, hipStream_
         hipLaunchKernelGGL((k_ragged_staged_pipe<false, true>), dim3(grid_blocks), dim3(kStgWaves8 * 64), 0, s, a);
 #endif
     else
-        hipLaunchKernelGGL(k_ragged_direct4, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+        hipLaunchKernelGGL(k_ragged_direct4<>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     return hipGetLastError();
 }
@@ -1339,9 +1418,17 @@ hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipSt
     return hipGetLastError();
 }
 
+hipError_t launch_ragged_direct_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
+    if (!a.spec || !a.spec_out || !a.spec_nseg || a.spec_seg < 9 || a.spec_seg >= (1ull << 31) || grid_blocks <= 0 ||
+        a.n_dev || a.spec_first + 8 > a.spec_seg)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ragged_direct4<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_ragged_direct_dev(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
     if (a.n_rec == 0 || !a.n_dev || !a.gate_len) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ragged_direct4, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    hipLaunchKernelGGL(k_ragged_direct4<>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     return hipGetLastError();
 }
 

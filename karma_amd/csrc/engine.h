@@ -294,9 +294,15 @@ struct WalSpec {
 // the header check and the payload CRC against the header's field, one atomicMin per wave; the
 // last workgroup writes the summary to a.spec_out and resets a.spec.  One launch per pass.
 hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew);
-// ... enqueued by the library (capi.cc): the lane blob, one workgroup per CU.
+// The same pass over payloads up to kSpecDirectMax bytes: the SPEC form of k_ragged_direct4 (4-lane
+// groups reading global memory, the quad blob).  A pass whose first payload is outside its kernel's
+// range reports WalSummary::spec = 3 with that payload in max_len (the host takes the other kernel).
+constexpr uint32_t kSpecDirectMax = 1024;
+hipError_t launch_ragged_direct_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s);
+// ... enqueued by the library (capi.cc): the blob, one workgroup per CU; direct: the 4-lane form.
 int ragged_spec_batch_dev(const void* d_wal, uint64_t nseg, uint64_t seg_bytes, uint64_t first_pos, uint64_t base0,
-                          uint64_t wal_end, WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew);
+                          uint64_t wal_end, WalSpec* d_spec, WalSummary* h_out, hipStream_t s, bool stage_skew,
+                          bool direct);
 
 // ---- WAL replay on the device (wal_device.hip, driven by wal.cc) -----------
 struct WalSegMeta {
@@ -330,9 +336,10 @@ struct WalSummary {
     uint64_t first_bad;  // the first candidate whose payload CRC differs (~0: none), set by the CRC check
     uint64_t bad_off;    // inline CRCs: that candidate's header offset relative to wal (k_wal_plan)
     uint32_t stage_skew; // the staged small-record batch met records on few LDS banks (RaggedArgs::stage_skew_seen)
-    uint32_t spec;       // the uniform-stride pass (k_wal_spec_finish): 0 not run, 1 its result is final
-                         // (n_all accepted records, w1 = slots per segment, max_len = payload,
-                         // bad_off = the stop's header offset relative to wal), 2 declined: the walk decides
+    uint32_t spec;       // the uniform-stride pass: 0 not run, 1 its result is final (n_all accepted
+                         // records, w1 = slots per segment, max_len = payload, bad_off = the stop's
+                         // header offset relative to wal), 2 declined: the walk decides, 3 the first
+                         // payload (max_len) is the other kernel's size class: the walk decides
 };
 static_assert(sizeof(WalSummary) == 56, "one 56-byte summary, read back in one copy");
 

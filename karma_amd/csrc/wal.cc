@@ -583,8 +583,10 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
         S->spec = 0;  // (the kernel's last workgroup overwrites it: 0 after the sync would be no result)
         // one launch: its workgroups read the stride from segment 0's first header, check every
         // slot, and the last one writes the summary straight into page-locked memory
+        // the 4-lane form when the last pass's payloads were over the staged kernel's gate
+        const bool direct = c.have_len_hint && c.len_hint > kStgGateLen;
         if (const int rc = ragged_spec_batch_dev(A.wal, nwork, seg_bytes, A.first_pos, base0, wal_bytes, d_spec, S, c.st,
-                                                 c.skew_hint))
+                                                 c.skew_hint, direct))
             return rc;
         // The host waits for the summary word itself, the kernel's last write, not for the stream
         // (0.0579 vs 0.0636 ms per rotated 1M x 180 B call, profiles/r06_replay_uniform_stride_ab.txt):
@@ -621,7 +623,12 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
             *h_status = (int)S->status;
             return 0;
         }
-        c.spec_skip = kSpecSkip;
+        if (S->spec == 3) {  // the other kernel's size class: the next pass takes it (no skipping)
+            c.have_len_hint = true;
+            c.len_hint = S->max_len;
+        } else {
+            c.spec_skip = kSpecSkip;
+        }
     }
     // 1. segment-parallel header walk (sub-range walkers when there are few segments)
     const WalWalkPlan plan =

@@ -32,6 +32,7 @@ hipError_t launch_wal_resolve_gather(const WalArgs&, uint64_t, hipStream_t) { re
 hipError_t launch_wal_compare(const WalArgs&, uint64_t, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_wal_publish(const WalSummary*, WalSummary*, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_ragged_staged_spec(const RaggedArgs&, int, hipStream_t, bool) { return hipErrorNoDevice; }
+hipError_t launch_ragged_direct_spec(const RaggedArgs&, int, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_fill_splitmix(uint8_t*, uint64_t, uint64_t, uint64_t, hipStream_t) { return hipErrorNoDevice; }
 hipError_t launch_stream_probe(const uint8_t*, uint64_t, uint32_t*, int, hipStream_t) { return hipErrorNoDevice; }
 

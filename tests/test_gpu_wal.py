@@ -702,13 +702,15 @@ def _uniform_wal(lib, size, seg, n, seed):
 
 
 _SPEC_CASES = ([(4096 + 4, s) for s in (1, 3, 4, 5, 15, 16, 17, 56, 120, 180, 182, 183)] +
-               [(65536, s) for s in (4, 17, 120, 180, 183)] + [(1 << 20, s) for s in (100, 180)])
+               [(65536, s) for s in (4, 17, 120, 180, 183)] + [(1 << 20, s) for s in (100, 180)] +
+               # payloads over the staged kernel's gate: the 4-lane form (kSpecDirectMax)
+               [(4096 + 4, s) for s in (184, 300)] + [(65536, s) for s in (500, 1000, 1024)] + [(1 << 20, 700)])
 
 
 @pytest.mark.parametrize("seg,size", _SPEC_CASES)
 def test_replay_uniform_stride_pass(lib, seg, size, monkeypatch):
     """The uniform-stride pass (engine.h WalSpec; tools build, KARMA_WAL_SPEC=2: tried on every call)
-    over WALs of one payload size.  Its result is taken (karma_ab_wal_spec_last 1) for the zero tail
+    over WALs of one payload size, up to 183 B (the staged kernel) and up to 1 KiB (the 4-lane one).  Its result is taken (karma_ab_wal_spec_last 1) for the zero tail
     after the last record (CORRUPT at the first unwritten header), segments filled to the image end
     (END), a corrupt payload or CRC field at a segment's first, middle or last slot, an empty record
     (all-zero header) and a zeroed padding header; it declines (2) and the walk decides for a changed
@@ -723,6 +725,9 @@ def test_replay_uniform_stride_pass(lib, seg, size, monkeypatch):
     tail = seg - per * sig
     n = per * 3 + per // 2
     wal, h = _uniform_wal(lib, size, seg, n, seed=size * 7 + seg)
+    # (a first call leaves this size class's hint: a pass whose kernel is the other class's reports 3)
+    _replay(lib, wal, seg=seg)
+    assert ab.karma_ab_wal_spec_last() in (1, 3)
 
     def check(img, spec, start=0, device=False):
         w = wal_model.replay(img.tobytes(), seg, start)
