@@ -195,7 +195,7 @@ int karma_wal_append_batch(const void* h_src, const uint64_t* h_src_off, const u
  * `start`, entirely on the device: segment-parallel header walk (sub-range walkers
  * stitched along the real chain when there are few segments), all payload CRCs in one
  * GPU batch, first mismatch.  A replay whose first record (at `start`) has a payload of at
- * most 183 bytes first tries the uniform-stride pass: the segments read as records of that
+ * most 1 KiB first tries the uniform-stride pass: the segments read as records of that
  * size, each header and CRC checked in one batch with no walk; its result is used only when
  * it is scan_record's (nothing before replay's stop breaks the stride), otherwise the walk
  * decides.  The image is d_wal when the caller already holds a device
