@@ -74,7 +74,7 @@ def replay(wal: bytes, seg: int, start: int = 0):
             return recs, off, BAD_TYPE
 
 
-def spec_replay(wal: bytes, seg: int, start: int = 0, gate: int = 183):
+def spec_replay(wal: bytes, seg: int, start: int = 0, gate: int = 1024):
     """The uniform-stride pass (engine.h WalSpec) restated: replay's first header (at `start`) gives
     the stride (k_ragged_staged_pipe's SPEC prologue); the slots are the rest of that segment from
     `start`, then every later segment from its first byte; every slot's header and CRC and every
