@@ -1403,7 +1403,7 @@ hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStr
 
 hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s, bool skew) {
     if (!a.spec || !a.spec_out || !a.spec_nseg || a.spec_seg < 9 || a.spec_seg >= (1ull << 31) || grid_blocks <= 0 ||
-        a.n_dev || a.spec_first + 8 > a.spec_seg)
+        a.n_dev || a.spec_first + 9 > a.spec_seg)
         return hipErrorInvalidValue;
 #ifdef KARMA_AB
     if (KARMA_AB_KNOB("KARMA_SPEC_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves, plain stage)
@@ -1420,7 +1420,7 @@ hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipSt
 
 hipError_t launch_ragged_direct_spec(const RaggedArgs& a, int grid_blocks, hipStream_t s) {
     if (!a.spec || !a.spec_out || !a.spec_nseg || a.spec_seg < 9 || a.spec_seg >= (1ull << 31) || grid_blocks <= 0 ||
-        a.n_dev || a.spec_first + 8 > a.spec_seg)
+        a.n_dev || a.spec_first + 9 > a.spec_seg)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_ragged_direct4<true>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     return hipGetLastError();

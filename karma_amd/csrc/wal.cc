@@ -565,7 +565,7 @@ int replay_pass(const uint8_t* d_wal, const ImageFill* fill, size_t wal_bytes, s
     const long spec_knob = KARMA_AB_KNOB("KARMA_WAL_SPEC", 1);
     // (a caller's forced sub-range size asks for the walk: karma_wal_tuning)
     const bool spec_try = spec_knob != 0 && dev_plan && !inline_crc && batch == KARMA_WAL_CRC_PLAN &&
-                          A.first_pos + 8 <= seg_bytes && !(tuning && tuning->walk_sub_bytes) && nwork <= kSpecMaxSeg &&
+                          A.first_pos + 9 <= seg_bytes && !(tuning && tuning->walk_sub_bytes) && nwork <= kSpecMaxSeg &&
                           (spec_knob == 2 || c.spec_skip == 0);
     if (!spec_try && c.spec_skip) --c.spec_skip;
     if (spec_try) {
