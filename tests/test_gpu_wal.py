@@ -806,3 +806,24 @@ def test_replay_uniform_stride_pass(lib, seg, size, monkeypatch):
         w = wal_model.replay(wal.tobytes(), seg, start)
         assert _replay(lib, wal, start=start, seg=seg) == (list(w[0]), w[1], w[2])
     check(wal, 1)  # and from the start again
+
+
+@pytest.mark.parametrize("walk", ["split", "spec", "spec0"])
+def test_replay_tiny_segments(lib, walk, monkeypatch):
+    """Segments of 8-40 bytes (a header and a few payload bytes, or less): one record per segment
+    or none, short rests, from the start and from every record; whatever path replay takes (the
+    uniform-stride pass needs a header and a byte after the start), scan_record's result."""
+    _walk_env(monkeypatch, walk)
+    for seg in (8, 9, 10, 16, 17, 24, 40):
+        for size in (1, 2, 7, 8, 16, 32):
+            if size + 8 > seg:
+                continue
+            n = 12
+            lens = np.full(n, size, np.uint32)
+            offs = (np.arange(n, dtype=np.uint64) * size).astype(np.uint64)
+            src = synth.splitmix_np(seg * 100 + size, 0, n * size + 16).copy()
+            wal = np.zeros((n // max(1, seg // (size + 8)) + 2) * seg, np.uint8)
+            cur, rec = _append(lib, src, offs, lens, wal, seg=seg)
+            for start in [0] + [int(x) for x in rec[:4]]:
+                w = wal_model.replay(wal.tobytes(), seg, start)
+                assert _replay(lib, wal, start=start, seg=seg) == (list(w[0]), w[1], w[2]), (seg, size, start)
