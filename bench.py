@@ -711,7 +711,7 @@ def config5_anchor():
     `bench.py --records-per-gpu 33554432` and committed under profiles/: the N = 8 line's per-GPU
     work at N = 1, so a scaling curve can separate shard size from scaling.  Not measured in
     this run; the source file is named."""
-    for name in ("r03_bench_config5_slice.json", "r02_bench_config5_slice.json"):
+    for name in ("r06final_bench_config5_slice.json", "r03_bench_config5_slice.json", "r02_bench_config5_slice.json"):
         path = os.path.join(ROOT, "profiles", name)
         try:
             with open(path) as f:
