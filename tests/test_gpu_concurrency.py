@@ -124,3 +124,56 @@ def test_replay_and_host_extend_from_many_threads(dev):
                     assert K.Value(src[o: o + ln]) == int(payload_crcs[j])
 
     _run_threads(work)
+
+
+def test_uniform_replay_beside_batches_from_many_threads(dev, cases):
+    """The uniform-stride replay pass (one launch whose last workgroup writes the summary the host
+    polls) while other threads' batches run on their own streams: half the threads replay WALs of
+    one record size (a clean one, one with a corrupt record, one that must decline), from the
+    start and from a checkpoint, over the device copies; the others run the batch layouts.  Every
+    result against the model / the oracle."""
+    import wal_model
+    lib = _lib.lib()
+    seg = 64 << 10
+    wals = []
+    for size, bad in ((180, None), (100, 700), (56, "length")):
+        n = 3000
+        lens = np.full(n, size, np.uint32)
+        offs = (np.arange(n, dtype=np.uint64) * size).astype(np.uint64)
+        src = synth.splitmix_np(size, 0, n * size + 16).copy()
+        wal = np.zeros((n * (size + 8) // (seg - 256) + 2) * seg, np.uint8)
+        cur, nf = ctypes.c_uint64(0), ctypes.c_size_t()
+        rec = np.zeros(n, np.uint64)
+        _lib.check("karma_wal_append_batch",
+                   lib.karma_wal_append_batch(src.ctypes.data, offs.ctypes.data, lens.ctypes.data, n, wal.ctypes.data,
+                                              wal.nbytes, seg, ctypes.byref(cur), rec.ctypes.data, ctypes.byref(nf), 0))
+        if bad == "length":
+            wal[int(rec[1500]) + 5] ^= 1
+        elif bad is not None:
+            wal[int(rec[bad]) + 8] ^= 1
+        starts = (0, int(rec[1234]))
+        wals.append((torch.from_numpy(wal).to(dev), wal.nbytes,
+                     {st: wal_model.replay(wal.tobytes(), seg, st) for st in starts}))
+    torch.cuda.synchronize()
+
+    def work(i):
+        s = torch.cuda.Stream(device=dev)
+        for r in range(ROUNDS):
+            if i % 2:
+                d_wal, nbytes, want = wals[(i + r) % len(wals)]
+                for st, w in want.items():
+                    n, stop, status = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+                    got = np.zeros(nbytes // 8, np.uint64)
+                    _lib.check("karma_wal_replay",
+                               lib.karma_wal_replay(None, d_wal.data_ptr(), nbytes, seg, st, ctypes.byref(n),
+                                                    ctypes.byref(stop), ctypes.byref(status), got.ctypes.data,
+                                                    got.size, 0))
+                    assert (list(got[: n.value]), stop.value, status.value) == (list(w[0]), w[1], w[2]), (i, r, st)
+            else:
+                with torch.cuda.stream(s):
+                    name, call, want = cases[(i + r) % len(cases)]
+                    got = call(s)
+                    s.synchronize()
+                    assert np.array_equal(got.cpu().numpy().astype(np.uint32), np.asarray(want, np.uint32)), name
+
+    _run_threads(work)
