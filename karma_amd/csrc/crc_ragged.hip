@@ -1119,10 +1119,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // batch also classifies the header after its last slot.  The wave's smallest keys go to
 // spec->stop_key / dev_key by one atomicMin, and the wave then ends: its later slots have larger
 // keys, which can change neither the first stop nor whether a break comes before it.
-template <bool SK, bool R8 = false, int TM = 0, int NWO = 0, bool SPEC = false>
+template <bool SK, bool R8 = false, int TM = 0, int NWO = 0, bool SPEC = false, bool P2 = false>
 __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
+    static_assert(!P2 || SPEC, "two batches in flight: the uniform-stride form only");
     static_assert(!(SK && R8), "the 8-copy form has the plain stage only");
-    static_assert(!(SPEC && (TM || NWO)), "the uniform-stride form has no timing forms");
+    static_assert(!(SPEC && NWO), "the uniform-stride form has no wave-count override");
     constexpr bool END = true;
     constexpr int NW = NWO ? NWO : R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : 24;
     constexpr int TW = R8 ? kRep8Words : kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
@@ -1183,6 +1184,17 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         ini = v ? (A.init ? A.init[ri] : A.init_scalar) : 0u;
     };
     auto extent = [&](uint64_t o, uint32_t n, uintptr_t& lo, uintptr_t& hi) {
+        if constexpr (SPEC) {  // consecutive slots from lane 0: arithmetic (no wave reduction)
+            const uint64_t live = __ballot(n != 0);
+            if (!live) {
+                lo = hi = 0;
+                return;
+            }
+            const uintptr_t p0 = reinterpret_cast<uintptr_t>(A.arena) + uniform64(o);  // (lane 0's slot)
+            lo = (p0 - 8) & ~uintptr_t(15);
+            hi = (p0 + (uint64_t)(__popcll(live) - 1) * G.sig + G.n + 15) & ~uintptr_t(15);
+            return;
+        }
         const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
         const uintptr_t p0 = SPEC ? p - 8 : p;  // (SPEC: from the record's header)
         uint64_t l = n ? (p0 & ~uintptr_t(15)) : ~0ull, h = n ? ((p + n + 15) & ~uintptr_t(15)) : 0ull;
@@ -1193,14 +1205,32 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)h, 63);
     };
     u32x4 v[kStgVecs];
-    auto issue = [&](uintptr_t lo, uintptr_t hi) {
+    auto issue_into = [&](u32x4 (&dst)[kStgVecs], uintptr_t lo, uintptr_t hi) {
         if constexpr ((TM & 2) != 0) return;
         const uint32_t nv = (uint32_t)((hi - lo) / 16);
 #pragma unroll
         for (int q = 0; q < kStgVecs; ++q) {
             const uint32_t j = lane + 64u * q;  // past the extent: its first block again (no branch)
-            v[q] = ldg<true>(reinterpret_cast<const uint8_t*>(lo + 16ull * (j < nv ? j : 0u)));
+            dst[q] = ldg<true>(reinterpret_cast<const uint8_t*>(lo + 16ull * (j < nv ? j : 0u)));
         }
+    };
+    auto issue = [&](uintptr_t lo, uintptr_t hi) { issue_into(v, lo, hi); };
+    auto store_stage = [&](const u32x4 (&src)[kStgVecs], bool sk) {
+#pragma unroll
+        for (int q = 0; q < kStgVecs; ++q) {
+            uint32_t at = kLead + 16u * (lane + 64u * q);
+            at = at >= kStgBytes ? 0u : at;  // (END) the last slot, past any extent, into the slack
+            if (sk) {  // 4 dwords in one 128-byte line: contiguous after the skew
+                const uint32_t d = at / 4 + at / 128;
+                stage32[d] = src[q].x;
+                stage32[d + 1] = src[q].y;
+                stage32[d + 2] = src[q].z;
+                stage32[d + 3] = src[q].w;
+            } else {
+                *reinterpret_cast<u32x4*>(stage + at) = src[q];
+            }
+        }
+        wave_lds_sync();
     };
     // batch `base`: meta (o, n, ini), extent; batch base + step: meta (o2, n2, ini2)
     uint64_t o, o2, gq = 0, gq2 = 0;
@@ -1212,9 +1242,14 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
     extent(o, n, lo, hi);
     bool fits = hi != 0 && hi - lo <= kFit;
     // does the batch at (o, n, lo) need the skewed stage?  (banks of the records' first dwords)
-    bool poor_seen = false;
+    bool poor_seen = false, poor_checked = false;
     auto skewed = [&](uint64_t o, uint32_t n, uintptr_t lo) {
-        if (!SK && !A.stage_skew_seen) return false;
+        if constexpr (SPEC && !SK) {  // (one stride: the wave's first batch reports for the hint)
+            if (poor_checked) return false;
+            poor_checked = true;
+        } else if (!SK && !A.stage_skew_seen) {
+            return false;
+        }
         const uintptr_t p = reinterpret_cast<uintptr_t>(A.arena) + o;
         uint32_t bits = n ? 1u << (((uint32_t)(p - lo) >> 2) & 31u) : 0u;
         bits = wave_or32(bits);
@@ -1225,40 +1260,11 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         poor_seen |= poor;
         return SK && poor;
     };
-    bool sk = fits && skewed(o, n, lo);
-    if (fits) issue(lo, hi);
-    for (bool run = !SPEC || base < n_rec; run;) {
-        if (fits && (TM & 2) == 0) {
-#pragma unroll
-            for (int q = 0; q < kStgVecs; ++q) {
-                uint32_t at = kLead + 16u * (lane + 64u * q);
-                at = at >= kStgBytes ? 0u : at;  // (END) the last slot, past any extent, into the slack
-                if (sk) {  // 4 dwords in one 128-byte line: contiguous after the skew
-                    const uint32_t d = at / 4 + at / 128;
-                    stage32[d] = v[q].x;
-                    stage32[d + 1] = v[q].y;
-                    stage32[d + 2] = v[q].z;
-                    stage32[d + 3] = v[q].w;
-                } else {
-                    *reinterpret_cast<u32x4*>(stage + at) = v[q];
-                }
-            }
-            wave_lds_sync();
-        }
-        const uint64_t nb = base + step;
-        const bool more = nb < n_rec;
-        uintptr_t lo2 = 0, hi2 = 0;
-        bool fits2 = false, sk2 = false;
-        uint64_t o3 = 0, gq3 = 0;
-        uint32_t n3 = 0, ini3 = 0;
-        bool lf3 = false;
-        if (more) {
-            extent(o2, n2, lo2, hi2);
-            fits2 = hi2 != 0 && hi2 - lo2 <= kFit;
-            sk2 = fits2 && skewed(o2, n2, lo2);
-            if (fits2) issue(lo2, hi2);
-            ld_meta(nb + step, o3, n3, ini3, gq3, lf3);
-        }
+    [[maybe_unused]] uint32_t tm_sink = 0;
+    // One batch: each lane's record from the stage (or global memory), its CRC stored (lists) or
+    // checked against its header (SPEC: true when the wave reported a key and is done).
+    auto proc = [&](uint64_t base, uint64_t o, uint32_t n, uint32_t ini, uintptr_t lo, bool fits, bool sk, uint64_t gq,
+                    bool lf) -> bool {
         const uint64_t ri = base + lane;
         [[maybe_unused]] uint32_t spec_res = 0;
         if (ri < n_rec) {
@@ -1321,8 +1327,74 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
                 spec_keys(G, hc, hs, spec_res, gq + lane, lf, KB_BYTES(reinterpret_cast<const uint8_t*>(p + n), lf ? 8u : 0u),
                           kstop, kdev);
             }
-            if (spec_report(A, kstop, kdev, lane)) break;
+            if constexpr (TM != 0) {  // (timing forms: every batch; the keys kept alive through a sink)
+                tm_sink ^= (uint32_t)kstop ^ (uint32_t)(kstop >> 32) ^ (uint32_t)kdev;
+            } else if (spec_report(A, kstop, kdev, lane)) {
+                return true;
+            }
         }
+        return false;
+    };
+    bool sk = fits && skewed(o, n, lo);
+    if constexpr (SPEC && P2) {
+        // Two batches in flight (the slots' meta is arithmetic): batch k's bytes in one register
+        // set while batch k + 1's land in the other; batch k + 2 is issued into the set batch k
+        // leaves once it is in the stage.  (The unrolled pair keeps the sets in registers.)
+        u32x4 v2[kStgVecs];
+        uintptr_t lo2 = 0, hi2 = 0;
+        bool fits2 = false, sk2 = false;
+        if (fits) issue_into(v, lo, hi);
+        if (base + step < n_rec) {
+            extent(o2, n2, lo2, hi2);
+            fits2 = hi2 != 0 && hi2 - lo2 <= kFit;
+            sk2 = fits2 && skewed(o2, n2, lo2);
+            if (fits2) issue_into(v2, lo2, hi2);
+        }
+        // one batch out of `cur` (its set), batch + 2 steps issued into it; false: the wave is done
+        auto step_one = [&](u32x4 (&cur)[kStgVecs]) -> bool {
+            if (fits && (TM & 2) == 0) store_stage(cur, sk);
+            const uint64_t nn = base + 2 * step;
+            uint64_t o3 = 0, gq3 = 0;
+            uint32_t n3 = 0, ini3 = 0;
+            bool lf3 = false, fits3 = false, sk3 = false;
+            uintptr_t lo3 = 0, hi3 = 0;
+            if (nn < n_rec) {
+                ld_meta(nn, o3, n3, ini3, gq3, lf3);
+                extent(o3, n3, lo3, hi3);
+                fits3 = hi3 != 0 && hi3 - lo3 <= kFit;
+                sk3 = fits3 && skewed(o3, n3, lo3);
+                if (fits3) issue_into(cur, lo3, hi3);
+            }
+            const bool done = proc(base, o, n, ini, lo, fits, sk, gq, lf);
+            wave_lds_sync();
+            if (done || base + step >= n_rec) return false;
+            base += step;
+            o = o2; n = n2; ini = ini2; gq = gq2; lf = lf2; lo = lo2; hi = hi2; fits = fits2; sk = sk2;
+            o2 = o3; n2 = n3; ini2 = ini3; gq2 = gq3; lf2 = lf3; lo2 = lo3; hi2 = hi3; fits2 = fits3; sk2 = sk3;
+            return true;
+        };
+        if (base < n_rec)
+            while (step_one(v) && step_one(v2)) {
+            }
+    } else {
+    if (fits) issue(lo, hi);
+    for (bool run = !SPEC || base < n_rec; run;) {
+        if (fits && (TM & 2) == 0) store_stage(v, sk);
+        const uint64_t nb = base + step;
+        const bool more = nb < n_rec;
+        uintptr_t lo2 = 0, hi2 = 0;
+        bool fits2 = false, sk2 = false;
+        uint64_t o3 = 0, gq3 = 0;
+        uint32_t n3 = 0, ini3 = 0;
+        bool lf3 = false;
+        if (more) {
+            extent(o2, n2, lo2, hi2);
+            fits2 = hi2 != 0 && hi2 - lo2 <= kFit;
+            sk2 = fits2 && skewed(o2, n2, lo2);
+            if (fits2) issue(lo2, hi2);
+            ld_meta(nb + step, o3, n3, ini3, gq3, lf3);
+        }
+        if (proc(base, o, n, ini, lo, fits, sk, gq, lf)) break;
         wave_lds_sync();
         if (!more) break;
         base = nb;
@@ -1330,7 +1402,9 @@ __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) voi
         o2 = o3; n2 = n3; ini2 = ini3; gq2 = gq3; lf2 = lf3;
         lo = lo2; hi = hi2; fits = fits2; sk = sk2;
     }
+    }  // (one batch in flight)
     if constexpr (SPEC) {
+        if (TM != 0 && tm_sink == 0x9e3779b9u) poor_seen = true;  // (never in practice: keeps the sink)
         spec_epilogue(A, sp_ok, G, poor_seen, stage32);
         return;
     }
@@ -1406,6 +1480,26 @@ hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipSt
         a.n_dev || a.spec_first + 9 > a.spec_seg)
         return hipErrorInvalidValue;
 #ifdef KARMA_AB
+    if (KARMA_AB_KNOB("KARMA_SPEC_P2", 0)) {  // (A/B: two batches in flight per wave)
+        if (const long tm = KARMA_AB_KNOB("KARMA_SPEC_TIMING", 0); tm == 1)
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 1, 0, true, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        else if (tm == 2)
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 2, 0, true, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 0, 0, true, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        return hipGetLastError();
+    }
+    // (timing forms, wrong results: 1 = no CRC steps, 2 = no record loads or stage stores, 3 = neither)
+    if (const long tm = KARMA_AB_KNOB("KARMA_SPEC_TIMING", 0); tm == 1) {
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 1, 0, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        return hipGetLastError();
+    } else if (tm == 2) {
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 2, 0, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        return hipGetLastError();
+    } else if (tm == 3) {
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 3, 0, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        return hipGetLastError();
+    }
     if (KARMA_AB_KNOB("KARMA_SPEC_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves, plain stage)
         hipLaunchKernelGGL((k_ragged_staged_pipe<false, true, 0, 0, true>), dim3(grid_blocks), dim3(kStgWaves8 * 64), 0, s, a);
         return hipGetLastError();
