@@ -1544,7 +1544,8 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
     // at once, one workgroup per CU (grid_blocks = the CU count); larger batches take rounds of 4
     const uint64_t cu = grid_blocks > 0 ? (uint64_t)grid_blocks : 1;
     const uint64_t nb1 = ragged_scan_blocks(a.n_rec);
-    const int R = KARMA_PLAN_RMAX == 1 || nb1 <= cu ? 1 : KARMA_PLAN_RMAX == 2 || nb1 <= 2 * cu ? 2 : 4;
+    int R = KARMA_PLAN_RMAX == 1 || nb1 <= cu ? 1 : KARMA_PLAN_RMAX == 2 || nb1 <= 2 * cu ? 2 : 4;
+    if (const long rf = KARMA_AB_KNOB("KARMA_PLAN_R", 0); rf == 1 || rf == 2 || rf == 4) R = (int)rf;  // (A/B)
     const unsigned pb = (unsigned)((nb1 + R - 1) / R);
     if (R == 1)
         hipLaunchKernelGGL(k_ragged_plan<1>, dim3(pb), dim3(kScanBlock), 0, s, a);
@@ -1602,7 +1603,8 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
         hipLaunchKernelGGL(k_units_ragged<>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     units_timer_end(s);
     const uint64_t fb1 = (a.n_rec + 1023) / 1024;  // 16 waves x 64 records per block
-    const int FR = fb1 <= cu ? 1 : fb1 <= 2 * cu ? 2 : 4;
+    int FR = fb1 <= cu ? 1 : fb1 <= 2 * cu ? 2 : 4;
+    if (const long ff = KARMA_AB_KNOB("KARMA_FINALIZE_FR", 0); ff == 1 || ff == 2 || ff == 4) FR = (int)ff;  // (A/B)
     const unsigned fblocks = (unsigned)std::min<uint64_t>((fb1 + FR - 1) / FR, cu);
 #ifdef KARMA_AB
     if (KARMA_AB_KNOB("KARMA_FINALIZE_LITE", 0)) {  // (A/B: the LDS fill without the huge records' maps)
