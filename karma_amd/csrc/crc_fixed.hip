@@ -277,7 +277,9 @@ __device__ uint64_t* g_seg_log;
 // loads the grid fold maps (any may fold).
 // R8 (tools build A/B, round 6): the 8-copy stride image (32 KiB, stride_step8) instead of the
 // 16-copy one (64 KiB): half the table fill the chunk loads queue behind.
-template <bool NT, bool ARRIVE = false, bool R8 = false>
+// LATE (tools build A/B, round 6): the comb maps only the workgroup fold uses (Z_8U .. Z_64U, 16 of
+// the fill's 49 KiB) loaded after the chunk loads and stored after the steps.
+template <bool NT, bool ARRIVE = false, bool R8 = false, bool LATE = false>
 __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     constexpr int TW = R8 ? kRep8Words : kRep16Words;
     constexpr int kSegZ4 = TW, kSegComb = kSegZ4 + kSmallWords, kSegGrid = kSegComb + kCombMaps * 1024;
@@ -308,7 +310,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     }
     LdsCopy<kSmallWords, kBlockThreads> small;
     small.load(A.blob + 1024);
-    LdsCopy<kCombMaps * 1024, kBlockThreads> comb;
+    constexpr int kEarlyMaps = LATE ? 3 : kCombMaps;  // (the wave trees use Z_U, Z_2U, Z_4U)
+    LdsCopy<kEarlyMaps * 1024, kBlockThreads> comb;
     comb.load(A.comb_maps);
     SEG_STAMP(6);
     // 2. this lane's unit (arithmetic only: it runs while the table loads are in flight)
@@ -332,6 +335,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     v[0] = ldg<NT>(ok0 ? L.w : L.lclamp);
 #pragma unroll
     for (int q = 1; q < kSegMaxChunks; ++q) v[q] = ldg<NT>(pmin(L.w + q * kChunk, L.lclamp));
+    LdsCopy<LATE ? (kCombMaps - 3) * 1024 : 1024, kBlockThreads> comb_late;  // (LATE: behind the chunks)
+    if constexpr (LATE) comb_late.load(A.comb_maps + 3 * 1024);
     SEG_STAMP(7);
     // 5. the unit's windows (stride_step16s: the 16-copy image in swapped lane order), the lane
     //    fold and the 8-lane tree
@@ -364,6 +369,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     c = zmap(lds, kSegComb + 2048, c) ^ tree_down<32>(c);
     if (lane == 0) wst[wave] = c;
     if (ARRIVE || last_wg) grid.store(lds + kSegGrid);
+    if constexpr (LATE) comb_late.store(lds + kSegComb + 3 * 1024);
     SEG_STAMP(2);
     __syncthreads();
     __shared__ uint32_t s_tag;
@@ -662,6 +668,8 @@ hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t 
 #ifdef KARMA_AB
     else if (KARMA_AB_KNOB("KARMA_SEGMENT_R8", 0))  // (A/B: the 8-copy stride image)
         hipLaunchKernelGGL((k_segment_once<true, false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (KARMA_AB_KNOB("KARMA_SEGMENT_LATE", 0))  // (A/B: the workgroup fold's maps behind the chunks)
+        hipLaunchKernelGGL((k_segment_once<true, false, false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
 #endif
     else
         hipLaunchKernelGGL((k_segment_once<true, false>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
