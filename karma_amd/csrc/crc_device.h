@@ -1005,6 +1005,43 @@ __device__ __forceinline__ uint32_t lane_record_end(const uint32_t* lds, uint32_
     w3 ^= (k0 == 3 ? lo32 : 0u) ^ (k0 == 2 ? hi32 : 0u);
     uint32_t carry = k0 == 3 ? hi32 : 0u;
     uint32_t a0 = w0, a1 = w1, a2 = w2, a3 = w3;
+    if constexpr ((SMODE & 88) == 88) {
+        // SMODE bit 6 (with the 16-copy image in swapped lane order): each window in three
+        // phases kept apart by scheduling barriers -- the 16 lookup indices; every LDS read of the
+        // window (the next window's stage dwords, then the 16 lookups) in flight together; the
+        // xors.  (Left to itself the compiler issues the lookups of two accumulators, waits for
+        // them, then issues the other two's: two LDS round trips per window.)
+        const bool swp = (threadIdx.x & 16u) != 0;
+        const uint32_t s0 = swp ? 0x0c0c0105u : 0x0c0c0004u, s1 = swp ? 0x0c0c0004u : 0x0c0c0105u;
+        const uint32_t s2 = swp ? 0x0c0c0307u : 0x0c0c0206u, s3 = swp ? 0x0c0c0206u : 0x0c0c0307u;
+        for (uint32_t j = 1; j < W; ++j) {
+            q += 4;
+            const uint32_t acc[4] = {a0, a1, a2, a3};
+            uint32_t ix[16], l[16];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                ix[4 * k] = __builtin_amdgcn_perm(X, acc[k], s0);
+                ix[4 * k + 1] = __builtin_amdgcn_perm(X, acc[k], s1);
+                ix[4 * k + 2] = __builtin_amdgcn_perm(X, acc[k], s2);
+                ix[4 * k + 3] = __builtin_amdgcn_perm(X, acc[k], s3);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            d0 = d4;
+            d1 = rd(q + 1);
+            d2 = rd(q + 2);
+            d3 = rd(q + 3);
+            d4 = rd(q + 4);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) l[k] = lds_at_byte(lds, ix[k]);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t vx = __builtin_amdgcn_alignbyte(d1, d0, sh) ^ carry;
+            carry = 0u;
+            a0 = xor3(xor3(l[0], l[1], vx), l[2], l[3]);
+            a1 = xor3(xor3(l[4], l[5], __builtin_amdgcn_alignbyte(d2, d1, sh)), l[6], l[7]);
+            a2 = xor3(xor3(l[8], l[9], __builtin_amdgcn_alignbyte(d3, d2, sh)), l[10], l[11]);
+            a3 = xor3(xor3(l[12], l[13], __builtin_amdgcn_alignbyte(d4, d3, sh)), l[14], l[15]);
+        }
+    } else
     for (uint32_t j = 1; j < W; ++j) {
         q += 4;
         d0 = d4;

@@ -1108,6 +1108,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // TM (timing attribution, tools build only, wrong CRCs): 1 = no CRC steps (each lane xors one
 // stage word into its result), 2 = no record loads or stage stores (the steps run over whatever
 // the stage holds), 3 = neither.
+// WIDE (not with R8): lane_record_end's phased window loop (SMODE bit 6): every LDS read of a
+// window in flight together, one round trip per window (tools build A/B KARMA_SPEC_WIDE=0 /
+// KARMA_STAGE_WIDE=0: the loop the compiler schedules, two; 1M x 180 B uniform pass 52.8 -> 51.1
+// us, profiles/r06_staged_phased_window_ab.txt).
 // NWO (tools build A/B, with R8): that many waves instead of kStgWaves8, leaving LDS for another
 // kernel's workgroups on the same CU (the sliced WAL replay's walkers, wal.cc).
 // SPEC (the uniform-stride WAL replay, engine.h WalSpec): every workgroup reads segment 0's first
@@ -1119,13 +1123,14 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // batch also classifies the header after its last slot.  The wave's smallest keys go to
 // spec->stop_key / dev_key by one atomicMin, and the wave then ends: its later slots have larger
 // keys, which can change neither the first stop nor whether a break comes before it.
-template <bool SK, bool R8 = false, int TM = 0, int NWO = 0, bool SPEC = false, bool P2 = false>
+template <bool SK, bool R8 = false, int TM = 0, int NWO = 0, bool SPEC = false, bool P2 = false, bool WIDE = !R8>
 __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     static_assert(!P2 || SPEC, "two batches in flight: the uniform-stride form only");
     static_assert(!(SK && R8), "the 8-copy form has the plain stage only");
     static_assert(!(SPEC && NWO), "the uniform-stride form has no wave-count override");
+    static_assert(!(WIDE && R8), "the phased window loop reads the 16-copy image");
     constexpr bool END = true;
-    constexpr int NW = NWO ? NWO : R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : 24;
+    constexpr int NW = NWO ? NWO : R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : WIDE ? 88 : 24;
     constexpr int TW = R8 ? kRep8Words : kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
     constexpr uint32_t kLead = 16u, kFit = kStgBytes - 32u;
     constexpr uint32_t kStride = SK ? kStgBytes + kStgBytes / 32 : kStgBytes;  // bytes per wave's stage
@@ -1468,6 +1473,8 @@ hipError_t launch_ragged_staged_dev(const RaggedArgs& a, int grid_blocks, hipStr
         // shipped: 1M x 180 B 0.1219 vs 0.1215 ms per replay call, 100-B payloads 0.0978 vs 0.1007)
         const uint64_t g = std::min<uint64_t>((uint64_t)grid_blocks, (a.n_rec + 64 * kStgWaves8 - 1) / (64 * kStgWaves8));
         hipLaunchKernelGGL((k_ragged_staged_pipe<false, true>), dim3((unsigned)g), dim3(kStgWaves8 * 64), 0, s, a);
+    } else if (!KARMA_AB_KNOB("KARMA_STAGE_WIDE", 1)) {  // (A/B: the window loop before the phased one)
+        hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 0, 0, false, false, false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
 #endif
     } else {
         hipLaunchKernelGGL((k_ragged_staged_pipe<false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
@@ -1498,6 +1505,13 @@ hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipSt
         return hipGetLastError();
     } else if (tm == 3) {
         hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 3, 0, true>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        return hipGetLastError();
+    }
+    if (!KARMA_AB_KNOB("KARMA_SPEC_WIDE", 1)) {  // (A/B: round 6's window loop, before the phased one)
+        if (skew)
+            hipLaunchKernelGGL((k_ragged_staged_pipe<true, false, 0, 0, true, false, false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 0, 0, true, false, false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
         return hipGetLastError();
     }
     if (KARMA_AB_KNOB("KARMA_SPEC_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves, plain stage)

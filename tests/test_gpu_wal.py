@@ -63,6 +63,8 @@ WALKS = {
     "spec": (True, 0, _lib.KARMA_WAL_CRC_PLAN),           # the uniform-stride pass tried on every call (KARMA_WAL_SPEC=2;
                                                           # the plan tries it unless the last try declined)
     "spec0": (True, 0, _lib.KARMA_WAL_CRC_PLAN),          # the plan with the uniform-stride pass off: the walk always
+    "specnarrow": (True, 0, _lib.KARMA_WAL_CRC_PLAN),     # "spec" without the phased window loop (KARMA_SPEC_WIDE=0)
+    "narrow": (True, 0, _lib.KARMA_WAL_CRC_PLAN),         # the walk's staged kernel without it (KARMA_STAGE_WIDE=0, pass off)
 }
 _LIST_CRC = ("listcrc", "listcrc4k")  # KARMA_WAL_LIST_CRC=1
 _NO_STAGED = ("sepdirect4",)  # KARMA_SMALL_STAGED=0
@@ -71,7 +73,9 @@ _SLICED = {"sliced": {"KARMA_WAL_SLICES": "2"},
            "sliced_r8": {"KARMA_WAL_SLICES": "2", "KARMA_STAGE_R8": "6", "KARMA_STAGE_SKEW": "0"},
            "rg0": {"KARMA_WAL_RG": "0"},
            "spec": {"KARMA_WAL_SPEC": "2"},
-           "spec0": {"KARMA_WAL_SPEC": "0"}}
+           "spec0": {"KARMA_WAL_SPEC": "0"},
+           "specnarrow": {"KARMA_WAL_SPEC": "2", "KARMA_SPEC_WIDE": "0"},
+           "narrow": {"KARMA_WAL_SPEC": "0", "KARMA_STAGE_WIDE": "0"}}
 _WALK = {"name": "split"}
 
 
@@ -89,7 +93,7 @@ def _walk_env(monkeypatch, walk):
         monkeypatch.setenv("KARMA_STAGE_R8", "1")
     else:
         monkeypatch.delenv("KARMA_STAGE_R8", raising=False)
-    for k in ("KARMA_WAL_SLICES", "KARMA_STAGE_SKEW", "KARMA_WAL_RG", "KARMA_WAL_SPEC"):
+    for k in ("KARMA_WAL_SLICES", "KARMA_STAGE_SKEW", "KARMA_WAL_RG", "KARMA_WAL_SPEC", "KARMA_SPEC_WIDE", "KARMA_STAGE_WIDE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in _SLICED.get(walk, {}).items():
         monkeypatch.setenv(k, v)
@@ -458,7 +462,7 @@ def test_replay_randomized_against_model(lib, monkeypatch):
 
 
 @pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc", "r8", "sliced", "sliced_r8", "rg0",
-                                  "spec", "spec0"])
+                                  "spec", "spec0", "specnarrow", "narrow"])
 @pytest.mark.parametrize("seg", [4096 + 4, 65536, 1 << 20])
 def test_replay_uniform_runs_speculative_walk(lib, seg, walk, monkeypatch):
     """Runs of one record size (the walker reads a round of headers at the last stride, lane j at
@@ -552,7 +556,7 @@ def test_replay_accepted_size0_records_advance_12(lib, seg, walk, monkeypatch):
     assert spills > 0, "some size-0 record must carry the chain into the next segment"
 
 
-@pytest.mark.parametrize("walk", ["split", "sep", "split4k", "r8", "sliced", "rg0", "spec", "spec0"])
+@pytest.mark.parametrize("walk", ["split", "sep", "split4k", "r8", "sliced", "rg0", "spec", "spec0", "narrow"])
 def test_replay_size_class_changes_between_calls(lib, walk, monkeypatch):
     """The device-planned replay launches one small-record kernel, chosen by the largest payload of
     the previous call on the same device (the staged kernel up to 183 B, the 4-lane kernel up to
@@ -707,8 +711,10 @@ _SPEC_CASES = ([(4096 + 4, s) for s in (1, 3, 4, 5, 15, 16, 17, 56, 120, 180, 18
                [(4096 + 4, s) for s in (184, 300)] + [(65536, s) for s in (500, 1000, 1024)] + [(1 << 20, 700)])
 
 
-@pytest.mark.parametrize("seg,size", _SPEC_CASES)
-def test_replay_uniform_stride_pass(lib, seg, size, monkeypatch):
+# (specnarrow: the staged kernel's sizes only, <= 183 B)
+@pytest.mark.parametrize("seg,size,walk", [(g, z, "spec") for g, z in _SPEC_CASES] +
+                         [(g, z, "specnarrow") for g, z in _SPEC_CASES if z <= 183])
+def test_replay_uniform_stride_pass(lib, seg, size, walk, monkeypatch):
     """The uniform-stride pass (engine.h WalSpec; tools build, KARMA_WAL_SPEC=2: tried on every call)
     over WALs of one payload size, up to 183 B (the staged kernel) and up to 1 KiB (the 4-lane one).  Its result is taken (karma_ab_wal_spec_last 1) for the zero tail
     after the last record (CORRUPT at the first unwritten header), segments filled to the image end
@@ -717,8 +723,8 @@ def test_replay_uniform_stride_pass(lib, seg, size, monkeypatch):
     length, a bad type, padding mid-segment, a size-0 record with the stale-word CRC (accepted, 12
     bytes), a length past the segment and a smaller record in a segment's tail; from checkpoints
     (records in segments 0-2) it is taken too.  Every result against the model, over the host image
-    and the device copy."""
-    _walk_env(monkeypatch, "spec")
+    and the device copy.  specnarrow: the staged kernel without its phased window loop (KARMA_SPEC_WIDE=0)."""
+    _walk_env(monkeypatch, walk)
     ab = _lib.load(_lib.AB_LIB_PATH)
     sig = size + 8
     per = seg // sig

@@ -55,7 +55,7 @@ def main():
     i = 0
     for r in range(args.rounds):
         for name, knobs in forms:
-            for k in ("KARMA_SPEC_TIMING", "KARMA_SPEC_P2"):
+            for k in ("KARMA_SPEC_TIMING", "KARMA_SPEC_P2", "KARMA_SPEC_WIDE", "KARMA_SPEC_R8"):
                 os.environ.pop(k, None)
             for kv in filter(None, knobs.split("+")):
                 k, v = kv.split(":")
@@ -71,6 +71,8 @@ def main():
                 _lib.check("replay", L.karma_wal_replay(None, d.data_ptr(), wal_bytes, seg, 0, ctypes.byref(nr),
                                                        ctypes.byref(stop), ctypes.byref(status), None, 0, 0))
                 e1.synchronize()
+                if "KARMA_SPEC_TIMING" not in knobs:  # (a form with true results: every record, CORRUPT at the tail)
+                    assert nr.value == n and status.value == 1, (name, nr.value, status.value)
                 if c >= 2:
                     res[name].append(e0.elapsed_time(e1) * 1e3)
         print(f"round {r}: " + "  ".join(f"{name} {np.median(res[name][-(args.calls - 2):]):.1f} us"
