@@ -283,6 +283,51 @@ __device__ __forceinline__ void step4(const uint32_t* lds, uint32_t X, uint32_t&
         a3 = stride_step8(lds, a3, v.w);
         return;
     }
+    if constexpr ((MODE & 88) == 88) {
+        // MODE bit 6 (with bits 3-4): phased, every lookup of the window in flight together -- the 16
+        // indices, the 16 reads, the xors, kept apart by scheduling barriers (lane_record_end's note)
+        const bool swp = (threadIdx.x & 16u) != 0;
+        const uint32_t s0 = swp ? 0x0c0c0105u : 0x0c0c0004u, s1 = swp ? 0x0c0c0004u : 0x0c0c0105u;
+        const uint32_t s2 = swp ? 0x0c0c0307u : 0x0c0c0206u, s3 = swp ? 0x0c0c0206u : 0x0c0c0307u;
+        const uint32_t acc[4] = {a0, a1, a2, a3};
+        uint32_t ix[16], l[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ix[4 * k] = __builtin_amdgcn_perm(X, acc[k], s0);
+            ix[4 * k + 1] = __builtin_amdgcn_perm(X, acc[k], s1);
+            ix[4 * k + 2] = __builtin_amdgcn_perm(X, acc[k], s2);
+            ix[4 * k + 3] = __builtin_amdgcn_perm(X, acc[k], s3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) l[k] = lds_at_byte(lds, ix[k]);
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = xor3(xor3(l[0], l[1], v.x), l[2], l[3]);
+        a1 = xor3(xor3(l[4], l[5], v.y), l[6], l[7]);
+        a2 = xor3(xor3(l[8], l[9], v.z), l[10], l[11]);
+        a3 = xor3(xor3(l[12], l[13], v.w), l[14], l[15]);
+        return;
+    }
+    if constexpr ((MODE & 88) == 64) {  // the same phasing on the 32-copy image (stride_step)
+        const uint32_t acc[4] = {a0, a1, a2, a3};
+        uint32_t ix[16], l[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ix[4 * k] = __builtin_amdgcn_perm(X, acc[k], kSel0);
+            ix[4 * k + 1] = __builtin_amdgcn_perm(X, acc[k], kSel1);
+            ix[4 * k + 2] = __builtin_amdgcn_perm(X, acc[k], kSel2);
+            ix[4 * k + 3] = __builtin_amdgcn_perm(X, acc[k], kSel3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) l[k] = lds_at_byte(lds, ix[k]);
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = xor3(xor3(l[0], l[1], v.x), l[2], l[3]);
+        a1 = xor3(xor3(l[4], l[5], v.y), l[6], l[7]);
+        a2 = xor3(xor3(l[8], l[9], v.z), l[10], l[11]);
+        a3 = xor3(xor3(l[12], l[13], v.w), l[14], l[15]);
+        return;
+    }
     if constexpr ((MODE & 24) == 24) {
         a0 = stride_step16s(lds, X, a0, v.x);
         a1 = stride_step16s(lds, X, a1, v.y);

@@ -279,7 +279,7 @@ __device__ uint64_t* g_seg_log;
 // 16-copy one (64 KiB): half the table fill the chunk loads queue behind.
 // LATE (tools build A/B, round 6): the comb maps only the workgroup fold uses (Z_8U .. Z_64U, 16 of
 // the fill's 49 KiB) loaded after the chunk loads and stored after the steps.
-template <bool NT, bool ARRIVE = false, bool R8 = false, bool LATE = false>
+template <bool NT, bool ARRIVE = false, bool R8 = false, bool LATE = false, bool WIDE = false>
 __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     constexpr int TW = R8 ? kRep8Words : kRep16Words;
     constexpr int kSegZ4 = TW, kSegComb = kSegZ4 + kSmallWords, kSegGrid = kSegComb + kCombMaps * 1024;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     uint32_t a0 = x0.x, a1 = x0.y, a2 = x0.z, a3 = x0.w;
 #pragma unroll
     for (int q = 1; q < kSegMaxChunks; ++q)
-        if (q < L.nch - 1 || (q == L.nch - 1 && L.lok)) step4<R8 ? 32 : 24>(lds, X, a0, a1, a2, a3, v[q]);
+        if (q < L.nch - 1 || (q == L.nch - 1 && L.lok)) step4<R8 ? 32 : WIDE ? 88 : 24>(lds, X, a0, a1, a2, a3, v[q]);
     LdsCopy<kCombMaps * 1024, kBlockThreads> grid;  // the last workgroup's fold maps, in flight meanwhile
     if (ARRIVE || last_wg) grid.load(A.block_blob);
     uint32_t tag = 0;  // wave 0 publishes the workgroup's state, tagged with the call's tag
@@ -668,6 +668,8 @@ hipError_t launch_segment_once(const FixedArgs& a, int grid_blocks, hipStream_t 
 #ifdef KARMA_AB
     else if (KARMA_AB_KNOB("KARMA_SEGMENT_R8", 0))  // (A/B: the 8-copy stride image)
         hipLaunchKernelGGL((k_segment_once<true, false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (KARMA_AB_KNOB("KARMA_SEGMENT_WIDE", 0))  // (A/B: the phased window step, step4 MODE 88)
+        hipLaunchKernelGGL((k_segment_once<true, false, false, false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (KARMA_AB_KNOB("KARMA_SEGMENT_LATE", 0))  // (A/B: the workgroup fold's maps behind the chunks)
         hipLaunchKernelGGL((k_segment_once<true, false, false, true>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
 #endif

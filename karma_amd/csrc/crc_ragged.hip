@@ -1612,6 +1612,8 @@ hipError_t launch_ragged_main(const RaggedArgs& a, int grid_blocks, hipStream_t 
         hipLaunchKernelGGL((k_units_ragged<kRaggedUnitsPF, 2>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else if (um == 3)
         hipLaunchKernelGGL((k_units_ragged<kRaggedUnitsPF, 3>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
+    else if (um == 64)  // (A/B: the phased window step, step4 MODE 64)
+        hipLaunchKernelGGL((k_units_ragged<kRaggedUnitsPF, 64>), dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);
     else
 #endif
         hipLaunchKernelGGL(k_units_ragged<>, dim3(grid_blocks), dim3(kBlockThreads), 0, s, a);

@@ -34,7 +34,8 @@ def main():
                    "(instead of the tools build's KARMA_SEGMENT_ONCE=1 / 0)")
     p.add_argument("--variants", default="1,0", help="KARMA_SEGMENT_ONCE values of the tools build (1 = the grid's "
                    "last workgroup folds, 2 = the last-arriving one, 0 = the looping fused kernel; r8 = 1 on the "
-                   "8-copy stride image; late = 1 with the workgroup fold's maps loaded behind the chunks)")
+                   "8-copy stride image; late = 1 with the workgroup fold's maps loaded behind the chunks; wide = 1 with the "
+                   "phased window step)")
     a = p.parse_args()
     dev = torch.device("cuda:0")
     nseg, top = 64, 64 << 20
@@ -57,8 +58,8 @@ def main():
         def call(v):
             lib = libs.get(v, L)
             if not libs:  # (r8 / late: KARMA_SEGMENT_ONCE=1 with KARMA_SEGMENT_R8=1 / KARMA_SEGMENT_LATE=1)
-                os.environ["KARMA_SEGMENT_ONCE"] = "1" if v in ("r8", "late") else v
-                for name, knob in (("r8", "KARMA_SEGMENT_R8"), ("late", "KARMA_SEGMENT_LATE")):
+                os.environ["KARMA_SEGMENT_ONCE"] = "1" if v in ("r8", "late", "wide") else v
+                for name, knob in (("r8", "KARMA_SEGMENT_R8"), ("late", "KARMA_SEGMENT_LATE"), ("wide", "KARMA_SEGMENT_WIDE")):
                     if v == name:
                         os.environ[knob] = "1"
                     else:
