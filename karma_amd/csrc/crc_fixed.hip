@@ -118,7 +118,15 @@ __device__ void fused_record_fold(const FixedArgs& A, uint32_t* lds, uint32_t* w
     }
 }
 
-template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = 0, bool BAL = true, int KW = 1, bool FUSE = false>
+// (KARMA_FIXED_STEP_MODE / KARMA_SEGMENT_STEP_WIDE: a build's default window step -- step4 MODE 64 / 88,
+// the phased step, for a whole-build A/B through tools/ragged_study.py LIBS; the shipped build: 0)
+#ifndef KARMA_FIXED_STEP_MODE
+#define KARMA_FIXED_STEP_MODE 0
+#endif
+#ifndef KARMA_SEGMENT_STEP_WIDE
+#define KARMA_SEGMENT_STEP_WIDE false
+#endif
+template <int PF, bool NT, bool HAS_INIT, bool WAVE_COMB, int MODE = KARMA_FIXED_STEP_MODE, bool BAL = true, int KW = 1, bool FUSE = false>
 __global__ __launch_bounds__(kBlockThreads) void k_units_fixed(FixedArgs A) {
     static_assert(!FUSE || WAVE_COMB, "the fused combine folds wave states");
     KB_SET_ARENA(reinterpret_cast<uintptr_t>(A.arena) & ~uintptr_t(15),
@@ -279,7 +287,7 @@ __device__ uint64_t* g_seg_log;
 // 16-copy one (64 KiB): half the table fill the chunk loads queue behind.
 // LATE (tools build A/B, round 6): the comb maps only the workgroup fold uses (Z_8U .. Z_64U, 16 of
 // the fill's 49 KiB) loaded after the chunk loads and stored after the steps.
-template <bool NT, bool ARRIVE = false, bool R8 = false, bool LATE = false, bool WIDE = false>
+template <bool NT, bool ARRIVE = false, bool R8 = false, bool LATE = false, bool WIDE = KARMA_SEGMENT_STEP_WIDE>
 __global__ __launch_bounds__(kBlockThreads) void k_segment_once(FixedArgs A) {
     constexpr int TW = R8 ? kRep8Words : kRep16Words;
     constexpr int kSegZ4 = TW, kSegComb = kSegZ4 + kSmallWords, kSegGrid = kSegComb + kCombMaps * 1024;
@@ -633,15 +641,15 @@ hipError_t launch_fixed(const FixedArgs& a, int grid_blocks, hipStream_t s) {
     // (1 KiB units: 0.700 vs 0.669 ms per 4 GiB; 4 KiB: 0.628 vs 0.641).
     if (a.fold_k) {  // k = fold_k units per record folded in the wave, units >= 2 KiB (planner)
 #define KARMA_FOLD(KW)                                                                                \
-    if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false, 0, true, KW>), grid, blk, 0, s, a); \
-    else hipLaunchKernelGGL((k_units_fixed<4, true, false, false, 0, true, KW>), grid, blk, 0, s, a);
+    if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, false, KARMA_FIXED_STEP_MODE, true, KW>), grid, blk, 0, s, a); \
+    else hipLaunchKernelGGL((k_units_fixed<4, true, false, false, KARMA_FIXED_STEP_MODE, true, KW>), grid, blk, 0, s, a);
         if (a.fold_k == 2) { KARMA_FOLD(2) } else if (a.fold_k == 4) { KARMA_FOLD(4) } else { KARMA_FOLD(8) }
 #undef KARMA_FOLD
     } else if (a.comb_maps && a.fctl) {  // one record, its wave states folded by the last workgroup
         if (a.n_rec != 1 || !a.block_blob || a.comb_m == 0 || a.units_per_rec / kGroupsPerWave > a.comb_m * 1024)
             return hipErrorInvalidValue;
-        if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true, 0, true, 1, true>), grid, blk, 0, s, a);
-        else hipLaunchKernelGGL((k_units_fixed<4, true, false, true, 0, true, 1, true>), grid, blk, 0, s, a);
+        if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true, KARMA_FIXED_STEP_MODE, true, 1, true>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_units_fixed<4, true, false, true, KARMA_FIXED_STEP_MODE, true, 1, true>), grid, blk, 0, s, a);
     } else if (a.comb_maps) {  // k % 8 == 0, units >= 2 KiB (planner)
         if (a.init) hipLaunchKernelGGL((k_units_fixed<4, true, true, true>), grid, blk, 0, s, a);
         else hipLaunchKernelGGL((k_units_fixed<4, true, false, true>), grid, blk, 0, s, a);

@@ -589,7 +589,10 @@ __device__ __forceinline__ uint64_t ragged_next_step(const RaggedArgs& A, uint32
     return wb_next;
 }
 
-template <int PF = kRaggedUnitsPF, int MODE = 0>
+#ifndef KARMA_UNITS_STEP_MODE  // (a build's default window step: 64 = the phased step4, whole-build A/B)
+#define KARMA_UNITS_STEP_MODE 0
+#endif
+template <int PF = kRaggedUnitsPF, int MODE = KARMA_UNITS_STEP_MODE>
 __global__ __launch_bounds__(kBlockThreads) void k_units_ragged(RaggedArgs A) {
     KB_SET_ARENA(A.kb_lo, A.kb_hi);
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
