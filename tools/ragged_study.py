@@ -96,6 +96,7 @@ layouts = {"aligned 4096": (np.full(GB // 4096, 4096, np.uint32), np.arange(GB /
 if os.environ.get("LAYOUTS"):  # a subset, e.g. LAYOUTS="aligned 4096,aligned 2048"
     layouts = {k: v for k, v in layouts.items() if k in os.environ["LAYOUTS"].split(",")}
 cases = {}
+first = next(iter(LIBS))
 for lib_name, L in LIBS.items():  # (every build: its CRCs compared with the first build's)
     cases[f"fixed 4096 [{lib_name}]"] = (fixed_case(L, 4096), "fixed 4096")
 for name, (ln, of) in layouts.items():
