@@ -346,7 +346,7 @@ def pmc_traffic(path: str, workload: str, n_bytes_per_launch: int):
     return d.get("hbm_bytes_per_launch")
 
 
-REPLAY_PMC = "r06spec_wal_replay_pmc.json"  # tools/pmc_replay.sh + tools/pmc_kernels.py: the uniform-stride pass
+REPLAY_PMC = "r06wide_wal_replay_pmc.json"  # tools/pmc_replay.sh + tools/pmc_kernels.py: the uniform-stride pass
 
 
 def replay_pmc_traffic(n_rec: int, rec_bytes: int):
