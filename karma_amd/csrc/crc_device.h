@@ -1059,6 +1059,32 @@ __device__ __forceinline__ uint32_t lane_record_end(const uint32_t* lds, uint32_
         const bool swp = (threadIdx.x & 16u) != 0;
         const uint32_t s0 = swp ? 0x0c0c0105u : 0x0c0c0004u, s1 = swp ? 0x0c0c0004u : 0x0c0c0105u;
         const uint32_t s2 = swp ? 0x0c0c0307u : 0x0c0c0206u, s3 = swp ? 0x0c0c0206u : 0x0c0c0307u;
+        // SMODE bit 7: when every active lane's windows are dword-aligned (sh == 0: payload sizes and
+        // strides that are multiples of 4), the windows are the stage dwords themselves, no funnel shifts
+        if ((SMODE & 128) != 0 && __ballot(sh != 0u) == 0) {
+            for (uint32_t j = 1; j < W; ++j) {
+                q += 4;
+                const uint32_t acc[4] = {a0, a1, a2, a3};
+                uint32_t ix[16], l[16];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    ix[4 * k] = __builtin_amdgcn_perm(X, acc[k], s0);
+                    ix[4 * k + 1] = __builtin_amdgcn_perm(X, acc[k], s1);
+                    ix[4 * k + 2] = __builtin_amdgcn_perm(X, acc[k], s2);
+                    ix[4 * k + 3] = __builtin_amdgcn_perm(X, acc[k], s3);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t e0 = rd(q), e1 = rd(q + 1), e2 = rd(q + 2), e3 = rd(q + 3);
+#pragma unroll
+                for (int k = 0; k < 16; ++k) l[k] = lds_at_byte(lds, ix[k]);
+                __builtin_amdgcn_sched_barrier(0);
+                a0 = xor3(xor3(l[0], l[1], e0 ^ carry), l[2], l[3]);
+                carry = 0u;
+                a1 = xor3(xor3(l[4], l[5], e1), l[6], l[7]);
+                a2 = xor3(xor3(l[8], l[9], e2), l[10], l[11]);
+                a3 = xor3(xor3(l[12], l[13], e3), l[14], l[15]);
+            }
+        } else
         for (uint32_t j = 1; j < W; ++j) {
             q += 4;
             const uint32_t acc[4] = {a0, a1, a2, a3};

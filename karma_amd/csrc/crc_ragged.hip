@@ -1115,6 +1115,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // window in flight together, one round trip per window (tools build A/B KARMA_SPEC_WIDE=0 /
 // KARMA_STAGE_WIDE=0: the loop the compiler schedules, two; 1M x 180 B uniform pass 52.8 -> 51.1
 // us, profiles/r06_staged_phased_window_ab.txt).
+// AL (with WIDE): the phased loop's fast path for windows that are whole stage dwords (every active
+// lane's sh == 0: no funnel shifts; 52.7 -> 51.9 us on 180 B, profiles/r06_staged_aligned_path_ab.txt;
+// tools build KARMA_SPEC_AL=0: without it).
 // NWO (tools build A/B, with R8): that many waves instead of kStgWaves8, leaving LDS for another
 // kernel's workgroups on the same CU (the sliced WAL replay's walkers, wal.cc).
 // SPEC (the uniform-stride WAL replay, engine.h WalSpec): every workgroup reads segment 0's first
@@ -1126,14 +1129,15 @@ __global__ __launch_bounds__(kBlockThreads) void k_ragged_direct4(RaggedArgs A) 
 // batch also classifies the header after its last slot.  The wave's smallest keys go to
 // spec->stop_key / dev_key by one atomicMin, and the wave then ends: its later slots have larger
 // keys, which can change neither the first stop nor whether a break comes before it.
-template <bool SK, bool R8 = false, int TM = 0, int NWO = 0, bool SPEC = false, bool P2 = false, bool WIDE = !R8>
+template <bool SK, bool R8 = false, int TM = 0, int NWO = 0, bool SPEC = false, bool P2 = false, bool WIDE = !R8,
+          bool AL = WIDE>
 __global__ __launch_bounds__((NWO ? NWO : R8 ? kStgWaves8 : kStgWaves) * 64) void k_ragged_staged_pipe(RaggedArgs A) {
     static_assert(!P2 || SPEC, "two batches in flight: the uniform-stride form only");
     static_assert(!(SK && R8), "the 8-copy form has the plain stage only");
     static_assert(!(SPEC && NWO), "the uniform-stride form has no wave-count override");
     static_assert(!(WIDE && R8), "the phased window loop reads the 16-copy image");
     constexpr bool END = true;
-    constexpr int NW = NWO ? NWO : R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : WIDE ? 88 : 24;
+    constexpr int NW = NWO ? NWO : R8 ? kStgWaves8 : kStgWaves, SMODE = R8 ? 32 : WIDE ? (AL ? 216 : 88) : 24;
     constexpr int TW = R8 ? kRep8Words : kRep16Words, Z4 = TW, T8 = TW + 1024, BUF = TW + 1280;
     constexpr uint32_t kLead = 16u, kFit = kStgBytes - 32u;
     constexpr uint32_t kStride = SK ? kStgBytes + kStgBytes / 32 : kStgBytes;  // bytes per wave's stage
@@ -1515,6 +1519,13 @@ hipError_t launch_ragged_staged_spec(const RaggedArgs& a, int grid_blocks, hipSt
             hipLaunchKernelGGL((k_ragged_staged_pipe<true, false, 0, 0, true, false, false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
         else
             hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 0, 0, true, false, false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        return hipGetLastError();
+    }
+    if (!KARMA_AB_KNOB("KARMA_SPEC_AL", 1)) {  // (A/B: the phased loop without its dword-aligned fast path)
+        if (skew)
+            hipLaunchKernelGGL((k_ragged_staged_pipe<true, false, 0, 0, true, false, true, false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_ragged_staged_pipe<false, false, 0, 0, true, false, true, false>), dim3(grid_blocks), dim3(kStgWaves * 64), 0, s, a);
         return hipGetLastError();
     }
     if (KARMA_AB_KNOB("KARMA_SPEC_R8", 0)) {  // (A/B: the 8-copy image, kStgWaves8 waves, plain stage)

@@ -65,6 +65,7 @@ WALKS = {
     "spec0": (True, 0, _lib.KARMA_WAL_CRC_PLAN),          # the plan with the uniform-stride pass off: the walk always
     "specnarrow": (True, 0, _lib.KARMA_WAL_CRC_PLAN),     # "spec" without the phased window loop (KARMA_SPEC_WIDE=0)
     "narrow": (True, 0, _lib.KARMA_WAL_CRC_PLAN),         # the walk's staged kernel without it (KARMA_STAGE_WIDE=0, pass off)
+    "specnoal": (True, 0, _lib.KARMA_WAL_CRC_PLAN),       # "spec" without the dword-aligned fast path (KARMA_SPEC_AL=0)
 }
 _LIST_CRC = ("listcrc", "listcrc4k")  # KARMA_WAL_LIST_CRC=1
 _NO_STAGED = ("sepdirect4",)  # KARMA_SMALL_STAGED=0
@@ -75,7 +76,8 @@ _SLICED = {"sliced": {"KARMA_WAL_SLICES": "2"},
            "spec": {"KARMA_WAL_SPEC": "2"},
            "spec0": {"KARMA_WAL_SPEC": "0"},
            "specnarrow": {"KARMA_WAL_SPEC": "2", "KARMA_SPEC_WIDE": "0"},
-           "narrow": {"KARMA_WAL_SPEC": "0", "KARMA_STAGE_WIDE": "0"}}
+           "narrow": {"KARMA_WAL_SPEC": "0", "KARMA_STAGE_WIDE": "0"},
+           "specnoal": {"KARMA_WAL_SPEC": "2", "KARMA_SPEC_AL": "0"}}
 _WALK = {"name": "split"}
 
 
@@ -93,7 +95,7 @@ def _walk_env(monkeypatch, walk):
         monkeypatch.setenv("KARMA_STAGE_R8", "1")
     else:
         monkeypatch.delenv("KARMA_STAGE_R8", raising=False)
-    for k in ("KARMA_WAL_SLICES", "KARMA_STAGE_SKEW", "KARMA_WAL_RG", "KARMA_WAL_SPEC", "KARMA_SPEC_WIDE", "KARMA_STAGE_WIDE"):
+    for k in ("KARMA_WAL_SLICES", "KARMA_STAGE_SKEW", "KARMA_WAL_RG", "KARMA_WAL_SPEC", "KARMA_SPEC_WIDE", "KARMA_STAGE_WIDE", "KARMA_SPEC_AL"):
         monkeypatch.delenv(k, raising=False)
     for k, v in _SLICED.get(walk, {}).items():
         monkeypatch.setenv(k, v)
@@ -462,7 +464,7 @@ def test_replay_randomized_against_model(lib, monkeypatch):
 
 
 @pytest.mark.parametrize("walk", ["whole", "split", "split4k", "inline", "listcrc", "r8", "sliced", "sliced_r8", "rg0",
-                                  "spec", "spec0", "specnarrow", "narrow"])
+                                  "spec", "spec0", "specnarrow", "narrow", "specnoal"])
 @pytest.mark.parametrize("seg", [4096 + 4, 65536, 1 << 20])
 def test_replay_uniform_runs_speculative_walk(lib, seg, walk, monkeypatch):
     """Runs of one record size (the walker reads a round of headers at the last stride, lane j at
@@ -713,7 +715,7 @@ _SPEC_CASES = ([(4096 + 4, s) for s in (1, 3, 4, 5, 15, 16, 17, 56, 120, 180, 18
 
 # (specnarrow: the staged kernel's sizes only, <= 183 B)
 @pytest.mark.parametrize("seg,size,walk", [(g, z, "spec") for g, z in _SPEC_CASES] +
-                         [(g, z, "specnarrow") for g, z in _SPEC_CASES if z <= 183])
+                         [(g, z, w) for g, z in _SPEC_CASES if z <= 183 for w in ("specnarrow", "specnoal")])
 def test_replay_uniform_stride_pass(lib, seg, size, walk, monkeypatch):
     """The uniform-stride pass (engine.h WalSpec; tools build, KARMA_WAL_SPEC=2: tried on every call)
     over WALs of one payload size, up to 183 B (the staged kernel) and up to 1 KiB (the 4-lane one).  Its result is taken (karma_ab_wal_spec_last 1) for the zero tail

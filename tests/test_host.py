@@ -246,7 +246,7 @@ def test_shipped_library_has_no_variant_knobs():
                  b"KARMA_RAGGED_DYN", b"KARMA_GATHER_PARTS", b"KARMA_SMALL_WHICH",
                  b"KARMA_STAGE_SKEW", b"KARMA_STAGE_R8", b"KARMA_SEGMENT_ONCE", b"KARMA_RAGGED_GRID",
                  b"KARMA_STAGE_TIMING", b"KARMA_STAGE_PAIR", b"KARMA_RAGGED_UNITS_MODE", b"KARMA_RAGGED_UNITS_FLAT",
-                 b"KARMA_RAGGED_UNITS_TWICE", b"KARMA_RAGGED_UNITS_FIXEDLOOP", b"KARMA_SPEC_WIDE", b"KARMA_STAGE_WIDE"):
+                 b"KARMA_RAGGED_UNITS_TWICE", b"KARMA_RAGGED_UNITS_FIXEDLOOP", b"KARMA_SPEC_WIDE", b"KARMA_STAGE_WIDE", b"KARMA_SPEC_AL"):
         assert knob not in blob, knob
 
 

@@ -55,7 +55,7 @@ def main():
     i = 0
     for r in range(args.rounds):
         for name, knobs in forms:
-            for k in ("KARMA_SPEC_TIMING", "KARMA_SPEC_P2", "KARMA_SPEC_WIDE", "KARMA_SPEC_R8"):
+            for k in ("KARMA_SPEC_TIMING", "KARMA_SPEC_P2", "KARMA_SPEC_WIDE", "KARMA_SPEC_R8", "KARMA_SPEC_AL"):
                 os.environ.pop(k, None)
             for kv in filter(None, knobs.split("+")):
                 k, v = kv.split(":")
